@@ -1,0 +1,1047 @@
+// Host runtime of libtvfem.so: context, mesh partition, device state, field
+// transfer, the Newton + Jacobi-PCG driver, the viscoelastic step and the RCCL
+// halo / reductions.  C-ABI in include/tvfem.h.
+//
+// Reference mapping (file:line under /root/reference):
+//   Ctx construction      ThermoViscoProblem.__init__ (ThermoViscoProblem.py:24-58)
+//   initial condition     _set_initial_condition (:187-233)
+//   tv_solve_T            _solve_T (:384-391) -> dolfinx NewtonSolver [3P]
+//                         configured at _setup_solver (:330-346)
+//   tv_visco_update       _solve_Tf .. _solve_stress (:393-595)
+//   tv_step               solve_timestep (:367-381) without _write_output
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "tv_internal.h"
+
+namespace tv {
+
+static std::mutex g_err_mu;
+static std::string g_err;
+
+static void set_global_error(const std::string& m) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_err = m;
+}
+
+struct FieldInfo {
+  double* ptr = nullptr;
+  int bs = 1;       // components
+  int space = 0;    // 0 T space, 1 sigma space
+  bool alloc = false;
+};
+
+struct Ctx {
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  tv_params P{};
+  tv_options O{};
+  int dim = 1;
+  int fam_T = TV_CG, fam_S = TV_CG;
+  int perm[3] = {0, -1, -1};  // storage axis -> physical axis (-1 degenerate)
+  int n_parts = 1, part = 0;
+  // global / local sizes
+  int Nnode_glob[3] = {1, 1, 1};  // per storage axis
+  int Ncell_glob[3] = {0, 0, 0};
+  int plane_begin = 0, plane_end = 0;  // owned global planes (CG) / cell layers (DG) along storage axis 2
+  CgGrid cg{};
+  DgGrid dg{};
+  int64_t nT = 0, nS = 0;          // local dofs incl. ghosts
+  int64_t ownT_off = 0, ownT_n = 0;
+  int64_t ownS_off = 0, ownS_n = 0;
+  int64_t globT_off = 0, globS_off = 0;
+  std::vector<std::vector<double>> coords;  // physical axes
+  FieldInfo f[TV_NUM_FIELDS];
+  double* coef[3] = {nullptr, nullptr, nullptr};
+  double* dgh[3] = {nullptr, nullptr, nullptr};
+  int* map = nullptr;
+  // PCG work (T space, local size)
+  double *r = nullptr, *z = nullptr, *pA = nullptr, *pB = nullptr, *w = nullptr, *dinv = nullptr;
+  double* partials = nullptr;
+  int n_partials_cap = 0;
+  double* sums = nullptr;
+  PcgState* st = nullptr;
+  PcgState* h_st = nullptr;  // pinned
+  double* h_sums = nullptr;  // pinned
+  double* scratch = nullptr;  // transfer scratch
+  size_t scratch_bytes = 0;
+  // comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // stats
+  int last_newton = 0, last_krylov = 0;
+  double last_dx = 0.0;
+  int pcg_hint = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+};
+
+#define HIPC(expr)                                                                              \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return c->fail(TV_ERR_HIP, std::string("HIP error ") + hipGetErrorString(e_) + " at " +  \
+                                     __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr); \
+  } while (0)
+
+#define NCCLC(expr)                                                                             \
+  do {                                                                                          \
+    ncclResult_t r_ = (expr);                                                                   \
+    if (r_ != ncclSuccess)                                                                      \
+      return c->fail(TV_ERR_COMM, std::string("RCCL error ") + ncclGetErrorString(r_) + " at " + \
+                                      std::to_string(__LINE__) + ": " #expr);                   \
+  } while (0)
+
+// --------------------------------------------------------------------------------------
+// geometry helpers
+// --------------------------------------------------------------------------------------
+static void axis_coefs(const std::vector<double>& X, int first, int count, std::vector<double>& out) {
+  // 1D P1 assembled mass / stiffness rows and adjacent cell lengths for global
+  // nodes [first, first+count) of an axis with node coordinates X.
+  const int n = (int)X.size();
+  out.assign((size_t)count * C_NCOEF, 0.0);
+  for (int q = 0; q < count; ++q) {
+    const int i = first + q;
+    double* c = &out[(size_t)q * C_NCOEF];
+    if (n == 1) {
+      c[C_MDI] = 1.0;
+      continue;
+    }
+    const double hlo = (i > 0) ? X[i] - X[i - 1] : 0.0;
+    const double hhi = (i < n - 1) ? X[i + 1] - X[i] : 0.0;
+    c[C_MLO] = hlo / 6.0;
+    c[C_MDI] = hlo / 3.0 + hhi / 3.0;
+    c[C_MUP] = hhi / 6.0;
+    c[C_KLO] = hlo > 0 ? -1.0 / hlo : 0.0;
+    c[C_KDI] = (hlo > 0 ? 1.0 / hlo : 0.0) + (hhi > 0 ? 1.0 / hhi : 0.0);
+    c[C_KUP] = hhi > 0 ? -1.0 / hhi : 0.0;
+    c[C_HLO] = hlo;
+    c[C_HHI] = hhi;
+  }
+}
+
+static const std::vector<double>& storage_coords(Ctx* c, int s, std::vector<double>& tmp) {
+  if (c->perm[s] < 0) {
+    tmp.assign(1, 0.0);
+    return tmp;
+  }
+  return c->coords[c->perm[s]];
+}
+
+static int alloc_field(Ctx* c, int id, int space, int bs) {
+  FieldInfo& fi = c->f[id];
+  fi.space = space;
+  fi.bs = bs;
+  const int64_t n = (space == 0 ? c->nT : c->nS);
+  HIPC(hipMalloc(&fi.ptr, sizeof(double) * (size_t)std::max<int64_t>(1, n * bs)));
+  HIPC(hipMemsetAsync(fi.ptr, 0, sizeof(double) * (size_t)(n * bs), c->stream));
+  fi.alloc = true;
+  return TV_OK;
+}
+
+static void alias_field(Ctx* c, int id, int target) {
+  c->f[id] = c->f[target];
+  c->f[id].alloc = false;
+}
+
+static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
+  const int d = m->dim;
+  if (d < 1 || d > 3) return c->fail(TV_ERR_ARG, "mesh dim must be 1..3");
+  c->dim = d;
+  c->coords.resize(d);
+  for (int a = 0; a < d; ++a) {
+    if (m->n_cells[a] < 1) return c->fail(TV_ERR_ARG, "n_cells must be >= 1 on every axis");
+    if (!m->coords[a]) return c->fail(TV_ERR_ARG, "coords missing");
+    c->coords[a].assign(m->coords[a], m->coords[a] + m->n_cells[a] + 1);
+    for (int i = 0; i < m->n_cells[a]; ++i)
+      if (!(c->coords[a][i + 1] > c->coords[a][i]))
+        return c->fail(TV_ERR_ARG, "node coordinates must be strictly increasing");
+  }
+  // storage axes: 0 = x; 2 = partition axis; 1 = remaining (or degenerate)
+  if (d == 1) {
+    c->perm[0] = 0; c->perm[1] = -1; c->perm[2] = -1;
+  } else if (d == 2) {
+    c->perm[0] = 0; c->perm[1] = -1; c->perm[2] = 1;
+  } else {
+    int pa = m->part_axis;
+    if (pa < 0) pa = (m->n_cells[1] >= m->n_cells[2]) ? 1 : 2;
+    if (pa != 1 && pa != 2) return c->fail(TV_ERR_ARG, "part_axis must be 1 (y) or 2 (z) for 3D meshes");
+    c->perm[0] = 0; c->perm[2] = pa; c->perm[1] = (pa == 1) ? 2 : 1;
+  }
+  c->n_parts = std::max(1, m->n_parts);
+  c->part = m->part;
+  if (c->part < 0 || c->part >= c->n_parts) return c->fail(TV_ERR_ARG, "part out of range");
+  if (c->n_parts > 1 && (d == 1 || c->fam_T != TV_CG || c->fam_S != TV_CG))
+    return c->fail(TV_ERR_ARG, "partitioned meshes require dim >= 2 and CG temperature and stress spaces");
+  for (int s = 0; s < 3; ++s) {
+    c->Ncell_glob[s] = (c->perm[s] < 0) ? 0 : m->n_cells[c->perm[s]];
+    c->Nnode_glob[s] = c->Ncell_glob[s] + 1;
+  }
+  std::vector<double> tmp;
+  if (c->fam_T == TV_CG) {
+    const int N2 = c->Nnode_glob[2];
+    const int P = c->n_parts, p = c->part;
+    const int b0 = (int)((int64_t)N2 * p / P), b1 = (int)((int64_t)N2 * (p + 1) / P);
+    if (b1 - b0 < 1) return c->fail(TV_ERR_ARG, "too many partitions for the mesh");
+    c->plane_begin = b0;
+    c->plane_end = b1;
+    CgGrid& g = c->cg;
+    g.n0 = c->Nnode_glob[0];
+    g.n1 = c->Nnode_glob[1];
+    g.g_lo = (p > 0) ? 1 : 0;
+    g.g_hi = (p < P - 1) ? 1 : 0;
+    g.n2 = (b1 - b0) + g.g_lo + g.g_hi;
+    g.k_begin = g.g_lo;
+    g.k_end = g.g_lo + (b1 - b0);
+    g.deg1 = (c->perm[1] < 0);
+    g.deg2 = (c->perm[2] < 0);
+    g.bnd[0][0] = g.bnd[0][1] = 1;
+    g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
+    g.bnd[2][0] = (!g.deg2 && p == 0) ? 1 : 0;
+    g.bnd[2][1] = (!g.deg2 && p == P - 1) ? 1 : 0;
+    const int first[3] = {0, 0, b0 - g.g_lo};
+    const int cnt[3] = {g.n0, g.n1, g.n2};
+    for (int s = 0; s < 3; ++s) {
+      std::vector<double> cf;
+      axis_coefs(storage_coords(c, s, tmp), first[s], cnt[s], cf);
+      HIPC(hipMalloc(&c->coef[s], cf.size() * sizeof(double)));
+      HIPC(hipMemcpy(c->coef[s], cf.data(), cf.size() * sizeof(double), hipMemcpyHostToDevice));
+      g.coef[s] = c->coef[s];
+    }
+    const int64_t plane = (int64_t)g.n0 * g.n1;
+    c->nT = plane * g.n2;
+    c->ownT_off = plane * g.k_begin;
+    c->ownT_n = plane * (g.k_end - g.k_begin);
+    c->globT_off = plane * b0;
+  } else {
+    DgGrid& g = c->dg;
+    g.c0 = c->Ncell_glob[0];
+    g.c1 = std::max(1, c->Ncell_glob[1]);
+    g.c2 = std::max(1, c->Ncell_glob[2]);
+    g.k_begin = 0;
+    g.k_end = g.c2;
+    g.deg1 = (c->perm[1] < 0);
+    g.deg2 = (c->perm[2] < 0);
+    g.bnd[0][0] = g.bnd[0][1] = 1;
+    g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
+    g.bnd[2][0] = g.bnd[2][1] = g.deg2 ? 0 : 1;
+    for (int s = 0; s < 3; ++s) {
+      const std::vector<double>& X = storage_coords(c, s, tmp);
+      std::vector<double> h;
+      if (X.size() == 1) h.assign(1, 1.0);
+      else for (size_t i = 0; i + 1 < X.size(); ++i) h.push_back(X[i + 1] - X[i]);
+      HIPC(hipMalloc(&c->dgh[s], h.size() * sizeof(double)));
+      HIPC(hipMemcpy(c->dgh[s], h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+      g.h[s] = c->dgh[s];
+    }
+    const int nl = 1 << d;
+    c->nT = (int64_t)g.c0 * g.c1 * g.c2 * nl;
+    c->ownT_off = 0;
+    c->ownT_n = c->nT;
+    c->globT_off = 0;
+    c->plane_begin = 0;
+    c->plane_end = g.c2;
+  }
+  // sigma space
+  if (c->fam_S == c->fam_T) {
+    c->nS = c->nT;
+    c->ownS_off = c->ownT_off;
+    c->ownS_n = c->ownT_n;
+    c->globS_off = c->globT_off;
+  } else {
+    const int nl = 1 << d;
+    const int64_t ncell = (int64_t)std::max(1, c->Ncell_glob[0]) * std::max(1, c->Ncell_glob[1]) *
+                          std::max(1, c->Ncell_glob[2]);
+    const int64_t nnode = (int64_t)c->Nnode_glob[0] * c->Nnode_glob[1] * c->Nnode_glob[2];
+    c->nS = (c->fam_S == TV_CG) ? nnode : ncell * nl;
+    c->ownS_off = 0;
+    c->ownS_n = c->nS;
+    c->globS_off = 0;
+    // fem::interpolate: cells in order, last cell written wins at shared sigma dofs
+    std::vector<int> map((size_t)c->nS, -1);
+    const int C0 = std::max(1, c->Ncell_glob[0]), C1 = std::max(1, c->Ncell_glob[1]);
+    const int N0 = c->Nnode_glob[0], N1 = c->Nnode_glob[1];
+    const int act[3] = {0, c->perm[1] >= 0, c->perm[2] >= 0};
+    for (int64_t cell = 0; cell < ncell; ++cell) {
+      const int ci[3] = {(int)(cell % C0), (int)((cell / C0) % C1), (int)(cell / ((int64_t)C0 * C1))};
+      for (int l = 0; l < nl; ++l) {
+        int bits[3] = {0, 0, 0};
+        int k = 0;
+        for (int s = 0; s < 3; ++s) {
+          if (s > 0 && !act[s]) continue;
+          bits[s] = (l >> k) & 1;
+          ++k;
+        }
+        const int64_t node = (int64_t)(ci[0] + bits[0]) + (int64_t)N0 * ((ci[1] + bits[1]) + (int64_t)N1 * (ci[2] + bits[2]));
+        // DG dof numbering (cell-major) in device layout [l][cell]
+        const int64_t dgdof = (int64_t)l * ncell + cell;
+        if (c->fam_S == TV_CG) map[(size_t)node] = (int)dgdof;  // sigma CG <- T DG
+        else map[(size_t)dgdof] = (int)node;                    // sigma DG <- T CG
+      }
+    }
+    HIPC(hipMalloc(&c->map, sizeof(int) * (size_t)c->nS));
+    HIPC(hipMemcpy(c->map, map.data(), sizeof(int) * (size_t)c->nS, hipMemcpyHostToDevice));
+  }
+  // thermal constants
+  const tv_params& P = c->P;
+  for (CgGrid* g = &c->cg; g; g = nullptr) {
+    g->dt = P.dt; g->dt_alpha = P.dt * P.alpha; g->dt_f = P.dt * P.f;
+    g->a_rad = 0.001 * (P.sigma * P.epsilon); g->a_conv = 0.001 * P.htc;
+    g->T_amb = P.T_ambient; g->T_amb4 = P.T_ambient * P.T_ambient * P.T_ambient * P.T_ambient;
+  }
+  {
+    DgGrid* g = &c->dg;
+    g->dt = P.dt; g->dt_alpha = P.dt * P.alpha; g->dt_f = P.dt * P.f;
+    g->a_rad = 0.001 * (P.sigma * P.epsilon); g->a_conv = 0.001 * P.htc;
+    g->T_amb = P.T_ambient; g->T_amb4 = P.T_ambient * P.T_ambient * P.T_ambient * P.T_ambient;
+    g->penalty = 5.0;
+  }
+  return TV_OK;
+}
+
+static int setup_fields(Ctx* c) {
+  const int d = c->dim, dd = d * d;
+  const bool all = c->O.materialize != 0;
+  int rc;
+#define AF(id, sp, bs) if ((rc = alloc_field(c, id, sp, bs)) != TV_OK) return rc
+  AF(TV_F_T, 0, 1);
+  AF(TV_F_T_PREV, 0, 1);
+  AF(TV_F_TF, 0, 1);
+  AF(TV_F_TF_PARTIAL, 0, 6);
+  AF(TV_F_PHI, 0, 1);
+  AF(TV_F_XI, 0, 1);
+  AF(TV_F_S_TILDE, 1, 6 * dd);
+  AF(TV_F_SIGMA_TILDE, 1, 6 * dd);
+  AF(TV_F_SIGMA, 1, dd);
+  if (all) {
+    AF(TV_F_T_NEXT, 0, 1);
+    AF(TV_F_PHI_NEXT, 0, 1);
+    AF(TV_F_THERMAL_STRAIN, 1, dd);
+    AF(TV_F_TOTAL_STRAIN, 1, dd);
+    AF(TV_F_DEVIATORIC_STRAIN, 1, dd);
+    AF(TV_F_DS_PARTIAL, 1, 6 * dd);
+    AF(TV_F_DSIGMA_PARTIAL, 1, 6 * dd);
+    AF(TV_F_S_PARTIAL, 1, 6 * dd);
+    AF(TV_F_SIGMA_PARTIAL, 1, 6 * dd);
+    alias_field(c, TV_F_S_PARTIAL_NEXT, TV_F_S_PARTIAL);
+    alias_field(c, TV_F_SIGMA_PARTIAL_NEXT, TV_F_SIGMA_PARTIAL);
+  }
+#undef AF
+  alias_field(c, TV_F_TF_PREV, TV_F_TF);
+  alias_field(c, TV_F_TF_PARTIAL_PREV, TV_F_TF_PARTIAL);
+  alias_field(c, TV_F_S_TILDE_NEXT, TV_F_S_TILDE);
+  alias_field(c, TV_F_SIGMA_TILDE_NEXT, TV_F_SIGMA_TILDE);
+  // PCG work vectors (T space, local size)
+  const size_t nb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nT);
+  HIPC(hipMalloc(&c->r, nb));
+  HIPC(hipMalloc(&c->z, nb));
+  HIPC(hipMalloc(&c->pA, nb));
+  HIPC(hipMalloc(&c->pB, nb));
+  HIPC(hipMalloc(&c->w, nb));
+  HIPC(hipMalloc(&c->dinv, nb));
+  for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv}) HIPC(hipMemsetAsync(p, 0, nb, c->stream));
+  c->f[TV_F_RESIDUAL].ptr = c->r; c->f[TV_F_RESIDUAL].bs = 1; c->f[TV_F_RESIDUAL].space = 0;
+  if (int e = alloc_field(c, TV_F_DX, 0, 1)) return e;
+  int np = std::max(kVecBlocks, 1);
+  if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
+  else np = std::max<int>(np, (int)((c->nT / (1 << c->dim) + kBlock - 1) / kBlock));
+  c->n_partials_cap = np;
+  HIPC(hipMalloc(&c->partials, sizeof(double) * 2 * (size_t)np));
+  HIPC(hipMalloc(&c->sums, sizeof(double) * 8));
+  HIPC(hipMalloc(&c->st, sizeof(PcgState)));
+  HIPC(hipHostMalloc(&c->h_st, sizeof(PcgState)));
+  HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
+  return TV_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// field transfer: reference interleaved layout <-> device component-major layout
+// --------------------------------------------------------------------------------------
+__global__ void k_interleave(int dir, double* __restrict__ buf, double* __restrict__ dev, int64_t ndof, int bs,
+                             int64_t stride, int64_t off, int dg_nl, int64_t dg_ncell) {
+  // dir 0: buf (host layout, dof*bs+comp) -> dev ; dir 1: dev -> buf
+  const int64_t total = ndof * bs;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t dof = t / bs;
+    const int comp = (int)(t % bs);
+    int64_t di = (dg_nl > 0) ? (dof % dg_nl) * dg_ncell + dof / dg_nl : off + dof;
+    double* p = dev + comp * stride + di;
+    if (dir == 0) *p = buf[t];
+    else buf[t] = *p;
+  }
+}
+
+static int transfer(Ctx* c, int field, double* host, size_t n, int dir) {
+  if (field < 0 || field >= TV_NUM_FIELDS) return c->fail(TV_ERR_ARG, "bad field id");
+  FieldInfo& fi = c->f[field];
+  if (!fi.ptr) return c->fail(TV_ERR_STATE, "field not materialized (options.materialize = 0 keeps state fields only)");
+  const int64_t ndof = (fi.space == 0) ? c->ownT_n : c->ownS_n;
+  const int64_t off = (fi.space == 0) ? c->ownT_off : c->ownS_off;
+  const int64_t stride = (fi.space == 0) ? c->nT : c->nS;
+  const size_t need = (size_t)ndof * fi.bs;
+  if (n != need)
+    return c->fail(TV_ERR_ARG, "size mismatch: expected " + std::to_string(need) + " values, got " + std::to_string(n));
+  const bool dgsp = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
+  const int nl = dgsp ? (1 << c->dim) : 0;
+  const int64_t ncell = dgsp ? ndof / nl : 0;
+  const size_t bytes = need * sizeof(double);
+  if (c->scratch_bytes < bytes) {
+    if (c->scratch) HIPC(hipFree(c->scratch));
+    c->scratch = nullptr;
+    HIPC(hipMalloc(&c->scratch, std::max<size_t>(bytes, 8)));
+    c->scratch_bytes = bytes;
+  }
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, ((int64_t)need + 255) / 256), 16384);
+  if (dir == 0) {
+    HIPC(hipMemcpyAsync(c->scratch, host, bytes, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_interleave, dim3(blocks), dim3(256), 0, c->stream, 0, c->scratch, fi.ptr, ndof, fi.bs,
+                       stride, off, nl, ncell);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(c->stream));
+  } else {
+    hipLaunchKernelGGL(k_interleave, dim3(blocks), dim3(256), 0, c->stream, 1, c->scratch, fi.ptr, ndof, fi.bs,
+                       stride, off, nl, ncell);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(host, c->scratch, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+  }
+  return TV_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// communication
+// --------------------------------------------------------------------------------------
+static int halo(Ctx* c, double* v) {
+  if (!c->comm || c->nranks <= 1 || c->fam_T != TV_CG) return TV_OK;
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  NCCLC(ncclGroupStart());
+  if (g.g_lo) {  // neighbour rank-1: send first owned plane, receive ghost plane 0
+    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclRecv(v, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+  }
+  if (g.g_hi) {
+    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
+static int allreduce(Ctx* c, double* v, int n) {
+  if (!c->comm || c->nranks <= 1) return TV_OK;
+  NCCLC(ncclAllReduce(v, v, n, ncclDouble, ncclSum, c->comm, c->stream));
+  return TV_OK;
+}
+
+// reduce partial records -> (allreduce) -> scalar logic
+static int reduce_logic(Ctx* c, int n, int W, int kind, int check_done) {
+  if (!c->comm || c->nranks <= 1) {
+    launch_reduce_logic(c->partials, n, W, c->sums, c->st, kind, check_done, c->stream);
+  } else {
+    launch_reduce_logic(c->partials, n, W, c->sums, c->st, 0, 0, c->stream);
+    if (int e = allreduce(c, c->sums, W)) return e;
+    if (kind) launch_logic(c->st, c->sums, kind, c->stream);
+  }
+  return TV_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// operators
+// --------------------------------------------------------------------------------------
+static void op_residual(Ctx* c, const double* T, const double* Tp, double* F) {
+  if (c->fam_T == TV_CG) launch_cg_residual(c->cg, T, Tp, F, c->stream);
+  else launch_dg_residual(c->dg, T, Tp, F, c->stream);
+}
+static void op_diag(Ctx* c, const double* T, double* d, int invert) {
+  if (c->fam_T == TV_CG) launch_cg_diag(c->cg, T, d, invert, c->stream);
+  else launch_dg_diag(c->dg, T, d, invert, c->stream);
+}
+static void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
+  if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
+  else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
+}
+static void op_japply_fused(Ctx* c, const double* T, int* np) {
+  if (c->fam_T == TV_CG)
+    launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
+  else
+    launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
+}
+
+// --------------------------------------------------------------------------------------
+// Jacobi-PCG for J(T) dx = r  (PETSc KSPCG restated; see tv_pcg.hip)
+// --------------------------------------------------------------------------------------
+static int pcg_iteration(Ctx* c, const double* T) {
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  int np = 0;
+  op_japply_fused(c, T, &np);                 // p <- z + b p ; w <- J p ; partial p.w
+  if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
+  launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
+                    c->r + off, c->z + off, c->partials, c->stream);
+  if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 3, 1)) return e;  // dp, beta, convergence
+  if (int e = halo(c, c->z)) return e;
+  return TV_OK;
+}
+
+static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  // state init
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  launch_pcg_init(n, c->r + off, c->dinv + off, c->z + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
+  if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 1, 0)) return e;
+  if (int e = halo(c, c->z)) return e;
+  int launched = 0;
+  int batch = std::max(1, c->pcg_hint > 2 ? c->pcg_hint - 1 : c->O.pcg_batch);
+  for (;;) {
+    for (int b = 0; b < batch; ++b) {
+      if (int e = pcg_iteration(c, T)) return e;
+    }
+    launched += batch;
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(c->h_st, c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (c->h_st->done) break;
+    if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    batch = std::max(1, c->O.pcg_batch);
+  }
+  *its = c->h_st->it;
+  *reason = c->h_st->reason;
+  c->pcg_hint = c->h_st->it;
+  return TV_OK;
+}
+
+static const char* reason_str(int r) {
+  switch (r) {
+    case R_DIV_ITS: return "DIVERGED_ITS";
+    case R_DIV_DTOL: return "DIVERGED_DTOL";
+    case R_DIV_INDEF_PC: return "DIVERGED_INDEFINITE_PC";
+    case R_DIV_NANINF: return "DIVERGED_NANORINF";
+    case R_DIV_INDEF_MAT: return "DIVERGED_INDEFINITE_MAT";
+    default: return "UNKNOWN";
+  }
+}
+
+// dolfinx NewtonSolver::solve, convergence_criterion = "incremental"
+static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
+  double* T = c->f[TV_F_T].ptr;
+  const double* Tp = c->f[TV_F_T_PREV].ptr;
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  int its = 0, kits = 0;
+  bool conv = false;
+  double r0 = 0.0, rn = 0.0;
+  op_residual(c, T, Tp, c->r);  // F(u)
+  while (!conv && its < c->O.newton_max_it) {
+    op_diag(c, T, c->dinv, 1);  // J(u) (matrix-free) + Jacobi PC setup
+    int k = 0, reason = 0;
+    if (int e = pcg_solve(c, T, &k, &reason)) return e;
+    kits += k;
+    if (reason < 0)
+      return c->fail(TV_ERR_KSP, std::string("Krylov solver did not converge (") + reason_str(reason) + ")");
+    launch_newton_update(n, T + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);  // u <- u - dx
+    if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
+    HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (int e = halo(c, T)) return e;
+    HIPC(hipStreamSynchronize(c->stream));
+    rn = std::sqrt(c->h_sums[0]);
+    ++its;
+    if (its == 1) {
+      r0 = rn;  // residual0 = ||dx_1||; no test at the first iteration
+      conv = false;
+    } else {
+      const double rel = rn / r0;
+      conv = (rel < c->O.newton_rtol) || (rn < c->O.newton_atol);
+    }
+    // dolfinx assembles F after every update; in the incremental criterion that
+    // last F is never read, so it is assembled only when another iteration follows.
+    if (!conv && its < c->O.newton_max_it) op_residual(c, T, Tp, c->r);
+  }
+  HIPC(hipGetLastError());
+  c->last_newton = its;
+  c->last_krylov = kits;
+  c->last_dx = rn;
+  if (out_its) *out_its = its;
+  if (out_kits) *out_kits = kits;
+  if (out_conv) *out_conv = conv ? 1 : 0;
+  if (!conv && c->O.error_on_nonconvergence)
+    return c->fail(TV_ERR_NOT_CONVERGED, "Newton solver did not converge because maximum number of iterations reached");
+  return TV_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// viscoelastic update
+// --------------------------------------------------------------------------------------
+static void visco_setup(Ctx* c, ViscoConst& k, ViscoFields& v) {
+  const tv_params& P = c->P;
+  k.H_over_Rg = P.H / P.Rg;
+  k.inv_Tb = 1.0 / P.Tb;
+  k.dt = P.dt;
+  k.half_dt = P.dt / 2;
+  k.alpha_s = P.alpha_solid;
+  k.dalpha = P.alpha_liquid - P.alpha_solid;
+  k.inv_dim = 1.0 / c->dim;
+  for (int i = 0; i < 6; ++i) {
+    k.lambda_m[i] = P.lambda_m[i]; k.m_n[i] = P.m_n[i];
+    k.lambda_g[i] = P.lambda_g[i]; k.g_n[i] = P.g_n[i];
+    k.lambda_k[i] = P.lambda_k[i]; k.k_n[i] = P.k_n[i];
+  }
+  std::memset(&v, 0, sizeof(v));
+  v.sT = c->nT;
+  v.sS = c->nS;
+  v.T = c->f[TV_F_T].ptr; v.Tp = c->f[TV_F_T_PREV].ptr; v.Tn = c->f[TV_F_T_NEXT].ptr;
+  v.phi = c->f[TV_F_PHI].ptr; v.phin = c->f[TV_F_PHI_NEXT].ptr; v.xi = c->f[TV_F_XI].ptr;
+  v.Tf = c->f[TV_F_TF].ptr; v.Tfp = c->f[TV_F_TF_PARTIAL].ptr;
+  v.th = c->f[TV_F_THERMAL_STRAIN].ptr; v.tot = c->f[TV_F_TOTAL_STRAIN].ptr; v.dev = c->f[TV_F_DEVIATORIC_STRAIN].ptr;
+  v.ds = c->f[TV_F_DS_PARTIAL].ptr; v.dsig = c->f[TV_F_DSIGMA_PARTIAL].ptr;
+  v.st = c->f[TV_F_S_TILDE].ptr; v.sgt = c->f[TV_F_SIGMA_TILDE].ptr;
+  v.sp = c->f[TV_F_S_PARTIAL].ptr; v.sgp = c->f[TV_F_SIGMA_PARTIAL].ptr;
+  v.sigma = c->f[TV_F_SIGMA].ptr;
+}
+
+static int visco(Ctx* c, bool copy_Tprev) {
+  ViscoConst k;
+  ViscoFields v;
+  visco_setup(c, k, v);
+  const int all = c->O.materialize ? 1 : 0;
+  if (c->fam_T == c->fam_S) {
+    v.n = c->ownT_n;
+    v.off_T = c->ownT_off;
+    v.off_S = c->ownS_off;
+    v.copy_Tprev = copy_Tprev ? 1 : 0;
+    launch_visco(c->dim, all, k, v, c->stream);
+    if (copy_Tprev && c->ownT_off > 0) {  // ghost planes of T_prev
+      launch_copy(v.Tp, v.T, c->ownT_off, c->stream);
+    }
+    if (copy_Tprev && c->nT > c->ownT_off + c->ownT_n) {
+      const int64_t o = c->ownT_off + c->ownT_n;
+      launch_copy(v.Tp + o, v.T + o, c->nT - o, c->stream);
+    }
+  } else {
+    v.n = c->ownT_n;
+    v.off_T = c->ownT_off;
+    launch_visco_Tpass(c->dim, all, k, v, c->stream);
+    v.n = c->ownS_n;
+    v.off_S = c->ownS_off;
+    v.map = c->map;
+    launch_visco_Spass(c->dim, all, k, v, c->stream);
+    if (copy_Tprev) launch_copy(v.Tp, v.T, c->nT, c->stream);
+  }
+  HIPC(hipGetLastError());
+  return TV_OK;
+}
+
+}  // namespace tv
+
+using namespace tv;
+
+// ======================================================================================
+// C-ABI
+// ======================================================================================
+extern "C" {
+
+int tv_abi_version(void) { return TV_ABI_VERSION; }
+
+const char* tv_last_error(const void* ctx) {
+  if (ctx) return static_cast<const Ctx*>(ctx)->err.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_err.c_str();
+}
+
+void tv_default_options(tv_options* o) {
+  o->newton_rtol = 1e-12;  // ThermoViscoProblem.py:336
+  o->newton_atol = 1e-10;  // dolfinx NewtonSolver default
+  o->newton_max_it = 50;   // dolfinx default
+  o->error_on_nonconvergence = 1;
+  o->ksp_rtol = 1e-5;      // PETSc defaults
+  o->ksp_atol = 1e-50;
+  o->ksp_dtol = 1e5;
+  o->ksp_max_it = 10000;
+  o->materialize = 1;
+  o->use_graphs = 0;
+  o->pcg_batch = 8;
+}
+
+void tv_default_params(tv_params* p) {
+  std::memset(p, 0, sizeof(*p));
+  // main.py:29-55
+  p->f = 0.0; p->epsilon = 0.93; p->sigma = 5.670e-8; p->T_ambient = 600.0; p->T_0 = 800.0;
+  p->alpha = 1.0; p->htc = 280.1; p->rho = 2500.0; p->cp = 1433.0; p->k = 1.0;
+  p->H = 627.8e3; p->Tb = 869.0; p->Rg = 8.314; p->alpha_solid = 9.10e-6; p->alpha_liquid = 25.10e-6;
+  p->Tf_init = 873.0;
+  // ViscoelasticModel.py:19-68
+  const double m[6] = {5.523e-2, 8.205e-2, 1.215e-1, 2.286e-1, 2.860e-1, 2.265e-1};
+  const double lm[6] = {5.965e-4, 1.077e-2, 1.362e-1, 1.505e-1, 6.747e+0, 2.963e+1};
+  const double g[6] = {1.585, 2.354, 3.486, 6.558, 8.205, 6.498};
+  const double lg[6] = {6.658e-5, 1.197e-3, 1.514e-2, 1.672e-1, 7.497e-1, 3.292e+0};
+  const double k[6] = {7.588e-1, 7.650e-1, 9.806e-1, 7.301e+0, 1.347e+1, 1.090e+1};
+  const double lk[6] = {5.009e-5, 9.945e-4, 2.022e-3, 1.925e-2, 1.199e-1, 2.033e+0};
+  for (int i = 0; i < 6; ++i) {
+    p->m_n[i] = m[i]; p->lambda_m[i] = lm[i]; p->g_n[i] = g[i];
+    p->lambda_g[i] = lg[i]; p->k_n[i] = k[i]; p->lambda_k[i] = lk[i];
+  }
+  p->dt = 0.1;  // main.py:16
+}
+
+int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params* params, const tv_options* opts,
+              int device, void** ctx_out) {
+  if (!mesh || !fe || !params || !ctx_out) {
+    set_global_error("tv_create: null argument");
+    return TV_ERR_ARG;
+  }
+  *ctx_out = nullptr;
+  auto c = std::make_unique<Ctx>();
+  if (fe->T_degree != 1 || fe->sigma_degree != 1) {
+    set_global_error("only degree-1 Lagrange elements are implemented");
+    return TV_ERR_ARG;
+  }
+  if ((fe->T_family != TV_CG && fe->T_family != TV_DG) || (fe->sigma_family != TV_CG && fe->sigma_family != TV_DG)) {
+    set_global_error("Only CG and DG elements are supported");
+    return TV_ERR_ARG;
+  }
+  if (!(params->dt > 0.0)) {
+    set_global_error("dt must be positive");
+    return TV_ERR_ARG;
+  }
+  c->fam_T = fe->T_family;
+  c->fam_S = fe->sigma_family;
+  c->P = *params;
+  if (opts) c->O = *opts;
+  else tv_default_options(&c->O);
+  c->device = device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_global_error("no HIP device available: libtvfem requires an MI355X (gfx950) GPU");
+    return TV_ERR_HIP;
+  }
+  if (device < 0 || device >= ndev) {
+    set_global_error("device index out of range");
+    return TV_ERR_ARG;
+  }
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    set_global_error("HIP stream/event creation failed");
+    return TV_ERR_HIP;
+  }
+  int rc = setup_mesh(c.get(), mesh);
+  if (rc == TV_OK) rc = setup_fields(c.get());
+  if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
+  if (rc != TV_OK) {
+    set_global_error(c->err);
+    tv_destroy(c.release());
+    return rc;
+  }
+  *ctx_out = c.release();
+  return TV_OK;
+}
+
+int tv_destroy(void* ctx) {
+  if (!ctx) return TV_OK;
+  Ctx* c = static_cast<Ctx*>(ctx);
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (int i = 0; i < TV_NUM_FIELDS; ++i)
+    if (c->f[i].alloc && c->f[i].ptr) hipFree(c->f[i].ptr);
+  for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
+    if (p) hipFree(p);
+  for (int s = 0; s < 3; ++s) {
+    if (c->coef[s]) hipFree(c->coef[s]);
+    if (c->dgh[s]) hipFree(c->dgh[s]);
+  }
+  if (c->map) hipFree(c->map);
+  if (c->st) hipFree(c->st);
+  if (c->h_st) hipHostFree(c->h_st);
+  if (c->h_sums) hipHostFree(c->h_sums);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return TV_OK;
+}
+
+int tv_num_dofs(void* ctx, int space, int64_t* n_owned, int64_t* global_offset) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (n_owned) *n_owned = space == 0 ? c->ownT_n : c->ownS_n;
+  if (global_offset) *global_offset = space == 0 ? c->globT_off : c->globS_off;
+  return TV_OK;
+}
+
+int tv_field_block_size(void* ctx, int field, int* bs) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || field < 0 || field >= TV_NUM_FIELDS) return TV_ERR_ARG;
+  const int dd = c->dim * c->dim;
+  static const int kind[TV_NUM_FIELDS] = {1, 1, 1, 1, 1, 6, 6, 1, 1, 1, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 3, 3, 2, 1, 1};
+  const int k = kind[field];
+  *bs = (k == 1) ? 1 : (k == 6 ? 6 : (k == 2 ? dd : 6 * dd));
+  return TV_OK;
+}
+
+int tv_dof_coordinates(void* ctx, int space, double* xyz, size_t n_dofs) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !xyz) return TV_ERR_ARG;
+  const int fam = space == 0 ? c->fam_T : c->fam_S;
+  const int64_t nown = space == 0 ? c->ownT_n : c->ownS_n;
+  if ((int64_t)n_dofs != nown) return c->fail(TV_ERR_ARG, "n_dofs mismatch");
+  std::vector<double> tmp;
+  const std::vector<double>* X[3];
+  std::vector<double> deg(1, 0.0);
+  for (int s = 0; s < 3; ++s) X[s] = (c->perm[s] < 0) ? &deg : &c->coords[c->perm[s]];
+  const int N0 = c->Nnode_glob[0], N1 = c->Nnode_glob[1];
+  if (fam == TV_CG) {
+    const int64_t base = (space == 0 ? c->globT_off : c->globS_off);
+    for (int64_t t = 0; t < nown; ++t) {
+      const int64_t g = base + t;
+      const int ijk[3] = {(int)(g % N0), (int)((g / N0) % N1), (int)(g / ((int64_t)N0 * N1))};
+      double p[3] = {0, 0, 0};
+      for (int s = 0; s < 3; ++s) if (c->perm[s] >= 0) p[c->perm[s]] = (*X[s])[ijk[s]];
+      for (int a = 0; a < 3; ++a) xyz[3 * t + a] = p[a];
+    }
+  } else {
+    const int nl = 1 << c->dim;
+    const int C0 = std::max(1, c->Ncell_glob[0]), C1 = std::max(1, c->Ncell_glob[1]);
+    const int act[3] = {1, c->perm[1] >= 0, c->perm[2] >= 0};
+    for (int64_t t = 0; t < nown; ++t) {
+      const int64_t cell = t / nl;
+      const int l = (int)(t % nl);
+      const int ci[3] = {(int)(cell % C0), (int)((cell / C0) % C1), (int)(cell / ((int64_t)C0 * C1))};
+      int bits[3] = {0, 0, 0}, k = 0;
+      for (int s = 0; s < 3; ++s) {
+        if (!act[s]) continue;
+        bits[s] = (l >> k) & 1;
+        ++k;
+      }
+      double p[3] = {0, 0, 0};
+      for (int s = 0; s < 3; ++s) if (c->perm[s] >= 0) p[c->perm[s]] = (*X[s])[ci[s] + bits[s]];
+      for (int a = 0; a < 3; ++a) xyz[3 * t + a] = p[a];
+    }
+  }
+  return TV_OK;
+}
+
+int tv_set_field(void* ctx, int field, const double* host, size_t n) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !host) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  int rc = transfer(c, field, const_cast<double*>(host), n, 0);
+  if (rc == TV_OK && (field == TV_F_T || field == TV_F_T_PREV)) rc = halo(c, c->f[field].ptr);
+  if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync");
+  return rc;
+}
+
+int tv_get_field(void* ctx, int field, double* host, size_t n) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !host) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  return transfer(c, field, host, n, 1);
+}
+
+int tv_field_device_ptr(void* ctx, int field, void** dev_ptr, int64_t* comp_stride) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || field < 0 || field >= TV_NUM_FIELDS) return TV_ERR_ARG;
+  if (!c->f[field].ptr) return c->fail(TV_ERR_STATE, "field not materialized");
+  if (dev_ptr) *dev_ptr = c->f[field].ptr;
+  if (comp_stride) *comp_stride = c->f[field].space == 0 ? c->nT : c->nS;
+  return TV_OK;
+}
+
+int tv_set_initial_condition(void* ctx, double T0) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  // __set_IC_T, __set_IC_Tf, __set_IC_Tf_partial (ThermoViscoProblem.py:193-233)
+  launch_fill(c->f[TV_F_T].ptr, c->nT, T0, c->stream);
+  launch_fill(c->f[TV_F_T_PREV].ptr, c->nT, T0, c->stream);
+  launch_fill(c->f[TV_F_TF].ptr, c->nT, T0, c->stream);
+  launch_fill(c->f[TV_F_TF_PARTIAL].ptr, c->nT * 6, T0, c->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_sync(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_residual(void* ctx, const double* T_dev, double* F_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !T_dev || !F_dev) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  op_residual(c, T_dev, c->f[TV_F_T_PREV].ptr, F_dev);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !x_dev || !y_dev) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  op_japply(c, c->f[TV_F_T].ptr, x_dev, y_dev, nullptr, nullptr);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_jacobian_diag(void* ctx, double* d_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !d_dev) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  op_diag(c, c->f[TV_F_T].ptr, d_dev, 0);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  return newton(c, newton_its, krylov_its, converged);
+}
+
+int tv_visco_update(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  if (int e = visco(c, false)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  int conv = 0;
+  if (int e = newton(c, newton_its, krylov_its, &conv)) return e;
+  if (!thermal_only) {
+    if (int e = visco(c, true)) return e;  // includes T_prev <- T (ThermoViscoProblem.py:378-379)
+  } else {
+    launch_copy(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, c->stream);
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_comm_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int tv_comm_get_unique_id(char* id_out) {
+  if (!id_out) return TV_ERR_ARG;
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    set_global_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    return TV_ERR_COMM;
+  }
+  std::memcpy(id_out, &id, sizeof(id));
+  return TV_OK;
+}
+
+int tv_comm_init(void* ctx, const char* id, int n_ranks, int rank) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !id) return TV_ERR_ARG;
+  if (n_ranks != c->n_parts || rank != c->part)
+    return c->fail(TV_ERR_ARG, "communicator size/rank must match the mesh partition (n_parts/part)");
+  hipSetDevice(c->device);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCLC(ncclCommInitRank(&c->comm, n_ranks, uid, rank));
+  c->nranks = n_ranks;
+  c->rank = rank;
+  // bring ghost planes of the state up to date
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_halo_exchange(void* ctx, int field) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || field < 0 || field >= TV_NUM_FIELDS || !c->f[field].ptr) return TV_ERR_ARG;
+  if (c->f[field].space != 0 || c->f[field].bs != 1) return c->fail(TV_ERR_ARG, "halo exchange: scalar T-space fields only");
+  if (int e = halo(c, c->f[field].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !bytes) return TV_ERR_ARG;
+  const double n = (double)c->ownT_n;
+  const int dd = c->dim * c->dim;
+  switch (kernel) {
+    case 0:  // J(T) x : read x, write y (geometry implicit, T only on boundary nodes)
+      *bytes = 16.0 * n;
+      break;
+    case 1: {  // fused visco update, per dof
+      double per = 8.0 * (2 + 6 + 2 * 6 * dd)           // read T, Tp, Tf_partial, s~, sigma~
+                   + 8.0 * (6 + 3 + 2 * 6 * dd + dd);    // write Tf_partial, Tf, phi, xi, s~, sigma~, sigma
+      if (c->O.materialize) per += 8.0 * (2 + 3 * dd + 4 * 6 * dd);
+      *bytes = per * n;
+      break;
+    }
+    case 2:  // residual: read T, Tp, write F
+      *bytes = 24.0 * n;
+      break;
+    default:
+      return c->fail(TV_ERR_ARG, "unknown kernel id");
+  }
+  return TV_OK;
+}
+
+int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !ms || reps < 1) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  auto one = [&]() -> int {
+    switch (kernel) {
+      case 0: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); return TV_OK;
+      case 1: return visco(c, false);
+      case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;
+      default: return c->fail(TV_ERR_ARG, "unknown kernel id");
+    }
+  };
+  if (int e = one()) return e;  // warm-up
+  HIPC(hipEventRecord(c->ev0, c->stream));
+  for (int i = 0; i < reps; ++i)
+    if (int e = one()) return e;
+  HIPC(hipEventRecord(c->ev1, c->stream));
+  HIPC(hipEventSynchronize(c->ev1));
+  float t = 0.f;
+  HIPC(hipEventElapsedTime(&t, c->ev0, c->ev1));
+  *ms = (double)t / reps;
+  return TV_OK;
+}
+
+int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (newton_its) *newton_its = c->last_newton;
+  if (krylov_its) *krylov_its = c->last_krylov;
+  if (dx_norm) *dx_norm = c->last_dx;
+  return TV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,440 @@
+// CG1 (Q1 hexahedra / P1 intervals) matrix-free operators on rectilinear grids,
+// gfx950.
+//
+// Replaces, for the temperature space of ThermoViscoProblem (T family CG):
+//   * the FFCx cell kernel of F dx (ThermoViscoProblem.py:295-300) and of its
+//     Jacobian, driven by dolfinx assemble_vector / assemble_matrix, and
+//   * the FFCx exterior-facet kernels of the Robin radiation + convection terms
+//     (ThermoViscoProblem.py:302-304) and their Jacobian,
+//   * PETSc MatMult / MatGetDiagonal on the assembled AIJ Jacobian.
+//
+// On a rectilinear grid the assembled Q1 operator factorises exactly:
+//     M = Mz (x) My (x) Mx,
+//     K = Mz (x) My (x) Kx + Mz (x) Ky (x) Mx + Kz (x) My (x) Mx
+// with the assembled 1D P1 mass / stiffness (tridiagonal, per-node coefficients
+// in CgGrid::coef).  The Robin facet integrals are evaluated per boundary node
+// with 3x3 Gauss points per facet (exact for the degree-5-per-direction
+// T^4 v and T^3 phi_i phi_j integrands).
+//
+// Execution shape (MI355X): one wavefront = one x-row segment of 64 nodes at
+// fixed (j, k).  Each lane gathers its 3x3 (j, k)-column neighbourhood (9
+// coalesced loads per wave-row, L1/L2-served for the neighbouring rows), folds
+// the y and z directions in registers (sum factorisation: 34 FMA), and takes
+// the x-neighbour partial sums from the adjacent lanes with DPP wave_shr /
+// wave_shl (no LDS, no barriers).  Lanes 1..62 produce output.  The four waves
+// of a workgroup take four consecutive j-rows so the j-neighbour rows are
+// shared in L1.
+#include "tv_internal.h"
+
+namespace tv {
+namespace {
+
+enum { MODE_RES = 0, MODE_JAC = 1 };
+
+__device__ __forceinline__ double shr1(double v) {  // lane l <- lane l-1
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double shl1(double v) {  // lane l <- lane l+1
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// 3-point Gauss-Legendre on [0, 1]
+__device__ constexpr double kGX[3] = {0.11270166537925831148, 0.5, 0.88729833462074168852};
+__device__ constexpr double kGW[3] = {5.0 / 18.0, 8.0 / 18.0, 5.0 / 18.0};
+
+__device__ __forceinline__ double g_rad_conv(const CgGrid& g, double T) {
+  const double T2 = T * T;
+  return g.a_rad * (T2 * T2 - g.T_amb4) + g.a_conv * (T - g.T_amb);
+}
+__device__ __forceinline__ double dg_rad_conv(const CgGrid& g, double T) {
+  return g.a_rad * 4.0 * (T * T * T) + g.a_conv;
+}
+
+// Robin facet contribution at a boundary node.  The node sits at the centre of
+// a 3x3 patch over the two tangential axes of its face; patch[u+1][v+1] holds
+// the value at tangential offset (u, v).  The up-to-four facets around the node
+// are integrated with 3x3 Gauss points; a degenerate tangential axis collapses
+// to a point (weight 1, basis 1) so the same code gives the 1D point evaluation
+// of ds at the interval end points.
+//   MODE_RES: dt * sum_f int_f g(T_h) phi_I
+//   MODE_JAC: dt * sum_f int_f g'(T_h) phi_I p_h       (diag: p_h -> phi_I)
+template <int MODE, bool DIAG, bool D1, bool D2>
+__device__ double facet_sum(const CgGrid& g, double h1lo, double h1hi, double h2lo, double h2hi,
+                            const double (&Tp)[3][3], const double (&Pp)[3][3]) {
+  double acc = 0.0;
+  constexpr int NS1 = D1 ? 1 : 2, NQ1 = D1 ? 1 : 3;
+  constexpr int NS2 = D2 ? 1 : 2, NQ2 = D2 ? 1 : 3;
+#pragma unroll
+  for (int s1 = 0; s1 < NS1; ++s1) {
+    const double h1 = D1 ? 1.0 : (s1 == 0 ? h1lo : h1hi);
+    if (!D1 && !(h1 > 0.0)) continue;
+    const int o1 = D1 ? 0 : (s1 == 0 ? -1 : 1);
+#pragma unroll
+    for (int s2 = 0; s2 < NS2; ++s2) {
+      const double h2 = D2 ? 1.0 : (s2 == 0 ? h2lo : h2hi);
+      if (!D2 && !(h2 > 0.0)) continue;
+      const int o2 = D2 ? 0 : (s2 == 0 ? -1 : 1);
+      const double T00 = Tp[1][1], T10 = Tp[1 + o1][1], T01 = Tp[1][1 + o2], T11 = Tp[1 + o1][1 + o2];
+      const double P00 = Pp[1][1], P10 = Pp[1 + o1][1], P01 = Pp[1][1 + o2], P11 = Pp[1 + o1][1 + o2];
+#pragma unroll
+      for (int q1 = 0; q1 < NQ1; ++q1) {
+        const double pc1 = D1 ? 1.0 : (s1 == 0 ? kGX[q1] : 1.0 - kGX[q1]);
+        const double po1 = 1.0 - pc1;
+        const double w1 = D1 ? 1.0 : kGW[q1] * h1;
+#pragma unroll
+        for (int q2 = 0; q2 < NQ2; ++q2) {
+          const double pc2 = D2 ? 1.0 : (s2 == 0 ? kGX[q2] : 1.0 - kGX[q2]);
+          const double po2 = 1.0 - pc2;
+          const double w = w1 * (D2 ? 1.0 : kGW[q2] * h2);
+          const double phiI = pc1 * pc2;
+          const double Th = phiI * T00 + po1 * pc2 * T10 + pc1 * po2 * T01 + po1 * po2 * T11;
+          if (MODE == MODE_RES) {
+            acc += w * g_rad_conv(g, Th) * phiI;
+          } else if (DIAG) {
+            acc += w * dg_rad_conv(g, Th) * phiI * phiI;
+          } else {
+            const double Ph = phiI * P00 + po1 * pc2 * P10 + pc1 * po2 * P01 + po1 * po2 * P11;
+            acc += w * dg_rad_conv(g, Th) * phiI * Ph;
+          }
+        }
+      }
+    }
+  }
+  return g.dt * acc;
+}
+
+// ---------------------------------------------------------------------------
+// Row-segment stencil kernel.
+//   MODE_RES : out = F(T; Tp)  (in0 = T, in1 = Tp)
+//   MODE_JAC : out = J(T) x    (in0 = x)                 [FUSEP = false]
+//              p = z + beta/betaold p_old, out = J(T) p  (in0 = z, in1 = p_old -> pout)
+//              (PETSc KSPCG "p <- z + b p" fused with MatMult, plus partial p.w)
+// ---------------------------------------------------------------------------
+template <int DIM, int MODE, bool FUSEP>
+__global__ __launch_bounds__(kBlock) void k_cg_rows(CgGrid g, const double* __restrict__ T,
+                                                    const double* __restrict__ in0,
+                                                    const double* in1,
+                                                    double* __restrict__ out, double* pout,
+                                                    const PcgState* __restrict__ st,
+                                                    double* __restrict__ partials, int nseg, int kfirst,
+                                                    int nplanes, int wmode) {
+  constexpr bool D1 = (DIM <= 2);  // storage axis 1 degenerate
+  constexpr bool D2 = (DIM == 1);  // storage axis 2 degenerate
+  __shared__ double red[kBlock / kWave];
+  if (FUSEP && st->done) return;  // uniform over the grid
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x >> 6;
+  int seg, j, kp;
+  if (wmode == 0) {
+    const int n1b = (g.n1 + 3) >> 2;
+    const int b = blockIdx.x;
+    seg = b % nseg;
+    const int t = b / nseg;
+    j = (t % n1b) * 4 + wave;
+    kp = t / n1b;
+  } else {
+    const int gw = blockIdx.x * 4 + wave;
+    seg = gw % nseg;
+    const int row = gw / nseg;
+    j = row % g.n1;
+    kp = row / g.n1;
+  }
+  const int k = kfirst + kp;
+  const bool row_ok = (j < g.n1) && (kp < nplanes);
+  const int i = seg * kSeg - 1 + lane;
+  const bool col_ok = row_ok && (i >= 0) && (i < g.n0);
+  const int n0 = g.n0, n1 = g.n1, n2 = g.n2;
+  const int64_t plane = (int64_t)n0 * n1;
+
+  double bcoef = 0.0;
+  bool first = false;
+  // FUSEP: p ping-pongs between two buffers (in1 = buffer A, pout = buffer B) so
+  // that p_old is never overwritten while neighbouring waves still read it.
+  // Iteration `it` writes buffer (it & 1 ? B : A) and reads the other.
+  const double* pold = in1;
+  if (FUSEP) {
+    const int it = st->it;
+    first = (it == 0);
+    bcoef = first ? 0.0 : st->beta / st->betaold;
+    if (it & 1) {
+      pold = in1;
+    } else {
+      pold = pout;
+      pout = const_cast<double*>(in1);
+    }
+  }
+
+  // ---- gather the 3x3 (j,k) column neighbourhood at x = i -------------------
+  double X[3][3];   // stiffness input (T for RES, p for JAC)
+  double Mm[3][3];  // mass input (T - Tp - dt f for RES)
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int jj = j + b - 1, kk = k + c - 1;
+      const bool ok = col_ok && (D1 ? b == 1 : (jj >= 0 && jj < n1)) && (D2 ? c == 1 : (kk >= 0 && kk < n2));
+      const int64_t idx = (int64_t)i + (int64_t)n0 * jj + plane * kk;
+      double v = 0.0, v2 = 0.0;
+      if (ok) {
+        v = in0[idx];
+        if (MODE == MODE_RES) v2 = in1[idx];
+        if (FUSEP) v = first ? v : v + bcoef * pold[idx];
+      }
+      X[b][c] = v;
+      if (MODE == MODE_RES) Mm[b][c] = v - v2 - g.dt_f;
+    }
+  }
+  const double* cy = g.coef[1] + (int64_t)(j < n1 ? j : 0) * C_NCOEF;
+  const double* cz = g.coef[2] + (int64_t)(k < n2 ? k : 0) * C_NCOEF;
+  const double My[3] = {cy[C_MLO], cy[C_MDI], cy[C_MUP]};
+  const double Ky[3] = {cy[C_KLO], cy[C_KDI], cy[C_KUP]};
+  const double Mz[3] = {cz[C_MLO], cz[C_MDI], cz[C_MUP]};
+  const double Kz[3] = {cz[C_KLO], cz[C_KDI], cz[C_KUP]};
+  const double da = g.dt_alpha;
+
+  // ---- fold y and z (sum factorisation) ---------------------------------------
+  double S1 = 0.0, S2 = 0.0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double us = 0.0, vs = 0.0, um = 0.0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      us += My[b] * X[b][c];
+      vs += Ky[b] * X[b][c];
+      if (MODE == MODE_RES) um += My[b] * Mm[b][c];
+    }
+    if (MODE != MODE_RES) um = us;
+    S1 += Mz[c] * (um + da * vs) + da * Kz[c] * us;
+    S2 += Mz[c] * us;
+  }
+  S2 *= da;
+
+  // ---- x direction via adjacent lanes ------------------------------------------
+  const double S1m = shr1(S1), S1p = shl1(S1), S2m = shr1(S2), S2p = shl1(S2);
+  const double* cx = g.coef[0] + (int64_t)(col_ok ? i : 0) * C_NCOEF;
+  double y = 0.0;
+  if (col_ok) {
+    y = cx[C_MLO] * S1m + cx[C_MDI] * S1 + cx[C_MUP] * S1p + cx[C_KLO] * S2m + cx[C_KDI] * S2 +
+        cx[C_KUP] * S2p;
+  }
+
+  // ---- Robin facets ---------------------------------------------------------------
+  // faces normal to storage axis 2 (wave-uniform)
+  if (!D2 && row_ok && ((k == 0 && g.bnd[2][0]) || (k == n2 - 1 && g.bnd[2][1]))) {
+    double Tp_[3][3], Pp_[3][3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {  // tangential axis 2 of the face = storage axis 1
+      double pc = X[v][1], tc;
+      if (MODE == MODE_RES) {
+        tc = pc;
+      } else {
+        const int jj = j + v - 1;
+        const bool ok = col_ok && (D1 ? v == 1 : (jj >= 0 && jj < n1));
+        tc = ok ? T[(int64_t)i + (int64_t)n0 * jj + plane * k] : 0.0;
+      }
+      Tp_[0][v] = shr1(tc); Tp_[1][v] = tc; Tp_[2][v] = shl1(tc);
+      Pp_[0][v] = shr1(pc); Pp_[1][v] = pc; Pp_[2][v] = shl1(pc);
+    }
+    if (col_ok) {
+      y += facet_sum<MODE, false, false, D1>(g, cx[C_HLO], cx[C_HHI], cy[C_HLO], cy[C_HHI], Tp_, Pp_);
+    }
+  }
+  // faces normal to storage axis 1 (wave-uniform)
+  if (!D1 && row_ok && ((j == 0 && g.bnd[1][0]) || (j == n1 - 1 && g.bnd[1][1]))) {
+    double Tp_[3][3], Pp_[3][3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {  // tangential axes (0, 2)
+      double pc = X[1][v], tc;
+      if (MODE == MODE_RES) {
+        tc = pc;
+      } else {
+        const int kk = k + v - 1;
+        const bool ok = col_ok && (D2 ? v == 1 : (kk >= 0 && kk < n2));
+        tc = ok ? T[(int64_t)i + (int64_t)n0 * j + plane * kk] : 0.0;
+      }
+      Tp_[0][v] = shr1(tc); Tp_[1][v] = tc; Tp_[2][v] = shl1(tc);
+      Pp_[0][v] = shr1(pc); Pp_[1][v] = pc; Pp_[2][v] = shl1(pc);
+    }
+    if (col_ok) {
+      y += facet_sum<MODE, false, false, D2>(g, cx[C_HLO], cx[C_HHI], cz[C_HLO], cz[C_HHI], Tp_, Pp_);
+    }
+  }
+  // faces normal to storage axis 0 (lane-divergent: i == 0 or i == n0-1)
+  if (col_ok && ((i == 0 && g.bnd[0][0]) || (i == n0 - 1 && g.bnd[0][1]))) {
+    double Tp_[3][3];
+    if (MODE == MODE_RES) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) Tp_[u][v] = X[u][v];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const int jj = j + u - 1, kk = k + v - 1;
+          const bool ok = (D1 ? u == 1 : (jj >= 0 && jj < n1)) && (D2 ? v == 1 : (kk >= 0 && kk < n2));
+          Tp_[u][v] = ok ? T[(int64_t)i + (int64_t)n0 * jj + plane * kk] : 0.0;
+        }
+      }
+    }
+    y += facet_sum<MODE, false, D1, D2>(g, cy[C_HLO], cy[C_HHI], cz[C_HLO], cz[C_HHI], Tp_, X);
+  }
+
+  // ---- outputs --------------------------------------------------------------------
+  const bool owned = (k >= g.k_begin) && (k < g.k_end);
+  const bool writer = col_ok && lane >= 1 && lane <= kSeg;
+  const int64_t me = (int64_t)i + (int64_t)n0 * j + plane * k;
+  if (writer) {
+    if (FUSEP) pout[me] = X[1][1];
+    if (owned) out[me] = y;
+  }
+  if (MODE == MODE_JAC && partials != nullptr) {
+    double d = (writer && owned) ? X[1][1] * y : 0.0;
+    d = wave_sum(d);
+    if (lane == 0) red[wave] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// diag(J): pointwise, facet terms with directly loaded patches.
+// ---------------------------------------------------------------------------
+template <int DIM>
+__global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __restrict__ T,
+                                                    double* __restrict__ out, int invert) {
+  constexpr bool D1 = (DIM <= 2);
+  constexpr bool D2 = (DIM == 1);
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  const int64_t nown = plane * (g.k_end - g.k_begin);
+  const int64_t base = plane * g.k_begin;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nown;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = base + t;
+    const int i = (int)(n % g.n0);
+    const int j = (int)((n / g.n0) % g.n1);
+    const int k = (int)(n / plane);
+    const double* cx = g.coef[0] + (int64_t)i * C_NCOEF;
+    const double* cy = g.coef[1] + (int64_t)j * C_NCOEF;
+    const double* cz = g.coef[2] + (int64_t)k * C_NCOEF;
+    double d = cx[C_MDI] * cy[C_MDI] * cz[C_MDI] +
+               g.dt_alpha * (cx[C_KDI] * cy[C_MDI] * cz[C_MDI] + cx[C_MDI] * cy[C_KDI] * cz[C_MDI] +
+                             cx[C_MDI] * cy[C_MDI] * cz[C_KDI]);
+    auto load_patch = [&](int sa, int sb, int64_t stride_a, int64_t stride_b, bool dega, bool degb,
+                          int ia, int na, int ib, int nb, double (&P)[3][3]) {
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+          const int aa = ia + u - 1, bb = ib + v - 1;
+          const bool ok = (dega ? u == 1 : (aa >= 0 && aa < na)) && (degb ? v == 1 : (bb >= 0 && bb < nb));
+          P[u][v] = ok ? T[n + (int64_t)(u - 1) * stride_a + (int64_t)(v - 1) * stride_b] : 0.0;
+        }
+      (void)sa; (void)sb;
+    };
+    double P[3][3];
+    if ((i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1])) {
+      load_patch(1, 2, g.n0, plane, D1, D2, j, g.n1, k, g.n2, P);
+      d += facet_sum<MODE_JAC, true, D1, D2>(g, cy[C_HLO], cy[C_HHI], cz[C_HLO], cz[C_HHI], P, P);
+    }
+    if (!D1 && ((j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]))) {
+      load_patch(0, 2, 1, plane, false, D2, i, g.n0, k, g.n2, P);
+      d += facet_sum<MODE_JAC, true, false, D2>(g, cx[C_HLO], cx[C_HHI], cz[C_HLO], cz[C_HHI], P, P);
+    }
+    if (!D2 && ((k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]))) {
+      load_patch(0, 1, 1, g.n0, false, D1, i, g.n0, j, g.n1, P);
+      d += facet_sum<MODE_JAC, true, false, D1>(g, cx[C_HLO], cx[C_HHI], cy[C_HLO], cy[C_HHI], P, P);
+    }
+    out[n] = invert ? 1.0 / d : d;
+  }
+}
+
+int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
+
+struct Launch {
+  int blocks, nseg, kfirst, nplanes, wmode;
+};
+
+Launch plan(const CgGrid& g, bool ghosts) {
+  Launch L;
+  L.nseg = (g.n0 + kSeg - 1) / kSeg;
+  L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
+  L.nplanes = (g.k_end - g.k_begin) + (ghosts ? g.g_lo + g.g_hi : 0);
+  L.wmode = (g.n1 >= 4) ? 0 : 1;
+  if (L.wmode == 0) {
+    L.blocks = L.nseg * ((g.n1 + 3) / 4) * L.nplanes;
+  } else {
+    const int64_t waves = (int64_t)L.nseg * g.n1 * L.nplanes;
+    L.blocks = (int)((waves + 3) / 4);
+  }
+  return L;
+}
+
+template <int MODE, bool FUSEP>
+void launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
+                 double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s) {
+  const Launch L = plan(g, ghosts);
+  if (L.blocks <= 0) return;
+  switch (dim_of(g)) {
+    case 1:
+      hipLaunchKernelGGL((k_cg_rows<1, MODE, FUSEP>), dim3(L.blocks), dim3(kBlock), 0, s, g, T, in0, in1, out,
+                         pout, st, partials, L.nseg, L.kfirst, L.nplanes, L.wmode);
+      break;
+    case 2:
+      hipLaunchKernelGGL((k_cg_rows<2, MODE, FUSEP>), dim3(L.blocks), dim3(kBlock), 0, s, g, T, in0, in1, out,
+                         pout, st, partials, L.nseg, L.kfirst, L.nplanes, L.wmode);
+      break;
+    default:
+      hipLaunchKernelGGL((k_cg_rows<3, MODE, FUSEP>), dim3(L.blocks), dim3(kBlock), 0, s, g, T, in0, in1, out,
+                         pout, st, partials, L.nseg, L.kfirst, L.nplanes, L.wmode);
+  }
+}
+
+}  // namespace
+
+int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).blocks; }
+
+void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
+  launch_rows<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, false, s);
+}
+
+void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
+                      int* n_partials, hipStream_t s) {
+  launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, nullptr, partials, false, s);
+  if (n_partials) *n_partials = plan(g, false).blocks;
+}
+
+void launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
+                            double* w, const PcgState* st, double* partials, int* n_partials,
+                            hipStream_t s) {
+  // neighbour values of p_new are recomputed from z and p_old; p_new goes to the
+  // other buffer of the pair (selected on device from st->it).
+  launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s);
+  if (n_partials) *n_partials = plan(g, true).blocks;
+}
+
+void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {
+  const int64_t nown = (int64_t)g.n0 * g.n1 * (g.k_end - g.k_begin);
+  int blocks = (int)std::min<int64_t>((nown + kBlock - 1) / kBlock, 4096);
+  if (blocks <= 0) return;
+  switch (dim_of(g)) {
+    case 1: hipLaunchKernelGGL(k_cg_diag<1>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
+    case 2: hipLaunchKernelGGL(k_cg_diag<2>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
+    default: hipLaunchKernelGGL(k_cg_diag<3>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
+  }
+}
+
+}  // namespace tv

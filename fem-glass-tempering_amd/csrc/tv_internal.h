@@ -1,0 +1,131 @@
+// Internal definitions shared by the HIP kernels and the host runtime of
+// libtvfem.so.  Not part of the C-ABI (see include/tvfem.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "tvfem.h"
+
+namespace tv {
+
+constexpr int kWave = 64;         // CDNA wavefront
+constexpr int kSeg = kWave - 2;   // outputs per wave of the x-row stencil kernels
+constexpr int kBlock = 256;       // 4 waves
+
+// Per-node coefficients of one storage axis of a rectilinear grid: the
+// assembled 1D P1 mass (lo, diag, up), 1D stiffness (lo, diag, up), and the
+// lengths of the cells below / above the node (0 where no cell exists).
+// A degenerate axis (1 node) carries M = (0, 1, 0), K = 0, h = 0.
+enum { C_MLO = 0, C_MDI, C_MUP, C_KLO, C_KDI, C_KUP, C_HLO, C_HHI, C_NCOEF };
+
+// Grid of the CG1 (Q1 / P1) temperature space on one partition.  Storage axis
+// 0 is physical x (fastest), storage axis 2 is the partition axis (slowest);
+// local node index = i + n0*(j + n1*k).  Along axis 2 the local array holds the
+// owned planes plus one ghost plane towards each neighbouring partition.
+struct CgGrid {
+  int n0, n1, n2;             // local node counts per storage axis (n2 incl. ghosts)
+  int k_begin, k_end;         // owned planes along axis 2, local indexing
+  int g_lo, g_hi;             // ghost planes present below / above
+  int deg1, deg2;             // storage axis 1 / 2 degenerate (single node)
+  int bnd[3][2];              // face of storage axis a at side s is a physical boundary here
+  const double* coef[3];      // device, C_NCOEF doubles per local node per axis
+  double dt, dt_alpha, dt_f;  // dt, dt*alpha, dt*f
+  double a_rad, a_conv;       // 0.001*sigma*epsilon, 0.001*htc
+  double T_amb, T_amb4;
+};
+
+// Grid of the DG1 temperature space: cells per storage axis; dof layout is
+// component-major [local vertex l][local cell], l = a + 2b + 4c (storage axes).
+struct DgGrid {
+  int c0, c1, c2;             // local cell counts (c2 incl. ghost layers)
+  int k_begin, k_end;         // owned cell layers along axis 2
+  int deg1, deg2;
+  int bnd[3][2];
+  const double* h[3];         // device: cell length per local cell per axis
+  double hdiam_inv;           // unused for rectilinear non-uniform (per-cell below)
+  double dt, dt_alpha, dt_f;
+  double a_rad, a_conv;
+  double T_amb, T_amb4;
+  double penalty;             // SIPG penalty (ThermoViscoProblem.py:313)
+};
+
+// Device-resident scalars of one PCG solve (PETSc KSPCG restated, preconditioned norm).
+struct PcgState {
+  double beta, betaold, dpi, dpiold, a, dp, rnorm0, ttol;
+  double rtol, atol, dtol;
+  int it, done, reason, max_it;
+  double dx_norm2;            // ||dx||^2 of the last Newton update
+  double pad[3];
+};
+
+enum PcgReason {
+  R_RUNNING = 0,
+  R_CONV_RTOL = 2, R_CONV_ATOL = 3,
+  R_DIV_ITS = -3, R_DIV_DTOL = -4, R_DIV_INDEF_PC = -8, R_DIV_NANINF = -9, R_DIV_INDEF_MAT = -10,
+};
+
+// Viscoelastic constants (ViscoelasticModel.py:15-83), uploaded as a kernel argument.
+struct ViscoConst {
+  double H_over_Rg, inv_Tb, dt, half_dt, alpha_s, dalpha, inv_dim;
+  double lambda_m[6], m_n[6], lambda_g[6], g_n[6], lambda_k[6], k_n[6];
+};
+
+// Pointers of the viscoelastic state (component-major, stride = n_local).
+struct ViscoFields {
+  int64_t n;                  // dofs processed (owned range length)
+  int64_t off_T, off_S;       // first processed dof in T-space / sigma-space arrays
+  int64_t sT, sS;             // component strides of T-space / sigma-space fields
+  const int* map;             // sigma dof -> T dof (mixed families) or nullptr
+  double* T; double* Tp; double* Tn; double* phi; double* phin; double* xi;
+  double* Tf; double* Tfp;    // Tf (== Tf_prev), Tf_partial (== Tf_partial_prev)
+  double* th; double* tot; double* dev;          // strains (materialize=all)
+  double* ds; double* dsig;                      // increments (materialize=all)
+  double* st; double* sgt;                       // s_tilde, sigma_tilde (state)
+  double* sp; double* sgp;                       // s, sigma partial (materialize=all)
+  double* sigma;                                 // total stress (state)
+  int copy_Tprev;             // fuse T_prev <- T (same family, single pass)
+};
+
+// ---- kernel launchers (tv_cg.hip, tv_dg.hip, tv_visco.hip, tv_pcg.hip) ----
+void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
+void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
+                      int* n_partials, hipStream_t s);
+void launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
+                            double* w, const PcgState* st, double* partials, int* n_partials,
+                            hipStream_t s);
+void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
+int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
+
+void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
+void launch_dg_japply(const DgGrid& g, const double* T, const double* x, double* y, double* partials,
+                      int* n_partials, hipStream_t s);
+void launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB,
+                            double* w, const PcgState* st, double* partials, int* n_partials,
+                            hipStream_t s);
+void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
+
+void launch_visco(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
+void launch_visco_Tpass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
+void launch_visco_Spass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
+
+// PCG vector kernels over the owned range [0, n) of already-offset pointers
+constexpr int kVecBlocks = 1024;
+void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx,
+                     double* partials, hipStream_t s);
+// p is taken from buffer (st->it & 1 ? pB : pA), matching the fused matvec
+void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
+                       const double* dinv, double* dx, double* r, double* z, double* partials,
+                       hipStream_t s);
+// one-block deterministic reduce of n records of width W (<= 2) into out[W];
+// kind: 0 none, 1 PCG init logic, 2 PCG p.w logic, 3 PCG update logic
+void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
+                         int check_done, hipStream_t s);
+void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s);
+void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s);
+int pcg_vec_blocks(int64_t n);
+void launch_fill(double* x, int64_t n, double v, hipStream_t s);
+void launch_copy(double* dst, const double* src, int64_t n, hipStream_t s);
+
+}  // namespace tv

@@ -1,0 +1,224 @@
+// Jacobi-preconditioned CG vector kernels, deterministic reductions and the
+// device-side scalar logic of PETSc KSPCG (preconditioned norm, zero initial
+// guess) + KSPConvergedDefault, gfx950.
+//
+// Replaces PETSc VecAXPY / VecAYPX / VecNorm / VecXDot / PCApply(Jacobi) and the
+// KSPSolve_CG control flow that the reference runs inside dolfinx's Newton
+// solver (ThermoViscoProblem.py:339-346).  All scalars live on the device
+// (PcgState) so a batch of iterations is launched without host round trips;
+// once converged every kernel of the batch exits at its first instruction.
+// Reductions: per-block partial sums (fixed order) -> one-block reduce, so the
+// result is bitwise reproducible run to run.
+#include "tv_internal.h"
+
+namespace tv {
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int W>
+__device__ __forceinline__ void block_partials(double (&v)[W], double* partials) {
+  __shared__ double red[W][kBlock / kWave];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const double s = wave_sum(v[w]);
+    if (lane == 0) red[w][wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < W) {
+    const int w = threadIdx.x;
+    partials[(int64_t)blockIdx.x * W + w] = (red[w][0] + red[w][1]) + (red[w][2] + red[w][3]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pcg_init(int64_t n, const double* __restrict__ r,
+                                                     const double* __restrict__ dinv, double* __restrict__ z,
+                                                     double* __restrict__ dx, double* __restrict__ partials) {
+  double acc[2] = {0.0, 0.0};
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    const double rr = r[t];
+    const double zz = dinv[t] * rr;  // PCApply (Jacobi)
+    z[t] = zz;
+    dx[t] = 0.0;
+    acc[0] += zz * zz;
+    acc[1] += zz * rr;
+  }
+  block_partials<2>(acc, partials);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState* __restrict__ st,
+                                                       const double* __restrict__ pA,
+                                                       const double* __restrict__ pB,
+                                                       const double* __restrict__ w,
+                                                       const double* __restrict__ dinv, double* __restrict__ dx,
+                                                       double* __restrict__ r, double* __restrict__ z,
+                                                       double* __restrict__ partials) {
+  if (st->done) return;
+  const double a = st->a;
+  const double* __restrict__ p = (st->it & 1) ? pB : pA;
+  double acc[2] = {0.0, 0.0};
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    dx[t] += a * p[t];                    // x <- x + a p
+    const double rr = r[t] - a * w[t];    // r <- r - a w
+    r[t] = rr;
+    const double zz = dinv[t] * rr;       // z <- B r
+    z[t] = zz;
+    acc[0] += zz * zz;
+    acc[1] += zz * rr;
+  }
+  block_partials<2>(acc, partials);
+}
+
+__global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __restrict__ T,
+                                                          const double* __restrict__ dx,
+                                                          double* __restrict__ partials) {
+  double acc[1] = {0.0};
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    const double d = dx[t];
+    T[t] -= d;  // x <- x - relaxation * dx   (relaxation 1)
+    acc[0] += d * d;
+  }
+  block_partials<1>(acc, partials);
+}
+
+// ---- scalar logic (PETSc KSPSolve_CG + KSPConvergedDefault) ------------------
+__device__ void logic_init(PcgState* st, const double* sums) {
+  const double dp = sqrt(sums[0]);
+  st->dp = dp;
+  st->rnorm0 = dp;
+  st->ttol = fmax(st->rtol * dp, st->atol);
+  st->it = 0;
+  st->done = 0;
+  st->reason = R_RUNNING;
+  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
+  st->beta = sums[1];
+  st->betaold = 1.0;
+  if (st->beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; }
+}
+
+__device__ void logic_dpi(PcgState* st, const double* sums) {
+  if (st->done) return;
+  const double dpi = sums[0];
+  if (!isfinite(dpi)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  const double dpiold = st->dpiold;
+  st->betaold = st->beta;
+  if (dpi == 0.0 || (st->it > 0 && ((dpi > 0.0) != (dpiold > 0.0)))) {
+    st->done = 1; st->reason = R_DIV_INDEF_MAT; return;
+  }
+  st->dpi = dpi;
+  st->dpiold = dpi;
+  st->a = st->beta / dpi;
+}
+
+__device__ void logic_update(PcgState* st, const double* sums) {
+  if (st->done) return;
+  const double dp = sqrt(sums[0]);
+  st->it += 1;
+  st->dp = dp;
+  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
+  if (dp >= st->dtol * st->rnorm0) { st->done = 1; st->reason = R_DIV_DTOL; return; }
+  if (st->it >= st->max_it) { st->done = 1; st->reason = R_DIV_ITS; return; }
+  const double beta = sums[1];
+  if (beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
+  if (beta * st->betaold < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
+  st->beta = beta;
+}
+
+// One-block deterministic reduction of `n` partial records of width W, then
+// (optionally) the scalar logic.  kind: 0 none, 1 init, 2 dpi, 3 update.
+__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ partials, int n, int W,
+                                                 double* __restrict__ out, PcgState* st, int kind,
+                                                 int check_done) {
+  if (check_done && st->done) return;
+  __shared__ double red[2][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double acc[2] = {0.0, 0.0};
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    acc[0] += partials[(int64_t)t * W];
+    if (W > 1) acc[1] += partials[(int64_t)t * W + 1];
+  }
+  for (int w = 0; w < W; ++w) {
+    const double s = wave_sum(acc[w]);
+    if (lane == 0) red[w][wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double sums[2] = {0.0, 0.0};
+    const int nw = blockDim.x >> 6;
+    for (int w = 0; w < W; ++w) {
+      double s = 0.0;
+      for (int q = 0; q < nw; ++q) s += red[w][q];
+      sums[w] = s;
+      out[w] = s;
+    }
+    if (kind == 1) logic_init(st, sums);
+    else if (kind == 2) logic_dpi(st, sums);
+    else if (kind == 3) logic_update(st, sums);
+  }
+}
+
+__global__ void k_logic(PcgState* st, const double* sums, int kind) {
+  if (kind == 1) logic_init(st, sums);
+  else if (kind == 2) logic_dpi(st, sums);
+  else if (kind == 3) logic_update(st, sums);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(double* x, int64_t n, double v) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = v;
+}
+__global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ d, const double* __restrict__ s, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) d[t] = s[t];
+}
+
+int vec_blocks(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b > kVecBlocks) b = kVecBlocks;
+  return b < 1 ? 1 : (int)b;
+}
+
+}  // namespace
+
+int pcg_vec_blocks(int64_t n) { return vec_blocks(n); }
+
+void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx, double* partials,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_pcg_init, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, r, dinv, z, dx, partials);
+}
+
+void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
+                       const double* dinv, double* dx, double* r, double* z, double* partials, hipStream_t s) {
+  hipLaunchKernelGGL(k_pcg_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx, r, z,
+                     partials);
+}
+
+void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s) {
+  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials);
+}
+
+void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
+                         int check_done, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, partials, n, W, out, st, kind, check_done);
+}
+
+void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s) {
+  hipLaunchKernelGGL(k_logic, dim3(1), dim3(1), 0, s, st, sums, kind);
+}
+
+void launch_fill(double* x, int64_t n, double v, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_fill, dim3(vec_blocks(n)), dim3(kBlock), 0, s, x, n, v);
+}
+
+void launch_copy(double* dst, const double* src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_copy, dim3(vec_blocks(n)), dim3(kBlock), 0, s, dst, src, n);
+}
+
+}  // namespace tv

@@ -1,0 +1,217 @@
+// Fused per-point viscoelastic update (Narayanaswamy shift, partial fictive
+// temperatures, strains, scaled time, Prony-series stress increments), gfx950.
+//
+// Replaces the 17 dolfinx fem::interpolate(Expression) passes of one time step
+// (ThermoViscoProblem.py:393-595) over the FFCx expression kernels of
+// ViscoelasticModel._init_expressions (ViscoelasticModel.py:86-242), together
+// with the _update_values copies (ThermoViscoProblem.py:349-354) and the final
+// T_prev <- T update (ThermoViscoProblem.py:378-379).
+//
+// For degree-1 Lagrange spaces every expression is a per-dof map, so one thread
+// owns one dof and carries the whole pipeline in registers: a single HBM pass
+// that reads T, T_prev, Tf_partial, s_tilde, sigma_tilde and writes the state
+// (Tf_partial, Tf, phi, xi, s_tilde, sigma_tilde, sigma) — plus every
+// intermediate Function of the reference when materialize = all.
+//
+// Semantics follow the reference, quirks included:
+//   Q1 phi is Eq. 5 (the Eq. 25 expression is overwritten, VEM:100 vs :156);
+//   Q2 Tf_prev is overwritten before the thermal strain reads it (TVP:481 vs
+//      :492), so the alpha_liquid term is (Tf - Tf) = 0;
+//   Q3 s_tilde / sigma_tilde are fed by their own previous values (VEM:196,205);
+//   Q4 xi = dt/2 (phi_next - phi) with "-" (VEM:171);
+//   Q5 xi == 0 gives 0/0 = NaN in ds / dsigma (VEM:178,187).
+// The arithmetic is written in the reference's operator order and this file is
+// compiled with -ffp-contract=off, so it performs the same IEEE operations as
+// the CPU oracle (exp() may differ by an ulp between libm and ocml).
+//
+// Layout: component-major (SoA) fields, comp * stride + dof, so every load and
+// store of a wavefront is one contiguous 512-byte segment.
+#include "tv_internal.h"
+
+namespace tv {
+namespace {
+
+__device__ __forceinline__ double taylor_E(double xi, double lam) {
+  // ViscoelasticModel._taylor_exponential: sum_{k=0}^{2} 1/k! (-xi/lam)^k,
+  // summed left to right (np.sum over a Python list).
+  const double x = (-xi) / lam;
+  const double t0 = 1.0;          // 1/0! * x**0 (== 1 also for NaN/inf x)
+  const double t1 = 1.0 * x;      // 1/1! * x**1
+  const double t2 = 0.5 * (x * x);  // 1/2! * x**2
+  return (t0 + t1) + t2;
+}
+
+struct TState {
+  double T, Tp, Tf, xi;
+};
+
+// T-family part: phi, Tf_partial, Tf, T_next, phi_next, xi at T-dof t.
+template <bool ALL>
+__device__ __forceinline__ TState t_part(const ViscoConst& c, const ViscoFields& f, int64_t t) {
+  TState o;
+  const double T = f.T[t];
+  const double Tp = f.Tp[t];
+  // Eq. 5 (VEM:156-161)
+  const double phi = exp(c.H_over_Rg * (c.inv_Tb - 1.0 / T));
+  // Eq. 24 (VEM:111-119), Tf_partial_prev -> Tf_partial (alias: TVP:469-470)
+  double Tf = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double prev = f.Tfp[i * f.sT + t];
+    const double cur = (c.lambda_m[i] * prev + T * c.dt * phi) / (c.lambda_m[i] + c.dt * phi);
+    f.Tfp[i * f.sT + t] = cur;
+    Tf = Tf + c.m_n[i] * cur;  // Eq. 26 inner(m, Tf_partial) (VEM:122-125)
+  }
+  f.Tf[t] = Tf;  // Tf_prev <- Tf (alias: TVP:481-482)
+  // extrapolation (VEM:150-153)
+  const double Tn = T + (T - Tp);
+  // phi again (identical, VEM:156) and phi_next (VEM:162-167)
+  const double phin = exp(c.H_over_Rg * (c.inv_Tb - 1.0 / Tn));
+  // Eq. 19 with "-" (VEM:170-173)
+  const double xi = c.half_dt * (phin - phi);
+  f.phi[t] = phi;
+  f.xi[t] = xi;
+  if (ALL) {
+    f.Tn[t] = Tn;
+    f.phin[t] = phin;
+  }
+  o.T = T; o.Tp = Tp; o.Tf = Tf; o.xi = xi;
+  return o;
+}
+
+// sigma-family part at sigma-dof s given the T-family values of its source dof.
+template <int D, bool ALL>
+__device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f, int64_t s, const TState& ts) {
+  constexpr int DD = D * D;
+  // Eq. 9 (VEM:128-133): I*(alpha_s (T - T_prev) + (alpha_l - alpha_s)(Tf - Tf_prev)), Tf_prev == Tf (Q2)
+  const double scal = c.alpha_s * (ts.T - ts.Tp) + c.dalpha * (ts.Tf - ts.Tf);
+  double tot[DD];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const double th = (i == j ? 1.0 : 0.0) * scal;
+      tot[i * D + j] = -th;  // Eq. 28 (VEM:136-139)
+      if (ALL) {
+        f.th[(i * D + j) * f.sS + s] = th;
+        f.tot[(i * D + j) * f.sS + s] = -th;
+      }
+    }
+  double tr = 0.0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) tr = tr + tot[i * D + i];
+  double dev[DD];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      // Eq. 29 (VEM:142-146): eps - 1/dim * I * tr(eps)
+      dev[i * D + j] = tot[i * D + j] - (c.inv_dim * (i == j ? 1.0 : 0.0)) * tr;
+      if (ALL) f.dev[(i * D + j) * f.sS + s] = dev[i * D + j];
+    }
+  const double xi = ts.xi;
+  double sig[DD];
+#pragma unroll
+  for (int n = 0; n < 6; ++n) {
+    const double Eg = taylor_E(xi, c.lambda_g[n]);
+    const double Ek = taylor_E(xi, c.lambda_k[n]);
+    const double twog = 2.0 * c.g_n[n];
+    const double omEg = 1.0 - Eg, omEk = 1.0 - Ek;
+#pragma unroll
+    for (int q = 0; q < DD; ++q) {
+      const int i = q / D, j = q % D;
+      const int64_t o = (int64_t)(n * DD + q) * f.sS + s;
+      // Eq. 15a + 20 (VEM:176-182)
+      const double ds = (((twog * dev[q]) / xi) * c.lambda_g[n]) * omEg;
+      // Eq. 16a (VEM:195-200)
+      const double st = f.st[o] * Eg;
+      // Eq. 17a (VEM:212-215)
+      const double sp = ds + st;
+      // Eq. 15b + 20 (VEM:185-191)
+      const double dsg = (((c.k_n[n] * (tr * (i == j ? 1.0 : 0.0))) / xi) * c.lambda_k[n]) * omEk;
+      // Eq. 16b (VEM:203-209)
+      const double sgt = f.sgt[o] * Ek;
+      // Eq. 17b (VEM:218-221)
+      const double sgp = dsg + sgt;
+      f.st[o] = st;    // next -> current copy (TVP:559-560)
+      f.sgt[o] = sgt;  // (TVP:578-581)
+      if (ALL) {
+        f.ds[o] = ds;
+        f.dsig[o] = dsg;
+        f.sp[o] = sp;
+        f.sgp[o] = sgp;
+      }
+      // Eq. 18 (VEM:224-228), np.sum over n left to right
+      sig[q] = (n == 0) ? (sp + sgp) : sig[q] + (sp + sgp);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < DD; ++q) f.sigma[(int64_t)q * f.sS + s] = sig[q];
+}
+
+template <int D, bool ALL>
+__global__ __launch_bounds__(kBlock) void k_visco_fused(ViscoConst c, ViscoFields f) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t dT = f.off_T + t;
+    const TState ts = t_part<ALL>(c, f, dT);
+    s_part<D, ALL>(c, f, f.off_S + t, ts);
+    if (f.copy_Tprev) f.Tp[dT] = ts.T;  // TVP:378-379, T_prev is not read after this point
+  }
+}
+
+template <bool ALL>
+__global__ __launch_bounds__(kBlock) void k_visco_T(ViscoConst c, ViscoFields f) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
+    (void)t_part<ALL>(c, f, f.off_T + t);
+  }
+}
+
+// mixed families: sigma dof s reads the T-family values of the dof that the
+// last cell written by fem::interpolate assigns to it (f.map).
+template <int D, bool ALL>
+__global__ __launch_bounds__(kBlock) void k_visco_S(ViscoConst c, ViscoFields f) {
+  for (int64_t s = blockIdx.x * (int64_t)kBlock + threadIdx.x; s < f.n; s += (int64_t)gridDim.x * kBlock) {
+    const int64_t t = f.map[s];
+    TState ts;
+    ts.T = f.T[t];
+    ts.Tp = f.Tp[t];
+    ts.Tf = f.Tf[t];
+    ts.xi = f.xi[t];
+    s_part<D, ALL>(c, f, f.off_S + s, ts);
+  }
+}
+
+int blocks_for(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b > 8192) b = 8192;
+  return b < 1 ? 1 : (int)b;
+}
+
+}  // namespace
+
+void launch_visco(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s) {
+  const int b = blocks_for(f.n);
+#define TV_V(D, A) hipLaunchKernelGGL((k_visco_fused<D, A>), dim3(b), dim3(kBlock), 0, s, c, f)
+  if (dim == 1) { if (all) TV_V(1, true); else TV_V(1, false); }
+  else if (dim == 2) { if (all) TV_V(2, true); else TV_V(2, false); }
+  else { if (all) TV_V(3, true); else TV_V(3, false); }
+#undef TV_V
+}
+
+void launch_visco_Tpass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s) {
+  (void)dim;
+  const int b = blocks_for(f.n);
+  if (all) hipLaunchKernelGGL((k_visco_T<true>), dim3(b), dim3(kBlock), 0, s, c, f);
+  else hipLaunchKernelGGL((k_visco_T<false>), dim3(b), dim3(kBlock), 0, s, c, f);
+}
+
+void launch_visco_Spass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s) {
+  const int b = blocks_for(f.n);
+#define TV_V(D, A) hipLaunchKernelGGL((k_visco_S<D, A>), dim3(b), dim3(kBlock), 0, s, c, f)
+  if (dim == 1) { if (all) TV_V(1, true); else TV_V(1, false); }
+  else if (dim == 2) { if (all) TV_V(2, true); else TV_V(2, false); }
+  else { if (all) TV_V(3, true); else TV_V(3, false); }
+#undef TV_V
+}
+
+}  // namespace tv

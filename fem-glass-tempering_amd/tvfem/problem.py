@@ -1,0 +1,317 @@
+"""``ThermoViscoProblem`` — drop-in host mirror of the reference driver
+(ThermoViscoProblem.py:23-620) over the MI355X C-ABI library.
+
+Same constructor arguments and meaning (``mesh_path, time, dt, config,
+model_parameters, jit_options``), same ``setup`` / ``solve`` /
+``solve_timestep`` methods and the same state dictionaries ``functions``,
+``functions_current``, ``functions_previous``, ``functions_next`` whose values
+expose ``.x.array`` in the reference's interleaved blocked layout
+(``x.array[dof*bs + comp]``).  The FEniCSx stack underneath (UFL forms, FFCx
+kernels, dolfinx assemblers, PETSc Newton/KSP) is replaced by libtvfem.so.
+
+Differences that are part of the contract:
+  * ``mesh_path`` may be a ``.msh`` file (1D line mesh, as the reference) or a
+    ``RectilinearMesh`` (structured 1D / 2D / 3D grids);
+  * the linear solver is matrix-free Jacobi-PCG (reference: CG + GAMG); T and
+    sigma agree with the CPU restatement within the tolerances stated in
+    tests/;
+  * file output (VTX / XDMF, :246-276) is not written by default.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time as _time
+from math import ceil
+
+import numpy as np
+
+try:
+    import xxhash as _xxhash
+except Exception:  # pragma: no cover
+    _xxhash = None
+
+from . import _native as N
+from .mesh import RectilinearMesh, read_msh
+from .models import ThermalModel, ViscoelasticModel
+
+_FAMILIES = {"CG": N.TV_CG, "DG": N.TV_DG}
+
+
+def _digest(a: np.ndarray):
+    if _xxhash is not None:
+        return _xxhash.xxh3_64_intdigest(memoryview(np.ascontiguousarray(a)).cast("B"))
+    return hash(a.tobytes())
+
+
+class FunctionSpaceInfo:
+    def __init__(self, problem, space, family, degree, bs):
+        self._p = problem
+        self.space = space
+        self.family = family
+        self.degree = degree
+        self.bs = bs
+
+    def tabulate_dof_coordinates(self):
+        return self._p._dof_coordinates(self.space)
+
+
+class _Vector:
+    def __init__(self, fn):
+        self._fn = fn
+
+    @property
+    def array(self):
+        return self._fn._problem._host_array(self._fn.field)
+
+    def scatter_forward(self):
+        """Ghost values live on the device and are exchanged there (RCCL)."""
+        return None
+
+
+class Function:
+    """Proxy of one device-resident field (a dolfinx ``Function`` of the reference)."""
+
+    def __init__(self, problem, field, space: FunctionSpaceInfo, name=None):
+        self._problem = problem
+        self.field = field
+        self.function_space = space
+        self.name = name or field
+        self.x = _Vector(self)
+
+    def interpolate(self, f):
+        """Interpolate a Python callable ``f(x) -> values`` (x of shape (3, n)) at the dofs."""
+        if not callable(f):
+            raise TypeError("only Python callables can be interpolated into device fields")
+        X = self.function_space.tabulate_dof_coordinates()
+        vals = np.asarray(f(X.T), dtype=np.float64)
+        bs = self._problem._bs[self.field]
+        if bs == 1:
+            vals = vals.reshape(-1)
+        else:
+            vals = vals.reshape(bs, -1).T.reshape(-1)
+        arr = self.x.array
+        arr[:] = vals
+
+    def __repr__(self):
+        return f"Function({self.name!r})"
+
+
+class ThermoViscoProblem:
+    def __init__(self, mesh_path, time: tuple, dt: float, config: dict, model_parameters: dict,
+                 jit_options: dict | None = None, *, device: int = 0, materialize: bool = True,
+                 ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
+                 verbose: bool = True) -> None:
+        if isinstance(mesh_path, RectilinearMesh):
+            self.mesh = mesh_path
+        elif isinstance(mesh_path, str):
+            self.mesh = read_msh(mesh_path)
+        else:
+            raise TypeError("mesh_path must be a .msh path or a tvfem.RectilinearMesh")
+        self.dim = self.mesh.dim
+        self.dt = dt
+        self.time = time
+        self.t = self.time[0]
+        self.n_steps = ceil((self.time[1] - self.time[0]) / self.dt)
+        self.verbose = verbose
+        self.material_model = ViscoelasticModel(mesh=self.mesh, model_parameters=model_parameters)
+        self.physical_model = ThermalModel(mesh=self.mesh, model_parameters=model_parameters)
+        self._ctx = None
+        self._cache = {}
+        self._device_version = 0
+        self.last_newton_iterations = 0
+        self.last_krylov_iterations = 0
+        self.__init_function_spaces(config=config)
+        self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis)
+        self.__init_functions()
+        self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
+                                              functions_current=self.functions_current,
+                                              functions_previous=self.functions_previous,
+                                              functions_next=self.functions_next, dt=self.dt)
+        self.jit_options = jit_options
+
+    # ---------------------------------------------------------------------------------
+    def __init_function_spaces(self, config: dict) -> None:
+        # Only CG and DG are supported (ThermoViscoProblem.py:70-71)
+        assert all(var["element"] in ["CG", "DG"] for var in config.values()), \
+            "Only CG and DG elements are supported"
+        for key in ("T", "sigma"):
+            if config[key]["degree"] != 1:
+                raise NotImplementedError("libtvfem implements degree-1 Lagrange spaces")
+        self.config = config
+        d = self.dim
+        self._fam = {"T": config["T"]["element"], "sigma": config["sigma"]["element"]}
+        self.functionSpaces = {
+            "T": FunctionSpaceInfo(self, 0, config["T"]["element"], 1, 1),
+            "Tf_partial": FunctionSpaceInfo(self, 0, config["T"]["element"], 1, 6),
+            "sigma": FunctionSpaceInfo(self, 1, config["sigma"]["element"], 1, d * d),
+            "sigma_partial": FunctionSpaceInfo(self, 1, config["sigma"]["element"], 1, 6 * d * d),
+        }
+
+    def __init_native(self, mp, device, materialize, ksp_rtol, n_parts, part, part_axis):
+        lib = N.load_library()
+        self._lib = lib
+        desc = N.MeshDesc()
+        desc.dim = self.dim
+        self._coord_bufs = []
+        for a in range(3):
+            if a < self.dim:
+                buf = np.ascontiguousarray(self.mesh.axes[a])
+                self._coord_bufs.append(buf)
+                desc.n_cells[a] = len(buf) - 1
+                desc.coords[a] = buf.ctypes.data_as(C.POINTER(C.c_double))
+            else:
+                desc.n_cells[a] = 0
+        desc.part_axis = part_axis
+        desc.n_parts = n_parts
+        desc.part = part
+        fe = N.FeConfig(_FAMILIES[self._fam["T"]], 1, _FAMILIES[self._fam["sigma"]], 1)
+        params = N.default_params(mp, self.dt)
+        opts = N.default_options()
+        opts.materialize = 1 if materialize else 0
+        opts.ksp_rtol = ksp_rtol
+        ctx = C.c_void_p()
+        N.check(lib.tv_create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
+        self._ctx = ctx
+        self.materialize = materialize
+        self._bs = {}
+        for name, fid in N.FIELD_ID.items():
+            bs = C.c_int()
+            N.check(lib.tv_field_block_size(ctx, fid, C.byref(bs)), ctx)
+            self._bs[name] = bs.value
+
+    def __init_functions(self) -> None:
+        S = self.functionSpaces
+        mk = lambda field, sp, name=None: Function(self, field, S[sp], name)  # noqa: E731
+        self.functions_previous = {"T": mk("T_prev", "T"), "Tf_partial": mk("Tf_partial_prev", "Tf_partial"),
+                                   "Tf": mk("Tf_prev", "T")}
+        self.functions_current = {
+            "T": mk("T", "T", "Temperature"), "Tf_partial": mk("Tf_partial", "Tf_partial", "Fictive_temperature"),
+            "Tf": mk("Tf", "T", "Fictive_Temperature"),
+            "s_tilde_partial": mk("s_tilde_partial", "sigma_partial"),
+            "sigma_tilde_partial": mk("sigma_tilde_partial", "sigma_partial"),
+            "s_partial": mk("s_partial", "sigma_partial"), "sigma_partial": mk("sigma_partial", "sigma_partial"),
+        }
+        self.functions_next = {
+            "T": mk("T_next", "T"), "phi": mk("phi_next", "T"),
+            "s_tilde_partial": mk("s_tilde_partial_next", "sigma_partial"),
+            "sigma_tilde_partial": mk("sigma_tilde_partial_next", "sigma_partial"),
+            "s_partial": mk("s_partial_next", "sigma_partial"),
+            "sigma_partial": mk("sigma_partial_next", "sigma_partial"),
+            "sigma": mk("sigma", "sigma", "Stress_tensor"),
+        }
+        self.functions = {
+            "phi": mk("phi", "T"), "xi": mk("xi", "T", "Shifted_time"),
+            "thermal_strain": mk("thermal_strain", "sigma"), "total_strain": mk("total_strain", "sigma"),
+            "deviatoric_strain": mk("deviatoric_strain", "sigma"),
+            "ds_partial": mk("ds_partial", "sigma_partial", "Deviatoric_stress_increment"),
+            "dsigma_partial": mk("dsigma_partial", "sigma_partial", "Hydrostatic_stress_increment"),
+        }
+
+    # ---- host mirrors of device fields -------------------------------------------------
+    def num_dofs(self, space=0):
+        n = C.c_int64()
+        off = C.c_int64()
+        N.check(self._lib.tv_num_dofs(self._ctx, space, C.byref(n), C.byref(off)), self._ctx)
+        return n.value, off.value
+
+    def _dof_coordinates(self, space):
+        n, _ = self.num_dofs(space)
+        X = np.zeros((n, 3))
+        N.check(self._lib.tv_dof_coordinates(self._ctx, space, X.ctypes.data_as(C.POINTER(C.c_double)), n),
+                self._ctx)
+        return X
+
+    def get_field(self, field: str) -> np.ndarray:
+        fid = N.FIELD_ID[field]
+        space = 1 if field in _SIGMA_FIELDS else 0
+        n, _ = self.num_dofs(space)
+        out = np.empty(n * self._bs[field])
+        N.check(self._lib.tv_get_field(self._ctx, fid, out.ctypes.data_as(C.POINTER(C.c_double)), out.size),
+                self._ctx)
+        return out
+
+    def set_field(self, field: str, values) -> None:
+        fid = N.FIELD_ID[field]
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1)
+        N.check(self._lib.tv_set_field(self._ctx, fid, v.ctypes.data_as(C.POINTER(C.c_double)), v.size),
+                self._ctx)
+        self._cache.pop(field, None)
+
+    def _host_array(self, field):
+        ent = self._cache.get(field)
+        if ent is not None and ent[2] == self._device_version:
+            return ent[0]
+        arr = self.get_field(field)
+        self._cache[field] = [arr, _digest(arr), self._device_version]
+        return arr
+
+    def _flush(self):
+        """Push host arrays that were modified in place back to the device."""
+        for field, (arr, dig, ver) in list(self._cache.items()):
+            if ver == self._device_version and _digest(arr) != dig:
+                self.set_field(field, arr)
+        self._cache.clear()
+
+    # ---- reference API -------------------------------------------------------------------
+    def setup(self, dirichlet_bc: bool = False, outfile_name: str = "visco", outfile_name1: str = "stresses") -> None:
+        self._set_initial_condition(temp_value=self.material_model.T_init)
+        if dirichlet_bc:
+            # ThermoViscoProblem.py:236-243 references the undefined self.fs and the
+            # bc is never passed to the solver (:331): the reference cannot run this.
+            raise AttributeError("'ThermoViscoProblem' object has no attribute 'fs' "
+                                 "(Dirichlet path of the reference is broken; not supported)")
+
+    def _set_initial_condition(self, temp_value: float) -> None:
+        self._cache.clear()
+        N.check(self._lib.tv_set_initial_condition(self._ctx, float(temp_value)), self._ctx)
+        self._device_version += 1
+
+    def solve_timestep(self, t=None, thermal_only: bool = False) -> None:
+        if self.verbose:
+            print(f"t={self.t}")
+        self._flush()
+        nits = C.c_int()
+        kits = C.c_int()
+        rc = self._lib.tv_step(self._ctx, 1 if thermal_only else 0, C.byref(nits), C.byref(kits))
+        self._device_version += 1
+        if rc == N.TV_ERR_NOT_CONVERGED:
+            msg = self._lib.tv_last_error(self._ctx).decode()
+            raise RuntimeError(msg)
+        N.check(rc, self._ctx)
+        self.last_newton_iterations = nits.value
+        self.last_krylov_iterations = kits.value
+
+    def _solve_T(self):
+        self._flush()
+        nits, kits, conv = C.c_int(), C.c_int(), C.c_int()
+        rc = self._lib.tv_solve_T(self._ctx, C.byref(nits), C.byref(kits), C.byref(conv))
+        self._device_version += 1
+        N.check(rc, self._ctx)
+        assert conv.value
+        return nits.value, kits.value
+
+    def solve(self, n_steps: int | None = None) -> None:
+        if self.verbose:
+            print("Starting solve")
+        t_start = _time.time()
+        for _ in range(self.n_steps if n_steps is None else n_steps):
+            self.t += self.dt
+            self.solve_timestep(t=self.t)
+        if self.verbose:
+            print(f"Solve finished in {_time.time() - t_start} seconds.")
+
+    def close(self):
+        if self._ctx is not None:
+            self._lib.tv_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_SIGMA_FIELDS = {"thermal_strain", "total_strain", "deviatoric_strain", "ds_partial", "dsigma_partial",
+                 "s_tilde_partial", "s_tilde_partial_next", "sigma_tilde_partial", "sigma_tilde_partial_next",
+                 "s_partial", "s_partial_next", "sigma_partial", "sigma_partial_next", "sigma"}

@@ -1,0 +1,203 @@
+/*
+ * tvfem.h — C-ABI of libtvfem.so, the MI355X (gfx950) native hot path of the
+ * thermo-viscoelastic glass-tempering solver (pzimbrod/fem-glass-tempering).
+ *
+ * Plain C types only (no torch, no HIP types in any signature).  One opaque
+ * context per GPU / per mesh partition.  Every function returns an int status
+ * (TV_OK = 0); the message of the last failure is available through
+ * tv_last_error(ctx) (or tv_last_error(NULL) for failures before a context
+ * exists).  All device work is stream-ordered on the context's HIP stream.
+ *
+ * What each entry point replaces in the reference (file:line under
+ * /root/reference; [3P] = third-party code the reference drives):
+ *
+ *   tv_create            ThermoViscoProblem.__init__ (ThermoViscoProblem.py:24-58):
+ *                        mesh read (:27-28), spaces (:61-103), functions
+ *                        (:106-173), ThermalModel/ViscoelasticModel constants
+ *                        (ThermalModel.py:7-29, ViscoelasticModel.py:10-84).
+ *   tv_set_initial_condition  _set_initial_condition (ThermoViscoProblem.py:187-233).
+ *   tv_set_field / tv_get_field  Function.x.array reads/writes of the state dicts
+ *                        functions/functions_current/_previous/_next (:112-171),
+ *                        in the reference's interleaved blocked layout
+ *                        x.array[dof*bs + comp].
+ *   tv_residual          NonlinearProblem.F -> dolfinx assemble_vector over the
+ *                        FFCx cell / exterior-facet / interior-facet kernels of
+ *                        the form at ThermoViscoProblem.py:293-325 [3P].
+ *   tv_jacobian_apply    NonlinearProblem.J (ufl.derivative of F, :331) assembled
+ *                        by dolfinx assemble_matrix [3P] and applied by PETSc
+ *                        MatMult inside KSPSolve — here matrix-free.
+ *   tv_jacobian_diag     PETSc MatGetDiagonal (PC setup) [3P].
+ *   tv_solve_T           _solve_T (:384-391): dolfinx NewtonSolver.solve
+ *                        (incremental criterion, rtol 1e-12, :334-337) with
+ *                        KSP cg (:343) — Jacobi-PCG instead of GAMG (:344).
+ *   tv_visco_update      _solve_Tf/_solve_strains/_solve_shifted_time/_solve_stress
+ *                        (:393-595): the 17 fem::interpolate(Expression) passes
+ *                        of ViscoelasticModel._init_expressions
+ *                        (ViscoelasticModel.py:86-242), fused into one pass.
+ *   tv_step              solve_timestep (:367-381) minus the file output (:374).
+ *   tv_comm_*            MPI COMM_WORLD + dolfinx Scatterer::scatter_forward
+ *                        (:351) + PETSc VecNorm/VecDot MPI_Allreduce [3P],
+ *                        replaced by RCCL over xGMI.
+ */
+#ifndef TVFEM_H
+#define TVFEM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TV_ABI_VERSION 1
+
+/* status codes */
+#define TV_OK 0
+#define TV_ERR_ARG 1          /* invalid argument */
+#define TV_ERR_HIP 2          /* HIP runtime failure */
+#define TV_ERR_NOT_CONVERGED 3 /* Newton did not converge (dolfinx raises) */
+#define TV_ERR_KSP 4          /* Krylov solver diverged */
+#define TV_ERR_STATE 5        /* field not available in this mode */
+#define TV_ERR_COMM 6         /* RCCL failure */
+
+/* finite element families (ThermoViscoProblem.py:70-71 allows CG and DG) */
+#define TV_CG 0
+#define TV_DG 1
+
+/* Mesh: rectilinear grid (tensor product of per-axis node coordinates).  Covers
+ * the reference's 1D interval meshes (geometry.py, any node spacing) and the
+ * structured 3D hexahedral plates of the benchmark configurations.
+ *   dim             topological dimension 1..3
+ *   n_cells[a]      cells along physical axis a (a < dim)
+ *   coords[a]       n_cells[a]+1 increasing node coordinates along axis a
+ *   part_axis       physical axis along which the mesh is sliced into
+ *                   partitions (-1: automatic = longest of the axes >= 1)
+ *   n_parts, part   number of partitions / this context's partition      */
+typedef struct {
+  int dim;
+  int n_cells[3];
+  const double* coords[3];
+  int part_axis;
+  int n_parts;
+  int part;
+} tv_mesh_desc;
+
+typedef struct {
+  int T_family;      /* TV_CG / TV_DG  (fe_config["T"]["element"])      */
+  int T_degree;      /* must be 1                                        */
+  int sigma_family;  /* TV_CG / TV_DG  (fe_config["sigma"]["element"])  */
+  int sigma_degree;  /* must be 1                                        */
+} tv_fe_config;
+
+/* model_params of main.py:29-55 plus the Prony tableaux of
+ * ViscoelasticModel.py:19-68 (6 terms each).  rho, cp, k and Tf_init are
+ * accepted and unused, exactly as in the reference. */
+typedef struct {
+  double f, epsilon, sigma, T_ambient, T_0, alpha, htc, rho, cp, k;
+  double H, Tb, Rg, alpha_solid, alpha_liquid, Tf_init;
+  double m_n[6], lambda_m[6], g_n[6], lambda_g[6], k_n[6], lambda_k[6];
+  double dt;
+} tv_params;
+
+/* Solver options.  Defaults (tv_default_options): dolfinx NewtonSolver
+ * (rtol 1e-12 set at ThermoViscoProblem.py:336; atol 1e-10, max_it 50,
+ * relaxation 1 [3P defaults]) and PETSc KSP (rtol 1e-5, atol 1e-50,
+ * dtol 1e5, max_it 10000 [3P defaults]). */
+typedef struct {
+  double newton_rtol, newton_atol;
+  int newton_max_it;
+  int error_on_nonconvergence;
+  double ksp_rtol, ksp_atol, ksp_dtol;
+  int ksp_max_it;
+  int materialize;        /* 0: state fields only, 1: every reference field  */
+  int use_graphs;         /* capture PCG iteration batches in hipGraphs      */
+  int pcg_batch;          /* iterations launched between convergence polls  */
+} tv_options;
+
+/* field ids (the reference's Function objects) */
+enum {
+  TV_F_T = 0,               /* functions_current["T"]                        */
+  TV_F_T_PREV,              /* functions_previous["T"]                       */
+  TV_F_T_NEXT,              /* functions_next["T"]                           */
+  TV_F_TF,                  /* functions_current["Tf"]                       */
+  TV_F_TF_PREV,             /* functions_previous["Tf"]                      */
+  TV_F_TF_PARTIAL,          /* functions_current["Tf_partial"]   (bs 6)      */
+  TV_F_TF_PARTIAL_PREV,     /* functions_previous["Tf_partial"]  (bs 6)      */
+  TV_F_PHI,                 /* functions["phi"]                              */
+  TV_F_PHI_NEXT,            /* functions_next["phi"]                         */
+  TV_F_XI,                  /* functions["xi"]                               */
+  TV_F_THERMAL_STRAIN,      /* functions["thermal_strain"]      (bs d*d)     */
+  TV_F_TOTAL_STRAIN,        /* functions["total_strain"]        (bs d*d)     */
+  TV_F_DEVIATORIC_STRAIN,   /* functions["deviatoric_strain"]   (bs d*d)     */
+  TV_F_DS_PARTIAL,          /* functions["ds_partial"]          (bs 6*d*d)   */
+  TV_F_DSIGMA_PARTIAL,      /* functions["dsigma_partial"]      (bs 6*d*d)   */
+  TV_F_S_TILDE,             /* functions_current["s_tilde_partial"]          */
+  TV_F_S_TILDE_NEXT,        /* functions_next["s_tilde_partial"]             */
+  TV_F_SIGMA_TILDE,         /* functions_current["sigma_tilde_partial"]      */
+  TV_F_SIGMA_TILDE_NEXT,    /* functions_next["sigma_tilde_partial"]         */
+  TV_F_S_PARTIAL,           /* functions_current["s_partial"]                */
+  TV_F_S_PARTIAL_NEXT,      /* functions_next["s_partial"]                   */
+  TV_F_SIGMA_PARTIAL,       /* functions_current["sigma_partial"]            */
+  TV_F_SIGMA_PARTIAL_NEXT,  /* functions_next["sigma_partial"]               */
+  TV_F_SIGMA,               /* functions_next["sigma"]          (bs d*d)     */
+  TV_F_RESIDUAL,            /* work: last assembled residual F               */
+  TV_F_DX,                  /* work: last Newton increment dx                */
+  TV_NUM_FIELDS
+};
+
+/* ---- library / context -------------------------------------------------- */
+int tv_abi_version(void);
+const char* tv_last_error(const void* ctx);      /* NULL ctx: global error   */
+void tv_default_options(tv_options* opts);
+void tv_default_params(tv_params* p);            /* main.py:29-55 + tableaux */
+
+int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
+              const tv_options* opts, int device, void** ctx_out);
+int tv_destroy(void* ctx);
+
+/* sizes: owned dofs of the T space / sigma space on this partition; block
+ * size of a field; global dof offset of this partition's first owned dof */
+int tv_num_dofs(void* ctx, int space /*0 T, 1 sigma*/, int64_t* n_owned, int64_t* global_offset);
+int tv_field_block_size(void* ctx, int field, int* bs);
+/* dof coordinates (owned dofs, 3 doubles each, zero-padded beyond dim) */
+int tv_dof_coordinates(void* ctx, int space, double* xyz, size_t n_dofs);
+
+/* host <-> device field transfer, owned dofs, interleaved reference layout */
+int tv_set_field(void* ctx, int field, const double* host, size_t n_values);
+int tv_get_field(void* ctx, int field, double* host, size_t n_values);
+/* device address of a field's storage (component-major: comp*stride + dof) */
+int tv_field_device_ptr(void* ctx, int field, void** dev_ptr, int64_t* comp_stride);
+
+int tv_set_initial_condition(void* ctx, double T0);
+int tv_sync(void* ctx);
+
+/* ---- operators (device pointers, owned T-dofs, length n_owned) ---------- */
+int tv_residual(void* ctx, const double* T_dev, double* F_dev);     /* F(T; T_prev) */
+int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev); /* J(T)·x      */
+int tv_jacobian_diag(void* ctx, double* d_dev);                       /* diag J(T)   */
+
+/* ---- solvers -------------------------------------------------------------- */
+int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged);
+int tv_visco_update(void* ctx);
+int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------- */
+int tv_comm_unique_id_size(void);
+int tv_comm_get_unique_id(char* id_out);   /* rank 0; broadcast it out-of-band */
+int tv_comm_init(void* ctx, const char* id, int n_ranks, int rank);
+int tv_halo_exchange(void* ctx, int field);
+
+/* ---- measurement ------------------------------------------------------------ */
+/* time `reps` launches of one hot kernel on the context stream with HIP events;
+ * kernel: 0 = CG Jacobian apply (matvec), 1 = fused viscoelastic update,
+ * 2 = residual.  Writes the mean duration per launch in ms. */
+int tv_time_kernel(void* ctx, int kernel, int reps, double* ms_per_launch);
+/* algorithmic bytes moved by one launch of `kernel` */
+int tv_kernel_bytes(void* ctx, int kernel, double* bytes);
+/* counters of the last tv_step / tv_solve_T */
+int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TVFEM_H */
