@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: coupled thermo-viscoelastic time steps
+(Newton + matrix-free Jacobi-PCG heat solve, fused viscoelastic update) on the
+structured 3D CG1 hexahedral plate of BASELINE.json configs[3] (C4: 50 x 50 x 5
+plate, 400 x 400 x 50 = 8M hex, 8,200,851 temperature dofs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+
+One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK /
+WORLD_SIZE); the mesh is sliced along y into N partitions with one ghost node
+plane per interface; RCCL exchanges the ghost planes and all-reduces the PCG /
+Newton dot products.  ``--scaling strong`` (default) partitions the fixed 8M-hex
+mesh; ``weak`` gives every rank its own 400 x 400 x 50 slab of a 400 x 400N x 50
+plate.  Rank 0 prints one JSON line (metric, value, roofline, cpu_baseline ...).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "fem-glass-tempering_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--cells", type=str, default="400,400,50", help="hex cells per axis (per rank for weak)")
+    ap.add_argument("--lengths", type=str, default="50,50,5")
+    ap.add_argument("--thermal-only", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
+    ap.add_argument("--kernel-reps", type=int, default=20)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE {world}")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from tvfem import box_mesh
+    from tvfem import _native as N
+    from tvfem.problem import ThermoViscoProblem
+
+    nc = [int(v) for v in a.cells.split(",")]
+    L = [float(v) for v in a.lengths.split(",")]
+    if a.scaling == "weak":
+        nc[1] *= world
+        L[1] *= world
+    mesh = box_mesh(L, nc)
+    mp = {
+        "f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0,
+        "htc": 280.1, "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0e0, "Rg": 8.314,
+        "alpha_solid": 9.10e-6, "alpha_liquid": 25.10e-6, "Tf_init": 873.0,
+    }  # main.py:29-55
+    cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+    prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=local_rank, materialize=False,
+                              n_parts=world, part=rank, part_axis=1, verbose=False)
+    lib, ctx = prob._lib, prob._ctx
+    if world > 1:
+        idsz = lib.tv_comm_unique_id_size()
+        buf = C.create_string_buffer(idsz)
+        if rank == 0:
+            N.check(lib.tv_comm_get_unique_id(buf))
+        obj = [buf.raw if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        N.check(lib.tv_comm_init(ctx, C.c_char_p(obj[0]), world, rank), ctx)
+    prob.setup()
+    n_owned, _ = prob.num_dofs(0)
+    n_global = int(np.prod([n + 1 for n in nc]))
+
+    def barrier_sync():
+        N.check(lib.tv_sync(ctx), ctx)
+        if dist is not None:
+            dist.barrier()
+
+    step = lambda: prob.solve_timestep(thermal_only=a.thermal_only)  # noqa: E731
+    for _ in range(a.warmup):
+        step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    nits = kits = 0
+    for _ in range(a.steps):
+        step()
+        nits += prob.last_newton_iterations
+        kits += prob.last_krylov_iterations
+    barrier_sync()
+    dt_local = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt_local], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    else:
+        elapsed = dt_local
+
+    # ---- per-kernel timing (HIP events on the context stream) and algorithmic bytes ----
+    kern = {}
+    names = {3: "pcg_matvec_fused", 4: "pcg_update", 0: "jacobian_apply", 2: "residual"}
+    if not a.thermal_only:
+        names[1] = "visco_update"
+    for kid, name in names.items():
+        ms = C.c_double()
+        by = C.c_double()
+        N.check(lib.tv_time_kernel(ctx, kid, a.kernel_reps, C.byref(ms)), ctx)
+        N.check(lib.tv_kernel_bytes(ctx, kid, C.byref(by)), ctx)
+        kern[name] = {"ms": ms.value, "bytes": by.value, "GBps": by.value / (ms.value * 1e-3) / 1e9}
+
+    dom = kern["pcg_matvec_fused"]
+    traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", f"pmc_matvec_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
+    if os.path.exists(pmc_file):
+        with open(pmc_file) as fh:
+            traffic = json.load(fh).get("hbm_bytes_per_launch")
+    roofline = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)",
+                "bytes_per_launch": dom["bytes"], "ms_per_launch": dom["ms"]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only)
+
+    prob.close()
+    if rank == 0:
+        value = n_global * a.steps / elapsed
+        out = {
+            "metric": "DOF-updates/sec (coupled thermo-visco time step, 3D CG1 hex)",
+            "value": value,
+            "unit": "DOF-updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (uniform T_0 = 800 K initial state, main.py parameters)",
+            "config": {"workload": f"C4 3D plate CG1/CG1 {nc[0]}x{nc[1]}x{nc[2]} hex "
+                                   f"({n_global} T-dofs), dt 0.1, "
+                                   + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
+                       "parallelism": f"mesh partition along y x{world} (RCCL halo + allreduce)",
+                       "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,
+                       "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},
+            "roofline": roofline,
+            "kernels": kern,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+
+
+def cpu_baseline(nc, L, mp, seconds, thermal_only):
+    """Time the oracle's C/OpenMP restatement (oracle/tv_cpu.c, a port of the same
+    algorithm) on a bounded sample of the same workload: the same mesh and
+    physics, as many full time steps as fit ~`seconds` (at least one)."""
+    try:
+        from oracle import tv_cpu
+    except Exception as e:  # the baseline is reported, never required
+        return {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    return tv_cpu.time_baseline(nc, L, mp, seconds, thermal_only)
+
+
+if __name__ == "__main__":
+    main()

@@ -65,6 +65,7 @@ struct Ctx {
   double* coef[3] = {nullptr, nullptr, nullptr};
   double* dgh[3] = {nullptr, nullptr, nullptr};
   int* map = nullptr;
+  int64_t* bnodes = nullptr;
   // PCG work (T space, local size)
   double *r = nullptr, *z = nullptr, *pA = nullptr, *pB = nullptr, *w = nullptr, *dinv = nullptr;
   double* partials = nullptr;
@@ -222,6 +223,23 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       g.coef[s] = c->coef[s];
     }
     const int64_t plane = (int64_t)g.n0 * g.n1;
+    if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
+      std::vector<int64_t> bn;
+      for (int k = g.k_begin; k < g.k_end; ++k)
+        for (int j = 0; j < g.n1; ++j)
+          for (int i = 0; i < g.n0; ++i) {
+            const bool on = (i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1]) ||
+                            (j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]) ||
+                            (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
+            if (on) bn.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
+          }
+      if (!bn.empty()) {
+        HIPC(hipMalloc(&c->bnodes, bn.size() * sizeof(int64_t)));
+        HIPC(hipMemcpy(c->bnodes, bn.data(), bn.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+      }
+      g.bnodes = c->bnodes;
+      g.n_bnodes = (int64_t)bn.size();
+    }
     c->nT = plane * g.n2;
     c->ownT_off = plane * g.k_begin;
     c->ownT_n = plane * (g.k_end - g.k_begin);
@@ -765,6 +783,7 @@ int tv_destroy(void* ctx) {
     if (c->dgh[s]) hipFree(c->dgh[s]);
   }
   if (c->map) hipFree(c->map);
+  if (c->bnodes) hipFree(c->bnodes);
   if (c->st) hipFree(c->st);
   if (c->h_st) hipHostFree(c->h_st);
   if (c->h_sums) hipHostFree(c->h_sums);
@@ -1005,6 +1024,12 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
     case 2:  // residual: read T, Tp, write F
       *bytes = 24.0 * n;
       break;
+    case 3:  // fused PCG matvec: read z, p_old, write p, w (T on boundary nodes only)
+      *bytes = 32.0 * n;
+      break;
+    case 4:  // PCG update: read p, w, dinv, dx, r; write dx, r, z
+      *bytes = 64.0 * n;
+      break;
     default:
       return c->fail(TV_ERR_ARG, "unknown kernel id");
   }
@@ -1015,11 +1040,23 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !ms || reps < 1) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  if (kernel == 3 || kernel == 4) {  // PCG kernels need a running solver state
+    PcgState h{};
+    h.beta = 1.0; h.betaold = 2.0; h.a = 1e-3; h.it = 1; h.done = 0; h.max_it = 1 << 30;
+    HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  }
   auto one = [&]() -> int {
+    int np = 0;
     switch (kernel) {
       case 0: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); return TV_OK;
       case 1: return visco(c, false);
       case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;
+      case 3: op_japply_fused(c, c->f[TV_F_T].ptr, &np); return TV_OK;
+      case 4:
+        launch_pcg_update(c->ownT_n, c->st, c->pA + c->ownT_off, c->pB + c->ownT_off, c->w + c->ownT_off,
+                          c->dinv + c->ownT_off, c->f[TV_F_DX].ptr + c->ownT_off, c->r + c->ownT_off,
+                          c->z + c->ownT_off, c->partials, c->stream);
+        return TV_OK;
       default: return c->fail(TV_ERR_ARG, "unknown kernel id");
     }
   };

@@ -24,6 +24,9 @@
 // wave_shl (no LDS, no barriers).  Lanes 1..62 produce output.  The four waves
 // of a workgroup take four consecutive j-rows so the j-neighbour rows are
 // shared in L1.
+#include <algorithm>
+#include <cstdlib>
+
 #include "tv_internal.h"
 
 namespace tv {
@@ -362,15 +365,320 @@ __global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __re
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// 2.5D marching kernel (3D grids): the production matvec / residual.
+//
+// A workgroup = kRows wavefronts = kRows consecutive "rows" (along storage axis
+// `raxis`) of one 64-wide x segment; it marches along the other axis (the
+// "plane" axis) through a chunk of planes.  Per plane every lane loads ONE
+// value of its own row (waves 0 / kRows-1 also load the two halo rows) into a
+// double-buffered LDS slab, reads its j-1 / j / j+1 neighbours back, folds the
+// row direction immediately (us = My.X, vs = Ky.X) and keeps (us, vs) of three
+// consecutive planes in registers (sliding window).  The x direction is taken
+// from the adjacent lanes with DPP.  HBM traffic ~ (kRows+2)/kRows x 8 B per
+// input array per node; L2 and LDS carry the rest; one barrier per plane.
+// Robin facets (<5% of nodes) gather their 3x3 patches directly.
+// ---------------------------------------------------------------------------
+constexpr int kRows = 16;      // rows (wavefronts) per marching workgroup
+constexpr int kMaxChunk = 254;  // planes per marching chunk (LDS coefficient stage)
+
+template <int MODE, bool FUSEP>
+__device__ double facet_direct(const CgGrid& g, int i, int j, int k, int ax, const double* __restrict__ T,
+                               const double* __restrict__ in0, const double* pold, double bcoef, bool first) {
+  const int t1 = (ax == 0) ? 1 : 0, t2 = (ax == 2) ? 1 : 2;
+  const int c[3] = {i, j, k};
+  const int n[3] = {g.n0, g.n1, g.n2};
+  const int64_t st[3] = {1, g.n0, (int64_t)g.n0 * g.n1};
+  const int64_t me = (int64_t)i + st[1] * j + st[2] * k;
+  double Tp[3][3], Pp[3][3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u)
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+      const int a = c[t1] + u - 1, b = c[t2] + v - 1;
+      const bool ok = a >= 0 && a < n[t1] && b >= 0 && b < n[t2];
+      const int64_t off = me + (int64_t)(u - 1) * st[t1] + (int64_t)(v - 1) * st[t2];
+      if (MODE == MODE_RES) {
+        Tp[u][v] = ok ? in0[off] : 0.0;
+        Pp[u][v] = 0.0;
+      } else {
+        Tp[u][v] = ok ? T[off] : 0.0;
+        double pv = ok ? in0[off] : 0.0;
+        if (FUSEP && ok && !first) pv = pv + bcoef * pold[off];
+        Pp[u][v] = pv;
+      }
+    }
+  const double* c1 = g.coef[t1] + (int64_t)c[t1] * C_NCOEF;
+  const double* c2 = g.coef[t2] + (int64_t)c[t2] * C_NCOEF;
+  return facet_sum<MODE, false, false, false>(g, c1[C_HLO], c1[C_HHI], c2[C_HLO], c2[C_HHI], Tp, Pp);
+}
+
+template <int MODE, bool FUSEP, int R>
+__global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* __restrict__ T,
+                                                        const double* __restrict__ in0, const double* in1,
+                                                        double* __restrict__ out, double* pout,
+                                                        const PcgState* __restrict__ st,
+                                                        double* __restrict__ partials, int nseg, int raxis,
+                                                        int qchunk) {
+  constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
+  __shared__ double lds[NA][2][R + 2][kWave];
+  __shared__ double red[R];
+  if (FUSEP && st->done) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = g.n0;
+  const int nR = (raxis == 1) ? g.n1 : g.n2;
+  const int nQ = (raxis == 1) ? g.n2 : g.n1;
+  const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
+  const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
+  const int qaxis = 3 - raxis;
+  const int nrb = (nR + R - 1) / R;
+  const int b = blockIdx.x;
+  const int seg = b % nseg;
+  const int t = b / nseg;
+  const int rb = t % nrb;
+  const int chunk = t / nrb;
+  const int r0 = rb * R;
+  const int r = r0 + wave;
+  const bool row_ok = r < nR;
+  const int q0 = chunk * qchunk;
+  const int q1 = min(q0 + qchunk, nQ);
+  const int i = seg * kSeg - 1 + lane;
+  const bool col_ok = (i >= 0) && (i < n0);
+  const bool writer = col_ok && lane >= 1 && lane <= kSeg;
+
+  double bcoef = 0.0;
+  bool first = false;
+  const double* pold = in1;
+  if (FUSEP) {
+    const int it = st->it;
+    first = (it == 0);
+    bcoef = first ? 0.0 : st->beta / st->betaold;
+    if (!(it & 1)) { pold = pout; pout = const_cast<double*>(in1); }
+  }
+  // ownership along storage axis 2 (partition axis)
+  const int kb = g.k_begin, ke = g.k_end;
+  const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
+
+  const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
+  const double My0 = cr[C_MLO], My1 = cr[C_MDI], My2 = cr[C_MUP];
+  const double Ky0 = cr[C_KLO], Ky1 = cr[C_KDI], Ky2 = cr[C_KUP];
+  const double* cx = g.coef[0] + (int64_t)(col_ok ? i : 0) * C_NCOEF;
+  const double Mx0 = cx[C_MLO], Mx1 = cx[C_MDI], Mx2 = cx[C_MUP];
+  const double Kx0 = cx[C_KLO], Kx1 = cx[C_KDI], Kx2 = cx[C_KUP];
+  const double da = g.dt_alpha;
+
+  // raw loads of one (row, plane) value (+ second array); the combination
+  // (p = z + b p_old, or T - Tp - dt f) happens one iteration later so the
+  // loads of plane L+1 are in flight while plane L is processed.
+  const double* __restrict__ second = (MODE == MODE_RES) ? in1 : pold;
+  constexpr bool TWO = (MODE == MODE_RES) || FUSEP;
+  // branch-free: out-of-range reads are redirected to element 0 and zeroed only
+  // when the value is consumed (one iteration later), so the loads of plane
+  // L+1 stay in flight across the barrier and the compute of plane L.
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < nR && L >= 0 && L < nQ; };
+  auto fetch = [&](int rr, int L, double& a0, double& a1) {
+    const int64_t idx = okf(rr, L) ? (int64_t)i + sR * rr + sQ * L : 0;
+    a0 = in0[idx];
+    a1 = TWO ? second[idx] : 0.0;
+  };
+  auto combine = [&](int rr, int L, double a0, double a1, double& v, double& vm) {
+    const bool ok = okf(rr, L);
+    a0 = ok ? a0 : 0.0;
+    a1 = (ok && !(FUSEP && first)) ? a1 : 0.0;
+    v = a0;
+    vm = 0.0;
+    if (MODE == MODE_RES) vm = a0 - a1 - g.dt_f;
+    if (FUSEP) v = first ? a0 : a0 + bcoef * a1;
+  };
+  // halo rows are loaded by waves 0 and R-1; the other waves re-load their own
+  // row (an L1 hit) so that every wave runs the same straight-line load stream
+  const bool halo = (wave == 0) || (wave == R - 1);
+  const int hrow = (wave == 0) ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
+  const int hslot = (wave == 0) ? 0 : R + 1;
+  // march-axis coefficients of the chunk, staged once in LDS (they are read by
+  // every wave each plane; vector loads of them would serialise on vmcnt)
+  __shared__ double cql[kMaxChunk + 2][6];
+  for (int e = threadIdx.x; e < (q1 - q0 + 2) * 6; e += R * kWave) {
+    const int qq = q0 - 1 + e / 6;
+    const int c = e % 6;
+    cql[e / 6][c] = (qq >= 0 && qq < nQ) ? g.coef[qaxis][(int64_t)qq * C_NCOEF + c] : 0.0;
+  }
+  __syncthreads();
+
+  // two register sets (A, B) alternate between "consumed now" and "prefetching
+  // the next plane" — a 2x unrolled loop, so no register copy has to wait for
+  // an in-flight load
+  double a0, a1, ah0, ah1, b0, b1, bh0, bh1;
+  fetch(r, q0 - 1, a0, a1);
+  fetch(hrow, q0 - 1, ah0, ah1);
+
+  double us_m = 0.0, us_c = 0.0, vs_m = 0.0, vs_c = 0.0, um_m = 0.0, um_c = 0.0;
+  double xc = 0.0;  // own-row value of the centre plane (p of the output node)
+  double dot = 0.0;
+  auto step = [&](int L, double c0, double c1, double h0, double h1) {
+    const int buf = L & 1;
+    double v, vm;
+    combine(r, L, c0, c1, v, vm);
+    if (FUSEP && writer && row_ok && L >= q0 && L < q1) pout[(int64_t)i + sR * r + sQ * L] = v;
+    lds[0][buf][wave + 1][lane] = v;
+    if (MODE == MODE_RES) lds[NA - 1][buf][wave + 1][lane] = vm;
+    if (halo) {
+      double hv, hvm;
+      combine(hrow, L, h0, h1, hv, hvm);
+      lds[0][buf][hslot][lane] = hv;
+      if (MODE == MODE_RES) lds[NA - 1][buf][hslot][lane] = hvm;
+    }
+    __syncthreads();
+    const double x0 = lds[0][buf][wave][lane], x1 = lds[0][buf][wave + 1][lane], x2 = lds[0][buf][wave + 2][lane];
+    const double us_p = My0 * x0 + My1 * x1 + My2 * x2;
+    const double vs_p = Ky0 * x0 + Ky1 * x1 + Ky2 * x2;
+    double um_p = us_p;
+    if (MODE == MODE_RES) {
+      const double m0 = lds[NA - 1][buf][wave][lane], m1 = lds[NA - 1][buf][wave + 1][lane],
+                   m2 = lds[NA - 1][buf][wave + 2][lane];
+      um_p = My0 * m0 + My1 * m1 + My2 * m2;
+    }
+    if (L >= q0 + 1) {
+      const int q = L - 1;
+      const double* cq = cql[q - q0 + 1];
+      const double Mz0 = cq[C_MLO], Mz1 = cq[C_MDI], Mz2 = cq[C_MUP];
+      const double Kz0 = cq[C_KLO], Kz1 = cq[C_KDI], Kz2 = cq[C_KUP];
+      const double S1 = Mz0 * (um_m + da * vs_m) + Mz1 * (um_c + da * vs_c) + Mz2 * (um_p + da * vs_p) +
+                        da * (Kz0 * us_m + Kz1 * us_c + Kz2 * us_p);
+      const double S2 = da * (Mz0 * us_m + Mz1 * us_c + Mz2 * us_p);
+      const double S1m = shr1(S1), S1p = shl1(S1), S2m = shr1(S2), S2p = shl1(S2);
+      const double y = Mx0 * S1m + Mx1 * S1 + Mx2 * S1p + Kx0 * S2m + Kx1 * S2 + Kx2 * S2p;
+      const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
+      if (writer && row_ok && row_owned && q_owned) {
+        // Robin facet terms of boundary nodes are added by k_cg_boundary
+        out[(int64_t)i + sR * r + sQ * q] = y;
+        if (MODE == MODE_JAC) dot += xc * y;
+      }
+    }
+    xc = x1;
+    us_m = us_c; us_c = us_p;
+    vs_m = vs_c; vs_c = vs_p;
+    um_m = um_c; um_c = um_p;
+  };
+  for (int L = q0 - 1; L <= q1; L += 2) {
+    fetch(r, L + 1, b0, b1);
+    fetch(hrow, L + 1, bh0, bh1);
+    step(L, a0, a1, ah0, ah1);
+    if (L + 1 > q1) break;
+    fetch(r, L + 2, a0, a1);
+    fetch(hrow, L + 2, ah0, ah1);
+    step(L + 1, b0, b1, bh0, bh1);
+  }
+  if (MODE == MODE_JAC && partials != nullptr) {
+    dot = wave_sum(dot);
+    if (lane == 0) red[wave] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < R; ++w) s += red[w];
+      partials[blockIdx.x] = s;
+    }
+  }
+}
+
+// Robin facet terms of the owned boundary nodes (list built at context
+// creation), added after the marching kernel: out[n] += dt * sum_f int_f ...,
+// and the matching p.w correction for the PCG dot product.  For the fused PCG
+// matvec the input is the freshly written p (buffer selected from st->it).
+template <int MODE, bool FUSEP>
+__global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t* __restrict__ bnodes, int64_t nb,
+                                                        const double* __restrict__ T, const double* in0,
+                                                        const double* pB, double* __restrict__ out,
+                                                        const PcgState* __restrict__ st,
+                                                        double* __restrict__ partials) {
+  __shared__ double red[kBlock / kWave];
+  if (FUSEP && st->done) return;
+  const double* x = in0;
+  if (FUSEP) x = (st->it & 1) ? pB : in0;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  double dot = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nb; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t n = bnodes[t];
+    const int i = (int)(n % g.n0), j = (int)((n / g.n0) % g.n1), k = (int)(n / plane);
+    const int c[3] = {i, j, k};
+    const int nn[3] = {g.n0, g.n1, g.n2};
+    double acc = 0.0;
+#pragma unroll 1
+    for (int a = 0; a < 3; ++a) {
+      if ((c[a] == 0 && g.bnd[a][0]) || (c[a] == nn[a] - 1 && g.bnd[a][1]))
+        acc += facet_direct<MODE, false>(g, i, j, k, a, T, x, nullptr, 0.0, true);
+    }
+    out[n] += acc;
+    if (MODE == MODE_JAC) dot += x[n] * acc;
+  }
+  if (MODE == MODE_JAC && partials != nullptr) {
+    dot = wave_sum(dot);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
 int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 
+static int march_rows() {
+  static int rows = 0;
+  if (!rows) {
+    const char* e = getenv("TVFEM_MARCH_ROWS");
+    rows = (e && atoi(e) == 8) ? 8 : kRows;
+  }
+  return rows;
+}
+
 struct Launch {
-  int blocks, nseg, kfirst, nplanes, wmode;
+  int blocks, nseg, kfirst, nplanes, wmode, rows;
+  int nparts;  // partial records written (JAC)
+  bool march;
+  int raxis, qchunk;
 };
 
+static int g_force_rows = -1;  // TVFEM_CG_KERNEL=rows selects the row kernel (testing)
+
+bool use_march(const CgGrid& g) {
+  if (g_force_rows < 0) {
+    const char* e = getenv("TVFEM_CG_KERNEL");
+    g_force_rows = (e && e[0] == 'r') ? 1 : 0;
+  }
+  return dim_of(g) == 3 && !g_force_rows;
+}
+
+int bnd_blocks(const CgGrid& g) {
+  int64_t b = (g.n_bnodes + kBlock - 1) / kBlock;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, 1024));
+}
+
 Launch plan(const CgGrid& g, bool ghosts) {
-  Launch L;
+  Launch L{};
   L.nseg = (g.n0 + kSeg - 1) / kSeg;
+  L.march = use_march(g);
+  if (L.march) {
+    // rows along the longer of storage axes 1/2, march along the shorter one;
+    // the kernel covers every local node (ghost planes included) so the fused
+    // PCG matvec refreshes p everywhere; outputs go to owned nodes only.
+    L.raxis = (g.n2 >= g.n1) ? 2 : 1;
+    L.rows = march_rows();
+    const int nR = (L.raxis == 1) ? g.n1 : g.n2;
+    const int nQ = (L.raxis == 1) ? g.n2 : g.n1;
+    const int nrb = (nR + L.rows - 1) / L.rows;
+    // enough workgroups to fill 256 CUs x ~4: split the march into chunks
+    int nchunks = 1;
+    while ((int64_t)L.nseg * nrb * nchunks < 512 && nQ / (nchunks * 2) >= 12) nchunks *= 2;
+    while ((nQ + nchunks - 1) / nchunks > kMaxChunk) ++nchunks;
+    L.qchunk = (nQ + nchunks - 1) / nchunks;
+    nchunks = (nQ + L.qchunk - 1) / L.qchunk;
+    L.blocks = L.nseg * nrb * nchunks;
+    L.nparts = L.blocks + (g.n_bnodes > 0 ? bnd_blocks(g) : 0);
+    return L;
+  }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
   L.nplanes = (g.k_end - g.k_begin) + (ghosts ? g.g_lo + g.g_hi : 0);
   L.wmode = (g.n1 >= 4) ? 0 : 1;
@@ -380,6 +688,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
     const int64_t waves = (int64_t)L.nseg * g.n1 * L.nplanes;
     L.blocks = (int)((waves + 3) / 4);
   }
+  L.nparts = L.blocks;
   return L;
 }
 
@@ -388,6 +697,20 @@ void launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
                  double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s) {
   const Launch L = plan(g, ghosts);
   if (L.blocks <= 0) return;
+  if (L.march) {
+    if (L.rows == 8)
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8>), dim3(L.blocks), dim3(8 * kWave), 0, s, g, T, in0, in1, out,
+                         pout, st, partials, L.nseg, L.raxis, L.qchunk);
+    else
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16>), dim3(L.blocks), dim3(16 * kWave), 0, s, g, T, in0, in1, out,
+                         pout, st, partials, L.nseg, L.raxis, L.qchunk);
+    if (g.n_bnodes > 0) {
+      hipLaunchKernelGGL((k_cg_boundary<MODE, FUSEP>), dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, g.bnodes,
+                         g.n_bnodes, T, FUSEP ? in1 : in0, pout, out, st,
+                         partials ? partials + L.blocks : nullptr);
+    }
+    return;
+  }
   switch (dim_of(g)) {
     case 1:
       hipLaunchKernelGGL((k_cg_rows<1, MODE, FUSEP>), dim3(L.blocks), dim3(kBlock), 0, s, g, T, in0, in1, out,
@@ -405,7 +728,7 @@ void launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
 
 }  // namespace
 
-int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).blocks; }
+int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }
 
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
   launch_rows<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, false, s);
@@ -414,7 +737,7 @@ void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, doub
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s) {
   launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, nullptr, partials, false, s);
-  if (n_partials) *n_partials = plan(g, false).blocks;
+  if (n_partials) *n_partials = plan(g, false).nparts;
 }
 
 void launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
@@ -423,7 +746,7 @@ void launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, d
   // neighbour values of p_new are recomputed from z and p_old; p_new goes to the
   // other buffer of the pair (selected on device from st->it).
   launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s);
-  if (n_partials) *n_partials = plan(g, true).blocks;
+  if (n_partials) *n_partials = plan(g, true).nparts;
 }
 
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {

@@ -34,6 +34,8 @@ struct CgGrid {
   double dt, dt_alpha, dt_f;  // dt, dt*alpha, dt*f
   double a_rad, a_conv;       // 0.001*sigma*epsilon, 0.001*htc
   double T_amb, T_amb4;
+  const int64_t* bnodes;      // owned nodes on physical boundary faces (3D marching path)
+  int64_t n_bnodes;
 };
 
 // Grid of the DG1 temperature space: cells per storage axis; dof layout is

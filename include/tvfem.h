@@ -189,8 +189,9 @@ int tv_halo_exchange(void* ctx, int field);
 
 /* ---- measurement ------------------------------------------------------------ */
 /* time `reps` launches of one hot kernel on the context stream with HIP events;
- * kernel: 0 = CG Jacobian apply (matvec), 1 = fused viscoelastic update,
- * 2 = residual.  Writes the mean duration per launch in ms. */
+ * kernel: 0 = Jacobian apply (matvec), 1 = fused viscoelastic update,
+ * 2 = residual, 3 = fused PCG matvec (p <- z + b p; w <- J p; p.w),
+ * 4 = PCG vector update.  Writes the mean duration per launch in ms. */
 int tv_time_kernel(void* ctx, int kernel, int reps, double* ms_per_launch);
 /* algorithmic bytes moved by one launch of `kernel` */
 int tv_kernel_bytes(void* ctx, int kernel, double* bytes);

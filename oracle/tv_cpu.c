@@ -1,0 +1,398 @@
+/*
+ * CPU ORACLE (C / OpenMP port) — test infrastructure only.
+ *
+ * A C restatement of the reference time step of pzimbrod/fem-glass-tempering
+ * for structured 3D CG1 hexahedral plates (rectilinear grids), used as the
+ * timed CPU baseline of bench.py ("kind": "port") and as a second CPU check.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+ * it; the product path never links it.
+ *
+ * Restates (file:line under /root/reference):
+ *   residual F and Jacobian of ThermoViscoProblem.py:293-306 (CG branch),
+ *   dolfinx NewtonSolver "incremental" (ThermoViscoProblem.py:334-337),
+ *   PETSc KSPCG (:343) with a Jacobi preconditioner in place of GAMG (:344),
+ *   the viscoelastic expressions ViscoelasticModel.py:100-228 in the call order
+ *   of ThermoViscoProblem.py:393-595 (state fields only).
+ * Parity: unpinned against dolfinx (see oracle/tv_oracle.py); checked against
+ * the numpy oracle in tests/test_cpu_port.py.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+enum { MLO, MDI, MUP, KLO, KDI, KUP, HLO, HHI, NC };
+
+typedef struct {
+  int n[3];
+  long long N;
+  double* c[3];
+  double dt, dta, dtf, arad, aconv, Ta, Ta4;
+  /* visco constants */
+  double HoR, iTb, as_, dal;
+  double lm[6], mn[6], lg[6], gn[6], lk[6], kn[6];
+  /* state */
+  double *T, *Tp, *Tf, *Tfp, *phi, *xi, *st, *sg, *sig;
+  /* work */
+  double *r, *z, *p, *w, *dx, *dinv;
+  int last_newton, last_krylov;
+} tvcpu;
+
+static const double GX[3] = {0.11270166537925831148, 0.5, 0.88729833462074168852};
+static const double GW[3] = {5.0 / 18.0, 8.0 / 18.0, 5.0 / 18.0};
+
+static double gfun(const tvcpu* h, double T) {
+  double T2 = T * T;
+  return h->arad * (T2 * T2 - h->Ta4) + h->aconv * (T - h->Ta);
+}
+static double dgfun(const tvcpu* h, double T) { return h->arad * 4.0 * (T * T * T) + h->aconv; }
+
+static void coefs(const double* X, int n, double* out) {
+  for (int i = 0; i < n; ++i) {
+    double* c = out + (size_t)i * NC;
+    double hlo = i > 0 ? X[i] - X[i - 1] : 0.0, hhi = i < n - 1 ? X[i + 1] - X[i] : 0.0;
+    c[MLO] = hlo / 6.0; c[MDI] = hlo / 3.0 + hhi / 3.0; c[MUP] = hhi / 6.0;
+    c[KLO] = hlo > 0 ? -1.0 / hlo : 0.0;
+    c[KDI] = (hlo > 0 ? 1.0 / hlo : 0.0) + (hhi > 0 ? 1.0 / hhi : 0.0);
+    c[KUP] = hhi > 0 ? -1.0 / hhi : 0.0;
+    c[HLO] = hlo; c[HHI] = hhi;
+  }
+}
+
+/* facet integral around a boundary node; patches indexed [u+1][v+1] over the
+ * face's two tangential axes. mode 0: g(T) phi ; 1: g'(T) phi p ; 2: g'(T) phi^2 */
+static double facet(const tvcpu* h, int mode, const double* c1, const double* c2, double Tp[3][3], double Pp[3][3]) {
+  double acc = 0.0;
+  for (int s1 = 0; s1 < 2; ++s1) {
+    double h1 = s1 ? c1[HHI] : c1[HLO];
+    if (!(h1 > 0)) continue;
+    int o1 = s1 ? 1 : -1;
+    for (int s2 = 0; s2 < 2; ++s2) {
+      double h2 = s2 ? c2[HHI] : c2[HLO];
+      if (!(h2 > 0)) continue;
+      int o2 = s2 ? 1 : -1;
+      for (int q1 = 0; q1 < 3; ++q1) {
+        double pc1 = s1 ? 1.0 - GX[q1] : GX[q1], po1 = 1.0 - pc1;
+        for (int q2 = 0; q2 < 3; ++q2) {
+          double pc2 = s2 ? 1.0 - GX[q2] : GX[q2], po2 = 1.0 - pc2;
+          double w = GW[q1] * h1 * GW[q2] * h2, phi = pc1 * pc2;
+          double Th = phi * Tp[1][1] + po1 * pc2 * Tp[1 + o1][1] + pc1 * po2 * Tp[1][1 + o2] + po1 * po2 * Tp[1 + o1][1 + o2];
+          if (mode == 0) acc += w * gfun(h, Th) * phi;
+          else if (mode == 2) acc += w * dgfun(h, Th) * phi * phi;
+          else {
+            double Ph = phi * Pp[1][1] + po1 * pc2 * Pp[1 + o1][1] + pc1 * po2 * Pp[1][1 + o2] + po1 * po2 * Pp[1 + o1][1 + o2];
+            acc += w * dgfun(h, Th) * phi * Ph;
+          }
+        }
+      }
+    }
+  }
+  return h->dt * acc;
+}
+
+#define IDX(i, j, k) ((long long)(i) + (long long)n0 * ((j) + (long long)n1 * (k)))
+
+static double at(const double* v, int n0, int n1, int n2, int i, int j, int k) {
+  if (i < 0 || j < 0 || k < 0 || i >= n0 || j >= n1 || k >= n2) return 0.0;
+  return v[IDX(i, j, k)];
+}
+
+/* mode 0: y = F(T; Tp) ; mode 1: y = J(T) x */
+static void apply(tvcpu* h, int mode, const double* x, double* y) {
+  const int n0 = h->n[0], n1 = h->n[1], n2 = h->n[2];
+  const double* T = h->T;
+  const double* Tp = h->Tp;
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int k = 0; k < n2; ++k)
+    for (int j = 0; j < n1; ++j) {
+      const double *cy = h->c[1] + (size_t)j * NC, *cz = h->c[2] + (size_t)k * NC;
+      for (int i = 0; i < n0; ++i) {
+        const double* cx = h->c[0] + (size_t)i * NC;
+        double S1[3], S2[3];
+        for (int a = -1; a <= 1; ++a) {
+          double s1 = 0.0, s2 = 0.0;
+          for (int c = -1; c <= 1; ++c) {
+            double us = 0.0, vs = 0.0, um = 0.0;
+            for (int b = -1; b <= 1; ++b) {
+              double xs = mode == 0 ? at(T, n0, n1, n2, i + a, j + b, k + c) : at(x, n0, n1, n2, i + a, j + b, k + c);
+              us += cy[MDI + b] * xs;
+              vs += cy[KDI + b] * xs;
+              if (mode == 0) {
+                int ok = !(i + a < 0 || j + b < 0 || k + c < 0 || i + a >= n0 || j + b >= n1 || k + c >= n2);
+                double m = ok ? xs - at(Tp, n0, n1, n2, i + a, j + b, k + c) - h->dtf : 0.0;
+                um += cy[MDI + b] * m;
+              }
+            }
+            if (mode != 0) um = us;
+            s1 += cz[MDI + c] * (um + h->dta * vs) + h->dta * cz[KDI + c] * us;
+            s2 += cz[MDI + c] * us;
+          }
+          S1[a + 1] = s1;
+          S2[a + 1] = h->dta * s2;
+        }
+        double v = 0.0;
+        for (int a = -1; a <= 1; ++a) v += cx[MDI + a] * S1[a + 1] + cx[KDI + a] * S2[a + 1];
+        /* facets */
+        double Tpch[3][3], Ppch[3][3];
+        const double* src = mode == 0 ? T : x;
+        if (k == 0 || k == n2 - 1) {
+          for (int u = 0; u < 3; ++u)
+            for (int w = 0; w < 3; ++w) {
+              Tpch[u][w] = at(T, n0, n1, n2, i + u - 1, j + w - 1, k);
+              Ppch[u][w] = at(src, n0, n1, n2, i + u - 1, j + w - 1, k);
+            }
+          v += facet(h, mode == 0 ? 0 : 1, cx, cy, Tpch, Ppch);
+        }
+        if (j == 0 || j == n1 - 1) {
+          for (int u = 0; u < 3; ++u)
+            for (int w = 0; w < 3; ++w) {
+              Tpch[u][w] = at(T, n0, n1, n2, i + u - 1, j, k + w - 1);
+              Ppch[u][w] = at(src, n0, n1, n2, i + u - 1, j, k + w - 1);
+            }
+          v += facet(h, mode == 0 ? 0 : 1, cx, cz, Tpch, Ppch);
+        }
+        if (i == 0 || i == n0 - 1) {
+          for (int u = 0; u < 3; ++u)
+            for (int w = 0; w < 3; ++w) {
+              Tpch[u][w] = at(T, n0, n1, n2, i, j + u - 1, k + w - 1);
+              Ppch[u][w] = at(src, n0, n1, n2, i, j + u - 1, k + w - 1);
+            }
+          v += facet(h, mode == 0 ? 0 : 1, cy, cz, Tpch, Ppch);
+        }
+        y[IDX(i, j, k)] = v;
+      }
+    }
+}
+
+static void diag_inv(tvcpu* h) {
+  const int n0 = h->n[0], n1 = h->n[1], n2 = h->n[2];
+  const double* T = h->T;
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int k = 0; k < n2; ++k)
+    for (int j = 0; j < n1; ++j)
+      for (int i = 0; i < n0; ++i) {
+        const double *cx = h->c[0] + (size_t)i * NC, *cy = h->c[1] + (size_t)j * NC, *cz = h->c[2] + (size_t)k * NC;
+        double d = cx[MDI] * cy[MDI] * cz[MDI] +
+                   h->dta * (cx[KDI] * cy[MDI] * cz[MDI] + cx[MDI] * cy[KDI] * cz[MDI] + cx[MDI] * cy[MDI] * cz[KDI]);
+        double P[3][3];
+        if (k == 0 || k == n2 - 1) {
+          for (int u = 0; u < 3; ++u) for (int w = 0; w < 3; ++w) P[u][w] = at(T, n0, n1, n2, i + u - 1, j + w - 1, k);
+          d += facet(h, 2, cx, cy, P, P);
+        }
+        if (j == 0 || j == n1 - 1) {
+          for (int u = 0; u < 3; ++u) for (int w = 0; w < 3; ++w) P[u][w] = at(T, n0, n1, n2, i + u - 1, j, k + w - 1);
+          d += facet(h, 2, cx, cz, P, P);
+        }
+        if (i == 0 || i == n0 - 1) {
+          for (int u = 0; u < 3; ++u) for (int w = 0; w < 3; ++w) P[u][w] = at(T, n0, n1, n2, i, j + u - 1, k + w - 1);
+          d += facet(h, 2, cy, cz, P, P);
+        }
+        h->dinv[IDX(i, j, k)] = 1.0 / d;
+      }
+}
+
+static int pcg(tvcpu* h, double rtol) {
+  const long long N = h->N;
+  double zz = 0, zr = 0;
+#pragma omp parallel for reduction(+ : zz, zr)
+  for (long long t = 0; t < N; ++t) {
+    h->z[t] = h->dinv[t] * h->r[t];
+    h->dx[t] = 0.0;
+    zz += h->z[t] * h->z[t];
+    zr += h->z[t] * h->r[t];
+  }
+  double dp = sqrt(zz), ttol = fmax(rtol * dp, 1e-50), rnorm0 = dp;
+  if (dp <= ttol) return 0;
+  double beta = zr, betaold = 1.0, dpiold = 0.0;
+  for (int it = 0; it < 10000; ++it) {
+    double b = it ? beta / betaold : 0.0;
+#pragma omp parallel for
+    for (long long t = 0; t < N; ++t) h->p[t] = it ? h->z[t] + b * h->p[t] : h->z[t];
+    apply(h, 1, h->p, h->w);
+    double dpi = 0;
+#pragma omp parallel for reduction(+ : dpi)
+    for (long long t = 0; t < N; ++t) dpi += h->p[t] * h->w[t];
+    if (dpi == 0.0 || (it > 0 && (dpi > 0) != (dpiold > 0))) return -it - 1;
+    dpiold = dpi;
+    betaold = beta;
+    double a = beta / dpi;
+    zz = 0; zr = 0;
+#pragma omp parallel for reduction(+ : zz, zr)
+    for (long long t = 0; t < N; ++t) {
+      h->dx[t] += a * h->p[t];
+      h->r[t] -= a * h->w[t];
+      h->z[t] = h->dinv[t] * h->r[t];
+      zz += h->z[t] * h->z[t];
+      zr += h->z[t] * h->r[t];
+    }
+    dp = sqrt(zz);
+    if (dp <= ttol) return it + 1;
+    if (dp >= 1e5 * rnorm0 || !isfinite(dp)) return -it - 1;
+    beta = zr;
+  }
+  return -10001;
+}
+
+static int newton(tvcpu* h) {
+  const long long N = h->N;
+  int its = 0, kits = 0, conv = 0;
+  double r0 = 0.0;
+  apply(h, 0, NULL, h->r);
+  while (!conv && its < 50) {
+    diag_inv(h);
+    int k = pcg(h, 1e-5);
+    if (k < 0) return -1;
+    kits += k;
+    double nn = 0;
+#pragma omp parallel for reduction(+ : nn)
+    for (long long t = 0; t < N; ++t) {
+      h->T[t] -= h->dx[t];
+      nn += h->dx[t] * h->dx[t];
+    }
+    double rn = sqrt(nn);
+    ++its;
+    if (its == 1) r0 = rn;
+    else conv = (rn / r0 < 1e-12) || (rn < 1e-10);
+    if (!conv) apply(h, 0, NULL, h->r);
+  }
+  h->last_newton = its;
+  h->last_krylov = kits;
+  return conv ? 0 : -2;
+}
+
+static double tE(double xi, double lam) {
+  double x = (-xi) / lam;
+  return (1.0 + 1.0 * x) + 0.5 * (x * x);
+}
+
+static void visco(tvcpu* h) {
+  const long long N = h->N;
+#pragma omp parallel for schedule(static)
+  for (long long t = 0; t < N; ++t) {
+    double T = h->T[t], Tp = h->Tp[t];
+    double phi = exp(h->HoR * (h->iTb - 1.0 / T));
+    double Tf = 0.0;
+    for (int i = 0; i < 6; ++i) {
+      double cur = (h->lm[i] * h->Tfp[i * N + t] + T * h->dt * phi) / (h->lm[i] + h->dt * phi);
+      h->Tfp[i * N + t] = cur;
+      Tf = Tf + h->mn[i] * cur;
+    }
+    h->Tf[t] = Tf;
+    double scal = h->as_ * (T - Tp) + h->dal * (Tf - Tf);
+    double tot[9], dev[9], tr = 0.0;
+    for (int q = 0; q < 9; ++q) tot[q] = -(((q / 3) == (q % 3) ? 1.0 : 0.0) * scal);
+    for (int i = 0; i < 3; ++i) tr = tr + tot[4 * i];
+    for (int q = 0; q < 9; ++q) dev[q] = tot[q] - ((1.0 / 3.0) * ((q / 3) == (q % 3) ? 1.0 : 0.0)) * tr;
+    double Tn = T + (T - Tp);
+    double phin = exp(h->HoR * (h->iTb - 1.0 / Tn));
+    double xi = (h->dt / 2) * (phin - phi);
+    h->phi[t] = phi;
+    h->xi[t] = xi;
+    double sig[9];
+    for (int n = 0; n < 6; ++n) {
+      double Eg = tE(xi, h->lg[n]), Ek = tE(xi, h->lk[n]);
+      for (int q = 0; q < 9; ++q) {
+        long long o = (long long)(n * 9 + q) * N + t;
+        double ds = (((2.0 * h->gn[n] * dev[q]) / xi) * h->lg[n]) * (1.0 - Eg);
+        double stv = h->st[o] * Eg;
+        double dsg = (((h->kn[n] * (tr * ((q / 3) == (q % 3) ? 1.0 : 0.0))) / xi) * h->lk[n]) * (1.0 - Ek);
+        double sgv = h->sg[o] * Ek;
+        h->st[o] = stv;
+        h->sg[o] = sgv;
+        double add = (ds + stv) + (dsg + sgv);
+        sig[q] = n == 0 ? add : sig[q] + add;
+      }
+    }
+    for (int q = 0; q < 9; ++q) h->sig[(long long)q * N + t] = sig[q];
+    h->Tp[t] = T;
+  }
+}
+
+/* ---------------- C entry points (ctypes) ---------------- */
+void* tvcpu_create(const int* ncells, const double* x, const double* y, const double* z, const double* params /* f eps sigma Ta T0 alpha htc H Tb Rg as al dt */,
+                   const double* tabs /* 36: m lm g lg k lk */) {
+  tvcpu* h = (tvcpu*)calloc(1, sizeof(tvcpu));
+  const double* X[3] = {x, y, z};
+  for (int a = 0; a < 3; ++a) {
+    h->n[a] = ncells[a] + 1;
+    h->c[a] = (double*)malloc(sizeof(double) * NC * h->n[a]);
+    coefs(X[a], h->n[a], h->c[a]);
+  }
+  h->N = (long long)h->n[0] * h->n[1] * h->n[2];
+  double f = params[0], eps = params[1], sg = params[2], Ta = params[3], T0 = params[4], al = params[5], htc = params[6];
+  h->dt = params[12];
+  h->dta = h->dt * al;
+  h->dtf = h->dt * f;
+  h->arad = 0.001 * (sg * eps);
+  h->aconv = 0.001 * htc;
+  h->Ta = Ta;
+  h->Ta4 = Ta * Ta * Ta * Ta;
+  h->HoR = params[7] / params[9];
+  h->iTb = 1.0 / params[8];
+  h->as_ = params[10];
+  h->dal = params[11] - params[10];
+  for (int i = 0; i < 6; ++i) {
+    h->mn[i] = tabs[i]; h->lm[i] = tabs[6 + i]; h->gn[i] = tabs[12 + i];
+    h->lg[i] = tabs[18 + i]; h->kn[i] = tabs[24 + i]; h->lk[i] = tabs[30 + i];
+  }
+  const long long N = h->N;
+  double** bufs[] = {&h->T, &h->Tp, &h->Tf, &h->phi, &h->xi, &h->r, &h->z, &h->p, &h->w, &h->dx, &h->dinv};
+  for (size_t q = 0; q < sizeof(bufs) / sizeof(bufs[0]); ++q) *bufs[q] = (double*)calloc((size_t)N, sizeof(double));
+  h->Tfp = (double*)calloc((size_t)N * 6, sizeof(double));
+  h->st = (double*)calloc((size_t)N * 54, sizeof(double));
+  h->sg = (double*)calloc((size_t)N * 54, sizeof(double));
+  h->sig = (double*)calloc((size_t)N * 9, sizeof(double));
+#pragma omp parallel for
+  for (long long t = 0; t < N; ++t) {
+    h->T[t] = T0; h->Tp[t] = T0; h->Tf[t] = T0;
+    for (int i = 0; i < 6; ++i) h->Tfp[i * N + t] = T0;
+  }
+  return h;
+}
+
+int tvcpu_step(void* hp, int thermal_only, int* newton_its, int* krylov_its) {
+  tvcpu* h = (tvcpu*)hp;
+  int rc = newton(h);
+  if (rc) return rc;
+  if (!thermal_only) visco(h);
+  else memcpy(h->Tp, h->T, sizeof(double) * (size_t)h->N);
+  if (newton_its) *newton_its = h->last_newton;
+  if (krylov_its) *krylov_its = h->last_krylov;
+  return 0;
+}
+
+long long tvcpu_num_dofs(void* hp) { return ((tvcpu*)hp)->N; }
+
+void tvcpu_get(void* hp, int which, double* out) {
+  tvcpu* h = (tvcpu*)hp;
+  const long long N = h->N;
+  switch (which) {
+    case 0: memcpy(out, h->T, sizeof(double) * N); break;
+    case 1: memcpy(out, h->phi, sizeof(double) * N); break;
+    case 2: memcpy(out, h->xi, sizeof(double) * N); break;
+    case 3: memcpy(out, h->Tf, sizeof(double) * N); break;
+    case 4: /* sigma, interleaved dof*9+q */
+      for (long long t = 0; t < N; ++t)
+        for (int q = 0; q < 9; ++q) out[t * 9 + q] = h->sig[(long long)q * N + t];
+      break;
+  }
+}
+
+int tvcpu_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+void tvcpu_destroy(void* hp) {
+  tvcpu* h = (tvcpu*)hp;
+  if (!h) return;
+  double* bufs[] = {h->T, h->Tp, h->Tf, h->phi, h->xi, h->r, h->z, h->p, h->w, h->dx, h->dinv, h->Tfp, h->st, h->sg, h->sig,
+                    h->c[0], h->c[1], h->c[2]};
+  for (size_t q = 0; q < sizeof(bufs) / sizeof(bufs[0]); ++q) free(bufs[q]);
+  free(h);
+}
