@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="rccl (production) or host-staged gloo transport (rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -75,17 +77,19 @@ def main():
         "alpha_solid": 9.10e-6, "alpha_liquid": 25.10e-6, "Tf_init": 873.0,
     }  # main.py:29-55
     cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
-    prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=local_rank, materialize=False,
+    device = local_rank
+    if a.comm == "host":  # rehearsal of several ranks on fewer GPUs (host-staged transport)
+        import torch
+        device = local_rank % max(1, torch.cuda.device_count())
+    prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
                               n_parts=world, part=rank, part_axis=1, verbose=False)
     lib, ctx = prob._lib, prob._ctx
     if world > 1:
-        idsz = lib.tv_comm_unique_id_size()
-        buf = C.create_string_buffer(idsz)
-        if rank == 0:
-            N.check(lib.tv_comm_get_unique_id(buf))
-        obj = [buf.raw if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        N.check(lib.tv_comm_init(ctx, C.c_char_p(obj[0]), world, rank), ctx)
+        from tvfem.parallel import init_host_comm, init_rccl
+        if a.comm == "host":
+            init_host_comm(prob, rank, world, dist)
+        else:
+            init_rccl(prob, rank, world, dist)
     prob.setup()
     n_owned, _ = prob.num_dofs(0)
     n_global = int(np.prod([n + 1 for n in nc]))
@@ -161,7 +165,8 @@ def main():
             "config": {"workload": f"C4 3D plate CG1/CG1 {nc[0]}x{nc[1]}x{nc[2]} hex "
                                    f"({n_global} T-dofs), dt 0.1, "
                                    + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
-                       "parallelism": f"mesh partition along y x{world} (RCCL halo + allreduce)",
+                       "parallelism": f"mesh partition along y x{world} ("
+                                      + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")",
                        "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},
             "roofline": roofline,

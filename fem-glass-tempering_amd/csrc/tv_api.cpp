@@ -66,19 +66,27 @@ struct Ctx {
   double* dgh[3] = {nullptr, nullptr, nullptr};
   int* map = nullptr;
   int64_t* bnodes = nullptr;
+  int64_t* enodes = nullptr;
+  double* bst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   // PCG work (T space, local size)
   double *r = nullptr, *z = nullptr, *pA = nullptr, *pB = nullptr, *w = nullptr, *dinv = nullptr;
   double* partials = nullptr;
   int n_partials_cap = 0;
   double* sums = nullptr;
+  unsigned* counters = nullptr;  // arrival counters of the in-kernel reduction tails
   PcgState* st = nullptr;
   PcgState* h_st = nullptr;  // pinned
   double* h_sums = nullptr;  // pinned
   double* scratch = nullptr;  // transfer scratch
   size_t scratch_bytes = 0;
-  // comm
+  // comm: RCCL (production) or host-staged callbacks (testing several ranks on one GPU)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  tv_host_allreduce_fn host_allreduce = nullptr;
+  tv_host_sendrecv_fn host_sendrecv = nullptr;
+  void* host_user = nullptr;
+  double* h_halo = nullptr;  // pinned staging: 2 send + 2 recv planes
+  size_t h_halo_n = 0;
   // stats
   int last_newton = 0, last_krylov = 0;
   double last_dx = 0.0;
@@ -158,6 +166,29 @@ static void alias_field(Ctx* c, int id, int target) {
   c->f[id].alloc = false;
 }
 
+// storage axes: 0 = x (fastest); 2 = partition axis (slowest); 1 = the remaining
+// axis (or degenerate).  Returns false for an invalid part_axis.
+static bool storage_perm(const tv_mesh_desc* m, int perm[3]) {
+  const int d = m->dim;
+  if (d == 1) {
+    perm[0] = 0; perm[1] = -1; perm[2] = -1;
+  } else if (d == 2) {
+    perm[0] = 0; perm[1] = -1; perm[2] = 1;
+  } else {
+    int pa = m->part_axis;
+    if (pa < 0) pa = (m->n_cells[1] >= m->n_cells[2]) ? 1 : 2;
+    if (pa != 1 && pa != 2) return false;
+    perm[0] = 0; perm[2] = pa; perm[1] = (pa == 1) ? 2 : 1;
+  }
+  return true;
+}
+
+// owned node planes [b0, b1) of partition p of P along the slowest storage axis
+static void part_planes(int N2, int P, int p, int* b0, int* b1) {
+  *b0 = (int)((int64_t)N2 * p / P);
+  *b1 = (int)((int64_t)N2 * (p + 1) / P);
+}
+
 static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   const int d = m->dim;
   if (d < 1 || d > 3) return c->fail(TV_ERR_ARG, "mesh dim must be 1..3");
@@ -171,17 +202,7 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       if (!(c->coords[a][i + 1] > c->coords[a][i]))
         return c->fail(TV_ERR_ARG, "node coordinates must be strictly increasing");
   }
-  // storage axes: 0 = x; 2 = partition axis; 1 = remaining (or degenerate)
-  if (d == 1) {
-    c->perm[0] = 0; c->perm[1] = -1; c->perm[2] = -1;
-  } else if (d == 2) {
-    c->perm[0] = 0; c->perm[1] = -1; c->perm[2] = 1;
-  } else {
-    int pa = m->part_axis;
-    if (pa < 0) pa = (m->n_cells[1] >= m->n_cells[2]) ? 1 : 2;
-    if (pa != 1 && pa != 2) return c->fail(TV_ERR_ARG, "part_axis must be 1 (y) or 2 (z) for 3D meshes");
-    c->perm[0] = 0; c->perm[2] = pa; c->perm[1] = (pa == 1) ? 2 : 1;
-  }
+  if (!storage_perm(m, c->perm)) return c->fail(TV_ERR_ARG, "part_axis must be 1 (y) or 2 (z) for 3D meshes");
   c->n_parts = std::max(1, m->n_parts);
   c->part = m->part;
   if (c->part < 0 || c->part >= c->n_parts) return c->fail(TV_ERR_ARG, "part out of range");
@@ -195,7 +216,8 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   if (c->fam_T == TV_CG) {
     const int N2 = c->Nnode_glob[2];
     const int P = c->n_parts, p = c->part;
-    const int b0 = (int)((int64_t)N2 * p / P), b1 = (int)((int64_t)N2 * (p + 1) / P);
+    int b0, b1;
+    part_planes(N2, P, p, &b0, &b1);
     if (b1 - b0 < 1) return c->fail(TV_ERR_ARG, "too many partitions for the mesh");
     c->plane_begin = b0;
     c->plane_end = b1;
@@ -224,7 +246,7 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     }
     const int64_t plane = (int64_t)g.n0 * g.n1;
     if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
-      std::vector<int64_t> bn;
+      std::vector<int64_t> bn, en;
       for (int k = g.k_begin; k < g.k_end; ++k)
         for (int j = 0; j < g.n1; ++j)
           for (int i = 0; i < g.n0; ++i) {
@@ -232,6 +254,10 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
                             (j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]) ||
                             (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
             if (on) bn.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
+            const int nf = ((i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1])) +
+                           ((j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1])) +
+                           ((k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]));
+            if (nf > 1) en.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
           }
       if (!bn.empty()) {
         HIPC(hipMalloc(&c->bnodes, bn.size() * sizeof(int64_t)));
@@ -239,6 +265,27 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       }
       g.bnodes = c->bnodes;
       g.n_bnodes = (int64_t)bn.size();
+      if (!en.empty()) {
+        HIPC(hipMalloc(&c->enodes, en.size() * sizeof(int64_t)));
+        HIPC(hipMemcpy(c->enodes, en.data(), en.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+      }
+      g.enodes = c->enodes;
+      g.n_enodes = (int64_t)en.size();
+      // facet-Jacobian stencil storage for every physical boundary face
+      const int nn[3] = {g.n0, g.n1, g.n2};
+      for (int f = 0; f < 6; ++f) {
+        const int ax = f >> 1, side = f & 1;
+        g.bst[f] = nullptr;
+        if (!g.bnd[ax][side]) continue;
+        const int t1 = (ax == 0) ? 1 : 0, t2 = (ax == 2) ? 1 : 2;
+        g.bst_n[f] = nn[t1];
+        g.bst_m[f] = nn[t2];
+        const size_t bytes = sizeof(double) * 9 * (size_t)nn[t1] * nn[t2];
+        HIPC(hipMalloc(&c->bst[f], bytes));
+        HIPC(hipMemsetAsync(c->bst[f], 0, bytes, c->stream));
+        g.bst[f] = c->bst[f];
+      }
+      g.bst_ok = 1;
     }
     c->nT = plane * g.n2;
     c->ownT_off = plane * g.k_begin;
@@ -379,6 +426,8 @@ static int setup_fields(Ctx* c) {
   c->n_partials_cap = np;
   HIPC(hipMalloc(&c->partials, sizeof(double) * 2 * (size_t)np));
   HIPC(hipMalloc(&c->sums, sizeof(double) * 8));
+  HIPC(hipMalloc(&c->counters, sizeof(unsigned) * 4));
+  HIPC(hipMemsetAsync(c->counters, 0, sizeof(unsigned) * 4, c->stream));
   HIPC(hipMalloc(&c->st, sizeof(PcgState)));
   HIPC(hipHostMalloc(&c->h_st, sizeof(PcgState)));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
@@ -442,8 +491,31 @@ static int transfer(Ctx* c, int field, double* host, size_t n, int dir) {
 // --------------------------------------------------------------------------------------
 // communication
 // --------------------------------------------------------------------------------------
+static bool multi_rank(const Ctx* c) { return c->nranks > 1 && (c->comm || c->host_sendrecv); }
+
+static int halo_host(Ctx* c, double* v) {
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  double* s_lo = c->h_halo;
+  double* s_hi = c->h_halo + plane;
+  double* r_lo = c->h_halo + 2 * plane;
+  double* r_hi = c->h_halo + 3 * plane;
+  if (g.g_lo) HIPC(hipMemcpyAsync(s_lo, v + plane * g.k_begin, plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (g.g_hi) HIPC(hipMemcpyAsync(s_hi, v + plane * (g.k_end - 1), plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (g.g_lo && c->host_sendrecv(s_lo, (size_t)plane, c->rank - 1, r_lo, (size_t)plane, c->rank - 1, c->host_user))
+    return c->fail(TV_ERR_COMM, "host sendrecv failed");
+  if (g.g_hi && c->host_sendrecv(s_hi, (size_t)plane, c->rank + 1, r_hi, (size_t)plane, c->rank + 1, c->host_user))
+    return c->fail(TV_ERR_COMM, "host sendrecv failed");
+  if (g.g_lo) HIPC(hipMemcpyAsync(v, r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (g.g_hi) HIPC(hipMemcpyAsync(v + plane * g.k_end, r_hi, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
 static int halo(Ctx* c, double* v) {
-  if (!c->comm || c->nranks <= 1 || c->fam_T != TV_CG) return TV_OK;
+  if (!multi_rank(c) || c->fam_T != TV_CG) return TV_OK;
+  if (c->host_sendrecv) return halo_host(c, v);
   const CgGrid& g = c->cg;
   const int64_t plane = (int64_t)g.n0 * g.n1;
   NCCLC(ncclGroupStart());
@@ -460,14 +532,21 @@ static int halo(Ctx* c, double* v) {
 }
 
 static int allreduce(Ctx* c, double* v, int n) {
-  if (!c->comm || c->nranks <= 1) return TV_OK;
+  if (!multi_rank(c)) return TV_OK;
+  if (c->host_allreduce) {
+    HIPC(hipMemcpyAsync(c->h_sums + 4, v, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (c->host_allreduce(c->h_sums + 4, n, c->host_user)) return c->fail(TV_ERR_COMM, "host allreduce failed");
+    HIPC(hipMemcpyAsync(v, c->h_sums + 4, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return TV_OK;
+  }
   NCCLC(ncclAllReduce(v, v, n, ncclDouble, ncclSum, c->comm, c->stream));
   return TV_OK;
 }
 
 // reduce partial records -> (allreduce) -> scalar logic
 static int reduce_logic(Ctx* c, int n, int W, int kind, int check_done) {
-  if (!c->comm || c->nranks <= 1) {
+  if (!multi_rank(c)) {
     launch_reduce_logic(c->partials, n, W, c->sums, c->st, kind, check_done, c->stream);
   } else {
     launch_reduce_logic(c->partials, n, W, c->sums, c->st, 0, 0, c->stream);
@@ -485,18 +564,24 @@ static void op_residual(Ctx* c, const double* T, const double* Tp, double* F) {
   else launch_dg_residual(c->dg, T, Tp, F, c->stream);
 }
 static void op_diag(Ctx* c, const double* T, double* d, int invert) {
-  if (c->fam_T == TV_CG) launch_cg_diag(c->cg, T, d, invert, c->stream);
-  else launch_dg_diag(c->dg, T, d, invert, c->stream);
+  // Jacobian "assembly": diagonal (Jacobi PC) + facet stencils for J(T)
+  if (c->fam_T == TV_CG) {
+    launch_cg_diag(c->cg, T, d, invert, c->stream);
+    launch_cg_bstencil(c->cg, T, c->stream);
+  }
+  else {
+    launch_dg_diag(c->dg, T, d, invert, c->stream);
+  }
 }
 static void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
   if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
   else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
 }
-static void op_japply_fused(Ctx* c, const double* T, int* np) {
+static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr) {
   if (c->fam_T == TV_CG)
-    launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
-  else
-    launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
+    return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail);
+  launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
+  return false;
 }
 
 // --------------------------------------------------------------------------------------
@@ -504,12 +589,26 @@ static void op_japply_fused(Ctx* c, const double* T, int* np) {
 // --------------------------------------------------------------------------------------
 static int pcg_iteration(Ctx* c, const double* T) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
+  const bool multi = multi_rank(c);
+  // single GPU: the last-arriving workgroup of each launch reduces the partial
+  // records and runs the KSPCG scalar logic in-kernel (no separate reduce
+  // launch); multi-GPU: it only reduces, RCCL all-reduces, then the logic runs.
+  RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2};
   int np = 0;
-  op_japply_fused(c, T, &np);                 // p <- z + b p ; w <- J p ; partial p.w
-  if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
+  const bool fused1 = op_japply_fused(c, T, &np, &t1);  // p <- z + b p ; w <- J p ; p.w
+  if (!fused1) {
+    if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
+  } else if (multi) {
+    if (int e = allreduce(c, c->sums, 1)) return e;
+    launch_logic(c->st, c->sums, 2, c->stream);
+  }
+  RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
-                    c->r + off, c->z + off, c->partials, c->stream);
-  if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 3, 1)) return e;  // dp, beta, convergence
+                    c->r + off, c->z + off, c->partials, c->stream, &t2);
+  if (multi) {  // dp, beta, convergence
+    if (int e = allreduce(c, c->sums, 2)) return e;
+    launch_logic(c->st, c->sums, 3, c->stream);
+  }
   if (int e = halo(c, c->z)) return e;
   return TV_OK;
 }
@@ -769,6 +868,32 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
   return TV_OK;
 }
 
+int tv_partition_layout(const tv_mesh_desc* m, int64_t* out) {
+  if (!m || !out || m->dim < 1 || m->dim > 3 || m->n_parts < 1 || m->part < 0 || m->part >= m->n_parts) {
+    set_global_error("tv_partition_layout: invalid arguments");
+    return TV_ERR_ARG;
+  }
+  int perm[3];
+  if (!storage_perm(m, perm)) {
+    set_global_error("part_axis must be 1 (y) or 2 (z) for 3D meshes");
+    return TV_ERR_ARG;
+  }
+  int N[3];
+  for (int s = 0; s < 3; ++s) N[s] = (perm[s] < 0) ? 1 : m->n_cells[perm[s]] + 1;
+  int b0, b1;
+  part_planes(N[2], m->n_parts, m->part, &b0, &b1);
+  const int64_t plane = (int64_t)N[0] * N[1];
+  const int glo = m->part > 0, ghi = m->part < m->n_parts - 1;
+  out[0] = perm[0]; out[1] = perm[1]; out[2] = perm[2];
+  out[3] = N[0]; out[4] = N[1]; out[5] = N[2];
+  out[6] = b0; out[7] = b1;
+  out[8] = plane * b0;                          // global offset of the first owned dof
+  out[9] = plane * (b1 - b0);                   // owned dofs
+  out[10] = plane * ((b1 - b0) + glo + ghi);   // local dofs (owned + ghost planes)
+  out[11] = glo; out[12] = ghi;
+  return TV_OK;
+}
+
 int tv_destroy(void* ctx) {
   if (!ctx) return TV_OK;
   Ctx* c = static_cast<Ctx*>(ctx);
@@ -784,9 +909,14 @@ int tv_destroy(void* ctx) {
   }
   if (c->map) hipFree(c->map);
   if (c->bnodes) hipFree(c->bnodes);
+  if (c->enodes) hipFree(c->enodes);
+  for (int f = 0; f < 6; ++f)
+    if (c->bst[f]) hipFree(c->bst[f]);
   if (c->st) hipFree(c->st);
+  if (c->counters) hipFree(c->counters);
   if (c->h_st) hipHostFree(c->h_st);
   if (c->h_sums) hipHostFree(c->h_sums);
+  if (c->h_halo) hipHostFree(c->h_halo);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
@@ -916,6 +1046,7 @@ int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !x_dev || !y_dev) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  if (c->fam_T == TV_CG) launch_cg_bstencil(c->cg, c->f[TV_F_T].ptr, c->stream);  // J(T) facet stencils
   op_japply(c, c->f[TV_F_T].ptr, x_dev, y_dev, nullptr, nullptr);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));
@@ -990,6 +1121,28 @@ int tv_comm_init(void* ctx, const char* id, int n_ranks, int rank) {
   c->nranks = n_ranks;
   c->rank = rank;
   // bring ghost planes of the state up to date
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
+                      tv_host_sendrecv_fn sendrecv_fn, void* user) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !allreduce_fn || !sendrecv_fn) return TV_ERR_ARG;
+  if (n_ranks != c->n_parts || rank != c->part)
+    return c->fail(TV_ERR_ARG, "communicator size/rank must match the mesh partition (n_parts/part)");
+  hipSetDevice(c->device);
+  c->nranks = n_ranks;
+  c->rank = rank;
+  c->host_allreduce = allreduce_fn;
+  c->host_sendrecv = sendrecv_fn;
+  c->host_user = user;
+  if (c->fam_T == TV_CG) {
+    const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
+    HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)plane));
+  }
   if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
   if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
   HIPC(hipStreamSynchronize(c->stream));

@@ -27,7 +27,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "tv_internal.h"
+#include "tv_device.h"
 
 namespace tv {
 namespace {
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_rows(CgGrid g, const double* __re
     d = wave_sum(d);
     if (lane == 0) red[wave] = d;
     __syncthreads();
-    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
   }
 }
 
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
                                                         double* __restrict__ partials, int nseg, int raxis,
                                                         int qchunk) {
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
-  __shared__ double lds[NA][2][R + 2][kWave];
+  __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
   __shared__ double red[R];
   if (FUSEP && st->done) return;
   const int lane = threadIdx.x & (kWave - 1);
@@ -552,9 +552,10 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
       const double y = Mx0 * S1m + Mx1 * S1 + Mx2 * S1p + Kx0 * S2m + Kx1 * S2 + Kx2 * S2p;
       const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
       if (writer && row_ok && row_owned && q_owned) {
-        // Robin facet terms of boundary nodes are added by k_cg_boundary
-        out[(int64_t)i + sR * r + sQ * q] = y;
-        if (MODE == MODE_JAC) dot += xc * y;
+        // Robin facet terms: k_cg_bapply (Jacobian) / k_cg_boundary (residual)
+        const double yb = y;
+        out[(int64_t)i + sR * r + sQ * q] = yb;
+        if (MODE == MODE_JAC) dot += xc * yb;
       }
     }
     xc = x1;
@@ -562,14 +563,23 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
     vs_m = vs_c; vs_c = vs_p;
     um_m = um_c; um_c = um_p;
   };
-  for (int L = q0 - 1; L <= q1; L += 2) {
-    fetch(r, L + 1, b0, b1);
-    fetch(hrow, L + 1, bh0, bh1);
+  // prefetch depth 2: three register sets rotate (3x unrolled), so two planes
+  // of loads are in flight while a plane is combined, exchanged and computed
+  double c0_, c1_, ch0, ch1;
+  fetch(r, q0, b0, b1);
+  fetch(hrow, q0, bh0, bh1);
+  for (int L = q0 - 1; L <= q1; L += 3) {
+    fetch(r, L + 2, c0_, c1_);
+    fetch(hrow, L + 2, ch0, ch1);
     step(L, a0, a1, ah0, ah1);
     if (L + 1 > q1) break;
-    fetch(r, L + 2, a0, a1);
-    fetch(hrow, L + 2, ah0, ah1);
+    fetch(r, L + 3, a0, a1);
+    fetch(hrow, L + 3, ah0, ah1);
     step(L + 1, b0, b1, bh0, bh1);
+    if (L + 2 > q1) break;
+    fetch(r, L + 4, b0, b1);
+    fetch(hrow, L + 4, bh0, bh1);
+    step(L + 2, c0_, c1_, ch0, ch1);
   }
   if (MODE == MODE_JAC && partials != nullptr) {
     dot = wave_sum(dot);
@@ -579,7 +589,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
       double s = 0.0;
 #pragma unroll
       for (int w = 0; w < R; ++w) s += red[w];
-      partials[blockIdx.x] = s;
+      store_partial(&partials[blockIdx.x], s);
     }
   }
 }
@@ -619,8 +629,188 @@ __global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t*
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) red[wave] = dot;
     __syncthreads();
-    if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
   }
+}
+
+
+// Per-node 3x3 face stencils of the Robin facet Jacobian,
+//   B_I(u,v) = dt * sum_f int_f g'(T_h) phi_I phi_(u,v),
+// for every node of one physical boundary face (SoA: coefficient-major), built
+// once per Newton iteration (T is fixed during the linear solve) and applied
+// by the marching kernel.  Tangential axes (t1 < t2) in storage order.
+__global__ __launch_bounds__(kBlock) void k_cg_bstencil(CgGrid g, int face, const double* __restrict__ T,
+                                                        double* __restrict__ B) {
+  const int a = face >> 1, side = face & 1;
+  const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+  const int n[3] = {g.n0, g.n1, g.n2};
+  const int64_t st[3] = {1, g.n0, (int64_t)g.n0 * g.n1};
+  const int64_t n2d = (int64_t)n[t1] * n[t2];
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n2d; t += (int64_t)gridDim.x * kBlock) {
+    int c[3];
+    c[t1] = (int)(t % n[t1]);
+    c[t2] = (int)(t / n[t1]);
+    c[a] = side ? n[a] - 1 : 0;
+    const int64_t me = (int64_t)c[0] + st[1] * c[1] + st[2] * c[2];
+    double Tp[3][3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const int x1 = c[t1] + u - 1, x2 = c[t2] + v - 1;
+        const bool ok = x1 >= 0 && x1 < n[t1] && x2 >= 0 && x2 < n[t2];
+        Tp[u][v] = ok ? T[me + (int64_t)(u - 1) * st[t1] + (int64_t)(v - 1) * st[t2]] : 0.0;
+      }
+    const double* c1 = g.coef[t1] + (int64_t)c[t1] * C_NCOEF;
+    const double* c2 = g.coef[t2] + (int64_t)c[t2] * C_NCOEF;
+    double Bl[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+#pragma unroll
+    for (int s1 = 0; s1 < 2; ++s1) {
+      const double h1 = s1 ? c1[C_HHI] : c1[C_HLO];
+      if (!(h1 > 0.0)) continue;
+      const int o1 = s1 ? 1 : -1;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const double h2 = s2 ? c2[C_HHI] : c2[C_HLO];
+        if (!(h2 > 0.0)) continue;
+        const int o2 = s2 ? 1 : -1;
+#pragma unroll
+        for (int q1 = 0; q1 < 3; ++q1) {
+          const double pc1 = s1 ? 1.0 - kGX[q1] : kGX[q1], po1 = 1.0 - pc1;
+#pragma unroll
+          for (int q2 = 0; q2 < 3; ++q2) {
+            const double pc2 = s2 ? 1.0 - kGX[q2] : kGX[q2], po2 = 1.0 - pc2;
+            const double phiI = pc1 * pc2;
+            const double Th = phiI * Tp[1][1] + po1 * pc2 * Tp[1 + o1][1] + pc1 * po2 * Tp[1][1 + o2] +
+                              po1 * po2 * Tp[1 + o1][1 + o2];
+            const double wg = kGW[q1] * h1 * kGW[q2] * h2 * dg_rad_conv(g, Th) * phiI;
+            Bl[1][1] += wg * phiI;
+            Bl[1 + o1][1] += wg * po1 * pc2;
+            Bl[1][1 + o2] += wg * pc1 * po2;
+            Bl[1 + o1][1 + o2] += wg * po1 * po2;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) B[(u * 3 + v) * n2d + t] = g.dt * Bl[u][v];
+  }
+}
+
+
+// Robin facet Jacobian of the boundary nodes from the precomputed face
+// stencils (k_cg_bstencil): out[n] += sum_faces sum_uv B_f(u,v)[n] x[n + ...],
+// plus the matching p.w correction, then (in the last-arriving workgroup) the
+// reduction tail of the whole matvec.  Face-major: workgroups [off[f],
+// off[f+1]) sweep face f (uniform face per workgroup: coefficient planes and
+// in-face neighbours are contiguous rows); nodes that lie on two or three
+// physical faces (edges, corners) are skipped there and summed by the last
+// segment (off[6], off[7]) from the edge list, so no node is written twice.
+struct FaceBlocks {
+  int off[8];
+};
+
+__device__ __forceinline__ int n_phys_faces(const CgGrid& g, const int (&c)[3], const int (&n)[3]) {
+  int k = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) k += ((c[a] == 0 && g.bnd[a][0]) || (c[a] == n[a] - 1 && g.bnd[a][1])) ? 1 : 0;
+  return k;
+}
+
+template <bool FUSEP>
+__global__ __launch_bounds__(kBlock) void k_cg_bapply(CgGrid g, const double* in0, const double* pB,
+                                                      double* __restrict__ out, const PcgState* __restrict__ st,
+                                                      double* __restrict__ partials, RedTail rt, int n_records,
+                                                      FaceBlocks fb) {
+  __shared__ double red[kBlock / kWave];
+  if (FUSEP && st->done) return;
+  const double* x = in0;
+  if (FUSEP) x = (st->it & 1) ? pB : in0;
+  const int n[3] = {g.n0, g.n1, g.n2};
+  const int64_t sst[3] = {1, g.n0, (int64_t)g.n0 * g.n1};
+  const int b = blockIdx.x;
+  int f = 0;
+  while (f < 7 && b >= fb.off[f + 1]) ++f;
+  const int nb = fb.off[f + 1] - fb.off[f];
+  const int lb = b - fb.off[f];
+  double dot = 0.0;
+  auto face_term = [&](int ff, const int (&c)[3], int64_t nd) {
+    const int a = ff >> 1;
+    const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+    const int64_t n2d = (int64_t)n[t1] * n[t2];
+    const int64_t ix = (int64_t)c[t1] + (int64_t)n[t1] * c[t2];
+    const double* B = g.bst[ff];
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const int a1 = c[t1] + u - 1, a2 = c[t2] + v - 1;
+        const bool ok = a1 >= 0 && a1 < n[t1] && a2 >= 0 && a2 < n[t2];
+        const int64_t o = ok ? nd + (int64_t)(u - 1) * sst[t1] + (int64_t)(v - 1) * sst[t2] : nd;
+        const double xv = x[o];
+        acc += B[(u * 3 + v) * n2d + ix] * (ok ? xv : 0.0);
+      }
+    return acc;
+  };
+  if (f < 6) {
+    const int a = f >> 1, side = f & 1;
+    const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+    const int64_t n2d = (int64_t)n[t1] * n[t2];
+    for (int64_t ix = (int64_t)lb * kBlock + threadIdx.x; ix < n2d; ix += (int64_t)nb * kBlock) {
+      int c[3];
+      c[t1] = (int)(ix % n[t1]);
+      c[t2] = (int)(ix / n[t1]);
+      c[a] = side ? n[a] - 1 : 0;
+      if (c[2] < g.k_begin || c[2] >= g.k_end) continue;  // ghost plane of the partition axis
+      if (n_phys_faces(g, c, n) > 1) continue;            // edge / corner: summed below
+      const int64_t nd = (int64_t)c[0] + sst[1] * c[1] + sst[2] * c[2];
+      const double acc = face_term(f, c, nd);
+      out[nd] += acc;
+      dot += x[nd] * acc;
+    }
+  } else {
+    for (int64_t t = (int64_t)lb * kBlock + threadIdx.x; t < g.n_enodes; t += (int64_t)nb * kBlock) {
+      const int64_t nd = g.enodes[t];
+      const int c[3] = {(int)(nd % n[0]), (int)((nd / n[0]) % n[1]), (int)(nd / sst[2])};
+      double acc = 0.0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int side = (c[a] == 0 && g.bnd[a][0]) ? 0 : ((c[a] == n[a] - 1 && g.bnd[a][1]) ? 1 : -1);
+        if (side >= 0) acc += face_term(2 * a + side, c, nd);
+      }
+      out[nd] += acc;
+      dot += x[nd] * acc;
+    }
+  }
+  if (partials != nullptr) {
+    dot = wave_sum(dot);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) red[wave] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
+    fused_reduce_tail<1>(rt, n_records);  // p.w of the marching launch + this one
+  }
+}
+
+FaceBlocks face_blocks(const CgGrid& g) {
+  FaceBlocks fb{};
+  const int n[3] = {g.n0, g.n1, g.n2};
+  int acc = 0;
+  for (int f = 0; f < 6; ++f) {
+    fb.off[f] = acc;
+    const int a = f >> 1;
+    if (!g.bst[f]) continue;
+    const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+    const int64_t n2d = (int64_t)n[t1] * n[t2];
+    acc += (int)std::min<int64_t>((n2d + kBlock - 1) / kBlock, 1024);
+  }
+  fb.off[6] = acc;
+  acc += (int)std::min<int64_t>((g.n_enodes + kBlock - 1) / kBlock, 256);
+  fb.off[7] = acc;
+  return fb;
 }
 
 int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
@@ -676,7 +866,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
     L.qchunk = (nQ + nchunks - 1) / nchunks;
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
     L.blocks = L.nseg * nrb * nchunks;
-    L.nparts = L.blocks + (g.n_bnodes > 0 ? bnd_blocks(g) : 0);
+    L.nparts = L.blocks + (g.n_bnodes > 0 ? std::max(bnd_blocks(g), (g.bst_ok ? face_blocks(g).off[7] : 0)) : 0);
     return L;
   }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
@@ -693,10 +883,11 @@ Launch plan(const CgGrid& g, bool ghosts) {
 }
 
 template <int MODE, bool FUSEP>
-void launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
-                 double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s) {
+bool launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
+                 double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s,
+                 const RedTail* tail = nullptr) {
   const Launch L = plan(g, ghosts);
-  if (L.blocks <= 0) return;
+  if (L.blocks <= 0) return false;
   if (L.march) {
     if (L.rows == 8)
       hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8>), dim3(L.blocks), dim3(8 * kWave), 0, s, g, T, in0, in1, out,
@@ -704,12 +895,22 @@ void launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     else
       hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16>), dim3(L.blocks), dim3(16 * kWave), 0, s, g, T, in0, in1, out,
                          pout, st, partials, L.nseg, L.raxis, L.qchunk);
-    if (g.n_bnodes > 0) {
+    if (g.n_bnodes > 0 && MODE == MODE_JAC && g.bst_ok) {
+      RedTail rt{};
+      if (tail && partials) rt = *tail;
+      const FaceBlocks fb = face_blocks(g);
+      if (fb.off[7] > 0) {
+        hipLaunchKernelGGL((k_cg_bapply<FUSEP>), dim3(fb.off[7]), dim3(kBlock), 0, s, g, FUSEP ? in1 : in0, pout,
+                           out, st, partials ? partials + L.blocks : nullptr, rt, L.nparts, fb);
+        return rt.counter != nullptr;
+      }
+      return false;
+    } else if (g.n_bnodes > 0) {
       hipLaunchKernelGGL((k_cg_boundary<MODE, FUSEP>), dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, g.bnodes,
                          g.n_bnodes, T, FUSEP ? in1 : in0, pout, out, st,
                          partials ? partials + L.blocks : nullptr);
     }
-    return;
+    return false;
   }
   switch (dim_of(g)) {
     case 1:
@@ -724,6 +925,7 @@ void launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
       hipLaunchKernelGGL((k_cg_rows<3, MODE, FUSEP>), dim3(L.blocks), dim3(kBlock), 0, s, g, T, in0, in1, out,
                          pout, st, partials, L.nseg, L.kfirst, L.nplanes, L.wmode);
   }
+  return false;
 }
 
 }  // namespace
@@ -740,13 +942,24 @@ void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double*
   if (n_partials) *n_partials = plan(g, false).nparts;
 }
 
-void launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
+bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
-                            hipStream_t s) {
+                            hipStream_t s, const RedTail* tail) {
   // neighbour values of p_new are recomputed from z and p_old; p_new goes to the
   // other buffer of the pair (selected on device from st->it).
-  launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s);
+  const bool fused = launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s, tail);
   if (n_partials) *n_partials = plan(g, true).nparts;
+  return fused;
+}
+
+void launch_cg_bstencil(const CgGrid& g, const double* T, hipStream_t s) {
+  if (!g.bst_ok) return;
+  for (int f = 0; f < 6; ++f) {
+    if (!g.bst[f]) continue;
+    const int64_t n2d = g.bst_n[f] * (int64_t)g.bst_m[f];
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n2d + kBlock - 1) / kBlock, 2048));
+    hipLaunchKernelGGL(k_cg_bstencil, dim3(blocks), dim3(kBlock), 0, s, g, f, T, g.bst[f]);
+  }
 }
 
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {

@@ -1,0 +1,139 @@
+// Device-side helpers shared by the kernels of libtvfem.so: wave / block
+// reductions, the last-arriving-workgroup hand-off (agent-scope release /
+// acquire, MI355X_MICROARCH.md "Workgroup dispatch ... visibility"), and the
+// scalar logic of PETSc KSPCG + KSPConvergedDefault (preconditioned norm).
+#pragma once
+#include "tv_internal.h"
+
+namespace tv {
+
+__device__ __forceinline__ double wave_sum64(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Arrival protocol of the in-kernel reduction tail.  Every workgroup stores its
+// partial record(s) WRITE-THROUGH (store_partial: sc1 / agent-scope atomic
+// store), drains them (s_waitcnt vmcnt(0) in every wave, then a workgroup
+// barrier), and one lane takes a ticket (relaxed agent-scope fetch_add).  The
+// workgroup that draws the last ticket reads every record with sc1 loads
+// (load_partial), so no agent release / acquire fence (buffer_wbl2 /
+// buffer_inv) is needed (MI355X_MICROARCH.md "Valid forms", table row 1).
+// The counter is re-armed (0) by the last workgroup.
+__device__ __forceinline__ void store_partial(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_partial(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool last_block_arrived(unsigned* counter, unsigned nblocks) {
+  __shared__ int amlast;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    amlast = (t == nblocks - 1) ? 1 : 0;
+    if (amlast) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return amlast != 0;
+}
+
+// Fixed-order reduction of n records of width W (<= 2) by one workgroup; the
+// result is in sums[] of thread 0.
+template <int W>
+__device__ __forceinline__ void block_reduce_records(const double* partials, int n, double (&sums)[2]) {
+  __shared__ double red[W][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double acc[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) acc[w] = 0.0;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) acc[w] += load_partial(&partials[(int64_t)t * W + w]);
+  }
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const double s = wave_sum64(acc[w]);
+    if (lane == 0) red[w][wave] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      double s = 0.0;
+      for (int q = 0; q < nw; ++q) s += red[w][q];
+      sums[w] = s;
+    }
+  }
+}
+
+// ---- PETSc KSPSolve_CG + KSPConvergedDefault scalar logic -------------------
+__device__ __forceinline__ void logic_init(PcgState* st, const double* sums) {
+  const double dp = sqrt(sums[0]);
+  st->dp = dp;
+  st->rnorm0 = dp;
+  st->ttol = fmax(st->rtol * dp, st->atol);
+  st->it = 0;
+  st->done = 0;
+  st->reason = R_RUNNING;
+  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
+  st->beta = sums[1];
+  st->betaold = 1.0;
+  if (st->beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; }
+}
+
+__device__ __forceinline__ void logic_dpi(PcgState* st, const double* sums) {
+  if (st->done) return;
+  const double dpi = sums[0];
+  if (!isfinite(dpi)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  const double dpiold = st->dpiold;
+  st->betaold = st->beta;
+  if (dpi == 0.0 || (st->it > 0 && ((dpi > 0.0) != (dpiold > 0.0)))) {
+    st->done = 1; st->reason = R_DIV_INDEF_MAT; return;
+  }
+  st->dpi = dpi;
+  st->dpiold = dpi;
+  st->a = st->beta / dpi;
+}
+
+__device__ __forceinline__ void logic_update(PcgState* st, const double* sums) {
+  if (st->done) return;
+  const double dp = sqrt(sums[0]);
+  st->it += 1;
+  st->dp = dp;
+  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
+  if (dp >= st->dtol * st->rnorm0) { st->done = 1; st->reason = R_DIV_DTOL; return; }
+  if (st->it >= st->max_it) { st->done = 1; st->reason = R_DIV_ITS; return; }
+  const double beta = sums[1];
+  if (beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
+  if (beta * st->betaold < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
+  st->beta = beta;
+}
+
+__device__ __forceinline__ void apply_logic(PcgState* st, const double* sums, int kind) {
+  if (kind == 1) logic_init(st, sums);
+  else if (kind == 2) logic_dpi(st, sums);
+  else if (kind == 3) logic_update(st, sums);
+}
+
+// Tail of a kernel that produced per-workgroup partial records: the last
+// workgroup reduces all `n` records into `out` and (kind > 0) runs the PCG logic.
+template <int W>
+__device__ __forceinline__ void fused_reduce_tail(const RedTail& rt, int n) {
+  if (rt.counter == nullptr) return;
+  if (!last_block_arrived(rt.counter, gridDim.x)) return;
+  double sums[2] = {0.0, 0.0};
+  block_reduce_records<W>(rt.partials, n, sums);
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < W; ++w) rt.out[w] = sums[w];
+    apply_logic(rt.st, sums, rt.kind);
+  }
+}
+
+}  // namespace tv

@@ -36,6 +36,13 @@ struct CgGrid {
   double T_amb, T_amb4;
   const int64_t* bnodes;      // owned nodes on physical boundary faces (3D marching path)
   int64_t n_bnodes;
+  // Robin facet Jacobian stencils per face f = 2*axis + side (3D marching path):
+  // 9 coefficient planes of bst_n[f] x bst_m[f] face nodes (tangential axes t1 < t2)
+  double* bst[6];
+  int bst_n[6], bst_m[6];
+  int bst_ok;
+  const int64_t* enodes;      // owned nodes on >= 2 physical faces (edges, corners)
+  int64_t n_enodes;
 };
 
 // Grid of the DG1 temperature space: cells per storage axis; dof layout is
@@ -60,6 +67,16 @@ struct PcgState {
   int it, done, reason, max_it;
   double dx_norm2;            // ||dx||^2 of the last Newton update
   double pad[3];
+};
+
+// In-kernel reduction tail (last-arriving workgroup reduces the partial records
+// of the launch (and of a preceding launch) and runs the PCG scalar logic).
+struct RedTail {
+  unsigned* counter;          // nullptr: no tail (separate reduce launch)
+  const double* partials;
+  double* out;                // reduced sums (read by RCCL allreduce on multi-GPU)
+  PcgState* st;
+  int kind;                   // 0 none, 1 init, 2 p.w, 3 update
 };
 
 enum PcgReason {
@@ -94,10 +111,13 @@ struct ViscoFields {
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s);
-void launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
+// returns true when the launch ends with the in-kernel reduction tail (the
+// caller then skips the separate reduce launch)
+bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
-                            hipStream_t s);
+                            hipStream_t s, const RedTail* tail = nullptr);
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
+void launch_cg_bstencil(const CgGrid& g, const double* T, hipStream_t s);
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 
 void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
@@ -119,7 +139,7 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 // p is taken from buffer (st->it & 1 ? pB : pA), matching the fused matvec
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* dinv, double* dx, double* r, double* z, double* partials,
-                       hipStream_t s);
+                       hipStream_t s, const RedTail* tail = nullptr);
 // one-block deterministic reduce of n records of width W (<= 2) into out[W];
 // kind: 0 none, 1 PCG init logic, 2 PCG p.w logic, 3 PCG update logic
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,

@@ -9,7 +9,7 @@
 // once converged every kernel of the batch exits at its first instruction.
 // Reductions: per-block partial sums (fixed order) -> one-block reduce, so the
 // result is bitwise reproducible run to run.
-#include "tv_internal.h"
+#include "tv_device.h"
 
 namespace tv {
 namespace {
@@ -32,7 +32,7 @@ __device__ __forceinline__ void block_partials(double (&v)[W], double* partials)
   __syncthreads();
   if (threadIdx.x < W) {
     const int w = threadIdx.x;
-    partials[(int64_t)blockIdx.x * W + w] = (red[w][0] + red[w][1]) + (red[w][2] + red[w][3]);
+    store_partial(&partials[(int64_t)blockIdx.x * W + w], (red[w][0] + red[w][1]) + (red[w][2] + red[w][3]));
   }
 }
 
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
                                                        const double* __restrict__ w,
                                                        const double* __restrict__ dinv, double* __restrict__ dx,
                                                        double* __restrict__ r, double* __restrict__ z,
-                                                       double* __restrict__ partials) {
+                                                       double* __restrict__ partials, RedTail rt) {
   if (st->done) return;
   const double a = st->a;
   const double* __restrict__ p = (st->it & 1) ? pB : pA;
@@ -72,6 +72,7 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
     acc[1] += zz * rr;
   }
   block_partials<2>(acc, partials);
+  fused_reduce_tail<2>(rt, gridDim.x);
 }
 
 __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __restrict__ T,
@@ -84,51 +85,6 @@ __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __r
     acc[0] += d * d;
   }
   block_partials<1>(acc, partials);
-}
-
-// ---- scalar logic (PETSc KSPSolve_CG + KSPConvergedDefault) ------------------
-__device__ void logic_init(PcgState* st, const double* sums) {
-  const double dp = sqrt(sums[0]);
-  st->dp = dp;
-  st->rnorm0 = dp;
-  st->ttol = fmax(st->rtol * dp, st->atol);
-  st->it = 0;
-  st->done = 0;
-  st->reason = R_RUNNING;
-  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
-  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
-  st->beta = sums[1];
-  st->betaold = 1.0;
-  if (st->beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; }
-}
-
-__device__ void logic_dpi(PcgState* st, const double* sums) {
-  if (st->done) return;
-  const double dpi = sums[0];
-  if (!isfinite(dpi)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
-  const double dpiold = st->dpiold;
-  st->betaold = st->beta;
-  if (dpi == 0.0 || (st->it > 0 && ((dpi > 0.0) != (dpiold > 0.0)))) {
-    st->done = 1; st->reason = R_DIV_INDEF_MAT; return;
-  }
-  st->dpi = dpi;
-  st->dpiold = dpi;
-  st->a = st->beta / dpi;
-}
-
-__device__ void logic_update(PcgState* st, const double* sums) {
-  if (st->done) return;
-  const double dp = sqrt(sums[0]);
-  st->it += 1;
-  st->dp = dp;
-  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
-  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
-  if (dp >= st->dtol * st->rnorm0) { st->done = 1; st->reason = R_DIV_DTOL; return; }
-  if (st->it >= st->max_it) { st->done = 1; st->reason = R_DIV_ITS; return; }
-  const double beta = sums[1];
-  if (beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
-  if (beta * st->betaold < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
-  st->beta = beta;
 }
 
 // One-block deterministic reduction of `n` partial records of width W, then
@@ -158,17 +114,11 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
       sums[w] = s;
       out[w] = s;
     }
-    if (kind == 1) logic_init(st, sums);
-    else if (kind == 2) logic_dpi(st, sums);
-    else if (kind == 3) logic_update(st, sums);
+    apply_logic(st, sums, kind);
   }
 }
 
-__global__ void k_logic(PcgState* st, const double* sums, int kind) {
-  if (kind == 1) logic_init(st, sums);
-  else if (kind == 2) logic_dpi(st, sums);
-  else if (kind == 3) logic_update(st, sums);
-}
+__global__ void k_logic(PcgState* st, const double* sums, int kind) { apply_logic(st, sums, kind); }
 
 __global__ __launch_bounds__(kBlock) void k_fill(double* x, int64_t n, double v) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = v;
@@ -193,9 +143,12 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 }
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
-                       const double* dinv, double* dx, double* r, double* z, double* partials, hipStream_t s) {
+                       const double* dinv, double* dx, double* r, double* z, double* partials, hipStream_t s,
+                       const RedTail* tail) {
+  RedTail rt{};
+  if (tail) rt = *tail;
   hipLaunchKernelGGL(k_pcg_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx, r, z,
-                     partials);
+                     partials, rt);
 }
 
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s) {

@@ -155,6 +155,13 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
               const tv_options* opts, int device, void** ctx_out);
 int tv_destroy(void* ctx);
 
+/* Host-only (no GPU needed): layout of partition `part` of a CG1 mesh —
+ * out[0..2] storage axis -> physical axis (-1 degenerate), out[3..5] global
+ * nodes per storage axis, out[6..7] owned node planes [b0, b1) along storage
+ * axis 2, out[8] global offset of the first owned dof, out[9] owned dofs,
+ * out[10] local dofs incl. ghost planes, out[11..12] ghost plane below/above. */
+int tv_partition_layout(const tv_mesh_desc* mesh, int64_t* out13);
+
 /* sizes: owned dofs of the T space / sigma space on this partition; block
  * size of a field; global dof offset of this partition's first owned dof */
 int tv_num_dofs(void* ctx, int space /*0 T, 1 sigma*/, int64_t* n_owned, int64_t* global_offset);
@@ -186,6 +193,15 @@ int tv_comm_unique_id_size(void);
 int tv_comm_get_unique_id(char* id_out);   /* rank 0; broadcast it out-of-band */
 int tv_comm_init(void* ctx, const char* id, int n_ranks, int rank);
 int tv_halo_exchange(void* ctx, int field);
+/* Host-staged communicator for running several partitions on one GPU (tests):
+ * the library stages ghost planes / partial sums through pinned host memory
+ * and calls these synchronously (return 0 on success).  Production multi-GPU
+ * runs use tv_comm_init (RCCL). */
+typedef int (*tv_host_allreduce_fn)(double* buf, int n, void* user);
+typedef int (*tv_host_sendrecv_fn)(const double* send, size_t n_send, int peer_send, double* recv,
+                                   size_t n_recv, int peer_recv, void* user);
+int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
+                      tv_host_sendrecv_fn sendrecv_fn, void* user);
 
 /* ---- measurement ------------------------------------------------------------ */
 /* time `reps` launches of one hot kernel on the context stream with HIP events;

@@ -1,0 +1,63 @@
+"""Partitioned run on one GPU (host-staged comm over gloo) vs the single-partition
+run of the same mesh: T, phi, xi and sigma must agree.  Launched by
+tests/test_partition.py as `torch.distributed.run --nproc-per-node P`."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fem-glass-tempering_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from tvfem import box_mesh  # noqa: E402
+from tvfem.parallel import init_host_comm  # noqa: E402
+from tvfem.problem import ThermoViscoProblem  # noqa: E402
+
+MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0, "htc": 280.1,
+      "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0, "Rg": 8.314, "alpha_solid": 9.1e-6,
+      "alpha_liquid": 25.1e-6}
+CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+
+
+def run(mesh, n_parts, part, steps, comm=None):
+    p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=0, n_parts=n_parts, part=part, part_axis=1,
+                           verbose=False)
+    if comm is not None:
+        comm(p)
+    p.setup()
+    its = []
+    for _ in range(steps):
+        p.solve_timestep()
+        its.append((p.last_newton_iterations, p.last_krylov_iterations))
+    out = {k: p.get_field(k) for k in ("T", "phi", "xi", "sigma")}
+    p.close()
+    return out, its
+
+
+def main():
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    mesh = box_mesh([2.0, 6.0, 1.0], [10, 30, 5])
+    steps = 4
+    loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
+    if rank == 0:
+        ref, its_ref = run(mesh, 1, 0, steps)
+        res = {"its_parts": its, "its_single": its_ref}
+        for k in ("T", "phi", "xi", "sigma"):
+            full = np.concatenate([np.asarray(g[k]) for g in gathered])
+            e = np.linalg.norm(full - ref[k]) / np.linalg.norm(ref[k])
+            res[k] = float(e)
+        print("PARTITION_CHECK " + json.dumps(res), flush=True)
+    dist.barrier()
+
+
+if __name__ == "__main__":
+    main()
