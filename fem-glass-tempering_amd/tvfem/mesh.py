@@ -123,7 +123,7 @@ def write_msh(path, mesh: RectilinearMesh):
     with open(path, "w") as fh:
         fh.write("$MeshFormat\n2.2 0 8\n$EndMeshFormat\n$Nodes\n%d\n" % len(x))
         for i, v in enumerate(x):
-            fh.write(f"{i + 1} {v!r} 0 0\n")
+            fh.write(f"{i + 1} {float(v)!r} 0 0\n")
         fh.write("$EndNodes\n$Elements\n%d\n" % (len(x) - 1))
         for i in range(len(x) - 1):
             fh.write(f"{i + 1} 1 2 0 1 {i + 1} {i + 2}\n")

@@ -1,0 +1,74 @@
+"""Mesh ingest: gmsh ASCII line meshes (the reference reads a 1D .msh with
+gdim=1, ThermoViscoProblem.py:27-28) and the graded bar of geometry.py."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_msh22_roundtrip(tmp_path):
+    from tvfem.mesh import RectilinearMesh, read_msh, write_msh
+    x = np.array([0.0, 0.1, 0.25, 1.0, 3.0])
+    p = tmp_path / "m.msh"
+    write_msh(str(p), RectilinearMesh([x]))
+    m = read_msh(str(p))
+    assert m.dim == 1 and np.array_equal(m.axes[0], x)
+
+
+def test_msh41_reader(tmp_path):
+    from tvfem.mesh import read_msh
+    txt = """$MeshFormat
+4.1 0 8
+$EndMeshFormat
+$Nodes
+2 4 1 4
+0 1 0 2
+1
+2
+0 0 0
+50 0 0
+1 1 0 2
+3
+4
+30 0 0
+10 0 0
+$EndNodes
+$Elements
+1 3 1 3
+1 1 1 3
+1 1 4
+2 4 3
+3 3 2
+$EndElements
+"""
+    p = tmp_path / "m41.msh"
+    p.write_text(txt)
+    m = read_msh(str(p))
+    assert np.array_equal(m.axes[0], [0.0, 10.0, 30.0, 50.0])
+
+
+def test_graded_bar_geometry(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "fem-glass-tempering_amd"))
+    import geometry
+    from tvfem.mesh import read_msh
+    p = tmp_path / "bar.msh"
+    geometry.create_mesh(str(p))
+    m = read_msh(str(p))
+    x = m.axes[0]
+    assert x[0] == 0.0 and x[-1] == 50.0
+    h = np.diff(x)
+    assert h.min() >= 0.05 and h.max() <= 3.0 + 1e-12
+    assert h[0] < 0.2 and h[len(h) // 2] > 2.0  # fine at the surface, coarse in the core
+
+
+def test_bad_mesh_rejected(tmp_path):
+    from tvfem.mesh import RectilinearMesh, read_msh
+    with pytest.raises(ValueError):
+        RectilinearMesh([np.array([0.0, 1.0, 0.5])])
+    p = tmp_path / "x.msh"
+    p.write_text("not a mesh")
+    with pytest.raises(ValueError):
+        read_msh(str(p))
