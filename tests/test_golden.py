@@ -25,7 +25,8 @@ def load(path):
     return meta, axes, {k: z[k] for k in z.files}
 
 
-def relerr(a, b, mask=None):
+def relerr(a, b, mask=None, scale=None):
+    """relative L2 error; ``scale`` (optional) replaces ||b|| in the denominator."""
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     if mask is not None:
@@ -33,22 +34,29 @@ def relerr(a, b, mask=None):
     na, nb = np.isnan(a), np.isnan(b)
     assert np.array_equal(na, nb), f"NaN pattern differs: {na.sum()} vs {nb.sum()}"
     a, b = a[~na], b[~nb]
-    den = np.linalg.norm(b)
+    den = np.linalg.norm(b) if scale is None else scale
     return np.linalg.norm(a - b) / den if den else np.linalg.norm(a - b)
 
 
 def _checks(z, d, get):
+    """(name, got, want, tol, mask, scale).  The deviatoric partial stresses
+    s_partial are rounding noise (the thermal strain is isotropic, so dev = tot -
+    tr/d I is 0 up to an ulp in 3D): they are measured against the volumetric
+    stress scale ||sigma_partial|| instead of their own norm."""
     d2 = d * d
     mT, mS = z["mask_T"], z["mask_S"]
+    m6 = np.repeat(mS, 6 * d2)
+    sg = z["sigma_partial"][m6]
+    sg_scale = float(np.linalg.norm(sg[~np.isnan(sg)]))
     return [
-        ("T", get("T"), z["T"], 1e-10, None),
-        ("Tf", get("Tf"), z["Tf"], 1e-10, None),
-        ("Tf_partial", get("Tf_partial"), z["Tf_partial"], 1e-10, None),
-        ("phi", get("phi"), z["phi"], 1e-9, None),
-        ("xi", get("xi"), z["xi"], 1e-6, mT),
-        ("sigma", get("sigma"), z["sigma"], 1e-6, np.repeat(mS, d2)),
-        ("s_partial", get("s_partial"), z["s_partial"], 1e-6, np.repeat(mS, 6 * d2)),
-        ("sigma_partial", get("sigma_partial"), z["sigma_partial"], 1e-6, np.repeat(mS, 6 * d2)),
+        ("T", get("T"), z["T"], 1e-10, None, None),
+        ("Tf", get("Tf"), z["Tf"], 1e-10, None, None),
+        ("Tf_partial", get("Tf_partial"), z["Tf_partial"], 1e-10, None, None),
+        ("phi", get("phi"), z["phi"], 1e-9, None, None),
+        ("xi", get("xi"), z["xi"], 1e-6, mT, None),
+        ("sigma", get("sigma"), z["sigma"], 1e-6, np.repeat(mS, d2), None),
+        ("s_partial", get("s_partial"), z["s_partial"], 1e-6, m6, sg_scale),
+        ("sigma_partial", get("sigma_partial"), z["sigma_partial"], 1e-6, m6, None),
     ]
 
 
@@ -70,8 +78,8 @@ def test_oracle_reproduces_golden(path):
            "Tf_partial": ref.functions_current["Tf_partial"], "phi": ref.functions["phi"],
            "xi": ref.functions["xi"], "sigma": ref.functions_next["sigma"],
            "s_partial": ref.functions_current["s_partial"], "sigma_partial": ref.functions_current["sigma_partial"]}
-    for name, got, want, tol, m in _checks(z, len(axes), src.__getitem__):
-        assert relerr(got, want, m) < min(tol, 1e-9), name
+    for name, got, want, tol, m, sc in _checks(z, len(axes), src.__getitem__):
+        assert relerr(got, want, m, sc) < min(tol, 1e-9), name
     assert [h[0] for h in ref.newton_history] == list(z["newton_its"])
 
 
@@ -85,7 +93,8 @@ def test_hip_path_reproduces_golden(path):
     from tvfem.problem import ThermoViscoProblem
     meta, axes, z = load(path)
     dev = ThermoViscoProblem(RectilinearMesh(axes), (0.0, meta["steps"] * meta["dt"]), meta["dt"],
-                             meta["config"], meta["model_parameters"], materialize=True, verbose=False)
+                             meta["config"], meta["model_parameters"], materialize=True, verbose=False,
+                             part_axis=2 if len(axes) == 3 else -1)  # storage order = oracle dof order
     dev.setup()
     for _ in range(meta["steps"]):
         dev.solve_timestep()
@@ -93,7 +102,7 @@ def test_hip_path_reproduces_golden(path):
               "phi": dev.functions, "xi": dev.functions, "sigma": dev.functions_next,
               "s_partial": dev.functions_current, "sigma_partial": dev.functions_current}
     get = lambda k: groups[k][k].x.array  # noqa: E731
-    for name, got, want, tol, m in _checks(z, len(axes), get):
-        e = relerr(got, want, m)
+    for name, got, want, tol, m, sc in _checks(z, len(axes), get):
+        e = relerr(got, want, m, sc)
         assert e < tol, (name, e, tol)
     dev.close()

@@ -1,0 +1,39 @@
+"""Drive the C4 hot-path kernels for a rocprofv3 --pmc pass.
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
+        python3 tools/pmc_kernels.py [--cells 400,400,50] [--reps 5]
+
+One coupled step (realistic state), then `reps` launches of each timed kernel
+(tv_time_kernel ids: 3 fused PCG matvec, 4 PCG update, 1 visco update).
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "fem-glass-tempering_amd"), ROOT]
+
+from tvfem import _native as N, box_mesh  # noqa: E402
+from tvfem.problem import ThermoViscoProblem  # noqa: E402
+
+MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0,
+      "htc": 280.1, "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0, "Rg": 8.314,
+      "alpha_solid": 9.10e-6, "alpha_liquid": 25.10e-6, "Tf_init": 873.0}  # main.py:29-55
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--cells", default="400,400,50")
+ap.add_argument("--reps", type=int, default=5)
+a = ap.parse_args()
+nc = [int(v) for v in a.cells.split(",")]
+cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+prob = ThermoViscoProblem(box_mesh([50.0, 50.0, 5.0], nc), (0.0, 1.0), 0.1, cfg, dict(MP),
+                          materialize=False, part_axis=1, verbose=False)
+prob.setup()
+prob.solve_timestep()
+lib, ctx = prob._lib, prob._ctx
+for kid in (3, 4, 1):
+    ms = C.c_double()
+    N.check(lib.tv_time_kernel(ctx, kid, a.reps, C.byref(ms)), ctx)
+    print(kid, ms.value, flush=True)
+prob.close()

@@ -1,0 +1,73 @@
+"""Summarise two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) into HBM bytes
+per launch for the hot-path kernels, with the gfx950 correction of
+/opt/skills/guides/MI355X_MICROARCH.md §HBM (FETCH_SIZE counts half of wide
+streaming reads: doubled here; WRITE_SIZE taken as is).  Counter values are in
+KB (rocprofv3 derived-counter unit) -> bytes x1024.
+
+    python tools/pmc_summarize.py FETCH_DIR WRITE_DIR OUT.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+GROUPS = {
+    "pcg_matvec_fused": ("k_cg_march<1, true", "k_cg_bapply<true>"),
+    "pcg_update": ("k_pcg_update",),
+    "visco_update": ("k_visco_fused",),
+}
+
+
+def per_kernel(d, counter):
+    vals = defaultdict(list)
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return vals
+
+
+def group_avg(vals, pats):
+    tot = 0.0
+    found = []
+    for pat in pats:
+        ks = [k for k in vals if pat in k]
+        if not ks:
+            return None, found
+        v = [x for k in ks for x in vals[k]]
+        found.append((ks[0][:80], len(v)))
+        tot += sum(v) / len(v)
+    return tot, found
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    fetch = per_kernel(fdir, "FETCH_SIZE")
+    write = per_kernel(wdir, "WRITE_SIZE")
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/pmc_kernels.py",
+           "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KB -> bytes x1024", "kernels": {}}
+    for name, pats in GROUPS.items():
+        fb, ff = group_avg(fetch, pats)
+        wb, wf = group_avg(write, pats)
+        if fb is None or wb is None:
+            continue
+        rd = 2.0 * fb * 1024.0
+        wr = wb * 1024.0
+        res["kernels"][name] = {"fetch_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+                                "dispatches": ff}
+    if "pcg_matvec_fused" in res["kernels"]:
+        res["hbm_bytes_per_launch"] = res["kernels"]["pcg_matvec_fused"]["hbm_bytes_per_launch"]
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
