@@ -66,8 +66,7 @@ struct Ctx {
   double* dgh[3] = {nullptr, nullptr, nullptr};
   int* map = nullptr;
   int64_t* bnodes = nullptr;
-  int64_t* enodes = nullptr;
-  double* bst[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  double* fface[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   // PCG work (T space, local size)
   double *r = nullptr, *z = nullptr, *pA = nullptr, *pB = nullptr, *w = nullptr, *dinv = nullptr;
   double* partials = nullptr;
@@ -246,7 +245,7 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     }
     const int64_t plane = (int64_t)g.n0 * g.n1;
     if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
-      std::vector<int64_t> bn, en;
+      std::vector<int64_t> bn;
       for (int k = g.k_begin; k < g.k_end; ++k)
         for (int j = 0; j < g.n1; ++j)
           for (int i = 0; i < g.n0; ++i) {
@@ -254,10 +253,6 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
                             (j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]) ||
                             (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
             if (on) bn.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
-            const int nf = ((i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1])) +
-                           ((j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1])) +
-                           ((k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]));
-            if (nf > 1) en.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
           }
       if (!bn.empty()) {
         HIPC(hipMalloc(&c->bnodes, bn.size() * sizeof(int64_t)));
@@ -265,29 +260,26 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       }
       g.bnodes = c->bnodes;
       g.n_bnodes = (int64_t)bn.size();
-      if (!en.empty()) {
-        HIPC(hipMalloc(&c->enodes, en.size() * sizeof(int64_t)));
-        HIPC(hipMemcpy(c->enodes, en.data(), en.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-      }
-      g.enodes = c->enodes;
-      g.n_enodes = (int64_t)en.size();
-      // facet-Jacobian stencil storage for every physical boundary face
+      // facet-Jacobian terms: one value per node of every physical boundary face
       const int nn[3] = {g.n0, g.n1, g.n2};
       for (int f = 0; f < 6; ++f) {
         const int ax = f >> 1, side = f & 1;
-        g.bst[f] = nullptr;
+        g.fface[f] = nullptr;
+        g.fn1[f] = g.fn2[f] = 0;
         if (!g.bnd[ax][side]) continue;
         const int t1 = (ax == 0) ? 1 : 0, t2 = (ax == 2) ? 1 : 2;
-        g.bst_n[f] = nn[t1];
-        g.bst_m[f] = nn[t2];
-        const size_t bytes = sizeof(double) * 9 * (size_t)nn[t1] * nn[t2];
-        HIPC(hipMalloc(&c->bst[f], bytes));
-        HIPC(hipMemsetAsync(c->bst[f], 0, bytes, c->stream));
-        g.bst[f] = c->bst[f];
+        g.fn1[f] = nn[t1];
+        g.fn2[f] = nn[t2];
+        const size_t bytes = sizeof(double) * (size_t)nn[t1] * nn[t2];
+        HIPC(hipMalloc(&c->fface[f], bytes));
+        HIPC(hipMemsetAsync(c->fface[f], 0, bytes, c->stream));
+        g.fface[f] = c->fface[f];
       }
-      g.bst_ok = 1;
     }
     c->nT = plane * g.n2;
+    // the CG kernels index local nodes with 32-bit integers (68 M nodes = 290 GB
+    // of state at materialize=1 would already exceed one MI355X)
+    if (c->nT >= (int64_t)INT32_MAX) return c->fail(TV_ERR_ARG, "partition too large: >= 2^31 local nodes");
     c->ownT_off = plane * g.k_begin;
     c->ownT_n = plane * (g.k_end - g.k_begin);
     c->globT_off = plane * b0;
@@ -564,14 +556,9 @@ static void op_residual(Ctx* c, const double* T, const double* Tp, double* F) {
   else launch_dg_residual(c->dg, T, Tp, F, c->stream);
 }
 static void op_diag(Ctx* c, const double* T, double* d, int invert) {
-  // Jacobian "assembly": diagonal (Jacobi PC) + facet stencils for J(T)
-  if (c->fam_T == TV_CG) {
-    launch_cg_diag(c->cg, T, d, invert, c->stream);
-    launch_cg_bstencil(c->cg, T, c->stream);
-  }
-  else {
-    launch_dg_diag(c->dg, T, d, invert, c->stream);
-  }
+  // Jacobian "assembly": the diagonal for the Jacobi PC (J(T) itself is matrix-free)
+  if (c->fam_T == TV_CG) launch_cg_diag(c->cg, T, d, invert, c->stream);
+  else launch_dg_diag(c->dg, T, d, invert, c->stream);
 }
 static void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
   if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
@@ -603,8 +590,9 @@ static int pcg_iteration(Ctx* c, const double* T) {
     launch_logic(c->st, c->sums, 2, c->stream);
   }
   RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3};
+  const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
-                    c->r + off, c->z + off, c->partials, c->stream, &t2);
+                    c->r + off, c->z + off, c->partials, c->stream, &t2, &fa);
   if (multi) {  // dp, beta, convergence
     if (int e = allreduce(c, c->sums, 2)) return e;
     launch_logic(c->st, c->sums, 3, c->stream);
@@ -909,9 +897,8 @@ int tv_destroy(void* ctx) {
   }
   if (c->map) hipFree(c->map);
   if (c->bnodes) hipFree(c->bnodes);
-  if (c->enodes) hipFree(c->enodes);
   for (int f = 0; f < 6; ++f)
-    if (c->bst[f]) hipFree(c->bst[f]);
+    if (c->fface[f]) hipFree(c->fface[f]);
   if (c->st) hipFree(c->st);
   if (c->counters) hipFree(c->counters);
   if (c->h_st) hipHostFree(c->h_st);
@@ -1046,7 +1033,6 @@ int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !x_dev || !y_dev) return TV_ERR_ARG;
   hipSetDevice(c->device);
-  if (c->fam_T == TV_CG) launch_cg_bstencil(c->cg, c->f[TV_F_T].ptr, c->stream);  // J(T) facet stencils
   op_japply(c, c->f[TV_F_T].ptr, x_dev, y_dev, nullptr, nullptr);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));
@@ -1205,11 +1191,13 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       case 1: return visco(c, false);
       case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;
       case 3: op_japply_fused(c, c->f[TV_F_T].ptr, &np); return TV_OK;
-      case 4:
+      case 4: {
+        const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, c->ownT_off) : FaceAdd{};
         launch_pcg_update(c->ownT_n, c->st, c->pA + c->ownT_off, c->pB + c->ownT_off, c->w + c->ownT_off,
                           c->dinv + c->ownT_off, c->f[TV_F_DX].ptr + c->ownT_off, c->r + c->ownT_off,
-                          c->z + c->ownT_off, c->partials, c->stream);
+                          c->z + c->ownT_off, c->partials, c->stream, nullptr, &fa);
         return TV_OK;
+      }
       default: return c->fail(TV_ERR_ARG, "unknown kernel id");
     }
   };

@@ -28,6 +28,8 @@
 #include <cstdlib>
 
 #include "tv_device.h"
+#include <cstdio>
+#include <vector>
 
 namespace tv {
 namespace {
@@ -44,6 +46,41 @@ __device__ __forceinline__ double shl1(double v) {  // lane l <- lane l+1
   int lo = __double2loint(v), hi = __double2hiint(v);
   lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xF, 0xF, false);
   hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Blocks are dispatched round-robin over the 8 XCDs; remap so that each XCD
+// gets a contiguous range of tile ids (bijective for any grid size), keeping
+// the halo rows / columns shared by neighbouring tiles in one L2.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// Raw buffer access (32-bit byte offsets against an SGPR descriptor).  The
+// hardware range check returns 0 for loads and drops stores at offsets past
+// the buffer, so out-of-domain neighbours and non-owned outputs are masked by
+// an out-of-range offset (kBadOff) instead of branches.
+using buf_t = __amdgpu_buffer_rsrc_t;
+using b64v = unsigned int __attribute__((ext_vector_type(2)));
+constexpr uint32_t kBadOff = 0x40000000u;  // > any buffer the march path accepts (host guard)
+__device__ __forceinline__ buf_t mk_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ double bload(buf_t r, uint32_t off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ void bstore(buf_t r, uint32_t off, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(b64v, v), r, (int)off, 0, 0);
+}
+
+__device__ __forceinline__ double uniform(double v) {  // wave-uniform value -> SGPR pair
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
   return __hiloint2double(hi, lo);
 }
 
@@ -380,8 +417,8 @@ __global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __re
 // input array per node; L2 and LDS carry the rest; one barrier per plane.
 // Robin facets (<5% of nodes) gather their 3x3 patches directly.
 // ---------------------------------------------------------------------------
-constexpr int kRows = 16;      // rows (wavefronts) per marching workgroup
-constexpr int kMaxChunk = 254;  // planes per marching chunk (LDS coefficient stage)
+constexpr int kRows = 8;       // rows (wavefronts) per marching workgroup
+constexpr int kFaceChunk = 16;  // max planes per marching chunk (LDS coefficient stage)
 
 template <int MODE, bool FUSEP>
 __device__ double facet_direct(const CgGrid& g, int i, int j, int k, int ax, const double* __restrict__ T,
@@ -414,17 +451,177 @@ __device__ double facet_direct(const CgGrid& g, int i, int j, int k, int ax, con
   return facet_sum<MODE, false, false, false>(g, c1[C_HLO], c1[C_HHI], c2[C_HLO], c2[C_HHI], Tp, Pp);
 }
 
+// ---------------------------------------------------------------------------
+// Robin facet Jacobian terms of the physical boundary faces,
+//   fface[f][c_t1 + n_t1 c_t2] = dt sum_facets int g'(T_h) phi_I p_h ds
+// (3x3 Gauss per facet, as facet_sum), evaluated matrix-free from the 3x3
+// in-face patches of T and p, one thread per face node.  Nodes on two or
+// three faces (edges, corners) get one term per face.
+// ---------------------------------------------------------------------------
+struct FaceOff {
+  int off[7];  // workgroup ranges per face f (in marching-workgroup units), off[6] = total
+};
+
+FaceOff face_offsets(const CgGrid& g, int threads) {
+  FaceOff fo{};
+  int acc = 0;
+  for (int f = 0; f < 6; ++f) {
+    fo.off[f] = acc;
+    if (g.fface[f]) acc += (2 * g.fn1[f] * g.fn2[f] + threads - 1) / threads;  // 2 threads per node
+  }
+  fo.off[6] = acc;
+  return fo;
+}
+
+// One facet of facet_sum<MODE_JAC> from its four corner values (corner 00 =
+// the node, 10 along t1, 01 along t2), rolled 3x3 Gauss loop: the face
+// workgroups share the marching kernel's register budget.
+__device__ __forceinline__ double facet_jac_one(const CgGrid& g, double h1, double h2, bool s1, bool s2,
+                                                double T00, double T10, double T01, double T11, double P00,
+                                                double P10, double P01, double P11) {
+  double acc = 0.0;
+  if (!(h1 > 0.0) || !(h2 > 0.0)) return 0.0;
+#pragma unroll 1
+  for (int q = 0; q < 9; ++q) {
+    const int q1 = q / 3, q2 = q - 3 * (q / 3);
+    const double g1 = q1 == 0 ? kGX[0] : (q1 == 1 ? kGX[1] : kGX[2]);
+    const double g2 = q2 == 0 ? kGX[0] : (q2 == 1 ? kGX[1] : kGX[2]);
+    const double w1 = q1 == 1 ? kGW[1] : kGW[0], w2 = q2 == 1 ? kGW[1] : kGW[0];
+    const double pc1 = s1 ? 1.0 - g1 : g1, po1 = 1.0 - pc1;
+    const double pc2 = s2 ? 1.0 - g2 : g2, po2 = 1.0 - pc2;
+    const double w = (w1 * h1) * (w2 * h2);
+    const double phiI = pc1 * pc2;
+    const double Th = phiI * T00 + po1 * pc2 * T10 + pc1 * po2 * T01 + po1 * po2 * T11;
+    const double Ph = phiI * P00 + po1 * pc2 * P10 + pc1 * po2 * P01 + po1 * po2 * P11;
+    acc += w * dg_rad_conv(g, Th) * phiI * Ph;
+  }
+  return acc;
+}
+
+// One face workgroup of the marching launch (Jacobian mode): face node per
+// thread, p = z + beta/betaold p_old (fused PCG) or p = x; writes fface and the
+// workgroup's p.(facet terms) partial record; takes part in the reduction tail.
+template <bool FUSEP, int R>
+__device__ void face_block(const CgGrid& g, const double* __restrict__ T, const double* __restrict__ in0,
+                           const double* pA, const double* pB, const PcgState* __restrict__ st,
+                           double* __restrict__ partials, const RedTail& rt, int nrec, int fb,
+                           const FaceOff& fo) {
+  __shared__ double redf[R];
+  int f = 0;
+  while (f < 5 && fb >= fo.off[f + 1]) ++f;
+  const int a = f >> 1, side = f & 1;
+  const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+  const int n[3] = {g.n0, g.n1, g.n2};
+  const int sst[3] = {1, g.n0, g.n0 * g.n1};
+  const int n1 = n[t1], n2 = n[t2];
+  const int t = (fb - fo.off[f]) * (R * kWave) + threadIdx.x;  // 2 threads per face node
+  double bcoef = 0.0;
+  bool first = true;
+  const double* pold = pA;
+  if (FUSEP) {
+    const int it = st->it;
+    first = (it == 0);
+    bcoef = first ? 0.0 : st->beta / st->betaold;
+    pold = (it & 1) ? pA : pB;
+  }
+  // two threads per face node: half h evaluates the two facets on side h of
+  // the second tangential axis (patch rows v = h, h + 1), summed over the pair
+  const int node = t >> 1, h = t & 1;
+  double dot = 0.0;
+  const bool okn = node < n1 * n2;
+  int c[3];
+  c[t1] = okn ? node % n1 : 0;
+  c[t2] = okn ? node / n1 : 0;
+  c[a] = side ? n[a] - 1 : 0;
+  const int nd = c[0] + sst[1] * c[1] + sst[2] * c[2];
+  double tv[3][2], pv[3][2];
+#pragma unroll
+  for (int u = 0; u < 3; ++u)
+#pragma unroll
+    for (int vv = 0; vv < 2; ++vv) {
+      const int v = h + vv;  // patch row 0..2
+      const int a1 = c[t1] + u - 1, a2 = c[t2] + v - 1;
+      const bool ok = okn && a1 >= 0 && a1 < n1 && a2 >= 0 && a2 < n2;
+      const int o = ok ? nd + (u - 1) * sst[t1] + (v - 1) * sst[t2] : nd;
+      tv[u][vv] = T[o];
+      const double zz = in0[o];
+      const double oo = FUSEP ? pold[o] : 0.0;
+      pv[u][vv] = (FUSEP && !first) ? zz + bcoef * oo : zz;
+    }
+  const double* c1 = g.coef[t1] + (int64_t)c[t1] * C_NCOEF;
+  const double* c2 = g.coef[t2] + (int64_t)c[t2] * C_NCOEF;
+  const double h2 = h ? c2[C_HHI] : c2[C_HLO];
+  // node row: vv = 1 - h (v = 1); the other patch row: vv = h
+  const int nr = 1 - h, orow = h;
+  double acc = facet_jac_one(g, c1[C_HLO], h2, false, h, tv[1][nr], tv[0][nr], tv[1][orow], tv[0][orow],
+                             pv[1][nr], pv[0][nr], pv[1][orow], pv[0][orow]);
+  acc += facet_jac_one(g, c1[C_HHI], h2, true, h, tv[1][nr], tv[2][nr], tv[1][orow], tv[2][orow], pv[1][nr],
+                       pv[2][nr], pv[1][orow], pv[2][orow]);
+  acc = g.dt * acc;
+  const double tot = acc + __shfl_xor(acc, 1, 64);  // the pair's two halves, fixed order per pair
+  const double tot0 = h ? __shfl_xor(tot, 1, 64) : tot;
+  if (okn && h == 0) {
+    const bool owned = c[2] >= g.k_begin && c[2] < g.k_end;
+    g.fface[f][node] = owned ? tot0 : 0.0;
+    dot = owned ? pv[1][nr] * tot0 : 0.0;
+  }
+  if (partials != nullptr) {
+    dot = wave_sum(dot);
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+    if (lane == 0) redf[wave] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < R; ++w) s += redf[w];
+      store_partial(&partials[blockIdx.x], s);
+    }
+    fused_reduce_tail<1>(rt, nrec);
+  }
+}
+
+// out[n] += sum of the facet terms of the owned boundary node n (every face
+// it lies on), for the non-fused J(T) x
+__global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t* __restrict__ bnodes, int64_t nb,
+                                                        double* __restrict__ out) {
+  const int n[3] = {g.n0, g.n1, g.n2};
+  for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < nb; e += (int64_t)gridDim.x * kBlock) {
+    const int nd = (int)bnodes[e];
+    const int c[3] = {nd % n[0], (nd / n[0]) % n[1], nd / (n[0] * n[1])};
+    double add = 0.0;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const double* F = g.fface[2 * a + side];
+        if (F && c[a] == (side ? n[a] - 1 : 0)) add += F[c[t1] + n[t1] * c[t2]];
+      }
+    }
+    out[nd] += add;
+  }
+}
+
 template <int MODE, bool FUSEP, int R>
 __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* __restrict__ T,
                                                         const double* __restrict__ in0, const double* in1,
                                                         double* __restrict__ out, double* pout,
                                                         const PcgState* __restrict__ st,
                                                         double* __restrict__ partials, int nseg, int raxis,
-                                                        int qchunk) {
+                                                        int qchunk, RedTail rt, int nrec, int nmarch,
+                                                        FaceOff fo) {
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
   __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
   __shared__ double red[R];
   if (FUSEP && st->done) return;
+  // Jacobian mode: workgroups past the marching tiles evaluate the Robin facet
+  // terms of the boundary faces (k_face_block) -- independent work that fills
+  // the tail of the march; the terms go to g.fface and are added to w by the
+  // consumer (PCG update / k_cg_addfaces), their p.w share joins the partials
+  if (MODE == MODE_JAC && (int)blockIdx.x >= nmarch) {
+    face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec, (int)blockIdx.x - nmarch, fo);
+    return;
+  }
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int n0 = g.n0;
@@ -433,12 +630,16 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
   const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
   const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
   const int qaxis = 3 - raxis;
-  const int nrb = (nR + R - 1) / R;
-  const int b = blockIdx.x;
-  const int seg = b % nseg;
-  const int t = b / nseg;
-  const int rb = t % nrb;
-  const int chunk = t / nrb;
+  // tile order: chunk fastest, then x segment, then row block; each XCD takes a
+  // contiguous run of tiles (xcd_remap), i.e. a compact group of columns with
+  // all their chunks -- neighbouring tiles share L2, and the boundary tiles
+  // (first / last chunk, first / last segment) spread evenly over the XCDs
+  const int nch = (nQ + qchunk - 1) / qchunk;
+  const int b = xcd_remap(blockIdx.x, nmarch);
+  const int chunk = b % nch;
+  const int t = b / nch;
+  const int seg = t % nseg;
+  const int rb = t / nseg;
   const int r0 = rb * R;
   const int r = r0 + wave;
   const bool row_ok = r < nR;
@@ -461,58 +662,81 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
   const int kb = g.k_begin, ke = g.k_end;
   const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
 
+  // row coefficients are wave-uniform: keep them in SGPRs
   const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
-  const double My0 = cr[C_MLO], My1 = cr[C_MDI], My2 = cr[C_MUP];
-  const double Ky0 = cr[C_KLO], Ky1 = cr[C_KDI], Ky2 = cr[C_KUP];
-  const double* cx = g.coef[0] + (int64_t)(col_ok ? i : 0) * C_NCOEF;
-  const double Mx0 = cx[C_MLO], Mx1 = cx[C_MDI], Mx2 = cx[C_MUP];
-  const double Kx0 = cx[C_KLO], Kx1 = cx[C_KDI], Kx2 = cx[C_KUP];
+  const double My0 = uniform(cr[C_MLO]), My1 = uniform(cr[C_MDI]), My2 = uniform(cr[C_MUP]);
+  const double Ky0 = uniform(cr[C_KLO]), Ky1 = uniform(cr[C_KDI]), Ky2 = uniform(cr[C_KUP]);
   const double da = g.dt_alpha;
 
   // raw loads of one (row, plane) value (+ second array); the combination
   // (p = z + b p_old, or T - Tp - dt f) happens one iteration later so the
-  // loads of plane L+1 are in flight while plane L is processed.
-  const double* __restrict__ second = (MODE == MODE_RES) ? in1 : pold;
+  // loads of plane L+1 are in flight while plane L is processed.  Buffer
+  // loads: a per-lane row offset (fixed for the march) plus a uniform plane
+  // offset; anything outside the domain reads 0 (range check).
+  const double* second = (MODE == MODE_RES) ? in1 : pold;
   constexpr bool TWO = (MODE == MODE_RES) || FUSEP;
-  // branch-free: out-of-range reads are redirected to element 0 and zeroed only
-  // when the value is consumed (one iteration later), so the loads of plane
-  // L+1 stay in flight across the barrier and the compute of plane L.
-  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < nR && L >= 0 && L < nQ; };
-  auto fetch = [&](int rr, int L, double& a0, double& a1) {
-    const int64_t idx = okf(rr, L) ? (int64_t)i + sR * rr + sQ * L : 0;
-    a0 = in0[idx];
-    a1 = TWO ? second[idx] : 0.0;
-  };
-  auto combine = [&](int rr, int L, double a0, double a1, double& v, double& vm) {
-    const bool ok = okf(rr, L);
-    a0 = ok ? a0 : 0.0;
-    a1 = (ok && !(FUSEP && first)) ? a1 : 0.0;
-    v = a0;
-    vm = 0.0;
-    if (MODE == MODE_RES) vm = a0 - a1 - g.dt_f;
-    if (FUSEP) v = first ? a0 : a0 + bcoef * a1;
-  };
+  const uint32_t nbytes = (uint32_t)g.n0 * (uint32_t)g.n1 * (uint32_t)g.n2 * 8u;
+  const buf_t rs0 = mk_rsrc(in0, nbytes);
+  const buf_t rs1 = mk_rsrc(TWO ? second : in0, (FUSEP && first) ? 0u : nbytes);  // p_old unused at it 0
+  const buf_t rso = mk_rsrc(out, nbytes);
+  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, FUSEP ? nbytes : 0u);
   // halo rows are loaded by waves 0 and R-1; the other waves re-load their own
   // row (an L1 hit) so that every wave runs the same straight-line load stream
   const bool halo = (wave == 0) || (wave == R - 1);
   const int hrow = (wave == 0) ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
   const int hslot = (wave == 0) ? 0 : R + 1;
-  // march-axis coefficients of the chunk, staged once in LDS (they are read by
-  // every wave each plane; vector loads of them would serialise on vmcnt)
-  __shared__ double cql[kMaxChunk + 2][6];
-  for (int e = threadIdx.x; e < (q1 - q0 + 2) * 6; e += R * kWave) {
-    const int qq = q0 - 1 + e / 6;
-    const int c = e % 6;
-    cql[e / 6][c] = (qq >= 0 && qq < nQ) ? g.coef[qaxis][(int64_t)qq * C_NCOEF + c] : 0.0;
-  }
-  __syncthreads();
-
-  // two register sets (A, B) alternate between "consumed now" and "prefetching
-  // the next plane" — a 2x unrolled loop, so no register copy has to wait for
-  // an in-flight load
+  auto lane_off = [&](int rr) -> uint32_t {
+    return (col_ok && rr >= 0 && rr < nR) ? (uint32_t)(i + sR * rr) * 8u : kBadOff;
+  };
+  const uint32_t vo_own = lane_off(r), vo_halo = lane_off(hrow);
+  const uint32_t vo_wr = writer ? vo_own : kBadOff;  // stores of the own row
+  auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? (uint32_t)(sQ * L) * 8u : kBadOff; };
+  auto fetch = [&](uint32_t vo, int L, double& a0, double& a1) {
+    const uint32_t o = vo + plane_off(L);
+    a0 = bload(rs0, o);
+    a1 = TWO ? bload(rs1, o) : 0.0;
+  };
+  auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
+    v = a0;
+    vm = 0.0;
+    if (MODE == MODE_RES) vm = (vo != kBadOff && L >= 0 && L < nQ) ? a0 - a1 - g.dt_f : 0.0;
+    if (FUSEP) v = a0 + bcoef * a1;  // a1 = 0 and bcoef = 0 at the first iteration
+  };
+  // Block start: ONE memory round trip for everything the march needs before
+  // its first plane -- the first two planes (prefetch), the coefficient
+  // stages and the Robin facet terms of the tile's boundary nodes -- issued
+  // back to back, prefetch first.
   double a0, a1, ah0, ah1, b0, b1, bh0, bh1;
-  fetch(r, q0 - 1, a0, a1);
-  fetch(hrow, q0 - 1, ah0, ah1);
+  fetch(vo_own, q0 - 1, a0, a1);
+  fetch(vo_halo, q0 - 1, ah0, ah1);
+  fetch(vo_own, q0, b0, b1);
+  fetch(vo_halo, q0, bh0, bh1);
+  // march-axis coefficients of the chunk and x-axis coefficients of the
+  // block's 64 columns, staged in LDS (read by every wave each plane; in VGPRs
+  // they would cost 12 registers for the whole march)
+  __shared__ double cql[kFaceChunk + 2][6];
+  __shared__ double cxl[6][kWave];
+  // (loads now; the LDS writes come after the face section, so that a single
+  // wait covers the prefetch, the stages and the face gathers)
+  // one coefficient per thread: thread e stages cql entry e (march axis) and
+  // cxl entry e (x axis: coefficient e / 64 of the block's column e % 64)
+  const bool st_q = (int)threadIdx.x < (q1 - q0 + 2) * 6;
+  const bool st_x = (int)threadIdx.x < 6 * kWave;
+  double cqv, cxv;
+  {
+    const int e = threadIdx.x;
+    const int qq = q0 - 1 + e / 6;
+    const bool okq = st_q && qq >= 0 && qq < nQ;
+    cqv = g.coef[qaxis][okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
+    cqv = okq ? cqv : 0.0;
+    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
+    const bool okx = st_x && ii >= 0 && ii < n0;
+    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + (e >> 6) : 0];
+    cxv = okx ? cxv : 0.0;
+  }
+  if (st_q) cql[threadIdx.x / 6][threadIdx.x % 6] = cqv;
+  if (st_x) cxl[threadIdx.x >> 6][threadIdx.x & (kWave - 1)] = cxv;
+  __syncthreads();
 
   double us_m = 0.0, us_c = 0.0, vs_m = 0.0, vs_c = 0.0, um_m = 0.0, um_c = 0.0;
   double xc = 0.0;  // own-row value of the centre plane (p of the output node)
@@ -520,13 +744,13 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
   auto step = [&](int L, double c0, double c1, double h0, double h1) {
     const int buf = L & 1;
     double v, vm;
-    combine(r, L, c0, c1, v, vm);
-    if (FUSEP && writer && row_ok && L >= q0 && L < q1) pout[(int64_t)i + sR * r + sQ * L] = v;
+    combine(vo_own, L, c0, c1, v, vm);
+    if (FUSEP) bstore(rsp, vo_wr + ((L >= q0 && L < q1) ? plane_off(L) : kBadOff), v);
     lds[0][buf][wave + 1][lane] = v;
     if (MODE == MODE_RES) lds[NA - 1][buf][wave + 1][lane] = vm;
     if (halo) {
       double hv, hvm;
-      combine(hrow, L, h0, h1, hv, hvm);
+      combine(vo_halo, L, h0, h1, hv, hvm);
       lds[0][buf][hslot][lane] = hv;
       if (MODE == MODE_RES) lds[NA - 1][buf][hslot][lane] = hvm;
     }
@@ -540,7 +764,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
                    m2 = lds[NA - 1][buf][wave + 2][lane];
       um_p = My0 * m0 + My1 * m1 + My2 * m2;
     }
-    if (L >= q0 + 1) {
+    if (L >= q0 + 1 && L <= q1) {
       const int q = L - 1;
       const double* cq = cql[q - q0 + 1];
       const double Mz0 = cq[C_MLO], Mz1 = cq[C_MDI], Mz2 = cq[C_MUP];
@@ -549,14 +773,14 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
                         da * (Kz0 * us_m + Kz1 * us_c + Kz2 * us_p);
       const double S2 = da * (Mz0 * us_m + Mz1 * us_c + Mz2 * us_p);
       const double S1m = shr1(S1), S1p = shl1(S1), S2m = shr1(S2), S2p = shl1(S2);
-      const double y = Mx0 * S1m + Mx1 * S1 + Mx2 * S1p + Kx0 * S2m + Kx1 * S2 + Kx2 * S2p;
+      const double y = cxl[C_MLO][lane] * S1m + cxl[C_MDI][lane] * S1 + cxl[C_MUP][lane] * S1p +
+                       cxl[C_KLO][lane] * S2m + cxl[C_KDI][lane] * S2 + cxl[C_KUP][lane] * S2p;
       const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
-      if (writer && row_ok && row_owned && q_owned) {
-        // Robin facet terms: k_cg_bapply (Jacobian) / k_cg_boundary (residual)
-        const double yb = y;
-        out[(int64_t)i + sR * r + sQ * q] = yb;
-        if (MODE == MODE_JAC) dot += xc * yb;
-      }
+      const bool wr = writer && row_ok && row_owned && q_owned;
+      // Robin facet terms: face workgroups (Jacobian) / k_cg_boundary (residual)
+      const double yb = y;
+      bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, yb);
+      if (MODE == MODE_JAC) dot += wr ? xc * yb : 0.0;
     }
     xc = x1;
     us_m = us_c; us_c = us_p;
@@ -566,19 +790,17 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
   // prefetch depth 2: three register sets rotate (3x unrolled), so two planes
   // of loads are in flight while a plane is combined, exchanged and computed
   double c0_, c1_, ch0, ch1;
-  fetch(r, q0, b0, b1);
-  fetch(hrow, q0, bh0, bh1);
+  // no early exits: steps past q1 only touch LDS (their stores are masked), so
+  // the three register sets keep fixed registers across the back edge
   for (int L = q0 - 1; L <= q1; L += 3) {
-    fetch(r, L + 2, c0_, c1_);
-    fetch(hrow, L + 2, ch0, ch1);
+    fetch(vo_own, L + 2, c0_, c1_);
+    fetch(vo_halo, L + 2, ch0, ch1);
     step(L, a0, a1, ah0, ah1);
-    if (L + 1 > q1) break;
-    fetch(r, L + 3, a0, a1);
-    fetch(hrow, L + 3, ah0, ah1);
+    fetch(vo_own, L + 3, a0, a1);
+    fetch(vo_halo, L + 3, ah0, ah1);
     step(L + 1, b0, b1, bh0, bh1);
-    if (L + 2 > q1) break;
-    fetch(r, L + 4, b0, b1);
-    fetch(hrow, L + 4, bh0, bh1);
+    fetch(vo_own, L + 4, b0, b1);
+    fetch(vo_halo, L + 4, bh0, bh1);
     step(L + 2, c0_, c1_, ch0, ch1);
   }
   if (MODE == MODE_JAC && partials != nullptr) {
@@ -591,6 +813,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
       for (int w = 0; w < R; ++w) s += red[w];
       store_partial(&partials[blockIdx.x], s);
     }
+    fused_reduce_tail<1>(rt, nrec);  // p.w over all tiles (+ KSPCG logic)
   }
 }
 
@@ -634,194 +857,24 @@ __global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t*
 }
 
 
-// Per-node 3x3 face stencils of the Robin facet Jacobian,
-//   B_I(u,v) = dt * sum_f int_f g'(T_h) phi_I phi_(u,v),
-// for every node of one physical boundary face (SoA: coefficient-major), built
-// once per Newton iteration (T is fixed during the linear solve) and applied
-// by the marching kernel.  Tangential axes (t1 < t2) in storage order.
-__global__ __launch_bounds__(kBlock) void k_cg_bstencil(CgGrid g, int face, const double* __restrict__ T,
-                                                        double* __restrict__ B) {
-  const int a = face >> 1, side = face & 1;
-  const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
-  const int n[3] = {g.n0, g.n1, g.n2};
-  const int64_t st[3] = {1, g.n0, (int64_t)g.n0 * g.n1};
-  const int64_t n2d = (int64_t)n[t1] * n[t2];
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n2d; t += (int64_t)gridDim.x * kBlock) {
-    int c[3];
-    c[t1] = (int)(t % n[t1]);
-    c[t2] = (int)(t / n[t1]);
-    c[a] = side ? n[a] - 1 : 0;
-    const int64_t me = (int64_t)c[0] + st[1] * c[1] + st[2] * c[2];
-    double Tp[3][3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        const int x1 = c[t1] + u - 1, x2 = c[t2] + v - 1;
-        const bool ok = x1 >= 0 && x1 < n[t1] && x2 >= 0 && x2 < n[t2];
-        Tp[u][v] = ok ? T[me + (int64_t)(u - 1) * st[t1] + (int64_t)(v - 1) * st[t2]] : 0.0;
-      }
-    const double* c1 = g.coef[t1] + (int64_t)c[t1] * C_NCOEF;
-    const double* c2 = g.coef[t2] + (int64_t)c[t2] * C_NCOEF;
-    double Bl[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-#pragma unroll
-    for (int s1 = 0; s1 < 2; ++s1) {
-      const double h1 = s1 ? c1[C_HHI] : c1[C_HLO];
-      if (!(h1 > 0.0)) continue;
-      const int o1 = s1 ? 1 : -1;
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const double h2 = s2 ? c2[C_HHI] : c2[C_HLO];
-        if (!(h2 > 0.0)) continue;
-        const int o2 = s2 ? 1 : -1;
-#pragma unroll
-        for (int q1 = 0; q1 < 3; ++q1) {
-          const double pc1 = s1 ? 1.0 - kGX[q1] : kGX[q1], po1 = 1.0 - pc1;
-#pragma unroll
-          for (int q2 = 0; q2 < 3; ++q2) {
-            const double pc2 = s2 ? 1.0 - kGX[q2] : kGX[q2], po2 = 1.0 - pc2;
-            const double phiI = pc1 * pc2;
-            const double Th = phiI * Tp[1][1] + po1 * pc2 * Tp[1 + o1][1] + pc1 * po2 * Tp[1][1 + o2] +
-                              po1 * po2 * Tp[1 + o1][1 + o2];
-            const double wg = kGW[q1] * h1 * kGW[q2] * h2 * dg_rad_conv(g, Th) * phiI;
-            Bl[1][1] += wg * phiI;
-            Bl[1 + o1][1] += wg * po1 * pc2;
-            Bl[1][1 + o2] += wg * pc1 * po2;
-            Bl[1 + o1][1 + o2] += wg * po1 * po2;
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) B[(u * 3 + v) * n2d + t] = g.dt * Bl[u][v];
-  }
-}
-
-
-// Robin facet Jacobian of the boundary nodes from the precomputed face
-// stencils (k_cg_bstencil): out[n] += sum_faces sum_uv B_f(u,v)[n] x[n + ...],
-// plus the matching p.w correction, then (in the last-arriving workgroup) the
-// reduction tail of the whole matvec.  Face-major: workgroups [off[f],
-// off[f+1]) sweep face f (uniform face per workgroup: coefficient planes and
-// in-face neighbours are contiguous rows); nodes that lie on two or three
-// physical faces (edges, corners) are skipped there and summed by the last
-// segment (off[6], off[7]) from the edge list, so no node is written twice.
-struct FaceBlocks {
-  int off[8];
-};
-
-__device__ __forceinline__ int n_phys_faces(const CgGrid& g, const int (&c)[3], const int (&n)[3]) {
-  int k = 0;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) k += ((c[a] == 0 && g.bnd[a][0]) || (c[a] == n[a] - 1 && g.bnd[a][1])) ? 1 : 0;
-  return k;
-}
-
-template <bool FUSEP>
-__global__ __launch_bounds__(kBlock) void k_cg_bapply(CgGrid g, const double* in0, const double* pB,
-                                                      double* __restrict__ out, const PcgState* __restrict__ st,
-                                                      double* __restrict__ partials, RedTail rt, int n_records,
-                                                      FaceBlocks fb) {
-  __shared__ double red[kBlock / kWave];
-  if (FUSEP && st->done) return;
-  const double* x = in0;
-  if (FUSEP) x = (st->it & 1) ? pB : in0;
-  const int n[3] = {g.n0, g.n1, g.n2};
-  const int64_t sst[3] = {1, g.n0, (int64_t)g.n0 * g.n1};
-  const int b = blockIdx.x;
-  int f = 0;
-  while (f < 7 && b >= fb.off[f + 1]) ++f;
-  const int nb = fb.off[f + 1] - fb.off[f];
-  const int lb = b - fb.off[f];
-  double dot = 0.0;
-  auto face_term = [&](int ff, const int (&c)[3], int64_t nd) {
-    const int a = ff >> 1;
-    const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
-    const int64_t n2d = (int64_t)n[t1] * n[t2];
-    const int64_t ix = (int64_t)c[t1] + (int64_t)n[t1] * c[t2];
-    const double* B = g.bst[ff];
-    double acc = 0.0;
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        const int a1 = c[t1] + u - 1, a2 = c[t2] + v - 1;
-        const bool ok = a1 >= 0 && a1 < n[t1] && a2 >= 0 && a2 < n[t2];
-        const int64_t o = ok ? nd + (int64_t)(u - 1) * sst[t1] + (int64_t)(v - 1) * sst[t2] : nd;
-        const double xv = x[o];
-        acc += B[(u * 3 + v) * n2d + ix] * (ok ? xv : 0.0);
-      }
-    return acc;
-  };
-  if (f < 6) {
-    const int a = f >> 1, side = f & 1;
-    const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
-    const int64_t n2d = (int64_t)n[t1] * n[t2];
-    for (int64_t ix = (int64_t)lb * kBlock + threadIdx.x; ix < n2d; ix += (int64_t)nb * kBlock) {
-      int c[3];
-      c[t1] = (int)(ix % n[t1]);
-      c[t2] = (int)(ix / n[t1]);
-      c[a] = side ? n[a] - 1 : 0;
-      if (c[2] < g.k_begin || c[2] >= g.k_end) continue;  // ghost plane of the partition axis
-      if (n_phys_faces(g, c, n) > 1) continue;            // edge / corner: summed below
-      const int64_t nd = (int64_t)c[0] + sst[1] * c[1] + sst[2] * c[2];
-      const double acc = face_term(f, c, nd);
-      out[nd] += acc;
-      dot += x[nd] * acc;
-    }
-  } else {
-    for (int64_t t = (int64_t)lb * kBlock + threadIdx.x; t < g.n_enodes; t += (int64_t)nb * kBlock) {
-      const int64_t nd = g.enodes[t];
-      const int c[3] = {(int)(nd % n[0]), (int)((nd / n[0]) % n[1]), (int)(nd / sst[2])};
-      double acc = 0.0;
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int side = (c[a] == 0 && g.bnd[a][0]) ? 0 : ((c[a] == n[a] - 1 && g.bnd[a][1]) ? 1 : -1);
-        if (side >= 0) acc += face_term(2 * a + side, c, nd);
-      }
-      out[nd] += acc;
-      dot += x[nd] * acc;
-    }
-  }
-  if (partials != nullptr) {
-    dot = wave_sum(dot);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) red[wave] = dot;
-    __syncthreads();
-    if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
-    fused_reduce_tail<1>(rt, n_records);  // p.w of the marching launch + this one
-  }
-}
-
-FaceBlocks face_blocks(const CgGrid& g) {
-  FaceBlocks fb{};
-  const int n[3] = {g.n0, g.n1, g.n2};
-  int acc = 0;
-  for (int f = 0; f < 6; ++f) {
-    fb.off[f] = acc;
-    const int a = f >> 1;
-    if (!g.bst[f]) continue;
-    const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
-    const int64_t n2d = (int64_t)n[t1] * n[t2];
-    acc += (int)std::min<int64_t>((n2d + kBlock - 1) / kBlock, 1024);
-  }
-  fb.off[6] = acc;
-  acc += (int)std::min<int64_t>((g.n_enodes + kBlock - 1) / kBlock, 256);
-  fb.off[7] = acc;
-  return fb;
-}
-
 int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 
 static int march_rows() {
   static int rows = 0;
   if (!rows) {
     const char* e = getenv("TVFEM_MARCH_ROWS");
-    rows = (e && atoi(e) == 8) ? 8 : kRows;
+    rows = (e && atoi(e) == 16) ? 16 : kRows;
   }
   return rows;
+}
+
+static int march_minblk() {  // workgroups the march grid is chunked up to (TVFEM_MARCH_MINBLK)
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("TVFEM_MARCH_MINBLK");
+    v = (e && atoi(e) > 0) ? atoi(e) : 1024;
+  }
+  return v;
 }
 
 struct Launch {
@@ -838,7 +891,9 @@ bool use_march(const CgGrid& g) {
     const char* e = getenv("TVFEM_CG_KERNEL");
     g_force_rows = (e && e[0] == 'r') ? 1 : 0;
   }
-  return dim_of(g) == 3 && !g_force_rows;
+  // the marching kernel addresses the fields with 32-bit buffer offsets
+  const int64_t bytes = (int64_t)g.n0 * g.n1 * g.n2 * 8;
+  return dim_of(g) == 3 && !g_force_rows && bytes < (int64_t)kBadOff;
 }
 
 int bnd_blocks(const CgGrid& g) {
@@ -861,12 +916,14 @@ Launch plan(const CgGrid& g, bool ghosts) {
     const int nrb = (nR + L.rows - 1) / L.rows;
     // enough workgroups to fill 256 CUs x ~4: split the march into chunks
     int nchunks = 1;
-    while ((int64_t)L.nseg * nrb * nchunks < 512 && nQ / (nchunks * 2) >= 12) nchunks *= 2;
-    while ((nQ + nchunks - 1) / nchunks > kMaxChunk) ++nchunks;
+    const int minblk = march_minblk();
+    while ((int64_t)L.nseg * nrb * nchunks < minblk && nQ / (nchunks * 2) >= 6) nchunks *= 2;
+    while ((nQ + nchunks - 1) / nchunks > kFaceChunk) ++nchunks;  // LDS coefficient stage bound
     L.qchunk = (nQ + nchunks - 1) / nchunks;
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
     L.blocks = L.nseg * nrb * nchunks;
-    L.nparts = L.blocks + (g.n_bnodes > 0 ? std::max(bnd_blocks(g), (g.bst_ok ? face_blocks(g).off[7] : 0)) : 0);
+    // Jacobian partial records: one per marching tile and face workgroup
+    L.nparts = L.blocks + face_offsets(g, L.rows * kWave).off[6];
     return L;
   }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
@@ -889,23 +946,26 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
   const Launch L = plan(g, ghosts);
   if (L.blocks <= 0) return false;
   if (L.march) {
-    if (L.rows == 8)
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8>), dim3(L.blocks), dim3(8 * kWave), 0, s, g, T, in0, in1, out,
-                         pout, st, partials, L.nseg, L.raxis, L.qchunk);
+    // Jacobian: the Robin facet terms come from k_cg_faces (launched first)
+    // and are added inside the marching launch, which also runs the p.w
+    // reduction tail
+    const bool folded = MODE == MODE_JAC;
+    RedTail rt{};
+    if (folded && tail && partials) rt = *tail;
+    const FaceOff fo = folded ? face_offsets(g, L.rows * kWave) : FaceOff{};
+    const int grid = L.blocks + fo.off[6];
+    if (L.rows == 16)
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16>), dim3(grid), dim3(16 * kWave), 0, s, g, T, in0, in1,
+                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo);
     else
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16>), dim3(L.blocks), dim3(16 * kWave), 0, s, g, T, in0, in1, out,
-                         pout, st, partials, L.nseg, L.raxis, L.qchunk);
-    if (g.n_bnodes > 0 && MODE == MODE_JAC && g.bst_ok) {
-      RedTail rt{};
-      if (tail && partials) rt = *tail;
-      const FaceBlocks fb = face_blocks(g);
-      if (fb.off[7] > 0) {
-        hipLaunchKernelGGL((k_cg_bapply<FUSEP>), dim3(fb.off[7]), dim3(kBlock), 0, s, g, FUSEP ? in1 : in0, pout,
-                           out, st, partials ? partials + L.blocks : nullptr, rt, L.nparts, fb);
-        return rt.counter != nullptr;
-      }
-      return false;
-    } else if (g.n_bnodes > 0) {
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
+                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo);
+    if (folded && !FUSEP && fo.off[6] > 0) {  // complete J x (the fused PCG adds them in the update)
+      const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.n_bnodes + kBlock - 1) / kBlock, 1024));
+      hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, g.bnodes, g.n_bnodes, out);
+    }
+    if (folded) return rt.counter != nullptr;
+    if (g.n_bnodes > 0) {
       hipLaunchKernelGGL((k_cg_boundary<MODE, FUSEP>), dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, g.bnodes,
                          g.n_bnodes, T, FUSEP ? in1 : in0, pout, out, st,
                          partials ? partials + L.blocks : nullptr);
@@ -932,6 +992,20 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
 
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }
 
+FaceAdd cg_face_add(const CgGrid& g, int64_t t_off) {
+  FaceAdd fa{};
+  if (!use_march(g)) return fa;  // the row kernel keeps the facet terms inline
+  fa.on = 1;
+  fa.n0 = g.n0;
+  fa.n1 = g.n1;
+  fa.n2 = g.n2;
+  fa.t_off = t_off;
+  fa.inv_n0 = 1.0 / g.n0;
+  fa.inv_plane = 1.0 / ((double)g.n0 * g.n1);
+  for (int f = 0; f < 6; ++f) fa.ff[f] = g.fface[f];
+  return fa;
+}
+
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
   launch_rows<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, false, s);
 }
@@ -950,16 +1024,6 @@ bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, d
   const bool fused = launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s, tail);
   if (n_partials) *n_partials = plan(g, true).nparts;
   return fused;
-}
-
-void launch_cg_bstencil(const CgGrid& g, const double* T, hipStream_t s) {
-  if (!g.bst_ok) return;
-  for (int f = 0; f < 6; ++f) {
-    if (!g.bst[f]) continue;
-    const int64_t n2d = g.bst_n[f] * (int64_t)g.bst_m[f];
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n2d + kBlock - 1) / kBlock, 2048));
-    hipLaunchKernelGGL(k_cg_bstencil, dim3(blocks), dim3(kBlock), 0, s, g, f, T, g.bst[f]);
-  }
 }
 
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {

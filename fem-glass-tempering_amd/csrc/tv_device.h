@@ -50,9 +50,22 @@ __device__ __forceinline__ void block_reduce_records(const double* partials, int
   double acc[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) acc[w] = 0.0;
-  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+  // U records per thread in flight at once (the loads are independent; a
+  // one-record loop would serialise n / blockDim HBM latencies), summed in a
+  // fixed order so the result stays bitwise reproducible.
+  constexpr int U = 8;
+  for (int base = threadIdx.x; base < n; base += blockDim.x * U) {
+    double v[U][W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) acc[w] += load_partial(&partials[(int64_t)t * W + w]);
+    for (int u = 0; u < U; ++u) {
+      const int t = base + u * (int)blockDim.x;
+#pragma unroll
+      for (int w = 0; w < W; ++w) v[u][w] = (t < n) ? load_partial(&partials[(int64_t)t * W + w]) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int w = 0; w < W; ++w) acc[w] += v[u][w];
   }
 #pragma unroll
   for (int w = 0; w < W; ++w) {

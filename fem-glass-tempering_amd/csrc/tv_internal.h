@@ -36,13 +36,11 @@ struct CgGrid {
   double T_amb, T_amb4;
   const int64_t* bnodes;      // owned nodes on physical boundary faces (3D marching path)
   int64_t n_bnodes;
-  // Robin facet Jacobian stencils per face f = 2*axis + side (3D marching path):
-  // 9 coefficient planes of bst_n[f] x bst_m[f] face nodes (tangential axes t1 < t2)
-  double* bst[6];
-  int bst_n[6], bst_m[6];
-  int bst_ok;
-  const int64_t* enodes;      // owned nodes on >= 2 physical faces (edges, corners)
-  int64_t n_enodes;
+  // Robin facet Jacobian terms per physical face f = 2*axis + side (3D marching
+  // path): one value per face node, fface[f][c_t1 + fn1[f] * c_t2] (tangential
+  // axes t1 < t2), rewritten by k_cg_faces before every Jacobian application
+  double* fface[6];
+  int fn1[6], fn2[6];
 };
 
 // Grid of the DG1 temperature space: cells per storage axis; dof layout is
@@ -117,7 +115,6 @@ bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, d
                             double* w, const PcgState* st, double* partials, int* n_partials,
                             hipStream_t s, const RedTail* tail = nullptr);
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
-void launch_cg_bstencil(const CgGrid& g, const double* T, hipStream_t s);
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 
 void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
@@ -137,9 +134,20 @@ constexpr int kVecBlocks = 1024;
 void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx,
                      double* partials, hipStream_t s);
 // p is taken from buffer (st->it & 1 ? pB : pA), matching the fused matvec
+// Robin facet terms the fused CG matvec leaves out of w (marching path): the
+// PCG update adds fface at the owned boundary nodes (see k_cg_march)
+struct FaceAdd {
+  int on;
+  int n0, n1, n2;
+  int64_t t_off;             // local index of the first owned node
+  double inv_n0, inv_plane;  // 1/n0, 1/(n0 n1) (index -> coordinates)
+  const double* ff[6];
+};
+FaceAdd cg_face_add(const CgGrid& g, int64_t t_off);
+
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* dinv, double* dx, double* r, double* z, double* partials,
-                       hipStream_t s, const RedTail* tail = nullptr);
+                       hipStream_t s, const RedTail* tail = nullptr, const FaceAdd* fa = nullptr);
 // one-block deterministic reduce of n records of width W (<= 2) into out[W];
 // kind: 0 none, 1 PCG init logic, 2 PCG p.w logic, 3 PCG update logic
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,

@@ -51,20 +51,46 @@ __global__ __launch_bounds__(kBlock) void k_pcg_init(int64_t n, const double* __
   block_partials<2>(acc, partials);
 }
 
+// Robin facet terms of node t (local index t + t_off) left out of w by the
+// fused CG matvec (marching path); 0 off the physical boundary faces
+__device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
+  const int nd = (int)(t + fa.t_off);
+  const int plane = fa.n0 * fa.n1;
+  int k = (int)((double)nd * fa.inv_plane);
+  k -= (k * plane > nd) ? 1 : 0;
+  k += ((k + 1) * plane <= nd) ? 1 : 0;
+  const int rem = nd - k * plane;
+  int j = (int)((double)rem * fa.inv_n0);
+  j -= (j * fa.n0 > rem) ? 1 : 0;
+  j += ((j + 1) * fa.n0 <= rem) ? 1 : 0;
+  const int i = rem - j * fa.n0;
+  double add = 0.0;
+  if (i == 0 && fa.ff[0]) add += fa.ff[0][j + fa.n1 * k];
+  if (i == fa.n0 - 1 && fa.ff[1]) add += fa.ff[1][j + fa.n1 * k];
+  if (j == 0 && fa.ff[2]) add += fa.ff[2][i + fa.n0 * k];
+  if (j == fa.n1 - 1 && fa.ff[3]) add += fa.ff[3][i + fa.n0 * k];
+  if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
+  if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
+  return add;
+}
+
+template <bool FACES>
 __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState* __restrict__ st,
                                                        const double* __restrict__ pA,
                                                        const double* __restrict__ pB,
                                                        const double* __restrict__ w,
                                                        const double* __restrict__ dinv, double* __restrict__ dx,
                                                        double* __restrict__ r, double* __restrict__ z,
-                                                       double* __restrict__ partials, RedTail rt) {
+                                                       double* __restrict__ partials, RedTail rt, FaceAdd fa) {
   if (st->done) return;
   const double a = st->a;
   const double* __restrict__ p = (st->it & 1) ? pB : pA;
   double acc[2] = {0.0, 0.0};
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     dx[t] += a * p[t];                    // x <- x + a p
-    const double rr = r[t] - a * w[t];    // r <- r - a w
+    double wt = w[t];
+    if (FACES) wt += face_terms(fa, t);   // w = J p incl. the Robin facet terms
+    const double rr = r[t] - a * wt;      // r <- r - a w
     r[t] = rr;
     const double zz = dinv[t] * rr;       // z <- B r
     z[t] = zz;
@@ -144,11 +170,15 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* dinv, double* dx, double* r, double* z, double* partials, hipStream_t s,
-                       const RedTail* tail) {
+                       const RedTail* tail, const FaceAdd* fa) {
   RedTail rt{};
   if (tail) rt = *tail;
-  hipLaunchKernelGGL(k_pcg_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx, r, z,
-                     partials, rt);
+  if (fa && fa->on)
+    hipLaunchKernelGGL(k_pcg_update<true>, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx, r,
+                       z, partials, rt, *fa);
+  else
+    hipLaunchKernelGGL(k_pcg_update<false>, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx,
+                       r, z, partials, rt, FaceAdd{});
 }
 
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s) {

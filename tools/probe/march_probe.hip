@@ -1,0 +1,344 @@
+// Micro-benchmark of 27-point tensor-product stencil sweeps on the C4 grid
+// (401 x 51 x 401 nodes, x fastest), to find what bounds the marching matvec.
+//   A: LDS-slab march (the library's design), R waves = R rows, prefetch depth 2
+//   B: register march, every wave independent (rows r-1, r, r+1 loaded by the wave)
+//   C: streaming copy references (8 B and 16 B per lane)
+// hipcc -O3 --offload-arch=gfx950 march_probe.hip -o march_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP error %s at %d\n",hipGetErrorString(e),__LINE__); exit(1);}}while(0)
+
+constexpr int W = 64, SEG = 62;
+
+__device__ __forceinline__ double shr1(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double shl1(double v) {
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+struct Grid { int n0, nQ, nR; long sQ, sR; };
+__constant__ double cM[3] = {1.0 / 6, 2.0 / 3, 1.0 / 6};
+__constant__ double cK[3] = {-1.0, 2.0, -1.0};
+
+__device__ __forceinline__ int remap(int b, int nb, bool xcd) {
+  if (!xcd) return b;
+  const int q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// ---------------- A: LDS slab march ------------------------------------------
+template <int R, bool STORE, bool XCD>
+__global__ __launch_bounds__(R * W) void kA(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                            int nseg, int qchunk) {
+  __shared__ double lds[2][R + 2][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int b = remap(blockIdx.x, gridDim.x, XCD);
+  const int seg = b % nseg, t = b / nseg, rb = t % nrb, chunk = t / nrb;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool writer = col_ok && lane >= 1 && lane <= SEG && r < g.nR;
+  const bool halo = wave == 0 || wave == R - 1;
+  const int hrow = wave == 0 ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
+  const int hslot = wave == 0 ? 0 : R + 1;
+  const double My0 = cM[0], My1 = cM[1], My2 = cM[2], Ky0 = cK[0], Ky1 = cK[1], Ky2 = cK[2];
+  const double da = 0.1;
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ; };
+  auto fetch = [&](int rr, int L) {
+    const long idx = okf(rr, L) ? (long)i + g.sR * rr + g.sQ * L : 0;
+    return in[idx];
+  };
+  double a = fetch(r, q0 - 1), ah = fetch(hrow, q0 - 1);
+  double bb = fetch(r, q0), bh = fetch(hrow, q0);
+  double c, ch;
+  double us_m = 0, us_c = 0, vs_m = 0, vs_c = 0;
+  auto step = [&](int L, double v, double hv) {
+    const int buf = L & 1;
+    v = okf(r, L) ? v : 0.0;
+    hv = okf(hrow, L) ? hv : 0.0;
+    lds[buf][wave + 1][lane] = v;
+    if (halo) lds[buf][hslot][lane] = hv;
+    __syncthreads();
+    const double x0 = lds[buf][wave][lane], x1 = lds[buf][wave + 1][lane], x2 = lds[buf][wave + 2][lane];
+    const double us_p = My0 * x0 + My1 * x1 + My2 * x2;
+    const double vs_p = Ky0 * x0 + Ky1 * x1 + Ky2 * x2;
+    if (L >= q0 + 1 && L <= q1) {
+      const double S1 = cM[0] * (us_m + da * vs_m) + cM[1] * (us_c + da * vs_c) + cM[2] * (us_p + da * vs_p) +
+                        da * (cK[0] * us_m + cK[1] * us_c + cK[2] * us_p);
+      const double S2 = da * (cM[0] * us_m + cM[1] * us_c + cM[2] * us_p);
+      const double y = cM[0] * shr1(S1) + cM[1] * S1 + cM[2] * shl1(S1) + cK[0] * shr1(S2) + cK[1] * S2 +
+                       cK[2] * shl1(S2);
+      if (writer && (STORE || y == 12345.678)) out[(long)i + g.sR * r + g.sQ * (L - 1)] = y;
+    }
+    us_m = us_c; us_c = us_p; vs_m = vs_c; vs_c = vs_p;
+  };
+  for (int L = q0 - 1; L <= q1; L += 3) {
+    c = fetch(r, L + 2); ch = fetch(hrow, L + 2);
+    step(L, a, ah);
+    a = fetch(r, L + 3); ah = fetch(hrow, L + 3);
+    step(L + 1, bb, bh);
+    bb = fetch(r, L + 4); bh = fetch(hrow, L + 4);
+    step(L + 2, c, ch);
+  }
+}
+
+// ---------------- A2: kA + face prologue on the first / last chunk -----------
+// 27 independent loads per lane (9 face-stencil planes B + 9 x values of a 3x3
+// in-plane patch, twice) into LDS before the march; added at the face planes.
+template <int R, int PRO>
+__global__ __launch_bounds__(R * W) void kA2(Grid g, const double* __restrict__ in, const double* __restrict__ Bf,
+                                             double* __restrict__ out, int nseg, int qchunk) {
+  __shared__ double lds[2][R + 2][W];
+  __shared__ double fq[2][R][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int nch = (g.nQ + qchunk - 1) / qchunk;
+  const int b = remap(blockIdx.x, gridDim.x, true);
+  const int chunk = b % nch, t = b / nch, seg = t % nseg, rb = t / nseg;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool writer = col_ok && lane >= 1 && lane <= SEG && r < g.nR;
+  const bool halo = wave == 0 || wave == R - 1;
+  const int hrow = wave == 0 ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
+  const int hslot = wave == 0 ? 0 : R + 1;
+  const double da = 0.1;
+  const bool h0 = PRO && q0 == 0, h1 = PRO && q1 == g.nQ;
+  const long n2d = (long)g.n0 * g.nR;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    if (!(side ? h1 : h0)) continue;
+    const int qf = side ? g.nQ - 1 : 0;
+    double bv[9], zv[9], ov[9];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const int k = u * 3 + v;
+        const int ii = min(max(i + u - 1, 0), g.n0 - 1), rr = min(max(r + v - 1, 0), g.nR - 1);
+        const long o = (long)ii + g.sR * rr + g.sQ * qf;
+        bv[k] = Bf[k * n2d + (col_ok && r < g.nR ? (long)i + (long)g.n0 * r : 0)];
+        zv[k] = in[o];
+        ov[k] = in[o + 1];
+      }
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc += bv[k] * (zv[k] + 0.5 * ov[k]);
+    fq[side][wave][lane] = acc;
+  }
+  __syncthreads();
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ; };
+  auto fetch = [&](int rr, int L) {
+    const long idx = okf(rr, L) ? (long)i + g.sR * rr + g.sQ * L : 0;
+    return in[idx];
+  };
+  double a = fetch(r, q0 - 1), ah = fetch(hrow, q0 - 1);
+  double bb = fetch(r, q0), bh = fetch(hrow, q0);
+  double c, ch;
+  double us_m = 0, us_c = 0, vs_m = 0, vs_c = 0;
+  auto step = [&](int L, double v, double hv) {
+    const int buf = L & 1;
+    v = okf(r, L) ? v : 0.0;
+    hv = okf(hrow, L) ? hv : 0.0;
+    lds[buf][wave + 1][lane] = v;
+    if (halo) lds[buf][hslot][lane] = hv;
+    __syncthreads();
+    const double x0 = lds[buf][wave][lane], x1 = lds[buf][wave + 1][lane], x2 = lds[buf][wave + 2][lane];
+    const double us_p = cM[0] * x0 + cM[1] * x1 + cM[2] * x2;
+    const double vs_p = cK[0] * x0 + cK[1] * x1 + cK[2] * x2;
+    if (L >= q0 + 1 && L <= q1) {
+      const double S1 = cM[0] * (us_m + da * vs_m) + cM[1] * (us_c + da * vs_c) + cM[2] * (us_p + da * vs_p) +
+                        da * (cK[0] * us_m + cK[1] * us_c + cK[2] * us_p);
+      const double S2 = da * (cM[0] * us_m + cM[1] * us_c + cM[2] * us_p);
+      double y = cM[0] * shr1(S1) + cM[1] * S1 + cM[2] * shl1(S1) + cK[0] * shr1(S2) + cK[1] * S2 +
+                 cK[2] * shl1(S2);
+      if (h0 && L - 1 == 0) y += fq[0][wave][lane];
+      if (h1 && L - 1 == g.nQ - 1) y += fq[1][wave][lane];
+      if (writer) out[(long)i + g.sR * r + g.sQ * (L - 1)] = y;
+    }
+    us_m = us_c; us_c = us_p; vs_m = vs_c; vs_c = vs_p;
+  };
+  for (int L = q0 - 1; L <= q1; L += 3) {
+    c = fetch(r, L + 2); ch = fetch(hrow, L + 2);
+    step(L, a, ah);
+    a = fetch(r, L + 3); ah = fetch(hrow, L + 3);
+    step(L + 1, bb, bh);
+    bb = fetch(r, L + 4); bh = fetch(hrow, L + 4);
+    step(L + 2, c, ch);
+  }
+}
+
+// ---------------- B: register march, waves independent ----------------------
+// WPB waves per block, consecutive rows; each wave loads rows r-1, r, r+1.
+template <int WPB, bool XCD>
+__global__ __launch_bounds__(WPB * W) void kB(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                              int nseg, int qchunk) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + WPB - 1) / WPB;
+  const int b = remap(blockIdx.x, gridDim.x, XCD);
+  const int seg = b % nseg, t = b / nseg, rb = t % nrb, chunk = t / nrb;
+  const int r = rb * WPB + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool writer = col_ok && lane >= 1 && lane <= SEG && r < g.nR;
+  const double da = 0.1;
+  auto ld = [&](int rr, int L) {
+    const bool ok = col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ;
+    return in[ok ? (long)i + g.sR * rr + g.sQ * L : 0];
+  };
+  auto okp = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ; };
+  double a0 = ld(r - 1, q0 - 1), a1 = ld(r, q0 - 1), a2 = ld(r + 1, q0 - 1);
+  double b0 = ld(r - 1, q0), b1 = ld(r, q0), b2 = ld(r + 1, q0);
+  double c0, c1, c2;
+  double us_m = 0, us_c = 0, vs_m = 0, vs_c = 0;
+  auto step = [&](int L, double x0, double x1, double x2) {
+    x0 = okp(r - 1, L) ? x0 : 0.0;
+    x1 = okp(r, L) ? x1 : 0.0;
+    x2 = okp(r + 1, L) ? x2 : 0.0;
+    const double us_p = cM[0] * x0 + cM[1] * x1 + cM[2] * x2;
+    const double vs_p = cK[0] * x0 + cK[1] * x1 + cK[2] * x2;
+    if (L >= q0 + 1 && L <= q1) {
+      const double S1 = cM[0] * (us_m + da * vs_m) + cM[1] * (us_c + da * vs_c) + cM[2] * (us_p + da * vs_p) +
+                        da * (cK[0] * us_m + cK[1] * us_c + cK[2] * us_p);
+      const double S2 = da * (cM[0] * us_m + cM[1] * us_c + cM[2] * us_p);
+      const double y = cM[0] * shr1(S1) + cM[1] * S1 + cM[2] * shl1(S1) + cK[0] * shr1(S2) + cK[1] * S2 +
+                       cK[2] * shl1(S2);
+      if (writer) out[(long)i + g.sR * r + g.sQ * (L - 1)] = y;
+    }
+    us_m = us_c; us_c = us_p; vs_m = vs_c; vs_c = vs_p;
+  };
+  for (int L = q0 - 1; L <= q1; L += 3) {
+    c0 = ld(r - 1, L + 2); c1 = ld(r, L + 2); c2 = ld(r + 1, L + 2);
+    step(L, a0, a1, a2);
+    a0 = ld(r - 1, L + 3); a1 = ld(r, L + 3); a2 = ld(r + 1, L + 3);
+    step(L + 1, b0, b1, b2);
+    b0 = ld(r - 1, L + 4); b1 = ld(r, L + 4); b2 = ld(r + 1, L + 4);
+    step(L + 2, c0, c1, c2);
+  }
+}
+
+__global__ void copy1(const double* __restrict__ a, double* __restrict__ b, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
+}
+__global__ void copy2(const double2* __restrict__ a, double2* __restrict__ b, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+template <typename F>
+float timeit(F f, int reps, hipEvent_t e0, hipEvent_t e1) {
+  f();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0));
+  for (int k = 0; k < reps; ++k) f();
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1e3f / reps;  // us
+}
+
+int chunks_for(int cols, int nQ, int minblk) {
+  int n = 1;
+  while (cols * n < minblk && nQ / (n * 2) >= 6) n *= 2;
+  return n;
+}
+
+int main(int argc, char** argv) {
+  Grid g{401, 51, 401, 401, 401L * 51};
+  const long N = (long)g.n0 * g.nQ * g.nR;
+  double *x, *y, *fl;
+  CK(hipMalloc(&x, N * 8));
+  CK(hipMalloc(&y, N * 8));
+  CK(hipMalloc(&fl, 1L << 30));
+  std::vector<double> h(N);
+  for (long k = 0; k < N; ++k) h[k] = 1.0 + 1e-3 * (k % 977);
+  CK(hipMemcpy(x, h.data(), N * 8, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 50;
+  const double bytes = 16.0 * N;
+  const int nseg = (g.n0 + SEG - 1) / SEG;
+  auto rep = [&](const char* name, float us, int blocks) {
+    printf("%-44s %8.2f us  %7.1f GB/s  blocks %d\n", name, us, bytes / (us * 1e-6) / 1e9, blocks);
+  };
+  rep("copy1 (8B/lane)", timeit([&] { copy1<<<4096, 256>>>(x, y, N); }, reps, e0, e1), 4096);
+  rep("copy2 (16B/lane)", timeit([&] { copy2<<<4096, 256>>>((double2*)x, (double2*)y, N / 2); }, reps, e0, e1), 4096);
+  for (int minblk : {512, 1024, 2048}) {
+#define RUN_A(RR, ST, XC)                                                                                  \
+  {                                                                                                        \
+    const int nrb = (g.nR + RR - 1) / RR;                                                                  \
+    const int nch = chunks_for(nseg * nrb, g.nQ, minblk);                                                  \
+    const int qc = (g.nQ + nch - 1) / nch;                                                                 \
+    const int nb = nseg * nrb * ((g.nQ + qc - 1) / qc);                                                    \
+    char nm[96];                                                                                           \
+    snprintf(nm, sizeof nm, "A R=%d store=%d xcd=%d minblk=%d", RR, ST, XC, minblk);                      \
+    rep(nm, timeit([&] { kA<RR, ST, XC><<<nb, RR * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nb);         \
+  }
+    RUN_A(16, true, false)
+    RUN_A(8, true, false)
+    RUN_A(8, false, false)
+    RUN_A(8, true, true)
+    RUN_A(4, true, true)
+#define RUN_B(WW, XC)                                                                                      \
+  {                                                                                                        \
+    const int nrb = (g.nR + WW - 1) / WW;                                                                  \
+    const int nch = chunks_for(nseg * nrb, g.nQ, minblk);                                                  \
+    const int qc = (g.nQ + nch - 1) / nch;                                                                 \
+    const int nb = nseg * nrb * ((g.nQ + qc - 1) / qc);                                                    \
+    char nm[96];                                                                                           \
+    snprintf(nm, sizeof nm, "B wpb=%d xcd=%d minblk=%d", WW, XC, minblk);                                 \
+    rep(nm, timeit([&] { kB<WW, XC><<<nb, WW * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nb);             \
+  }
+    RUN_B(4, false)
+    RUN_B(4, true)
+    RUN_B(8, true)
+    RUN_B(2, true)
+  }
+  {
+    double* Bf;
+    CK(hipMalloc(&Bf, 9L * g.n0 * g.nR * 8));
+    CK(hipMemset(Bf, 0, 9L * g.n0 * g.nR * 8));
+    for (int minblk : {512, 1024, 2048}) {
+      const int nrb = (g.nR + 7) / 8;
+      const int nch = chunks_for(nseg * nrb, g.nQ, minblk);
+      const int qc = (g.nQ + nch - 1) / nch;
+      const int nb = nseg * nrb * ((g.nQ + qc - 1) / qc);
+      char nm[96];
+      snprintf(nm, sizeof nm, "A2 R=8 no-prologue minblk=%d", minblk);
+      rep(nm, timeit([&] { kA2<8, 0><<<nb, 8 * W>>>(g, x, Bf, y, nseg, qc); }, reps, e0, e1), nb);
+      snprintf(nm, sizeof nm, "A2 R=8 prologue minblk=%d", minblk);
+      rep(nm, timeit([&] { kA2<8, 1><<<nb, 8 * W>>>(g, x, Bf, y, nseg, qc); }, reps, e0, e1), nb);
+    }
+  }
+  // correctness cross-check A vs B
+  {
+    const int nrb8 = (g.nR + 7) / 8, nrb4 = (g.nR + 3) / 4;
+    kA<8, true, false><<<nseg * nrb8, 8 * W>>>(g, x, y, nseg, g.nQ);
+    std::vector<double> ya(N), yb(N);
+    CK(hipMemcpy(ya.data(), y, N * 8, hipMemcpyDeviceToHost));
+    CK(hipMemset(y, 0, N * 8));
+    kB<4, true><<<nseg * nrb4, 4 * W>>>(g, x, y, nseg, g.nQ);
+    CK(hipMemcpy(yb.data(), y, N * 8, hipMemcpyDeviceToHost));
+    double md = 0;
+    for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
+    printf("max |A-B| = %g\n", md);
+  }
+  return 0;
+}
