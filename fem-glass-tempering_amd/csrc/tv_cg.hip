@@ -609,7 +609,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
                                                         const PcgState* __restrict__ st,
                                                         double* __restrict__ partials, int nseg, int raxis,
                                                         int qchunk, RedTail rt, int nrec, int nmarch,
-                                                        FaceOff fo) {
+                                                        FaceOff fo, int ffirst) {
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
   __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
   __shared__ double red[R];
@@ -618,8 +618,13 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
   // terms of the boundary faces (k_face_block) -- independent work that fills
   // the tail of the march; the terms go to g.fface and are added to w by the
   // consumer (PCG update / k_cg_addfaces), their p.w share joins the partials
-  if (MODE == MODE_JAC && (int)blockIdx.x >= nmarch) {
-    face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec, (int)blockIdx.x - nmarch, fo);
+  // face workgroups first (dispatched early, alongside the first marching
+  // round) or last (ffirst = 0)
+  const int nface = (int)gridDim.x - nmarch;
+  const int bid = ffirst ? (int)blockIdx.x - nface : (int)blockIdx.x;
+  if (MODE == MODE_JAC && (bid < 0 || bid >= nmarch)) {
+    face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec,
+                         ffirst ? (int)blockIdx.x : (int)blockIdx.x - nmarch, fo);
     return;
   }
   const int lane = threadIdx.x & (kWave - 1);
@@ -635,7 +640,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* 
   // all their chunks -- neighbouring tiles share L2, and the boundary tiles
   // (first / last chunk, first / last segment) spread evenly over the XCDs
   const int nch = (nQ + qchunk - 1) / qchunk;
-  const int b = xcd_remap(blockIdx.x, nmarch);
+  const int b = xcd_remap(bid, nmarch);
   const int chunk = b % nch;
   const int t = b / nch;
   const int seg = t % nseg;
@@ -877,6 +882,15 @@ static int march_minblk() {  // workgroups the march grid is chunked up to (TVFE
   return v;
 }
 
+static int face_first() {  // face workgroups ahead of the marching tiles (TVFEM_FACE_FIRST=0|1)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("TVFEM_FACE_FIRST");
+    v = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  return v;
+}
+
 struct Launch {
   int blocks, nseg, kfirst, nplanes, wmode, rows;
   int nparts;  // partial records written (JAC)
@@ -956,10 +970,10 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     const int grid = L.blocks + fo.off[6];
     if (L.rows == 16)
       hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16>), dim3(grid), dim3(16 * kWave), 0, s, g, T, in0, in1,
-                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo);
+                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
     else
       hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
-                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo);
+                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
     if (folded && !FUSEP && fo.off[6] > 0) {  // complete J x (the fused PCG adds them in the update)
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.n_bnodes + kBlock - 1) / kBlock, 1024));
       hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, g.bnodes, g.n_bnodes, out);
