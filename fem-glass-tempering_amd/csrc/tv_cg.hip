@@ -462,12 +462,14 @@ struct FaceOff {
   int off[7];  // workgroup ranges per face f (in marching-workgroup units), off[6] = total
 };
 
-FaceOff face_offsets(const CgGrid& g, int threads) {
+// face tiles: kSeg nodes along t1 (one wavefront, two halo lanes) x `rows`
+// nodes along t2 (one wavefront per row)
+FaceOff face_offsets(const CgGrid& g, int rows) {
   FaceOff fo{};
   int acc = 0;
   for (int f = 0; f < 6; ++f) {
     fo.off[f] = acc;
-    if (g.fface[f]) acc += (2 * g.fn1[f] * g.fn2[f] + threads - 1) / threads;  // 2 threads per node
+    if (g.fface[f]) acc += ((g.fn1[f] + kSeg - 1) / kSeg) * ((g.fn2[f] + rows - 1) / rows);
   }
   fo.off[6] = acc;
   return fo;
@@ -498,15 +500,19 @@ __device__ __forceinline__ double facet_jac_one(const CgGrid& g, double h1, doub
   return acc;
 }
 
-// One face workgroup of the marching launch (Jacobian mode): face node per
-// thread, p = z + beta/betaold p_old (fused PCG) or p = x; writes fface and the
-// workgroup's p.(facet terms) partial record; takes part in the reduction tail.
+// One face workgroup of the marching launch (Jacobian mode): a tile of kSeg x R
+// nodes of face f.  Each wavefront stages one face row of T and p (p = z +
+// beta/betaold p_old in the fused PCG, else p = x) in LDS (waves 0 and R-1
+// also the two halo rows), then every node takes its 3x3 patch from LDS and
+// the adjacent lanes: ~4 loads per node instead of 27 gathers.  Writes fface
+// and the workgroup's p.(facet terms) record; takes part in the tail.
 template <bool FUSEP, int R>
 __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const double* __restrict__ in0,
                            const double* pA, const double* pB, const PcgState* __restrict__ st,
                            double* __restrict__ partials, const RedTail& rt, int nrec, int fb,
                            const FaceOff& fo) {
   __shared__ double redf[R];
+  __shared__ double sT[R + 2][kWave], sP[R + 2][kWave];
   int f = 0;
   while (f < 5 && fb >= fo.off[f + 1]) ++f;
   const int a = f >> 1, side = f & 1;
@@ -514,7 +520,14 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
   const int n[3] = {g.n0, g.n1, g.n2};
   const int sst[3] = {1, g.n0, g.n0 * g.n1};
   const int n1 = n[t1], n2 = n[t2];
-  const int t = (fb - fo.off[f]) * (R * kWave) + threadIdx.x;  // 2 threads per face node
+  const int nseg1 = (n1 + kSeg - 1) / kSeg;
+  const int tile = fb - fo.off[f];
+  const int seg = tile % nseg1, tb = tile / nseg1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c1 = seg * kSeg - 1 + lane;
+  const int c2 = tb * R + wave;
+  const bool ok1 = c1 >= 0 && c1 < n1;
   double bcoef = 0.0;
   bool first = true;
   const double* pold = pA;
@@ -524,50 +537,58 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
     bcoef = first ? 0.0 : st->beta / st->betaold;
     pold = (it & 1) ? pA : pB;
   }
-  // two threads per face node: half h evaluates the two facets on side h of
-  // the second tangential axis (patch rows v = h, h + 1), summed over the pair
-  const int node = t >> 1, h = t & 1;
+  auto node_of = [&](int cc1, int cc2) {
+    int c[3];
+    c[t1] = cc1;
+    c[t2] = cc2;
+    c[a] = side ? n[a] - 1 : 0;
+    return c[0] + sst[1] * c[1] + sst[2] * c[2];
+  };
+  auto stage = [&](int row, int cc2) {
+    const bool ok = ok1 && cc2 >= 0 && cc2 < n2;
+    const int o = ok ? node_of(c1, cc2) : 0;
+    const double tt = T[o], zz = in0[o];
+    const double oo = FUSEP ? pold[o] : 0.0;
+    sT[row][lane] = ok ? tt : 0.0;
+    sP[row][lane] = ok ? ((FUSEP && !first) ? zz + bcoef * oo : zz) : 0.0;
+  };
+  stage(wave + 1, c2);
+  if (wave == 0) stage(0, tb * R - 1);
+  if (wave == R - 1) stage(R + 1, tb * R + R);
+  __syncthreads();
   double dot = 0.0;
-  const bool okn = node < n1 * n2;
-  int c[3];
-  c[t1] = okn ? node % n1 : 0;
-  c[t2] = okn ? node / n1 : 0;
-  c[a] = side ? n[a] - 1 : 0;
-  const int nd = c[0] + sst[1] * c[1] + sst[2] * c[2];
-  double tv[3][2], pv[3][2];
+  const bool wr = ok1 && lane >= 1 && lane <= kSeg && c2 < n2;
+  // patch rows v = 0, 1, 2 (t2 offsets -1, 0, +1), columns via the adjacent lanes
+  double tv[3], pv[3];
 #pragma unroll
-  for (int u = 0; u < 3; ++u)
-#pragma unroll
-    for (int vv = 0; vv < 2; ++vv) {
-      const int v = h + vv;  // patch row 0..2
-      const int a1 = c[t1] + u - 1, a2 = c[t2] + v - 1;
-      const bool ok = okn && a1 >= 0 && a1 < n1 && a2 >= 0 && a2 < n2;
-      const int o = ok ? nd + (u - 1) * sst[t1] + (v - 1) * sst[t2] : nd;
-      tv[u][vv] = T[o];
-      const double zz = in0[o];
-      const double oo = FUSEP ? pold[o] : 0.0;
-      pv[u][vv] = (FUSEP && !first) ? zz + bcoef * oo : zz;
-    }
-  const double* c1 = g.coef[t1] + (int64_t)c[t1] * C_NCOEF;
-  const double* c2 = g.coef[t2] + (int64_t)c[t2] * C_NCOEF;
-  const double h2 = h ? c2[C_HHI] : c2[C_HLO];
-  // node row: vv = 1 - h (v = 1); the other patch row: vv = h
-  const int nr = 1 - h, orow = h;
-  double acc = facet_jac_one(g, c1[C_HLO], h2, false, h, tv[1][nr], tv[0][nr], tv[1][orow], tv[0][orow],
-                             pv[1][nr], pv[0][nr], pv[1][orow], pv[0][orow]);
-  acc += facet_jac_one(g, c1[C_HHI], h2, true, h, tv[1][nr], tv[2][nr], tv[1][orow], tv[2][orow], pv[1][nr],
-                       pv[2][nr], pv[1][orow], pv[2][orow]);
-  acc = g.dt * acc;
-  const double tot = acc + __shfl_xor(acc, 1, 64);  // the pair's two halves, fixed order per pair
-  const double tot0 = h ? __shfl_xor(tot, 1, 64) : tot;
-  if (okn && h == 0) {
+  for (int v = 0; v < 3; ++v) {
+    tv[v] = sT[wave + v][lane];
+    pv[v] = sP[wave + v][lane];
+  }
+  const double tl0 = shr1(tv[0]), tl1 = shr1(tv[1]), tl2 = shr1(tv[2]);
+  const double tr0 = shl1(tv[0]), tr1 = shl1(tv[1]), tr2 = shl1(tv[2]);
+  const double pl0 = shr1(pv[0]), pl1 = shr1(pv[1]), pl2 = shr1(pv[2]);
+  const double pr0 = shl1(pv[0]), pr1 = shl1(pv[1]), pr2 = shl1(pv[2]);
+  if (wr) {
+    const double* cp1 = g.coef[t1] + (int64_t)c1 * C_NCOEF;
+    const double* cp2 = g.coef[t2] + (int64_t)c2 * C_NCOEF;
+    const double h1lo = cp1[C_HLO], h1hi = cp1[C_HHI], h2lo = cp2[C_HLO], h2hi = cp2[C_HHI];
+    // facets (s1, s2): corners node, t1-neighbour, t2-neighbour, diagonal
+    double acc = facet_jac_one(g, h1lo, h2lo, false, false, tv[1], tl1, tv[0], tl0, pv[1], pl1, pv[0], pl0);
+    acc += facet_jac_one(g, h1hi, h2lo, true, false, tv[1], tr1, tv[0], tr0, pv[1], pr1, pv[0], pr0);
+    acc += facet_jac_one(g, h1lo, h2hi, false, true, tv[1], tl1, tv[2], tl2, pv[1], pl1, pv[2], pl2);
+    acc += facet_jac_one(g, h1hi, h2hi, true, true, tv[1], tr1, tv[2], tr2, pv[1], pr1, pv[2], pr2);
+    acc = g.dt * acc;
+    int c[3];
+    c[t1] = c1;
+    c[t2] = c2;
+    c[a] = side ? n[a] - 1 : 0;
     const bool owned = c[2] >= g.k_begin && c[2] < g.k_end;
-    g.fface[f][node] = owned ? tot0 : 0.0;
-    dot = owned ? pv[1][nr] * tot0 : 0.0;
+    g.fface[f][c1 + n1 * c2] = owned ? acc : 0.0;
+    dot = owned ? pv[1] * acc : 0.0;
   }
   if (partials != nullptr) {
     dot = wave_sum(dot);
-    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
     if (lane == 0) redf[wave] = dot;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -602,8 +623,10 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t*
   }
 }
 
-template <int MODE, bool FUSEP, int R>
-__global__ __launch_bounds__(R * kWave) void k_cg_march(CgGrid g, const double* __restrict__ T,
+// WPE: minimum waves per SIMD the register allocation must allow (8: <= 64
+// VGPRs, four 8-wave tiles per CU, at the price of a few spills)
+template <int MODE, bool FUSEP, int R, int WPE>
+__global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cg_march(CgGrid g, const double* __restrict__ T,
                                                         const double* __restrict__ in0, const double* in1,
                                                         double* __restrict__ out, double* pout,
                                                         const PcgState* __restrict__ st,
@@ -882,6 +905,15 @@ static int march_minblk() {  // workgroups the march grid is chunked up to (TVFE
   return v;
 }
 
+static int march_wpe() {  // TVFEM_MARCH_WPE=8: register budget for 8 waves / SIMD
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("TVFEM_MARCH_WPE");
+    v = (e && atoi(e) == 8) ? 8 : 1;
+  }
+  return v;
+}
+
 static int face_first() {  // face workgroups ahead of the marching tiles (TVFEM_FACE_FIRST=0|1)
   static int v = -1;
   if (v < 0) {
@@ -937,7 +969,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
     L.blocks = L.nseg * nrb * nchunks;
     // Jacobian partial records: one per marching tile and face workgroup
-    L.nparts = L.blocks + face_offsets(g, L.rows * kWave).off[6];
+    L.nparts = L.blocks + face_offsets(g, L.rows).off[6];
     return L;
   }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
@@ -966,13 +998,16 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     const bool folded = MODE == MODE_JAC;
     RedTail rt{};
     if (folded && tail && partials) rt = *tail;
-    const FaceOff fo = folded ? face_offsets(g, L.rows * kWave) : FaceOff{};
+    const FaceOff fo = folded ? face_offsets(g, L.rows) : FaceOff{};
     const int grid = L.blocks + fo.off[6];
     if (L.rows == 16)
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16>), dim3(grid), dim3(16 * kWave), 0, s, g, T, in0, in1,
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16, 1>), dim3(grid), dim3(16 * kWave), 0, s, g, T, in0, in1,
+                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
+    else if (march_wpe() == 8)
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8, 8>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
                          out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
     else
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
+      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8, 1>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
                          out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
     if (folded && !FUSEP && fo.off[6] > 0) {  // complete J x (the fused PCG adds them in the update)
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.n_bnodes + kBlock - 1) / kBlock, 1024));
