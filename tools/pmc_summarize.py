@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 GROUPS = {
-    "pcg_matvec_fused": ("k_cg_march<1, true", "k_cg_bapply<true>"),
+    "pcg_matvec_fused": ("k_cg_march<1, true",),  # marching tiles + face workgroups, one launch
     "pcg_update": ("k_pcg_update",),
     "visco_update": ("k_visco_fused",),
 }
