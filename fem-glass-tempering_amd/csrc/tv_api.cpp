@@ -76,6 +76,7 @@ struct Ctx {
   PcgState* st = nullptr;
   PcgState* h_st = nullptr;  // pinned
   double* h_sums = nullptr;  // pinned
+  int* tflag = nullptr;       // device: s_tilde / sigma_tilde all +0.0 (0) or general (1), see ViscoFields
   double* scratch = nullptr;  // transfer scratch
   size_t scratch_bytes = 0;
   // comm: RCCL (production) or host-staged callbacks (testing several ranks on one GPU)
@@ -421,6 +422,8 @@ static int setup_fields(Ctx* c) {
   HIPC(hipMalloc(&c->counters, sizeof(unsigned) * 4));
   HIPC(hipMemsetAsync(c->counters, 0, sizeof(unsigned) * 4, c->stream));
   HIPC(hipMalloc(&c->st, sizeof(PcgState)));
+  HIPC(hipMalloc(&c->tflag, sizeof(int)));
+  HIPC(hipMemsetAsync(c->tflag, 0, sizeof(int), c->stream));  // the tilde fields start at +0.0
   HIPC(hipHostMalloc(&c->h_st, sizeof(PcgState)));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
   return TV_OK;
@@ -465,6 +468,17 @@ static int transfer(Ctx* c, int field, double* host, size_t n, int dir) {
   }
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, ((int64_t)need + 255) / 256), 16384);
   if (dir == 0) {
+    const bool tilde = field == TV_F_S_TILDE || field == TV_F_S_TILDE_NEXT || field == TV_F_SIGMA_TILDE ||
+                       field == TV_F_SIGMA_TILDE_NEXT;
+    if (tilde) {  // values other than +0.0 end the all-zero tracking of the tilde fields
+      const uint64_t* b = reinterpret_cast<const uint64_t*>(host);
+      uint64_t any = 0;
+      for (size_t k = 0; k < need; ++k) any |= b[k];
+      if (any) {
+        static const int one = 1;
+        HIPC(hipMemcpyAsync(c->tflag, &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
+      }
+    }
     HIPC(hipMemcpyAsync(c->scratch, host, bytes, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(k_interleave, dim3(blocks), dim3(256), 0, c->stream, 0, c->scratch, fi.ptr, ndof, fi.bs,
                        stride, off, nl, ncell);
@@ -564,9 +578,9 @@ static void op_japply(Ctx* c, const double* T, const double* x, double* y, doubl
   if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
   else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
 }
-static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr) {
+static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr, int it = 0) {
   if (c->fam_T == TV_CG)
-    return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail);
+    return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail, it);
   launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
   return false;
 }
@@ -574,7 +588,9 @@ static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tai
 // --------------------------------------------------------------------------------------
 // Jacobi-PCG for J(T) dx = r  (PETSc KSPCG restated; see tv_pcg.hip)
 // --------------------------------------------------------------------------------------
-static int pcg_iteration(Ctx* c, const double* T) {
+// it: index of this iteration within the solve (the device counter st->it
+// equals it until convergence, after which every kernel exits at once)
+static int pcg_iteration(Ctx* c, const double* T, int it) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
   const bool multi = multi_rank(c);
   // single GPU: the last-arriving workgroup of each launch reduces the partial
@@ -582,7 +598,7 @@ static int pcg_iteration(Ctx* c, const double* T) {
   // launch); multi-GPU: it only reduces, RCCL all-reduces, then the logic runs.
   RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2};
   int np = 0;
-  const bool fused1 = op_japply_fused(c, T, &np, &t1);  // p <- z + b p ; w <- J p ; p.w
+  const bool fused1 = op_japply_fused(c, T, &np, &t1, it);  // p <- z + b p ; w <- J p ; p.w
   if (!fused1) {
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
   } else if (multi) {
@@ -592,7 +608,7 @@ static int pcg_iteration(Ctx* c, const double* T) {
   RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3};
   const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
-                    c->r + off, c->z + off, c->partials, c->stream, &t2, &fa);
+                    c->r + off, c->z + off, c->partials, c->stream, &t2, &fa, it);
   if (multi) {  // dp, beta, convergence
     if (int e = allreduce(c, c->sums, 2)) return e;
     launch_logic(c->st, c->sums, 3, c->stream);
@@ -617,7 +633,7 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   int batch = std::max(1, c->pcg_hint > 2 ? c->pcg_hint - 1 : c->O.pcg_batch);
   for (;;) {
     for (int b = 0; b < batch; ++b) {
-      if (int e = pcg_iteration(c, T)) return e;
+      if (int e = pcg_iteration(c, T, launched + b)) return e;
     }
     launched += batch;
     HIPC(hipGetLastError());
@@ -718,6 +734,7 @@ static void visco_setup(Ctx* c, ViscoConst& k, ViscoFields& v) {
   v.st = c->f[TV_F_S_TILDE].ptr; v.sgt = c->f[TV_F_SIGMA_TILDE].ptr;
   v.sp = c->f[TV_F_S_PARTIAL].ptr; v.sgp = c->f[TV_F_SIGMA_PARTIAL].ptr;
   v.sigma = c->f[TV_F_SIGMA].ptr;
+  v.tflag = c->tflag;
 }
 
 static int visco(Ctx* c, bool copy_Tprev) {
@@ -900,6 +917,7 @@ int tv_destroy(void* ctx) {
   for (int f = 0; f < 6; ++f)
     if (c->fface[f]) hipFree(c->fface[f]);
   if (c->st) hipFree(c->st);
+  if (c->tflag) hipFree(c->tflag);
   if (c->counters) hipFree(c->counters);
   if (c->h_st) hipHostFree(c->h_st);
   if (c->h_sums) hipHostFree(c->h_sums);
@@ -1154,8 +1172,11 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       *bytes = 16.0 * n;
       break;
     case 1: {  // fused visco update, per dof
-      double per = 8.0 * (2 + 6 + 2 * 6 * dd)           // read T, Tp, Tf_partial, s~, sigma~
-                   + 8.0 * (6 + 3 + 2 * 6 * dd + dd);    // write Tf_partial, Tf, phi, xi, s~, sigma~, sigma
+      int tf = 1;
+      HIPC(hipMemcpy(&tf, c->tflag, sizeof(int), hipMemcpyDeviceToHost));
+      const int tilde = tf ? 2 * 6 * dd : 0;  // s~, sigma~ are not touched while they are all +0.0
+      double per = 8.0 * (2 + 6 + tilde)            // read T, Tp, Tf_partial (, s~, sigma~)
+                   + 8.0 * (6 + 3 + tilde + dd);    // write Tf_partial, Tf, phi, xi (, s~, sigma~), sigma
       if (c->O.materialize) per += 8.0 * (2 + 3 * dd + 4 * 6 * dd);
       *bytes = per * n;
       break;
@@ -1190,12 +1211,12 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       case 0: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); return TV_OK;
       case 1: return visco(c, false);
       case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;
-      case 3: op_japply_fused(c, c->f[TV_F_T].ptr, &np); return TV_OK;
+      case 3: op_japply_fused(c, c->f[TV_F_T].ptr, &np, nullptr, 1); return TV_OK;  // st->it = 1 below
       case 4: {
         const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, c->ownT_off) : FaceAdd{};
         launch_pcg_update(c->ownT_n, c->st, c->pA + c->ownT_off, c->pB + c->ownT_off, c->w + c->ownT_off,
                           c->dinv + c->ownT_off, c->f[TV_F_DX].ptr + c->ownT_off, c->r + c->ownT_off,
-                          c->z + c->ownT_off, c->partials, c->stream, nullptr, &fa);
+                          c->z + c->ownT_off, c->partials, c->stream, nullptr, &fa, 1);
         return TV_OK;
       }
       default: return c->fail(TV_ERR_ARG, "unknown kernel id");

@@ -462,57 +462,77 @@ struct FaceOff {
   int off[7];  // workgroup ranges per face f (in marching-workgroup units), off[6] = total
 };
 
-// face tiles: kSeg nodes along t1 (one wavefront, two halo lanes) x `rows`
-// nodes along t2 (one wavefront per row)
-FaceOff face_offsets(const CgGrid& g, int rows) {
+// face tiles: kSeg nodes along t1 (one wavefront, two halo lanes) x (R - 1)
+// node rows along t2 (R wavefronts: one facet row each, see face_block).  The
+// faces normal to the march axis `qaxis` are integrated inside the marching
+// tiles instead (k_cg_march) and get no face tiles.
+FaceOff face_offsets(const CgGrid& g, int R, int qaxis) {
   FaceOff fo{};
   int acc = 0;
+  const int rows = R - 1;
   for (int f = 0; f < 6; ++f) {
     fo.off[f] = acc;
-    if (g.fface[f]) acc += ((g.fn1[f] + kSeg - 1) / kSeg) * ((g.fn2[f] + rows - 1) / rows);
+    if (g.fface[f] && (f >> 1) != qaxis) acc += ((g.fn1[f] + kSeg - 1) / kSeg) * ((g.fn2[f] + rows - 1) / rows);
   }
   fo.off[6] = acc;
   return fo;
 }
 
-// One facet of facet_sum<MODE_JAC> from its four corner values (corner 00 =
-// the node, 10 along t1, 01 along t2), rolled 3x3 Gauss loop: the face
-// workgroups share the marching kernel's register budget.
-__device__ __forceinline__ double facet_jac_one(const CgGrid& g, double h1, double h2, bool s1, bool s2,
-                                                double T00, double T10, double T01, double T11, double P00,
-                                                double P10, double P01, double P11) {
-  double acc = 0.0;
-  if (!(h1 > 0.0) || !(h2 > 0.0)) return 0.0;
-#pragma unroll 1
-  for (int q = 0; q < 9; ++q) {
-    const int q1 = q / 3, q2 = q - 3 * (q / 3);
-    const double g1 = q1 == 0 ? kGX[0] : (q1 == 1 ? kGX[1] : kGX[2]);
-    const double g2 = q2 == 0 ? kGX[0] : (q2 == 1 ? kGX[1] : kGX[2]);
-    const double w1 = q1 == 1 ? kGW[1] : kGW[0], w2 = q2 == 1 ? kGW[1] : kGW[0];
-    const double pc1 = s1 ? 1.0 - g1 : g1, po1 = 1.0 - pc1;
-    const double pc2 = s2 ? 1.0 - g2 : g2, po2 = 1.0 - pc2;
-    const double w = (w1 * h1) * (w2 * h2);
-    const double phiI = pc1 * pc2;
-    const double Th = phiI * T00 + po1 * pc2 * T10 + pc1 * po2 * T01 + po1 * po2 * T11;
-    const double Ph = phiI * P00 + po1 * pc2 * P10 + pc1 * po2 * P01 + po1 * po2 * P11;
-    acc += w * dg_rad_conv(g, Th) * phiI * Ph;
+// Robin facet Jacobian of ONE facet (c1, c1+1) x (row, row+1) of a boundary
+// face: the corner contributions dt int_f g'(T_h) phi_X p_h ds for X = a (c1,
+// row), b (c1+1, row), c (c1, row+1), d (c1+1, row+1), 3x3 Gauss points (exact
+// for the degree-5 per direction integrand).  Ta/Tc, Pa/Pc: T and p at the
+// lane's node of the lower / upper row; the c1+1 values come from the next lane
+// (DPP), so every lane of the wave must call this (uniform control flow).
+__device__ __forceinline__ void facet_corners(const CgGrid& g, bool ok, double h1, double h2, double Ta,
+                                              double Tc, double Pa, double Pc, double& ya, double& yb,
+                                              double& yc, double& yd) {
+  const double Tb = shl1(Ta), Td = shl1(Tc), Pb = shl1(Pa), Pd = shl1(Pc);
+  ya = yb = yc = yd = 0.0;
+  if (ok) {
+#pragma unroll
+    for (int q1 = 0; q1 < 3; ++q1) {
+#pragma unroll
+      for (int q2 = 0; q2 < 3; ++q2) {
+        const double sx = kGX[q1], tx = kGX[q2];
+        const double fa = (1.0 - sx) * (1.0 - tx), fb = sx * (1.0 - tx), fc = (1.0 - sx) * tx, fd = sx * tx;
+        const double Th = fa * Ta + fb * Tb + fc * Tc + fd * Td;
+        const double Ph = fa * Pa + fb * Pb + fc * Pc + fd * Pd;
+        const double G = (kGW[q1] * kGW[q2]) * dg_rad_conv(g, Th) * Ph;
+        ya += G * fa;
+        yb += G * fb;
+        yc += G * fc;
+        yd += G * fd;
+      }
+    }
+    const double sc = g.dt * (h1 * h2);
+    ya *= sc; yb *= sc; yc *= sc; yd *= sc;
   }
-  return acc;
 }
 
-// One face workgroup of the marching launch (Jacobian mode): a tile of kSeg x R
-// nodes of face f.  Each wavefront stages one face row of T and p (p = z +
-// beta/betaold p_old in the fused PCG, else p = x) in LDS (waves 0 and R-1
-// also the two halo rows), then every node takes its 3x3 patch from LDS and
-// the adjacent lanes: ~4 loads per node instead of 27 gathers.  Writes fface
-// and the workgroup's p.(facet terms) record; takes part in the tail.
+// One face workgroup of the marching launch (Jacobian mode): the Robin facet
+// Jacobian terms dt * int_f g'(T_h) phi_I p_h ds of a tile of face nodes,
+// evaluated per FACET: lane = facet (c1, c1+1) x (f, f+1) of wave w's facet
+// row f = r0 - 1 + w; its 9 Gauss points (3x3, exact for the degree-5 per
+// direction integrand) give the four corner contributions at once (4x less
+// arithmetic than integrating the up-to-4 facets of every node separately).
+// A node sums the corners of its 4 facets: t1 neighbours by DPP, the facet
+// row below through LDS.  T and p (p = z + beta/betaold p_old in the fused
+// PCG, else p = x) of the R + 1 node rows r0-1 .. r0+R-1 are staged in LDS;
+// waves 1..R-1 write node rows r0 .. r0+R-2 of fface and the workgroup's
+// p.(facet terms) record, then the tile takes part in the reduction tail.
 template <bool FUSEP, int R>
 __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const double* __restrict__ in0,
                            const double* pA, const double* pB, const PcgState* __restrict__ st,
                            double* __restrict__ partials, const RedTail& rt, int nrec, int fb,
-                           const FaceOff& fo) {
+                           const FaceOff& fo, double* sm, int it_host) {
   __shared__ double redf[R];
-  __shared__ double sT[R + 2][kWave], sP[R + 2][kWave];
+  // LDS carved from the kernel's shared buffer (the marching tiles use it for
+  // their own face planes): T and p of R + 1 node rows, and the upper-corner
+  // contributions (c: c1, d: c1 + 1) of each facet row
+  double (*sT)[kWave] = reinterpret_cast<double (*)[kWave]>(sm);
+  double (*sP)[kWave] = reinterpret_cast<double (*)[kWave]>(sm + (R + 1) * kWave);
+  double (*sCD)[R][kWave] = reinterpret_cast<double (*)[R][kWave]>(sm + 2 * (R + 1) * kWave);
   int f = 0;
   while (f < 5 && fb >= fo.off[f + 1]) ++f;
   const int a = f >> 1, side = f & 1;
@@ -526,16 +546,15 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c1 = seg * kSeg - 1 + lane;
-  const int c2 = tb * R + wave;
+  const int r0 = tb * (R - 1);
   const bool ok1 = c1 >= 0 && c1 < n1;
   double bcoef = 0.0;
   bool first = true;
   const double* pold = pA;
-  if (FUSEP) {
-    const int it = st->it;
-    first = (it == 0);
+  if (FUSEP) {  // iteration parity from the host (no dependent load before the staging loads)
+    first = (it_host == 0);
     bcoef = first ? 0.0 : st->beta / st->betaold;
-    pold = (it & 1) ? pA : pB;
+    pold = (it_host & 1) ? pA : pB;
   }
   auto node_of = [&](int cc1, int cc2) {
     int c[3];
@@ -552,50 +571,45 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
     sT[row][lane] = ok ? tt : 0.0;
     sP[row][lane] = ok ? ((FUSEP && !first) ? zz + bcoef * oo : zz) : 0.0;
   };
-  stage(wave + 1, c2);
-  if (wave == 0) stage(0, tb * R - 1);
-  if (wave == R - 1) stage(R + 1, tb * R + R);
+  // facet (c1, c1 + 1) x (fr, fr + 1), corners a = (c1, fr), b = (c1+1, fr),
+  // c = (c1, fr+1), d = (c1+1, fr+1); its cell lengths load with the staging
+  const int fr = r0 - 1 + wave;
+  const bool facet_ok = c1 >= 0 && c1 < n1 - 1 && fr >= 0 && fr < n2 - 1;
+  const double h1 = g.coef[t1][(int64_t)(facet_ok ? c1 : 0) * C_NCOEF + C_HHI];
+  const double h2 = g.coef[t2][(int64_t)(facet_ok ? fr : 0) * C_NCOEF + C_HHI];
+  stage(wave, r0 - 1 + wave);
+  if (wave == R - 1) stage(R, r0 + R - 1);
+  __syncthreads();
+  const double Pa = sP[wave][lane];
+  double ya, yb, yc, yd;
+  facet_corners(g, facet_ok, h1, h2, sT[wave][lane], sT[wave + 1][lane], Pa, sP[wave + 1][lane], ya, yb, yc, yd);
+  sCD[0][wave][lane] = yc;
+  sCD[1][wave][lane] = yd;
+  const double ybl = shr1(yb);  // facet (c1 - 1) contributes its b corner to node c1
   __syncthreads();
   double dot = 0.0;
-  const bool wr = ok1 && lane >= 1 && lane <= kSeg && c2 < n2;
-  // patch rows v = 0, 1, 2 (t2 offsets -1, 0, +1), columns via the adjacent lanes
-  double tv[3], pv[3];
-#pragma unroll
-  for (int v = 0; v < 3; ++v) {
-    tv[v] = sT[wave + v][lane];
-    pv[v] = sP[wave + v][lane];
-  }
-  const double tl0 = shr1(tv[0]), tl1 = shr1(tv[1]), tl2 = shr1(tv[2]);
-  const double tr0 = shl1(tv[0]), tr1 = shl1(tv[1]), tr2 = shl1(tv[2]);
-  const double pl0 = shr1(pv[0]), pl1 = shr1(pv[1]), pl2 = shr1(pv[2]);
-  const double pr0 = shl1(pv[0]), pr1 = shl1(pv[1]), pr2 = shl1(pv[2]);
+  const int c2 = r0 - 1 + wave;  // node row of wave w (w >= 1)
+  const bool wr = wave >= 1 && ok1 && lane >= 1 && lane <= kSeg && c2 < n2;
   if (wr) {
-    const double* cp1 = g.coef[t1] + (int64_t)c1 * C_NCOEF;
-    const double* cp2 = g.coef[t2] + (int64_t)c2 * C_NCOEF;
-    const double h1lo = cp1[C_HLO], h1hi = cp1[C_HHI], h2lo = cp2[C_HLO], h2hi = cp2[C_HHI];
-    // facets (s1, s2): corners node, t1-neighbour, t2-neighbour, diagonal
-    double acc = facet_jac_one(g, h1lo, h2lo, false, false, tv[1], tl1, tv[0], tl0, pv[1], pl1, pv[0], pl0);
-    acc += facet_jac_one(g, h1hi, h2lo, true, false, tv[1], tr1, tv[0], tr0, pv[1], pr1, pv[0], pr0);
-    acc += facet_jac_one(g, h1lo, h2hi, false, true, tv[1], tl1, tv[2], tl2, pv[1], pl1, pv[2], pl2);
-    acc += facet_jac_one(g, h1hi, h2hi, true, true, tv[1], tr1, tv[2], tr2, pv[1], pr1, pv[2], pr2);
-    acc = g.dt * acc;
+    // facets below (row c2 - 1): corners c (same c1) and d (from c1 - 1)
+    const double acc = (ya + ybl) + (sCD[0][wave - 1][lane] + sCD[1][wave - 1][lane - 1]);
     int c[3];
     c[t1] = c1;
     c[t2] = c2;
     c[a] = side ? n[a] - 1 : 0;
     const bool owned = c[2] >= g.k_begin && c[2] < g.k_end;
     g.fface[f][c1 + n1 * c2] = owned ? acc : 0.0;
-    dot = owned ? pv[1] * acc : 0.0;
+    dot = owned ? Pa * acc : 0.0;
   }
   if (partials != nullptr) {
     dot = wave_sum(dot);
     if (lane == 0) redf[wave] = dot;
     __syncthreads();
     if (threadIdx.x == 0) {
-      double s = 0.0;
+      double s2 = 0.0;
 #pragma unroll
-      for (int w = 0; w < R; ++w) s += redf[w];
-      store_partial(&partials[blockIdx.x], s);
+      for (int w = 0; w < R; ++w) s2 += redf[w];
+      store_partial(&partials[blockIdx.x], s2);
     }
     fused_reduce_tail<1>(rt, nrec);
   }
@@ -604,7 +618,7 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
 // out[n] += sum of the facet terms of the owned boundary node n (every face
 // it lies on), for the non-fused J(T) x
 __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t* __restrict__ bnodes, int64_t nb,
-                                                        double* __restrict__ out) {
+                                                        double* __restrict__ out, int qaxis) {
   const int n[3] = {g.n0, g.n1, g.n2};
   for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < nb; e += (int64_t)gridDim.x * kBlock) {
     const int nd = (int)bnodes[e];
@@ -612,6 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t*
     double add = 0.0;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
+      if (a == qaxis) continue;  // integrated inside the marching tiles
       const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
@@ -625,18 +640,22 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t*
 
 // WPE: minimum waves per SIMD the register allocation must allow (8: <= 64
 // VGPRs, four 8-wave tiles per CU, at the price of a few spills)
-template <int MODE, bool FUSEP, int R, int WPE>
+// PF: prefetch depth (planes whose loads are in flight while one is computed)
+template <int MODE, bool FUSEP, int R, int WPE, int PF>
 __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cg_march(CgGrid g, const double* __restrict__ T,
                                                         const double* __restrict__ in0, const double* in1,
                                                         double* __restrict__ out, double* pout,
                                                         const PcgState* __restrict__ st,
                                                         double* __restrict__ partials, int nseg, int raxis,
                                                         int qchunk, RedTail rt, int nrec, int nmarch,
-                                                        FaceOff fo, int ffirst) {
+                                                        FaceOff fo, int ffirst, int exp, int it_host) {
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
   __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
   __shared__ double red[R];
-  if (FUSEP && st->done) return;
+  // face LDS: face workgroups (face_block) or the marching tiles' own face
+  // planes -- [2 faces][T, p][R + 2 rows] slabs + corner exchange [2 faces][c, d][R rows]
+  constexpr int kFaceLds = (MODE == MODE_JAC) ? (8 * R + 8) * kWave : 1;
+  __shared__ double fsm[kFaceLds];
   // Jacobian mode: workgroups past the marching tiles evaluate the Robin facet
   // terms of the boundary faces (k_face_block) -- independent work that fills
   // the tail of the march; the terms go to g.fface and are added to w by the
@@ -646,8 +665,10 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const int nface = (int)gridDim.x - nmarch;
   const int bid = ffirst ? (int)blockIdx.x - nface : (int)blockIdx.x;
   if (MODE == MODE_JAC && (bid < 0 || bid >= nmarch)) {
+    if (exp & 16) return;  // timing experiment only (TVFEM_MARCH_EXP): no face work
+    if (FUSEP && st->done) return;
     face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec,
-                         ffirst ? (int)blockIdx.x : (int)blockIdx.x - nmarch, fo);
+                         ffirst ? (int)blockIdx.x : (int)blockIdx.x - nmarch, fo, fsm, it_host);
     return;
   }
   const int lane = threadIdx.x & (kWave - 1);
@@ -680,15 +701,27 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   double bcoef = 0.0;
   bool first = false;
   const double* pold = in1;
-  if (FUSEP) {
-    const int it = st->it;
-    first = (it == 0);
-    bcoef = first ? 0.0 : st->beta / st->betaold;
-    if (!(it & 1)) { pold = pout; pout = const_cast<double*>(in1); }
+  if (FUSEP) {  // iteration parity from the host: the prefetch does not wait for a load of st
+    first = (it_host == 0);
+    if (!(it_host & 1)) { pold = pout; pout = const_cast<double*>(in1); }
   }
   // ownership along storage axis 2 (partition axis)
   const int kb = g.k_begin, ke = g.k_end;
   const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
+
+  // Robin facet terms of the faces normal to the march axis (Jacobian): the
+  // tile's first / last chunk holds that face's plane.  They are integrated in
+  // the tile's prologue -- T and p of the face plane's R + 2 rows staged in
+  // LDS, one facet row per wave (wave 0 also the row below the tile), corner
+  // exchange through LDS -- and added to that plane's output in the march.
+  const bool fq0 = (MODE == MODE_JAC) && q0 == 0 && g.bnd[qaxis][0] && !(exp & 32);
+  const bool fq1 = (MODE == MODE_JAC) && q1 == nQ && g.bnd[qaxis][1] && !(exp & 32);
+  double (*sFq)[2][R + 2][kWave] = reinterpret_cast<double (*)[2][R + 2][kWave]>(fsm);  // [face][T, p]
+  double (*sCD)[2][R][kWave] = reinterpret_cast<double (*)[2][R][kWave]>(fsm + 4 * (R + 2) * kWave);
+  double yq0 = 0.0, yq1 = 0.0;
+  // facet-row cell lengths along the row axis (own facet row r; r0 - 1 for wave 0)
+  const double hq_own = uniform(g.coef[raxis][(int64_t)(row_ok ? r : 0) * C_NCOEF + C_HHI]);
+  const double hq_low = uniform(g.coef[raxis][(int64_t)(r0 >= 1 ? r0 - 1 : 0) * C_NCOEF + C_HHI]);
 
   // row coefficients are wave-uniform: keep them in SGPRs
   const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
@@ -704,10 +737,15 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const double* second = (MODE == MODE_RES) ? in1 : pold;
   constexpr bool TWO = (MODE == MODE_RES) || FUSEP;
   const uint32_t nbytes = (uint32_t)g.n0 * (uint32_t)g.n1 * (uint32_t)g.n2 * 8u;
-  const buf_t rs0 = mk_rsrc(in0, nbytes);
-  const buf_t rs1 = mk_rsrc(TWO ? second : in0, (FUSEP && first) ? 0u : nbytes);  // p_old unused at it 0
-  const buf_t rso = mk_rsrc(out, nbytes);
-  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, FUSEP ? nbytes : 0u);
+  // exp (TVFEM_MARCH_EXP, timing experiments only, wrong results): a zero-sized
+  // descriptor drops one stream's loads / stores while the instruction stream stays
+  const buf_t rs0 = mk_rsrc(in0, (exp & 8) ? 0u : nbytes);
+  const buf_t rs1 = mk_rsrc(TWO ? second : in0, ((FUSEP && first) || (exp & 4)) ? 0u : nbytes);  // p_old unused at it 0
+  const buf_t rso = mk_rsrc(out, (exp & 1) ? 0u : nbytes);
+  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, (FUSEP && !(exp & 1)) ? nbytes : 0u);
+  const buf_t rsT = mk_rsrc(T, (fq0 || fq1) ? nbytes : 0u);
+  const buf_t rsZ = mk_rsrc(in0, (fq0 || fq1) ? nbytes : 0u);
+  const buf_t rsO = mk_rsrc(TWO ? second : in0, ((fq0 || fq1) && FUSEP && !first) ? nbytes : 0u);
   // halo rows are loaded by waves 0 and R-1; the other waves re-load their own
   // row (an L1 hit) so that every wave runs the same straight-line load stream
   const bool halo = (wave == 0) || (wave == R - 1);
@@ -716,7 +754,9 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   auto lane_off = [&](int rr) -> uint32_t {
     return (col_ok && rr >= 0 && rr < nR) ? (uint32_t)(i + sR * rr) * 8u : kBadOff;
   };
-  const uint32_t vo_own = lane_off(r), vo_halo = lane_off(hrow);
+  // the halo row offset of the other waves is out of range: their halo loads
+  // return 0 without a memory request, the instruction stream stays uniform
+  const uint32_t vo_own = lane_off(r), vo_halo = (halo && !(exp & 2)) ? lane_off(hrow) : kBadOff;
   const uint32_t vo_wr = writer ? vo_own : kBadOff;  // stores of the own row
   auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? (uint32_t)(sQ * L) * 8u : kBadOff; };
   auto fetch = [&](uint32_t vo, int L, double& a0, double& a1) {
@@ -724,6 +764,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     a0 = bload(rs0, o);
     a1 = TWO ? bload(rs1, o) : 0.0;
   };
+
   auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
     v = a0;
     vm = 0.0;
@@ -734,22 +775,43 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   // its first plane -- the first two planes (prefetch), the coefficient
   // stages and the Robin facet terms of the tile's boundary nodes -- issued
   // back to back, prefetch first.
-  double a0, a1, ah0, ah1, b0, b1, bh0, bh1;
-  fetch(vo_own, q0 - 1, a0, a1);
-  fetch(vo_halo, q0 - 1, ah0, ah1);
-  fetch(vo_own, q0, b0, b1);
-  fetch(vo_halo, q0, bh0, bh1);
-  // march-axis coefficients of the chunk and x-axis coefficients of the
-  // block's 64 columns, staged in LDS (read by every wave each plane; in VGPRs
-  // they would cost 12 registers for the whole march)
-  __shared__ double cql[kFaceChunk + 2][6];
-  __shared__ double cxl[6][kWave];
-  // (loads now; the LDS writes come after the face section, so that a single
-  // wait covers the prefetch, the stages and the face gathers)
-  // one coefficient per thread: thread e stages cql entry e (march axis) and
-  // cxl entry e (x axis: coefficient e / 64 of the block's column e % 64)
-  const bool st_q = (int)threadIdx.x < (q1 - q0 + 2) * 6;
-  const bool st_x = (int)threadIdx.x < 6 * kWave;
+  // prefetch ring: PF + 1 register sets rotate through a fully unrolled loop,
+  // so PF planes of loads are in flight while a plane is combined, exchanged
+  // and computed
+  double ra0[PF + 1], ra1[PF + 1], rh0[PF + 1], rh1[PF + 1];
+#pragma unroll
+  for (int s = 0; s < PF; ++s) {
+    fetch(vo_own, q0 - 1 + s, ra0[s], ra1[s]);
+    fetch(vo_halo, q0 - 1 + s, rh0[s], rh1[s]);
+  }
+  // the solver state is read only now, so its latency overlaps the prefetch;
+  // once the PCG has converged every launch of the batch exits here
+  if (FUSEP) {
+    if (st->done) return;
+    bcoef = first ? 0.0 : st->beta / st->betaold;
+  }
+  // face planes: T, z (, p_old) of the own and halo rows
+  double fT[2][2], fZ[2][2], fO[2][2];  // [face][own, halo]
+  if (fq0 || fq1) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const uint32_t po = plane_off(f == 0 ? (fq0 ? 0 : -1) : (fq1 ? nQ - 1 : -1));
+      fT[f][0] = bload(rsT, vo_own + po); fT[f][1] = bload(rsT, vo_halo + po);
+      fZ[f][0] = bload(rsZ, vo_own + po); fZ[f][1] = bload(rsZ, vo_halo + po);
+      fO[f][0] = FUSEP ? bload(rsO, vo_own + po) : 0.0;
+      fO[f][1] = FUSEP ? bload(rsO, vo_halo + po) : 0.0;
+    }
+  }
+  // march-axis coefficients of the chunk, pre-scaled per plane q into
+  // (Mz0, Mz1, Mz2, da Kz0, da Kz1, da Kz2, da Mz0, da Mz1, da Mz2, 0): read
+  // as 5 uniform 16-byte LDS loads per plane; x-axis coefficients of the
+  // block's 64 columns as (Mlo, Klo), (Mdi, Kdi), (Mup, Kup), (Hhi, -) pairs
+  // per lane: 3 conflict-free 16-byte LDS loads per plane
+  __shared__ double2 cql[kFaceChunk + 2][5];
+  __shared__ double2 cxl[4][kWave];
+  const int nqs = q1 - q0 + 2;
+  const bool st_q = (int)threadIdx.x < nqs * 6;
+  const bool st_x = (int)threadIdx.x < 8 * kWave;
   double cqv, cxv;
   {
     const int e = threadIdx.x;
@@ -759,14 +821,65 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     cqv = okq ? cqv : 0.0;
     const int ii = seg * kSeg - 1 + (e & (kWave - 1));
     const bool okx = st_x && ii >= 0 && ii < n0;
-    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + (e >> 6) : 0];
-    cxv = okx ? cxv : 0.0;
+    const int k = e >> 6;  // slot: pair k >> 1, half k & 1
+    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
+    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
+    cxv = (okx && k < 7) ? cxv : 0.0;
   }
-  if (st_q) cql[threadIdx.x / 6][threadIdx.x % 6] = cqv;
-  if (st_x) cxl[threadIdx.x >> 6][threadIdx.x & (kWave - 1)] = cxv;
+  if (st_q) {
+    const int qs = threadIdx.x / 6, c = threadIdx.x % 6;
+    double* row = reinterpret_cast<double*>(cql[qs]);
+    if (c < 3) {
+      row[c] = cqv;            // Mz
+      row[6 + c] = da * cqv;   // da Mz
+    } else {
+      row[c] = da * cqv;       // da Kz
+    }
+    if (c == 0) row[9] = 0.0;
+  }
+  if (st_x) reinterpret_cast<double*>(cxl[(threadIdx.x >> 6) >> 1])[2 * (threadIdx.x & (kWave - 1)) + ((threadIdx.x >> 6) & 1)] = cxv;
+  if (fq0 || fq1) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      sFq[f][0][wave + 1][lane] = fT[f][0];
+      sFq[f][1][wave + 1][lane] = FUSEP ? fZ[f][0] + bcoef * fO[f][0] : fZ[f][0];
+      if (halo) {
+        sFq[f][0][hslot][lane] = fT[f][1];
+        sFq[f][1][hslot][lane] = FUSEP ? fZ[f][1] + bcoef * fO[f][1] : fZ[f][1];
+      }
+    }
+  }
   __syncthreads();
+  if (fq0 || fq1) {  // facet row r (rows r, r + 1) of each face plane; wave 0 also row r0 - 1
+    const bool cok = i >= 0 && i < n0 - 1;
+    const double h1 = cxl[3][lane].x;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      if (!(f == 0 ? fq0 : fq1)) continue;  // block-uniform: only the face planes this chunk holds
+      double ya, yb, yc, yd;
+      facet_corners(g, cok && r < nR - 1, h1, hq_own, sFq[f][0][wave + 1][lane], sFq[f][0][wave + 2][lane],
+                    sFq[f][1][wave + 1][lane], sFq[f][1][wave + 2][lane], ya, yb, yc, yd);
+      double yq = ya + shr1(yb);
+      sCD[f][0][wave][lane] = yc;
+      sCD[f][1][wave][lane] = yd;
+      if (wave == 0) {
+        facet_corners(g, cok && r0 >= 1 && r0 - 1 < nR - 1, h1, hq_low, sFq[f][0][0][lane], sFq[f][0][1][lane],
+                      sFq[f][1][0][lane], sFq[f][1][1][lane], ya, yb, yc, yd);
+        yq += yc + shr1(yd);
+      }
+      if (f == 0) yq0 = yq; else yq1 = yq;
+    }
+    __syncthreads();
+    if (wave >= 1) {
+      const int lm = lane >= 1 ? lane - 1 : 0;
+      yq0 += sCD[0][0][wave - 1][lane] + sCD[0][1][wave - 1][lm];
+      yq1 += sCD[1][0][wave - 1][lane] + sCD[1][1][wave - 1][lm];
+    }
+  }
 
-  double us_m = 0.0, us_c = 0.0, vs_m = 0.0, vs_c = 0.0, um_m = 0.0, um_c = 0.0;
+  // sliding window over three planes of the row-folded values
+  //   us = My . x (mass), t = My . m + da Ky . x (m = x, or T - Tp - dt f for RES)
+  double us_m = 0.0, us_c = 0.0, t_m = 0.0, t_c = 0.0;
   double xc = 0.0;  // own-row value of the centre plane (p of the output node)
   double dot = 0.0;
   auto step = [&](int L, double c0, double c1, double h0, double h1) {
@@ -783,53 +896,50 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       if (MODE == MODE_RES) lds[NA - 1][buf][hslot][lane] = hvm;
     }
     __syncthreads();
-    const double x0 = lds[0][buf][wave][lane], x1 = lds[0][buf][wave + 1][lane], x2 = lds[0][buf][wave + 2][lane];
+    // the own row (x1) stays in registers; rows r - 1 and r + 1 from the slab
+    const double x0 = lds[0][buf][wave][lane], x1 = v, x2 = lds[0][buf][wave + 2][lane];
     const double us_p = My0 * x0 + My1 * x1 + My2 * x2;
     const double vs_p = Ky0 * x0 + Ky1 * x1 + Ky2 * x2;
     double um_p = us_p;
-    if (MODE == MODE_RES) {
-      const double m0 = lds[NA - 1][buf][wave][lane], m1 = lds[NA - 1][buf][wave + 1][lane],
-                   m2 = lds[NA - 1][buf][wave + 2][lane];
-      um_p = My0 * m0 + My1 * m1 + My2 * m2;
-    }
+    if (MODE == MODE_RES) um_p = My0 * lds[NA - 1][buf][wave][lane] + My1 * vm + My2 * lds[NA - 1][buf][wave + 2][lane];
+    const double t_p = um_p + da * vs_p;
     if (L >= q0 + 1 && L <= q1) {
       const int q = L - 1;
-      const double* cq = cql[q - q0 + 1];
-      const double Mz0 = cq[C_MLO], Mz1 = cq[C_MDI], Mz2 = cq[C_MUP];
-      const double Kz0 = cq[C_KLO], Kz1 = cq[C_KDI], Kz2 = cq[C_KUP];
-      const double S1 = Mz0 * (um_m + da * vs_m) + Mz1 * (um_c + da * vs_c) + Mz2 * (um_p + da * vs_p) +
-                        da * (Kz0 * us_m + Kz1 * us_c + Kz2 * us_p);
-      const double S2 = da * (Mz0 * us_m + Mz1 * us_c + Mz2 * us_p);
-      const double S1m = shr1(S1), S1p = shl1(S1), S2m = shr1(S2), S2p = shl1(S2);
-      const double y = cxl[C_MLO][lane] * S1m + cxl[C_MDI][lane] * S1 + cxl[C_MUP][lane] * S1p +
-                       cxl[C_KLO][lane] * S2m + cxl[C_KDI][lane] * S2 + cxl[C_KUP][lane] * S2p;
+      const double2* cq = cql[q - q0 + 1];
+      const double2 c01 = cq[0], c23 = cq[1], c45 = cq[2], c67 = cq[3], c89 = cq[4];
+      //   S1 = Mz . t + da Kz . us ,  S2 = da Mz . us          (march axis)
+      const double S1 = c01.x * t_m + c01.y * t_c + c23.x * t_p + (c23.y * us_m + c45.x * us_c + c45.y * us_p);
+      const double S2 = c67.x * us_m + c67.y * us_c + c89.x * us_p;
+      // x axis by symmetry of the assembled 1D rows (Mlo_i = Mup_{i-1}, Klo_i = Kup_{i-1}):
+      //   y_i = Mdi S1_i + Kdi S2_i + [Mup S1 + Kup S2]_{i-1} + [Mlo S1 + Klo S2]_{i+1}
+      const double2 xlo = cxl[0][lane], xdi = cxl[1][lane], xup = cxl[2][lane];
+      const double Lt = xup.x * S1 + xup.y * S2;
+      const double Rt = xlo.x * S1 + xlo.y * S2;
+      const double y = (xdi.x * S1 + xdi.y * S2) + (shr1(Lt) + shl1(Rt));
       const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
       const bool wr = writer && row_ok && row_owned && q_owned;
-      // Robin facet terms: face workgroups (Jacobian) / k_cg_boundary (residual)
-      const double yb = y;
+      // Robin facet terms: in-tile face planes (above), face workgroups
+      // (other faces, added by the consumer) / k_cg_boundary (residual)
+      double yb = y;
+      if (fq0 && q == 0) yb += yq0;
+      if (fq1 && q == nQ - 1) yb += yq1;
       bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, yb);
       if (MODE == MODE_JAC) dot += wr ? xc * yb : 0.0;
     }
     xc = x1;
     us_m = us_c; us_c = us_p;
-    vs_m = vs_c; vs_c = vs_p;
-    um_m = um_c; um_c = um_p;
+    t_m = t_c; t_c = t_p;
   };
-  // prefetch depth 2: three register sets rotate (3x unrolled), so two planes
-  // of loads are in flight while a plane is combined, exchanged and computed
-  double c0_, c1_, ch0, ch1;
   // no early exits: steps past q1 only touch LDS (their stores are masked), so
-  // the three register sets keep fixed registers across the back edge
-  for (int L = q0 - 1; L <= q1; L += 3) {
-    fetch(vo_own, L + 2, c0_, c1_);
-    fetch(vo_halo, L + 2, ch0, ch1);
-    step(L, a0, a1, ah0, ah1);
-    fetch(vo_own, L + 3, a0, a1);
-    fetch(vo_halo, L + 3, ah0, ah1);
-    step(L + 1, b0, b1, bh0, bh1);
-    fetch(vo_own, L + 4, b0, b1);
-    fetch(vo_halo, L + 4, bh0, bh1);
-    step(L + 2, c0_, c1_, ch0, ch1);
+  // the register sets keep fixed registers across the back edge
+  for (int L = q0 - 1; L <= q1; L += PF + 1) {
+#pragma unroll
+    for (int s = 0; s <= PF; ++s) {
+      const int sf = (s + PF) % (PF + 1);  // the set consumed one step ago
+      fetch(vo_own, L + s + PF, ra0[sf], ra1[sf]);
+      fetch(vo_halo, L + s + PF, rh0[sf], rh1[sf]);
+      step(L + s, ra0[s], ra1[s], rh0[s], rh1[s]);
+    }
   }
   if (MODE == MODE_JAC && partials != nullptr) {
     dot = wave_sum(dot);
@@ -914,6 +1024,25 @@ static int march_wpe() {  // TVFEM_MARCH_WPE=8: register budget for 8 waves / SI
   return v;
 }
 
+static int march_pf() {  // prefetch depth of the march (TVFEM_MARCH_PF = 2 | 3 | 4)
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("TVFEM_MARCH_PF");
+    v = e ? atoi(e) : 2;  // 2 measured best: deeper rings cost occupancy (66 -> 89 VGPRs)
+    if (v < 2 || v > 4) v = 2;
+  }
+  return v;
+}
+
+static int march_exp() {  // TVFEM_MARCH_EXP: timing-experiment bits (see k_cg_march); 0 in production
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("TVFEM_MARCH_EXP");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
+}
+
 static int face_first() {  // face workgroups ahead of the marching tiles (TVFEM_FACE_FIRST=0|1)
   static int v = -1;
   if (v < 0) {
@@ -969,7 +1098,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
     L.blocks = L.nseg * nrb * nchunks;
     // Jacobian partial records: one per marching tile and face workgroup
-    L.nparts = L.blocks + face_offsets(g, L.rows).off[6];
+    L.nparts = L.blocks + face_offsets(g, L.rows, 3 - L.raxis).off[6];
     return L;
   }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
@@ -988,7 +1117,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
 template <int MODE, bool FUSEP>
 bool launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
                  double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s,
-                 const RedTail* tail = nullptr) {
+                 const RedTail* tail = nullptr, int it_host = 0) {
   const Launch L = plan(g, ghosts);
   if (L.blocks <= 0) return false;
   if (L.march) {
@@ -998,20 +1127,22 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     const bool folded = MODE == MODE_JAC;
     RedTail rt{};
     if (folded && tail && partials) rt = *tail;
-    const FaceOff fo = folded ? face_offsets(g, L.rows) : FaceOff{};
+    const FaceOff fo = folded ? face_offsets(g, L.rows, 3 - L.raxis) : FaceOff{};
     const int grid = L.blocks + fo.off[6];
-    if (L.rows == 16)
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 16, 1>), dim3(grid), dim3(16 * kWave), 0, s, g, T, in0, in1,
-                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
-    else if (march_wpe() == 8)
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8, 8>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
-                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
-    else
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, 8, 1>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1,
-                         out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first());
+#define TV_MARCH(RR, WW, PP)                                                                                  \
+  hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, RR, WW, PP>), dim3(grid), dim3(RR * kWave), 0, s, g, T, in0, in1, \
+                     out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first(), \
+                     march_exp(), it_host)
+    const int pf = march_pf();
+    if (L.rows == 16) TV_MARCH(16, 1, 4);
+    else if (march_wpe() == 8) TV_MARCH(8, 8, 2);
+    else if (pf == 2) TV_MARCH(8, 1, 2);
+    else if (pf == 3) TV_MARCH(8, 1, 3);
+    else TV_MARCH(8, 1, 4);
+#undef TV_MARCH
     if (folded && !FUSEP && fo.off[6] > 0) {  // complete J x (the fused PCG adds them in the update)
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.n_bnodes + kBlock - 1) / kBlock, 1024));
-      hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, g.bnodes, g.n_bnodes, out);
+      hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, g.bnodes, g.n_bnodes, out, 3 - L.raxis);
     }
     if (folded) return rt.counter != nullptr;
     if (g.n_bnodes > 0) {
@@ -1051,7 +1182,8 @@ FaceAdd cg_face_add(const CgGrid& g, int64_t t_off) {
   fa.t_off = t_off;
   fa.inv_n0 = 1.0 / g.n0;
   fa.inv_plane = 1.0 / ((double)g.n0 * g.n1);
-  for (int f = 0; f < 6; ++f) fa.ff[f] = g.fface[f];
+  const int qaxis = 3 - plan(g, true).raxis;  // faces normal to the march axis: added inside the march
+  for (int f = 0; f < 6; ++f) fa.ff[f] = ((f >> 1) == qaxis) ? nullptr : g.fface[f];
   return fa;
 }
 
@@ -1067,10 +1199,10 @@ void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double*
 
 bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
-                            hipStream_t s, const RedTail* tail) {
+                            hipStream_t s, const RedTail* tail, int it_host) {
   // neighbour values of p_new are recomputed from z and p_old; p_new goes to the
   // other buffer of the pair (selected on device from st->it).
-  const bool fused = launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s, tail);
+  const bool fused = launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s, tail, it_host);
   if (n_partials) *n_partials = plan(g, true).nparts;
   return fused;
 }

@@ -103,6 +103,9 @@ struct ViscoFields {
   double* sp; double* sgp;                       // s, sigma partial (materialize=all)
   double* sigma;                                 // total stress (state)
   int copy_Tprev;             // fuse T_prev <- T (same family, single pass)
+  // device word: 0 = s_tilde and sigma_tilde hold +0.0 at every dof (quirk Q3
+  // keeps them there), so the update neither reads nor rewrites them; 1 = general
+  int* tflag;
 };
 
 // ---- kernel launchers (tv_cg.hip, tv_dg.hip, tv_visco.hip, tv_pcg.hip) ----
@@ -111,9 +114,11 @@ void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double*
                       int* n_partials, hipStream_t s);
 // returns true when the launch ends with the in-kernel reduction tail (the
 // caller then skips the separate reduce launch)
+// it_host: the PCG iteration index the host launches (== st->it while the
+// solve runs), selects the p buffer pair without a dependent device load
 bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
-                            hipStream_t s, const RedTail* tail = nullptr);
+                            hipStream_t s, const RedTail* tail = nullptr, int it_host = 0);
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 
@@ -147,7 +152,8 @@ FaceAdd cg_face_add(const CgGrid& g, int64_t t_off);
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* dinv, double* dx, double* r, double* z, double* partials,
-                       hipStream_t s, const RedTail* tail = nullptr, const FaceAdd* fa = nullptr);
+                       hipStream_t s, const RedTail* tail = nullptr, const FaceAdd* fa = nullptr,
+                       int it_host = 0);
 // one-block deterministic reduce of n records of width W (<= 2) into out[W];
 // kind: 0 none, 1 PCG init logic, 2 PCG p.w logic, 3 PCG update logic
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,

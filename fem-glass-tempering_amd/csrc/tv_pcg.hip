@@ -81,10 +81,11 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
                                                        const double* __restrict__ w,
                                                        const double* __restrict__ dinv, double* __restrict__ dx,
                                                        double* __restrict__ r, double* __restrict__ z,
-                                                       double* __restrict__ partials, RedTail rt, FaceAdd fa) {
+                                                       double* __restrict__ partials, RedTail rt, FaceAdd fa,
+                                                       int it_host) {
   if (st->done) return;
   const double a = st->a;
-  const double* __restrict__ p = (st->it & 1) ? pB : pA;
+  const double* __restrict__ p = (it_host & 1) ? pB : pA;  // == st->it while the solve runs
   double acc[2] = {0.0, 0.0};
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     dx[t] += a * p[t];                    // x <- x + a p
@@ -170,15 +171,15 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* dinv, double* dx, double* r, double* z, double* partials, hipStream_t s,
-                       const RedTail* tail, const FaceAdd* fa) {
+                       const RedTail* tail, const FaceAdd* fa, int it_host) {
   RedTail rt{};
   if (tail) rt = *tail;
   if (fa && fa->on)
     hipLaunchKernelGGL(k_pcg_update<true>, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx, r,
-                       z, partials, rt, *fa);
+                       z, partials, rt, *fa, it_host);
   else
     hipLaunchKernelGGL(k_pcg_update<false>, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx,
-                       r, z, partials, rt, FaceAdd{});
+                       r, z, partials, rt, FaceAdd{}, it_host);
 }
 
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s) {

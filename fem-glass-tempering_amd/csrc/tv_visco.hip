@@ -9,9 +9,12 @@
 //
 // For degree-1 Lagrange spaces every expression is a per-dof map, so one thread
 // owns one dof and carries the whole pipeline in registers: a single HBM pass
-// that reads T, T_prev, Tf_partial, s_tilde, sigma_tilde and writes the state
-// (Tf_partial, Tf, phi, xi, s_tilde, sigma_tilde, sigma) — plus every
-// intermediate Function of the reference when materialize = all.
+// that reads T, T_prev, Tf_partial and writes the state (Tf_partial, Tf, phi,
+// xi, sigma) — plus every intermediate Function of the reference when
+// materialize = all.  s_tilde / sigma_tilde (Q3: fed only by themselves, so
+// +0.0 from the zero initial state on) are read and rewritten only once a
+// value other than +0.0 has appeared (ViscoFields::tflag); until then they
+// cost no HBM traffic.
 //
 // Semantics follow the reference, quirks included:
 //   Q1 phi is Eq. 5 (the Eq. 25 expression is overwritten, VEM:100 vs :156);
@@ -80,8 +83,15 @@ __device__ __forceinline__ TState t_part(const ViscoConst& c, const ViscoFields&
 }
 
 // sigma-family part at sigma-dof s given the T-family values of its source dof.
-template <int D, bool ALL>
-__device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f, int64_t s, const TState& ts) {
+// LEAN: s_tilde / sigma_tilde are known to be +0.0 everywhere (f.tflag == 0);
+// the products 0 * E are formed exactly as in the reference (one value per
+// Prony term: the same for all d*d components), but stored only when one of
+// them is not +0.0 (E not finite, e.g. xi = NaN) -- a single rare branch per
+// dof -- which also raises `dirty` so the next launches read the fields
+// again.  Memory therefore always holds the exact values, in both modes.
+template <int D, bool ALL, bool LEAN>
+__device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f, int64_t s, const TState& ts,
+                                       bool& dirty) {
   constexpr int DD = D * D;
   // Eq. 9 (VEM:128-133): I*(alpha_s (T - T_prev) + (alpha_l - alpha_s)(Tf - Tf_prev)), Tf_prev == Tf (Q2)
   const double scal = c.alpha_s * (ts.T - ts.Tp) + c.dalpha * (ts.Tf - ts.Tf);
@@ -111,8 +121,8 @@ __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f
     }
   const double xi = ts.xi;
   double sig[DD];
-#pragma unroll
-  for (int n = 0; n < 6; ++n) {
+  uint64_t tz = 0;  // LEAN: bits of every 0 * E product
+  auto term = [&](const int n) {
     const double Eg = taylor_E(xi, c.lambda_g[n]);
     const double Ek = taylor_E(xi, c.lambda_k[n]);
     const double twog = 2.0 * c.g_n[n];
@@ -124,17 +134,21 @@ __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f
       // Eq. 15a + 20 (VEM:176-182)
       const double ds = (((twog * dev[q]) / xi) * c.lambda_g[n]) * omEg;
       // Eq. 16a (VEM:195-200)
-      const double st = f.st[o] * Eg;
+      const double st = (LEAN ? 0.0 : f.st[o]) * Eg;
+      if (LEAN) tz |= (uint64_t)__double_as_longlong(st);
       // Eq. 17a (VEM:212-215)
       const double sp = ds + st;
       // Eq. 15b + 20 (VEM:185-191)
       const double dsg = (((c.k_n[n] * (tr * (i == j ? 1.0 : 0.0))) / xi) * c.lambda_k[n]) * omEk;
       // Eq. 16b (VEM:203-209)
-      const double sgt = f.sgt[o] * Ek;
+      const double sgt = (LEAN ? 0.0 : f.sgt[o]) * Ek;
+      if (LEAN) tz |= (uint64_t)__double_as_longlong(sgt);
       // Eq. 17b (VEM:218-221)
       const double sgp = dsg + sgt;
-      f.st[o] = st;    // next -> current copy (TVP:559-560)
-      f.sgt[o] = sgt;  // (TVP:578-581)
+      if (!LEAN) {
+        f.st[o] = st;    // next -> current copy (TVP:559-560)
+        f.sgt[o] = sgt;  // (TVP:578-581)
+      }
       if (ALL) {
         f.ds[o] = ds;
         f.dsig[o] = dsg;
@@ -144,19 +158,49 @@ __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f
       // Eq. 18 (VEM:224-228), np.sum over n left to right
       sig[q] = (n == 0) ? (sp + sgp) : sig[q] + (sp + sgp);
     }
+    };
+  if constexpr (LEAN) {  // no loads: the whole term chain unrolled
+#pragma unroll
+    for (int n = 0; n < 6; ++n) term(n);
+  } else {  // 2 d*d tilde loads per term in flight, not 12 d*d (register budget)
+#pragma unroll 1
+    for (int n = 0; n < 6; ++n) term(n);
   }
 #pragma unroll
   for (int q = 0; q < DD; ++q) f.sigma[(int64_t)q * f.sS + s] = sig[q];
+  if (LEAN && tz != 0) {  // a non-finite E: materialise this dof's tilde values
+#pragma unroll 1
+    for (int n = 0; n < 6; ++n) {
+      const double st = 0.0 * taylor_E(xi, c.lambda_g[n]);
+      const double sgt = 0.0 * taylor_E(xi, c.lambda_k[n]);
+#pragma unroll 1
+      for (int q = 0; q < DD; ++q) {
+        const int64_t o = (int64_t)(n * DD + q) * f.sS + s;
+        f.st[o] = st;
+        f.sgt[o] = sgt;
+      }
+    }
+    dirty = true;
+  }
+}
+
+template <int D, bool ALL, bool LEAN>
+__device__ __forceinline__ void fused_loop(const ViscoConst& c, const ViscoFields& f) {
+  bool dirty = false;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
+    const int64_t dT = f.off_T + t;
+    const TState ts = t_part<ALL>(c, f, dT);
+    s_part<D, ALL, LEAN>(c, f, f.off_S + t, ts, dirty);
+    if (f.copy_Tprev) f.Tp[dT] = ts.T;  // TVP:378-379, T_prev is not read after this point
+  }
+  if (dirty) *f.tflag = 1;
 }
 
 template <int D, bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_fused(ViscoConst c, ViscoFields f) {
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
-    const int64_t dT = f.off_T + t;
-    const TState ts = t_part<ALL>(c, f, dT);
-    s_part<D, ALL>(c, f, f.off_S + t, ts);
-    if (f.copy_Tprev) f.Tp[dT] = ts.T;  // TVP:378-379, T_prev is not read after this point
-  }
+  // read once: a flag raised later in this launch changes nothing (see s_part)
+  if (*f.tflag == 0) fused_loop<D, ALL, true>(c, f);
+  else fused_loop<D, ALL, false>(c, f);
 }
 
 template <bool ALL>
@@ -168,8 +212,9 @@ __global__ __launch_bounds__(kBlock) void k_visco_T(ViscoConst c, ViscoFields f)
 
 // mixed families: sigma dof s reads the T-family values of the dof that the
 // last cell written by fem::interpolate assigns to it (f.map).
-template <int D, bool ALL>
-__global__ __launch_bounds__(kBlock) void k_visco_S(ViscoConst c, ViscoFields f) {
+template <int D, bool ALL, bool LEAN>
+__device__ __forceinline__ void s_loop(const ViscoConst& c, const ViscoFields& f) {
+  bool dirty = false;
   for (int64_t s = blockIdx.x * (int64_t)kBlock + threadIdx.x; s < f.n; s += (int64_t)gridDim.x * kBlock) {
     const int64_t t = f.map[s];
     TState ts;
@@ -177,8 +222,15 @@ __global__ __launch_bounds__(kBlock) void k_visco_S(ViscoConst c, ViscoFields f)
     ts.Tp = f.Tp[t];
     ts.Tf = f.Tf[t];
     ts.xi = f.xi[t];
-    s_part<D, ALL>(c, f, f.off_S + s, ts);
+    s_part<D, ALL, LEAN>(c, f, f.off_S + s, ts, dirty);
   }
+  if (dirty) *f.tflag = 1;
+}
+
+template <int D, bool ALL>
+__global__ __launch_bounds__(kBlock) void k_visco_S(ViscoConst c, ViscoFields f) {
+  if (*f.tflag == 0) s_loop<D, ALL, true>(c, f);
+  else s_loop<D, ALL, false>(c, f);
 }
 
 int blocks_for(int64_t n) {
