@@ -44,6 +44,7 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t evp[2] = {nullptr, nullptr};  // PCG convergence polls (double-buffered)
   tv_params P{};
   tv_options O{};
   int dim = 1;
@@ -74,7 +75,7 @@ struct Ctx {
   double* sums = nullptr;
   unsigned* counters = nullptr;  // arrival counters of the in-kernel reduction tails
   PcgState* st = nullptr;
-  PcgState* h_st = nullptr;  // pinned
+  PcgState* h_st = nullptr;  // pinned, 2 slots (PCG polls)
   double* h_sums = nullptr;  // pinned
   int* tflag = nullptr;       // device: s_tilde / sigma_tilde all +0.0 (0) or general (1), see ViscoFields
   double* scratch = nullptr;  // transfer scratch
@@ -87,6 +88,14 @@ struct Ctx {
   void* host_user = nullptr;
   double* h_halo = nullptr;  // pinned staging: 2 send + 2 recv planes
   size_t h_halo_n = 0;
+  // in-solve kernel timing (tv_kernel_timing): HIP events around the fused
+  // matvec and the PCG update of every iteration, and around the visco update
+  bool ktime = false;
+  int kstride = 8;                   // every kstride-th PCG iteration is timed (events cost ~4 us each)
+  std::vector<hipEvent_t> kev;       // 3 per timed PCG iteration of the current solve
+  hipEvent_t vev[2] = {nullptr, nullptr};
+  double ksum[3] = {0.0, 0.0, 0.0};  // ms: fused matvec, PCG update, visco update
+  int64_t kcnt[3] = {0, 0, 0};
   // stats
   int last_newton = 0, last_krylov = 0;
   double last_dx = 0.0;
@@ -424,7 +433,8 @@ static int setup_fields(Ctx* c) {
   HIPC(hipMalloc(&c->st, sizeof(PcgState)));
   HIPC(hipMalloc(&c->tflag, sizeof(int)));
   HIPC(hipMemsetAsync(c->tflag, 0, sizeof(int), c->stream));  // the tilde fields start at +0.0
-  HIPC(hipHostMalloc(&c->h_st, sizeof(PcgState)));
+  HIPC(hipHostMalloc(&c->h_st, 2 * sizeof(PcgState)));
+  for (int k = 0; k < 2; ++k) HIPC(hipEventCreateWithFlags(&c->evp[k], hipEventDisableTiming));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
   return TV_OK;
 }
@@ -590,7 +600,26 @@ static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tai
 // --------------------------------------------------------------------------------------
 // it: index of this iteration within the solve (the device counter st->it
 // equals it until convergence, after which every kernel exits at once)
+static int kev_at(Ctx* c, int i, hipEvent_t* e) {  // event i of the current solve (pool grows)
+  while ((int)c->kev.size() <= i) {
+    hipEvent_t ev;
+    HIPC(hipEventCreate(&ev));
+    c->kev.push_back(ev);
+  }
+  *e = c->kev[i];
+  return TV_OK;
+}
+
 static int pcg_iteration(Ctx* c, const double* T, int it) {
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  const bool timed = c->ktime && (it % c->kstride) == 0;
+  if (timed) {
+    const int k = it / c->kstride;
+    if (int e = kev_at(c, 3 * k, &e0)) return e;
+    if (int e = kev_at(c, 3 * k + 1, &e1)) return e;
+    if (int e = kev_at(c, 3 * k + 2, &e2)) return e;
+    HIPC(hipEventRecord(e0, c->stream));
+  }
   const int64_t off = c->ownT_off, n = c->ownT_n;
   const bool multi = multi_rank(c);
   // single GPU: the last-arriving workgroup of each launch reduces the partial
@@ -599,6 +628,7 @@ static int pcg_iteration(Ctx* c, const double* T, int it) {
   RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2};
   int np = 0;
   const bool fused1 = op_japply_fused(c, T, &np, &t1, it);  // p <- z + b p ; w <- J p ; p.w
+  if (timed) HIPC(hipEventRecord(e1, c->stream));
   if (!fused1) {
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
   } else if (multi) {
@@ -609,6 +639,7 @@ static int pcg_iteration(Ctx* c, const double* T, int it) {
   const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
                     c->r + off, c->z + off, c->partials, c->stream, &t2, &fa, it);
+  if (timed) HIPC(hipEventRecord(e2, c->stream));
   if (multi) {  // dp, beta, convergence
     if (int e = allreduce(c, c->sums, 2)) return e;
     launch_logic(c->st, c->sums, 3, c->stream);
@@ -629,23 +660,46 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   launch_pcg_init(n, c->r + off, c->dinv + off, c->z + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
   if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 1, 0)) return e;
   if (int e = halo(c, c->z)) return e;
-  int launched = 0;
-  int batch = std::max(1, c->pcg_hint > 2 ? c->pcg_hint - 1 : c->O.pcg_batch);
-  for (;;) {
-    for (int b = 0; b < batch; ++b) {
+  // Batches of iterations are queued one ahead of the convergence poll: while
+  // the host waits for the state copied at the end of batch k, batch k + 1 is
+  // already in the stream, so the GPU never idles on the host's turnaround.
+  // After convergence the queued launches exit at their first instruction.
+  int launched = 0, slot = 0;
+  auto enqueue = [&](int nb, int k) -> int {
+    for (int b = 0; b < nb; ++b)
       if (int e = pcg_iteration(c, T, launched + b)) return e;
-    }
-    launched += batch;
+    launched += nb;
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(c->h_st, c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipStreamSynchronize(c->stream));
-    if (c->h_st->done) break;
-    if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
-    batch = std::max(1, c->O.pcg_batch);
+    HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[k], c->stream));
+    return TV_OK;
+  };
+  const int small = std::max(1, c->O.pcg_batch / 2);
+  if (int e = enqueue(std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
+  for (;;) {
+    if (int e = enqueue(small, slot ^ 1)) return e;
+    HIPC(hipEventSynchronize(c->evp[slot]));
+    if (c->h_st[slot].done) break;
+    if (launched > c->O.ksp_max_it + 2 * small + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    slot ^= 1;
   }
-  *its = c->h_st->it;
-  *reason = c->h_st->reason;
-  c->pcg_hint = c->h_st->it;
+  // (the batch queued behind the converged one exits early; stream order covers it)
+  *its = c->h_st[slot].it;
+  *reason = c->h_st[slot].reason;
+  c->pcg_hint = c->h_st[slot].it;
+  if (c->ktime) {  // productive iterations only (their events precede the converged poll)
+    int nt = 0;
+    for (int it = 0; it < *its; it += c->kstride, ++nt) {
+      const int k = it / c->kstride;
+      float a = 0.f, b = 0.f;
+      HIPC(hipEventElapsedTime(&a, c->kev[3 * k], c->kev[3 * k + 1]));
+      HIPC(hipEventElapsedTime(&b, c->kev[3 * k + 1], c->kev[3 * k + 2]));
+      c->ksum[0] += a;
+      c->ksum[1] += b;
+    }
+    c->kcnt[0] += nt;
+    c->kcnt[1] += nt;
+  }
   return TV_OK;
 }
 
@@ -925,6 +979,11 @@ int tv_destroy(void* ctx) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  for (int k = 0; k < 2; ++k) {
+    if (c->evp[k]) hipEventDestroy(c->evp[k]);
+    if (c->vev[k]) hipEventDestroy(c->vev[k]);
+  }
+  for (hipEvent_t e : c->kev) hipEventDestroy(e);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return TV_OK;
@@ -1090,7 +1149,16 @@ int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its) {
   int conv = 0;
   if (int e = newton(c, newton_its, krylov_its, &conv)) return e;
   if (!thermal_only) {
+    if (c->ktime) HIPC(hipEventRecord(c->vev[0], c->stream));
     if (int e = visco(c, true)) return e;  // includes T_prev <- T (ThermoViscoProblem.py:378-379)
+    if (c->ktime) {
+      HIPC(hipEventRecord(c->vev[1], c->stream));
+      HIPC(hipEventSynchronize(c->vev[1]));
+      float a = 0.f;
+      HIPC(hipEventElapsedTime(&a, c->vev[0], c->vev[1]));
+      c->ksum[2] += a;
+      c->kcnt[2] += 1;
+    }
   } else {
     launch_copy(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, c->stream);
   }
@@ -1185,9 +1253,13 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       *bytes = 24.0 * n;
       break;
     case 3:  // fused PCG matvec: read z, p_old, write p, w (T on boundary nodes only)
+    case 5:
+    case 7:
       *bytes = 32.0 * n;
       break;
     case 4:  // PCG update: read p, w, dinv, dx, r; write dx, r, z
+    case 6:
+    case 8:
       *bytes = 64.0 * n;
       break;
     default:
@@ -1200,7 +1272,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !ms || reps < 1) return TV_ERR_ARG;
   hipSetDevice(c->device);
-  if (kernel == 3 || kernel == 4) {  // PCG kernels need a running solver state
+  if (kernel >= 3 && kernel <= 8) {  // PCG kernels need a running solver state
     PcgState h{};
     h.beta = 1.0; h.betaold = 2.0; h.a = 1e-3; h.it = 1; h.done = 0; h.max_it = 1 << 30;
     HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
@@ -1222,6 +1294,39 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       default: return c->fail(TV_ERR_ARG, "unknown kernel id");
     }
   };
+  if (kernel >= 5 && kernel <= 8) {
+    // matvec / update timed inside whole PCG iterations (march then update,
+    // alternating, as in the solve), with (5, 6) or without (7, 8) the
+    // in-kernel reduction tails (kind 0: reduce only, the state is not touched)
+    if (c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "kernel ids 5-8: CG temperature space only");
+    const bool tails = kernel <= 6;
+    std::vector<hipEvent_t> ev(3 * (size_t)(reps + 1));
+    for (auto& e : ev) HIPC(hipEventCreate(&e));
+    const FaceAdd fa = cg_face_add(c->cg, c->ownT_off);
+    const int64_t off = c->ownT_off, n = c->ownT_n;
+    int np = 0;
+    for (int i = 0; i <= reps; ++i) {
+      RedTail t1{tails ? c->counters : nullptr, c->partials, c->sums, c->st, 0};
+      RedTail t2{tails ? c->counters + 1 : nullptr, c->partials, c->sums, c->st, 0};
+      HIPC(hipEventRecord(ev[3 * i], c->stream));
+      op_japply_fused(c, c->f[TV_F_T].ptr, &np, &t1, 1);
+      HIPC(hipEventRecord(ev[3 * i + 1], c->stream));
+      launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
+                        c->r + off, c->z + off, c->partials, c->stream, &t2, &fa, 1);
+      HIPC(hipEventRecord(ev[3 * i + 2], c->stream));
+    }
+    HIPC(hipEventSynchronize(ev.back()));
+    double sum = 0.0;
+    const int k0 = (kernel == 5 || kernel == 7) ? 0 : 1;
+    for (int i = 1; i <= reps; ++i) {  // rep 0 is the warm-up
+      float t = 0.f;
+      HIPC(hipEventElapsedTime(&t, ev[3 * i + k0], ev[3 * i + k0 + 1]));
+      sum += t;
+    }
+    for (auto& e : ev) hipEventDestroy(e);
+    *ms = sum / reps;
+    return TV_OK;
+  }
   if (int e = one()) return e;  // warm-up
   HIPC(hipEventRecord(c->ev0, c->stream));
   for (int i = 0; i < reps; ++i)
@@ -1231,6 +1336,31 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
   float t = 0.f;
   HIPC(hipEventElapsedTime(&t, c->ev0, c->ev1));
   *ms = (double)t / reps;
+  return TV_OK;
+}
+
+int tv_kernel_timing(void* ctx, int on) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  for (int k = 0; k < 2; ++k)
+    if (!c->vev[k]) HIPC(hipEventCreate(&c->vev[k]));
+  c->ktime = on > 0;
+  c->kstride = on > 1 ? on : 8;
+  for (int k = 0; k < 3; ++k) {
+    c->ksum[k] = 0.0;
+    c->kcnt[k] = 0;
+  }
+  return TV_OK;
+}
+
+int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !ms_avg) return TV_ERR_ARG;
+  const int k = (kernel == 3) ? 0 : (kernel == 4) ? 1 : (kernel == 1) ? 2 : -1;
+  if (k < 0) return c->fail(TV_ERR_ARG, "tv_kernel_stats: kernel 3 (fused matvec), 4 (PCG update) or 1 (visco)");
+  *ms_avg = c->kcnt[k] ? c->ksum[k] / (double)c->kcnt[k] : 0.0;
+  if (launches) *launches = c->kcnt[k];
   return TV_OK;
 }
 

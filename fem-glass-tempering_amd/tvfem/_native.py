@@ -30,7 +30,7 @@ EXPORTS = [
     "tv_num_dofs", "tv_field_block_size", "tv_dof_coordinates", "tv_set_field", "tv_get_field",
     "tv_field_device_ptr", "tv_set_initial_condition", "tv_sync", "tv_residual", "tv_jacobian_apply",
     "tv_jacobian_diag", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
-    "tv_comm_get_unique_id", "tv_comm_init", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes",
+    "tv_comm_get_unique_id", "tv_comm_init", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes", "tv_kernel_timing", "tv_kernel_stats",
     "tv_last_stats", "tv_comm_init_host", "tv_partition_layout",
 ]
 
@@ -121,6 +121,8 @@ def load_library():
         "tv_halo_exchange": (C.c_int, [vp, C.c_int]),
         "tv_time_kernel": (C.c_int, [vp, C.c_int, C.c_int, dp]),
         "tv_kernel_bytes": (C.c_int, [vp, C.c_int, dp]),
+        "tv_kernel_timing": (C.c_int, [vp, C.c_int]),
+        "tv_kernel_stats": (C.c_int, [vp, C.c_int, dp, C.POINTER(C.c_int64)]),
         "tv_last_stats": (C.c_int, [vp, ip, ip, dp]),
         "tv_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, HOST_ALLREDUCE_FN, HOST_SENDRECV_FN, vp]),
         "tv_partition_layout": (C.c_int, [C.POINTER(MeshDesc), i64p]),

@@ -250,3 +250,36 @@ def test_storage_permutation_consistent():
     T = dev.functions_current["T"].x.array
     assert relerr(T[od], ref.functions_current["T"][orr]) < 1e-10
     dev.close()
+
+
+def test_visco_lean_tilde_tracking_nonfinite():
+    """s~ / sigma~ start at +0.0 and are then neither read nor written (lean
+    update) until a non-finite E appears: a dof with T < 0 gives phi = inf,
+    xi = NaN, so 0 * E = NaN there.  The lean pass must store exactly those
+    NaNs, and the next pass (general path) must match the oracle again."""
+    _torch()
+    axes = AXES["3d"]
+    dev, ref = make_pair(axes, {"T": CG, "sigma": CG})
+    rng = np.random.default_rng(7)
+    n = ref.VT.n
+    T = rng.uniform(780.0, 880.0, n)
+    T[n // 3] = -5.0
+    Tp = T + rng.uniform(-2.0, 2.0, n)
+    for fld, v in (("T", T), ("T_prev", Tp)):
+        dev.set_field(fld, v)
+    ref.functions_current["T"][:] = T
+    ref.functions_previous["T"][:] = Tp
+    for it in range(2):
+        assert dev._lib.tv_visco_update(dev._ctx) == 0
+        dev._device_version += 1
+        with np.errstate(all="ignore"):
+            ref.visco_update()
+        for k, v in (("s_tilde_partial", ref.functions_current["s_tilde_partial"]),
+                     ("sigma_tilde_partial", ref.functions_current["sigma_tilde_partial"]),
+                     ("sigma", ref.functions_next["sigma"]), ("xi", ref.functions["xi"])):
+            got = dev.get_field(k)
+            assert np.array_equal(np.isnan(got), np.isnan(v)), (it, k)
+            assert relerr(got, v) < 1e-9, (it, k)
+        st = dev.get_field("s_tilde_partial")
+        assert np.isnan(st).any() and (st[~np.isnan(st)] == 0.0).all()
+    dev.close()

@@ -7,7 +7,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 echo "[gpu_check] tests" && \
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/tests.log 2>&1 && tail -3 $OUT/tests.log && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1 && tail -3 $OUT/tests.log && \
 echo "[gpu_check] pmc fetch" && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 tools/pmc_kernels.py > $OUT/pmc_fetch.log 2>&1 && \
 echo "[gpu_check] pmc write" && \
