@@ -110,8 +110,10 @@ def main():
     for _ in range(a.warmup):
         step()
     barrier_sync()
-    # the hot kernels are timed inside the timed steps themselves (HIP events on
-    # the context stream around every converging PCG iteration's launches)
+    # the hot kernels are timed inside the timed steps themselves: the fused
+    # matvec and the update of every converging PCG iteration write device clock
+    # stamps (first workgroup's start, reduction tail's end), the visco update is
+    # bracketed by HIP events
     if not a.no_kernel_timing:
         N.check(lib.tv_kernel_timing(ctx, 1), ctx)
     t0 = time.perf_counter()
@@ -131,8 +133,9 @@ def main():
         elapsed = dt_local
 
     # ---- per-kernel timing and algorithmic bytes ----
-    # "ms": mean launch duration inside the timed steps (HIP events around every
-    # launch of the converging PCG iterations / the visco update); "ms_isolated":
+    # "ms": mean launch duration inside the timed steps (device clock stamps of
+    # every launch of the converging PCG iterations / HIP events around the visco
+    # update); "ms_isolated":
     # back-to-back launches after the timed region (inputs partly Infinity-Cache
     # resident, so faster than in the solve; reported for reference only)
     kern = {}

@@ -88,11 +88,16 @@ struct Ctx {
   void* host_user = nullptr;
   double* h_halo = nullptr;  // pinned staging: 2 send + 2 recv planes
   size_t h_halo_n = 0;
-  // in-solve kernel timing (tv_kernel_timing): HIP events around the fused
-  // matvec and the PCG update of every iteration, and around the visco update
+  // in-solve kernel timing (tv_kernel_timing): the fused matvec and the PCG
+  // update stamp the device REALTIME clock at their start (workgroup 0) and at
+  // the end of their reduction tail into d_ts (4 stamps per PCG iteration, one
+  // slot per iteration, read back in bulk); HIP events around the visco update
   bool ktime = false;
-  int kstride = 8;                   // every kstride-th PCG iteration is timed (events cost ~4 us each)
-  std::vector<hipEvent_t> kev;       // 3 per timed PCG iteration of the current solve
+  int kstride = 1;                   // every kstride-th PCG iteration is timed
+  uint64_t* d_ts = nullptr;          // kTsCap slots x {matvec start, end, update start, end}
+  int ts_next = 0;                   // first free slot
+  std::vector<int> ts_pending;       // slots of productive iterations not yet read back
+  double ts_khz = 0.0;               // REALTIME clock (hipDeviceAttributeWallClockRate)
   hipEvent_t vev[2] = {nullptr, nullptr};
   double ksum[3] = {0.0, 0.0, 0.0};  // ms: fused matvec, PCG update, visco update
   int64_t kcnt[3] = {0, 0, 0};
@@ -600,46 +605,53 @@ static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tai
 // --------------------------------------------------------------------------------------
 // it: index of this iteration within the solve (the device counter st->it
 // equals it until convergence, after which every kernel exits at once)
-static int kev_at(Ctx* c, int i, hipEvent_t* e) {  // event i of the current solve (pool grows)
-  while ((int)c->kev.size() <= i) {
-    hipEvent_t ev;
-    HIPC(hipEventCreate(&ev));
-    c->kev.push_back(ev);
+constexpr int kTsCap = 1 << 15;
+
+// reads the pending timestamp slots back and adds them to the stats
+static int ts_flush(Ctx* c) {
+  if (!c->d_ts) return TV_OK;
+  if (!c->ts_pending.empty()) {
+    std::vector<uint64_t> h((size_t)4 * c->ts_next);
+    HIPC(hipMemcpyAsync(h.data(), c->d_ts, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (int sl : c->ts_pending) {
+      const uint64_t* t = &h[(size_t)4 * sl];
+      for (int k = 0; k < 2; ++k) {
+        if (t[2 * k] == 0 || t[2 * k + 1] < t[2 * k]) continue;  // launch without a timed tail
+        c->ksum[k] += (double)(t[2 * k + 1] - t[2 * k]) / c->ts_khz;
+        c->kcnt[k] += 1;
+      }
+    }
+    c->ts_pending.clear();
   }
-  *e = c->kev[i];
+  c->ts_next = 0;
+  HIPC(hipMemsetAsync(c->d_ts, 0, (size_t)4 * kTsCap * sizeof(uint64_t), c->stream));
   return TV_OK;
 }
 
 static int pcg_iteration(Ctx* c, const double* T, int it) {
-  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-  const bool timed = c->ktime && (it % c->kstride) == 0;
-  if (timed) {
-    const int k = it / c->kstride;
-    if (int e = kev_at(c, 3 * k, &e0)) return e;
-    if (int e = kev_at(c, 3 * k + 1, &e1)) return e;
-    if (int e = kev_at(c, 3 * k + 2, &e2)) return e;
-    HIPC(hipEventRecord(e0, c->stream));
-  }
   const int64_t off = c->ownT_off, n = c->ownT_n;
+  // timestamp slot of this iteration (see ts_flush); the matvec launchers
+  // without a reduction tail (DG, 1D/2D CG) leave theirs at 0
+  const int slot = c->ts_next + it;
+  uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
   const bool multi = multi_rank(c);
   // single GPU: the last-arriving workgroup of each launch reduces the partial
   // records and runs the KSPCG scalar logic in-kernel (no separate reduce
   // launch); multi-GPU: it only reduces, RCCL all-reduces, then the logic runs.
-  RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2};
+  RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2, ts};
   int np = 0;
   const bool fused1 = op_japply_fused(c, T, &np, &t1, it);  // p <- z + b p ; w <- J p ; p.w
-  if (timed) HIPC(hipEventRecord(e1, c->stream));
   if (!fused1) {
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
   } else if (multi) {
     if (int e = allreduce(c, c->sums, 1)) return e;
     launch_logic(c->st, c->sums, 2, c->stream);
   }
-  RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3};
+  RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
   const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
                     c->r + off, c->z + off, c->partials, c->stream, &t2, &fa, it);
-  if (timed) HIPC(hipEventRecord(e2, c->stream));
   if (multi) {  // dp, beta, convergence
     if (int e = allreduce(c, c->sums, 2)) return e;
     launch_logic(c->st, c->sums, 3, c->stream);
@@ -660,6 +672,8 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   launch_pcg_init(n, c->r + off, c->dinv + off, c->z + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
   if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 1, 0)) return e;
   if (int e = halo(c, c->z)) return e;
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 4 * c->O.pcg_batch + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
   // Batches of iterations are queued one ahead of the convergence poll: while
   // the host waits for the state copied at the end of batch k, batch k + 1 is
   // already in the stream, so the GPU never idles on the host's turnaround.
@@ -674,7 +688,7 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipEventRecord(c->evp[k], c->stream));
     return TV_OK;
   };
-  const int small = std::max(1, c->O.pcg_batch / 2);
+  const int small = std::max(1, c->O.pcg_batch / 4);  // batches queued behind the first: 2 iterations
   if (int e = enqueue(std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
   for (;;) {
     if (int e = enqueue(small, slot ^ 1)) return e;
@@ -687,18 +701,10 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   *its = c->h_st[slot].it;
   *reason = c->h_st[slot].reason;
   c->pcg_hint = c->h_st[slot].it;
-  if (c->ktime) {  // productive iterations only (their events precede the converged poll)
-    int nt = 0;
-    for (int it = 0; it < *its; it += c->kstride, ++nt) {
-      const int k = it / c->kstride;
-      float a = 0.f, b = 0.f;
-      HIPC(hipEventElapsedTime(&a, c->kev[3 * k], c->kev[3 * k + 1]));
-      HIPC(hipEventElapsedTime(&b, c->kev[3 * k + 1], c->kev[3 * k + 2]));
-      c->ksum[0] += a;
-      c->ksum[1] += b;
-    }
-    c->kcnt[0] += nt;
-    c->kcnt[1] += nt;
+  if (c->ktime) {  // productive iterations only (launches queued behind convergence exit at once)
+    for (int it = 0; it < *its; it += c->kstride)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
   }
   return TV_OK;
 }
@@ -983,7 +989,7 @@ int tv_destroy(void* ctx) {
     if (c->evp[k]) hipEventDestroy(c->evp[k]);
     if (c->vev[k]) hipEventDestroy(c->vev[k]);
   }
-  for (hipEvent_t e : c->kev) hipEventDestroy(e);
+  if (c->d_ts) hipFree(c->d_ts);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
   return TV_OK;
@@ -1345,8 +1351,18 @@ int tv_kernel_timing(void* ctx, int on) {
   hipSetDevice(c->device);
   for (int k = 0; k < 2; ++k)
     if (!c->vev[k]) HIPC(hipEventCreate(&c->vev[k]));
+  if (!c->d_ts) {
+    int khz = 0;
+    HIPC(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    if (khz <= 0) return c->fail(TV_ERR_HIP, "tv_kernel_timing: no device wall clock rate");
+    c->ts_khz = (double)khz;
+    HIPC(hipMalloc(&c->d_ts, (size_t)4 * kTsCap * sizeof(uint64_t)));
+  }
+  c->ts_pending.clear();
+  c->ts_next = kTsCap;  // zeroes the stamps
+  if (int e = ts_flush(c)) return e;
   c->ktime = on > 0;
-  c->kstride = on > 1 ? on : 8;
+  c->kstride = on > 1 ? on : 1;
   for (int k = 0; k < 3; ++k) {
     c->ksum[k] = 0.0;
     c->kcnt[k] = 0;
@@ -1359,6 +1375,8 @@ int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches) {
   if (!c || !ms_avg) return TV_ERR_ARG;
   const int k = (kernel == 3) ? 0 : (kernel == 4) ? 1 : (kernel == 1) ? 2 : -1;
   if (k < 0) return c->fail(TV_ERR_ARG, "tv_kernel_stats: kernel 3 (fused matvec), 4 (PCG update) or 1 (visco)");
+  hipSetDevice(c->device);
+  if (int e = ts_flush(c)) return e;
   *ms_avg = c->kcnt[k] ? c->ksum[k] / (double)c->kcnt[k] : 0.0;
   if (launches) *launches = c->kcnt[k];
   return TV_OK;

@@ -651,6 +651,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
                                                         double* __restrict__ partials, int nseg, int raxis,
                                                         int qchunk, RedTail rt, int nrec, int nmarch,
                                                         FaceOff fo, int ffirst, int exp, int it_host) {
+  stamp_start(rt);
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
   __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
   __shared__ double red[R];
@@ -1008,6 +1009,7 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march_dma(CgGrid g, const doub
                                                             double* __restrict__ partials, int nseg, int raxis,
                                                             int qchunk, RedTail rt, int nrec, int nmarch, FaceOff fo,
                                                             int exp, int it_host) {
+  stamp_start(rt);
   constexpr int NA = FUSEP ? 2 : 1;                 // arrays per row: z (x) [, p_old]
   // plane slab: rows r0 - 1 .. r0 + R (slots 0 .. R + 1) and slot R + 2, the
   // target of the non-halo waves' halo DMAs (all of a step's DMAs stay inside

@@ -146,7 +146,14 @@ __device__ __forceinline__ void fused_reduce_tail(const RedTail& rt, int n) {
   if (threadIdx.x == 0) {
     for (int w = 0; w < W; ++w) rt.out[w] = sums[w];
     apply_logic(rt.st, sums, rt.kind);
+    if (rt.ts) rt.ts[1] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+// Start stamp of a launch with a timed reduction tail: workgroup 0 is the
+// first one the dispatcher places, so its entry time is the launch's start.
+__device__ __forceinline__ void stamp_start(const RedTail& rt) {
+  if (rt.ts && blockIdx.x == 0 && threadIdx.x == 0) rt.ts[0] = __builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace tv

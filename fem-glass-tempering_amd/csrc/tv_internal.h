@@ -75,6 +75,9 @@ struct RedTail {
   double* out;                // reduced sums (read by RCCL allreduce on multi-GPU)
   PcgState* st;
   int kind;                   // 0 none, 1 init, 2 p.w, 3 update
+  // in-solve kernel timing (tv_kernel_timing), or nullptr: ts[0] = REALTIME
+  // clock when workgroup 0 starts, ts[1] = when the tail workgroup finishes
+  uint64_t* ts;
 };
 
 enum PcgReason {

@@ -100,6 +100,7 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
                                                        double* __restrict__ r, double* __restrict__ z,
                                                        double* __restrict__ partials, RedTail rt, FaceAdd fa,
                                                        int it_host) {
+  stamp_start(rt);
   if (st->done) return;
   const double a = st->a;
   const double* __restrict__ p = (it_host & 1) ? pB : pA;  // == st->it while the solve runs

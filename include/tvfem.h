@@ -211,10 +211,12 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
 int tv_time_kernel(void* ctx, int kernel, int reps, double* ms_per_launch);
 /* algorithmic bytes moved by one launch of `kernel` */
 int tv_kernel_bytes(void* ctx, int kernel, double* bytes);
-/* in-solve timing: with `on` > 0, every following tv_step records HIP events on
- * the context stream around the fused PCG matvec (kernel 3) and the PCG update
- * (4) of every `on`-th converging iteration (on = 1: 8th) and around the
- * viscoelastic update (1); the counters restart at every call.
+/* in-solve timing: with `on` > 0, every following tv_step times the fused PCG
+ * matvec (kernel 3) and the PCG update (4) of every converging iteration
+ * (on > 1: every on-th) from device clock stamps the launches write themselves
+ * (first workgroup's start, reduction tail's end: what a kernel trace reports),
+ * and the viscoelastic update (1) with HIP events; the counters restart at every
+ * call.  Kernel 3 is timed on the 3D CG marching path only (launches 0 else).
  * tv_kernel_stats returns the mean duration (ms) and the number of timed launches. */
 int tv_kernel_timing(void* ctx, int on);
 int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches);

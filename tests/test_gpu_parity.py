@@ -283,3 +283,40 @@ def test_visco_lean_tilde_tracking_nonfinite():
         st = dev.get_field("s_tilde_partial")
         assert np.isnan(st).any() and (st[~np.isnan(st)] == 0.0).all()
     dev.close()
+
+
+def test_in_solve_kernel_timing():
+    """tv_kernel_timing: the fused matvec and the update of every converging PCG
+    iteration stamp their own start / end; the stamps must not change the
+    solution, and every productive iteration must be counted once."""
+    _torch()
+    import ctypes as C
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    axes = [np.linspace(0.0, 2.0, 41), np.linspace(0.0, 2.0, 37), np.linspace(0.0, 1.0, 11)]
+    cfg = {"T": CG, "sigma": CG}
+    runs = []
+    for timing in (False, True):
+        p = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                               part_axis=2, materialize=False, verbose=False)
+        p.setup()
+        if timing:
+            assert p._lib.tv_kernel_timing(p._ctx, 1) == 0
+        its = 0
+        for _ in range(2):
+            p.solve_timestep()
+            its += p.last_krylov_iterations
+        stats = {}
+        if timing:
+            for kid in (3, 4, 1):
+                ms, cnt = C.c_double(), C.c_int64()
+                assert p._lib.tv_kernel_stats(p._ctx, kid, C.byref(ms), C.byref(cnt)) == 0
+                stats[kid] = (ms.value, cnt.value)
+        runs.append((p.get_field("T"), its, stats))
+        p.close()
+    (T0, its0, _), (T1, its1, st) = runs
+    assert np.array_equal(T0, T1) and its0 == its1
+    assert st[3][1] == its1 and st[4][1] == its1, (st, its1)
+    assert st[1][1] == 2
+    for kid in (3, 4, 1):
+        assert 0.0 < st[kid][0] < 50.0, st

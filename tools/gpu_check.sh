@@ -17,3 +17,8 @@ cp $OUT/pmc_matvec_400x400x50_n1.json profiles/ && \
 echo "[gpu_check] bench" && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o run --output-format csv -- python3 bench.py > $OUT/bench.json 2> $OUT/bench.err && \
 cat $OUT/bench.json
+[ $? -eq 0 ] && \
+python3 tools/profile_summary.py $OUT/prof_bench $OUT/bench.json $OUT/profile_summary.json > $OUT/profile_summary.log 2>&1 && \
+echo "[gpu_check] bench (no profiler)" && \
+timeout -k 10 600 python3 bench.py > $OUT/bench_plain.json 2> $OUT/bench_plain.err && \
+cat $OUT/bench_plain.json
