@@ -651,7 +651,7 @@ static int pcg_iteration(Ctx* c, const double* T, int it) {
   RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
   const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
-                    c->r + off, c->z + off, c->partials, c->stream, &t2, &fa, it);
+                    c->z + off, c->partials, c->stream, &t2, &fa, it);
   if (multi) {  // dp, beta, convergence
     if (int e = allreduce(c, c->sums, 2)) return e;
     launch_logic(c->st, c->sums, 3, c->stream);
@@ -700,6 +700,7 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   // (the batch queued behind the converged one exits early; stream order covers it)
   *its = c->h_st[slot].it;
   *reason = c->h_st[slot].reason;
+  launch_pcg_dx_tail(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
   c->pcg_hint = c->h_st[slot].it;
   if (c->ktime) {  // productive iterations only (launches queued behind convergence exit at once)
     for (int it = 0; it < *its; it += c->kstride)
@@ -1263,10 +1264,10 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
     case 7:
       *bytes = 32.0 * n;
       break;
-    case 4:  // PCG update: read p, w, dinv, dx, r; write dx, r, z
+    case 4:  // PCG update, mean of an even / odd pair: read w, dinv, z, write z (+ odd: read p_prev, p, dx, write dx)
     case 6:
     case 8:
-      *bytes = 64.0 * n;
+      *bytes = 48.0 * n;
       break;
     default:
       return c->fail(TV_ERR_ARG, "unknown kernel id");
@@ -1283,6 +1284,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     h.beta = 1.0; h.betaold = 2.0; h.a = 1e-3; h.it = 1; h.done = 0; h.max_it = 1 << 30;
     HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
   }
+  int upd_it = 0;
   auto one = [&]() -> int {
     int np = 0;
     switch (kernel) {
@@ -1293,8 +1295,8 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       case 4: {
         const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, c->ownT_off) : FaceAdd{};
         launch_pcg_update(c->ownT_n, c->st, c->pA + c->ownT_off, c->pB + c->ownT_off, c->w + c->ownT_off,
-                          c->dinv + c->ownT_off, c->f[TV_F_DX].ptr + c->ownT_off, c->r + c->ownT_off,
-                          c->z + c->ownT_off, c->partials, c->stream, nullptr, &fa, 1);
+                          c->dinv + c->ownT_off, c->f[TV_F_DX].ptr + c->ownT_off, c->z + c->ownT_off,
+                          c->partials, c->stream, nullptr, &fa, upd_it++);  // even / odd alternate
         return TV_OK;
       }
       default: return c->fail(TV_ERR_ARG, "unknown kernel id");
@@ -1315,10 +1317,10 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       RedTail t1{tails ? c->counters : nullptr, c->partials, c->sums, c->st, 0};
       RedTail t2{tails ? c->counters + 1 : nullptr, c->partials, c->sums, c->st, 0};
       HIPC(hipEventRecord(ev[3 * i], c->stream));
-      op_japply_fused(c, c->f[TV_F_T].ptr, &np, &t1, 1);
+      op_japply_fused(c, c->f[TV_F_T].ptr, &np, &t1, i + 1);  // both parities, as in the solve
       HIPC(hipEventRecord(ev[3 * i + 1], c->stream));
       launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
-                        c->r + off, c->z + off, c->partials, c->stream, &t2, &fa, 1);
+                        c->z + off, c->partials, c->stream, &t2, &fa, i + 1);
       HIPC(hipEventRecord(ev[3 * i + 2], c->stream));
     }
     HIPC(hipEventSynchronize(ev.back()));

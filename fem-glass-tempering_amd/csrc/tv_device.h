@@ -111,6 +111,7 @@ __device__ __forceinline__ void logic_dpi(PcgState* st, const double* sums) {
   }
   st->dpi = dpi;
   st->dpiold = dpi;
+  st->a_prev = st->a;
   st->a = st->beta / dpi;
 }
 

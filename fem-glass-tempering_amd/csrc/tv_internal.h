@@ -64,7 +64,8 @@ struct PcgState {
   double rtol, atol, dtol;
   int it, done, reason, max_it;
   double dx_norm2;            // ||dx||^2 of the last Newton update
-  double pad[3];
+  double a_prev;              // step length of the previous iteration (dx is updated every 2nd)
+  double pad[2];
 };
 
 // In-kernel reduction tail (last-arriving workgroup reduces the partial records
@@ -141,7 +142,11 @@ void launch_visco_Spass(int dim, int all, const ViscoConst& c, const ViscoFields
 constexpr int kVecBlocks = 1024;
 void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx,
                      double* partials, hipStream_t s);
-// p is taken from buffer (st->it & 1 ? pB : pA), matching the fused matvec
+// PCG update of iteration it_host: w += facet terms, r <- r - a w, z <- B r
+// with r = z / dinv (r is not stored: its recurrence runs through z), and on
+// odd iterations dx <- dx + a_prev p_prev + a p (both p buffers are live, so
+// the dx stream is read and written every second iteration only); p is taken
+// from buffer (it_host & 1 ? pB : pA), matching the fused matvec
 // Robin facet terms the fused CG matvec leaves out of w (marching path): the
 // PCG update adds fface at the owned boundary nodes (see k_cg_march)
 struct FaceAdd {
@@ -154,9 +159,12 @@ struct FaceAdd {
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off);
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
-                       const double* dinv, double* dx, double* r, double* z, double* partials,
-                       hipStream_t s, const RedTail* tail = nullptr, const FaceAdd* fa = nullptr,
-                       int it_host = 0);
+                       const double* dinv, double* dx, double* z, double* partials, hipStream_t s,
+                       const RedTail* tail = nullptr, const FaceAdd* fa = nullptr, int it_host = 0);
+// after a solve of `its` iterations with its odd: dx <- dx + a p of the last
+// iteration (the step the pairwise dx update has not applied yet)
+void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, int its,
+                        hipStream_t s);
 // one-block deterministic reduce of n records of width W (<= 2) into out[W];
 // kind: 0 none, 1 PCG init logic, 2 PCG p.w logic, 3 PCG update logic
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,

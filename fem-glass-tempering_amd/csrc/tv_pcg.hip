@@ -76,8 +76,8 @@ __device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
   return add;
 }
 
-// Cache policy of the update's streams (TVFEM_NT bits, default 7): 1 = w, dx, r
-// loads non-temporal, 2 = dx, r stores non-temporal, 4 = dinv load
+// Cache policy of the update's streams (TVFEM_NT bits, default 7): 1 = w, dx,
+// p_prev loads non-temporal, 2 = dx stores non-temporal, 4 = dinv load
 // non-temporal.  Only p (the next matvec's p_old) and z (its input) are written
 // or read with the default policy, so they are what the Infinity Cache keeps
 // between the two launches of a PCG iteration: measured inside the iteration
@@ -91,33 +91,72 @@ __device__ __forceinline__ void stc(double* p, double v) {
   else *p = v;
 }
 
-template <bool FACES, int NT>
+// DXU: odd iteration, applies the dx steps of this and the previous iteration.
+// Streams: w, dinv (+ p_prev, p, dx) read, z read and written (+ dx written):
+// 32 B per node on even iterations, 64 B on odd ones.
+template <bool FACES, int NT, bool DXU>
 __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState* __restrict__ st,
                                                        const double* __restrict__ pA,
                                                        const double* __restrict__ pB,
                                                        const double* __restrict__ w,
                                                        const double* __restrict__ dinv, double* __restrict__ dx,
-                                                       double* __restrict__ r, double* __restrict__ z,
-                                                       double* __restrict__ partials, RedTail rt, FaceAdd fa,
-                                                       int it_host) {
+                                                       double* __restrict__ z, double* __restrict__ partials,
+                                                       RedTail rt, FaceAdd fa, int it_host) {
   stamp_start(rt);
   if (st->done) return;
   const double a = st->a;
-  const double* __restrict__ p = (it_host & 1) ? pB : pA;  // == st->it while the solve runs
+  const double ap = DXU ? st->a_prev : 0.0;
+  const double* __restrict__ p = (it_host & 1) ? pB : pA;   // this iteration's p (== st->it parity)
+  const double* __restrict__ pp = (it_host & 1) ? pA : pB;  // the previous iteration's
+  constexpr bool NT1 = (NT & 1) != 0, NT2 = (NT & 2) != 0, NT4 = (NT & 4) != 0;
   double acc[2] = {0.0, 0.0};
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
-    stc<(NT & 2) != 0>(&dx[t], ldc<(NT & 1) != 0>(&dx[t]) + a * p[t]);  // x <- x + a p
-    double wt = ldc<(NT & 1) != 0>(&w[t]);
-    if (FACES) wt += face_terms(fa, t);   // w = J p incl. the Robin facet terms
-    const double rr = ldc<(NT & 1) != 0>(&r[t]) - a * wt;  // r <- r - a w
-    stc<(NT & 2) != 0>(&r[t], rr);
-    const double zz = ldc<(NT & 4) != 0>(&dinv[t]) * rr;    // z <- B r
-    z[t] = zz;
+  // one node: v = {w, dinv, z, dx, p_prev, p} as loaded
+  auto node = [&](int64_t q, const double (&v)[6]) {
+    if (DXU) stc<NT2>(&dx[q], (v[3] + ap * v[4]) + a * v[5]);  // x <- (x + a_prev p_prev) + a p
+    double wt = v[0];
+    if (FACES) wt += face_terms(fa, q);  // w = J p incl. the Robin facet terms
+    const double rr = v[2] / v[1] - a * wt;  // r <- r - a w, r = B^-1 z
+    const double zz = v[1] * rr;             // z <- B r
+    z[q] = zz;
     acc[0] += zz * zz;
     acc[1] += zz * rr;
+  };
+  auto load = [&](int64_t q, double (&v)[6]) {
+    v[0] = ldc<NT1>(&w[q]);
+    v[1] = ldc<NT4>(&dinv[q]);
+    v[2] = z[q];
+    if (DXU) {
+      v[3] = ldc<NT1>(&dx[q]);
+      v[4] = ldc<NT1>(&pp[q]);
+      v[5] = p[q];
+    }
+  };
+  // U nodes per thread and round, every load of the round issued before the
+  // first store: 3 (6) loads per node alone leave too few bytes in flight
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  for (; t + (U - 1) * stride < n; t += U * stride) {
+    double v[U][6];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load(t + u * stride, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) node(t + u * stride, v[u]);
+  }
+  for (; t < n; t += stride) {
+    double v[6];
+    load(t, v);
+    node(t, v);
   }
   block_partials<2>(acc, partials);
   fused_reduce_tail<2>(rt, gridDim.x);
+}
+
+__global__ __launch_bounds__(kBlock) void k_dx_tail(int64_t n, const PcgState* __restrict__ st,
+                                                    const double* __restrict__ p, double* __restrict__ dx) {
+  const double a = st->a;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
+    dx[t] += a * p[t];
 }
 
 __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __restrict__ T,
@@ -188,31 +227,38 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 }
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
-                       const double* dinv, double* dx, double* r, double* z, double* partials, hipStream_t s,
+                       const double* dinv, double* dx, double* z, double* partials, hipStream_t s,
                        const RedTail* tail, const FaceAdd* fa, int it_host) {
   RedTail rt{};
   if (tail) rt = *tail;
-  static int nt = -1;
+  static int nt = -1;  // TVFEM_NT: 7 (default) or 0 (every stream with the default policy)
   if (nt < 0) {
     const char* e = getenv("TVFEM_NT");
-    nt = e ? (atoi(e) & 7) : 7;
+    nt = (e && atoi(e) == 0) ? 0 : 7;
   }
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
-#define TV_UPD(F, N)                                                                                         \
-  hipLaunchKernelGGL((k_pcg_update<F, N>), dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, dx, r, \
-                     z, partials, rt, f, it_host)
-  const bool faces = fa && fa->on;
-  switch (nt) {
-    case 1: if (faces) TV_UPD(true, 1); else TV_UPD(false, 1); break;
-    case 2: if (faces) TV_UPD(true, 2); else TV_UPD(false, 2); break;
-    case 3: if (faces) TV_UPD(true, 3); else TV_UPD(false, 3); break;
-    case 4: if (faces) TV_UPD(true, 4); else TV_UPD(false, 4); break;
-    case 5: if (faces) TV_UPD(true, 5); else TV_UPD(false, 5); break;
-    case 6: if (faces) TV_UPD(true, 6); else TV_UPD(false, 6); break;
-    case 7: if (faces) TV_UPD(true, 7); else TV_UPD(false, 7); break;
-    default: if (faces) TV_UPD(true, 0); else TV_UPD(false, 0);
+  const int v = (fa && fa->on ? 4 : 0) | (nt ? 2 : 0) | (it_host & 1);
+#define TV_UPD(F, N, D)                                                                                       \
+  hipLaunchKernelGGL((k_pcg_update<F, N, D>), dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, \
+                     dx, z, partials, rt, f, it_host);                                                          \
+  break
+  switch (v) {
+    case 0: TV_UPD(false, 0, false);
+    case 1: TV_UPD(false, 0, true);
+    case 2: TV_UPD(false, 7, false);
+    case 3: TV_UPD(false, 7, true);
+    case 4: TV_UPD(true, 0, false);
+    case 5: TV_UPD(true, 0, true);
+    case 6: TV_UPD(true, 7, false);
+    default: TV_UPD(true, 7, true);
   }
 #undef TV_UPD
+}
+
+void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, int its,
+                        hipStream_t s) {
+  if (!(its & 1)) return;
+  hipLaunchKernelGGL(k_dx_tail, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, (its - 1) & 1 ? pB : pA, dx);
 }
 
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s) {
