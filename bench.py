@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--cells", type=str, default="400,400,50", help="hex cells per axis (per rank for weak)")
     ap.add_argument("--lengths", type=str, default="50,50,5")
     ap.add_argument("--thermal-only", action="store_true")
+    ap.add_argument("--family", choices=["CG", "DG"], default="CG",
+                    help="element family of T and sigma (degree 1): CG (C1-C4) or DG (C5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--kernel-reps", type=int, default=20)
@@ -78,7 +80,7 @@ def main():
         "htc": 280.1, "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0e0, "Rg": 8.314,
         "alpha_solid": 9.10e-6, "alpha_liquid": 25.10e-6, "Tf_init": 873.0,
     }  # main.py:29-55
-    cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+    cfg = {"T": {"element": a.family, "degree": 1}, "sigma": {"element": a.family, "degree": 1}}
     device = local_rank
     if a.comm == "host":  # rehearsal of several ranks on fewer GPUs (host-staged transport)
         import torch
@@ -99,7 +101,9 @@ def main():
                 init_host_comm(prob, rank, world, dist)
     prob.setup()
     n_owned, _ = prob.num_dofs(0)
-    n_global = int(np.prod([n + 1 for n in nc]))
+    n_global = int(np.prod([n + 1 for n in nc])) if a.family == "CG" else 8 * int(np.prod(nc))
+    cname = {("CG", (100, 100, 10)): "C2", ("CG", (200, 200, 25)): "C3", ("CG", (400, 400, 50)): "C4",
+             ("DG", (200, 200, 25)): "C5"}.get((a.family, tuple(nc)), "custom")
 
     def barrier_sync():
         N.check(lib.tv_sync(ctx), ctx)
@@ -173,13 +177,18 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only)
+        if a.family == "CG":
+            cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only)
+        else:
+            cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
+                   "sample": "no DG1 path in oracle/tv_cpu.c (the numpy oracle covers DG1 parity only)"}
 
     prob.close()
     if rank == 0:
         value = n_global * a.steps / elapsed
         out = {
-            "metric": "DOF-updates/sec (coupled thermo-visco time step, 3D CG1 hex)",
+            "metric": f"DOF-updates/sec ({'thermal Newton' if a.thermal_only else 'coupled thermo-visco'} "
+                      f"time step, 3D {a.family}1 hex)",
             "value": value,
             "unit": "DOF-updates/s",
             "n_gpus": world,
@@ -191,7 +200,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (uniform T_0 = 800 K initial state, main.py parameters)",
-            "config": {"workload": f"C4 3D plate CG1/CG1 {nc[0]}x{nc[1]}x{nc[2]} hex "
+            "config": {"workload": f"{cname} 3D plate {a.family}1/{a.family}1 {nc[0]}x{nc[1]}x{nc[2]} hex "
                                    f"({n_global} T-dofs), dt 0.1, "
                                    + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
                        "parallelism": f"mesh partition along y x{world} ("
