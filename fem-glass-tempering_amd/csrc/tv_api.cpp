@@ -429,7 +429,7 @@ static int setup_fields(Ctx* c) {
   if (int e = alloc_field(c, TV_F_DX, 0, 1)) return e;
   int np = std::max(kVecBlocks, 1);
   if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
-  else np = std::max<int>(np, (int)((c->nT / (1 << c->dim) + kBlock - 1) / kBlock));
+  else np = std::max(np, dg_num_blocks(c->dg));
   c->n_partials_cap = np;
   HIPC(hipMalloc(&c->partials, sizeof(double) * 2 * (size_t)np));
   HIPC(hipMalloc(&c->sums, sizeof(double) * 8));

@@ -36,27 +36,6 @@ namespace {
 
 enum { MODE_RES = 0, MODE_JAC = 1 };
 
-__device__ __forceinline__ double shr1(double v) {  // lane l <- lane l-1
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xF, 0xF, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double shl1(double v) {  // lane l <- lane l+1
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xF, 0xF, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// Blocks are dispatched round-robin over the 8 XCDs; remap so that each XCD
-// gets a contiguous range of tile ids (bijective for any grid size), keeping
-// the halo rows / columns shared by neighbouring tiles in one L2.
-__device__ __forceinline__ int xcd_remap(int b, int nb) {
-  const int q = nb >> 3, r = nb & 7, x = b & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
-}
-
 // Raw buffer access (32-bit byte offsets against an SGPR descriptor).  The
 // hardware range check returns 0 for loads and drops stores at offsets past
 // the buffer, so out-of-domain neighbours and non-owned outputs are masked by

@@ -7,6 +7,27 @@
 
 namespace tv {
 
+__device__ __forceinline__ double shr1(double v) {  // lane l <- lane l-1
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double shl1(double v) {  // lane l <- lane l+1
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xF, 0xF, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Blocks are dispatched round-robin over the 8 XCDs; remap so that each XCD
+// gets a contiguous range of tile ids (bijective for any grid size), keeping
+// the halo rows / columns shared by neighbouring tiles in one L2.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ double wave_sum64(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);

@@ -16,7 +16,10 @@
 // interior facet is the lower-index cell (the cell below along the facet
 // normal).  One thread owns one cell and produces its 2^d rows; dof layout is
 // component-major [local dof][cell] so the 2^d loads of a wave are coalesced.
-#include "tv_internal.h"
+#include <algorithm>
+#include <cstdlib>
+
+#include "tv_device.h"
 
 namespace tv {
 namespace {
@@ -226,6 +229,287 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// 3D Jacobian apply on an (x-segment x rows) tile of cells marching through a
+// chunk of planes: the SIPG J x of k_dg_cells<3, MODE_JAC>, restructured for
+// the hardware.
+//   * lane = cell along storage axis 0 (62 outputs per wave, lanes 0 / 63 are
+//     the x-halo cells); x-neighbour values come from the next / previous lane
+//     (DPP wave shifts), not from memory;
+//   * wave = row along axis `ra`; R compute waves plus one halo wave above and
+//     below exchange their 8 values per cell through LDS (one barrier);
+//   * the neighbours along the march axis `pa` are the previous / next plane,
+//     held in registers (plane L + 1 is loaded while plane L is computed);
+//   * every operator term is sum-factorised: 2x2 mass / stiffness factors per
+//     axis for the cell term; for each interior facet the 4-column normal SIPG
+//     matrix, then the two tangential 2x2 masses (~0.5 kflop per cell, not ~3).
+// FUSEP: x = p = z + beta/betaold p_old formed on the fly and stored (as
+// k_dg_cells); out = w on owned cells; one p.w partial per workgroup.
+// ---------------------------------------------------------------------------
+constexpr int kDgRows = 6;  // + 2 halo waves: 512 threads, up to 256 VGPRs (no spills)
+
+// v <- (M_e (x) I) v along storage axis e (local bit e), M_e = h [1/3 1/6; 1/6 1/3]
+__device__ __forceinline__ void mass_axis(double (&v)[8], int e, double h) {
+  const double d = h * (1.0 / 3.0), o = h * (1.0 / 6.0);
+#pragma unroll
+  for (int l = 0; l < 8; ++l)
+    if (!((l >> e) & 1)) {
+      const double a = v[l], b = v[l | (1 << e)];
+      v[l] = d * a + o * b;
+      v[l | (1 << e)] = o * a + d * b;
+    }
+}
+// out <- (K_e (x) I) v, K_e = (1/h) [1 -1; -1 1]; ih = 1/h
+__device__ __forceinline__ void stiff_axis(const double (&v)[8], double (&out)[8], int e, double ih) {
+#pragma unroll
+  for (int l = 0; l < 8; ++l)
+    if (!((l >> e) & 1)) {
+      const double dlt = (v[l] - v[l | (1 << e)]) * ih;
+      out[l] = dlt;
+      out[l | (1 << e)] = -dlt;
+    }
+}
+
+template <bool FUSEP>
+__global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, const double* __restrict__ T,
+                                                                  const double* __restrict__ in0,
+                                                                  const double* in1, double* __restrict__ out,
+                                                                  double* pout, const PcgState* __restrict__ st,
+                                                                  double* __restrict__ partials, int nseg, int ra,
+                                                                  int qchunk, int nch) {
+  constexpr int R = kDgRows;
+  __shared__ double sX[2][R + 2][8][kWave];  // double-buffered plane slab: one barrier per plane
+  __shared__ double red[R + 2];
+  if (FUSEP && st->done) return;  // uniform over the grid
+  const int pa = 3 - ra;
+  const int cn[3] = {g.c0, g.c1, g.c2};
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int64_t cst[3] = {1, g.c0, (int64_t)g.c0 * g.c1};
+  const int npl = cn[pa];
+  // chunk fastest: the chunks of one column of tiles share their boundary
+  // planes and land on one XCD (contiguous range after the remap)
+  const int b = xcd_remap((int)blockIdx.x, (int)gridDim.x);
+  const int chunk = b % nch;
+  const int t = b / nch;
+  const int seg = t % nseg;
+  const int rb = t / nseg;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, npl);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+  const int r = rb * R - 1 + wave;  // row along ra (waves 0 and R + 1: halo rows)
+  const int i = seg * kSeg - 1 + lane;
+  const bool valid = i >= 0 && i < g.c0 && r >= 0 && r < cn[ra];
+  const bool compute = wave >= 1 && wave <= R;
+  const bool writer = compute && valid && lane >= 1 && lane <= kSeg;
+  const int64_t cbase = (valid ? i : 0) + cst[ra] * (valid ? r : 0);  // cell of plane 0
+
+  double bcoef = 0.0;
+  bool first = false;
+  const double* pold = in1;
+  if (FUSEP) {
+    const int it = st->it;
+    first = (it == 0);
+    bcoef = first ? 0.0 : st->beta / st->betaold;
+    if (!(it & 1)) { pold = pout; pout = const_cast<double*>(in1); }
+  }
+  // raw loads of this lane's cell in plane L (0 outside the grid), then the
+  // input values (p = z + b p_old for FUSEP)
+  auto fetch = [&](int L, double (&rz)[8], double (&ro)[8]) {
+    const bool ok = valid && L >= 0 && L < npl;
+    const int64_t c = cbase + cst[pa] * (ok ? L : 0);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int64_t o = (int64_t)l * ncell + c;
+      rz[l] = ok ? in0[o] : 0.0;
+      ro[l] = (FUSEP && !first && ok) ? pold[o] : 0.0;
+    }
+  };
+  auto form = [&](const double (&rz)[8], const double (&ro)[8], double (&v)[8]) {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) v[l] = FUSEP ? rz[l] + bcoef * ro[l] : rz[l];
+  };
+  double xl[8], x[8], xu[8];  // planes L - 1, L, L + 1
+  double rz[8], ro[8];        // raw loads of plane L + 2, in flight during step L
+  fetch(q0 - 1, rz, ro);
+  form(rz, ro, xl);
+  fetch(q0, rz, ro);
+  form(rz, ro, x);
+  fetch(q0 + 1, rz, ro);
+  form(rz, ro, xu);
+  double dot = 0.0;
+  for (int L = q0; L < q1; ++L) {
+    fetch(L + 2, rz, ro);
+    const int sb = L & 1;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) sX[sb][wave][l][lane] = x[l];
+    const int64_t cid = cbase + cst[pa] * L;
+    if (FUSEP && writer) {
+#pragma unroll
+      for (int l = 0; l < 8; ++l) pout[(int64_t)l * ncell + cid] = x[l];
+    }
+    __syncthreads();
+    if (compute) {  // wave-uniform: every lane runs the DPP exchanges below; stores are masked
+      int ci[3];
+      ci[0] = valid ? i : 0;
+      ci[ra] = valid ? r : 0;
+      ci[pa] = L;
+      double h[3];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) h[e] = g.h[e][ci[e]];
+      const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
+      const double ih[3] = {1.0 / h[0], 1.0 / h[1], 1.0 / h[2]};
+      const double pen_up = g.penalty / sqrt(hd2);  // upper facets: this cell is '+'
+      double y[8];
+      // ---- cell term: Mz(My Mx x + da (My Kx x + Ky Mx x)) + da Kz (My Mx x) ----
+      {
+        double A[8], B[8], AK[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) A[l] = x[l];
+        stiff_axis(x, B, 0, ih[0]);  // Kx x
+        mass_axis(A, 0, h[0]);       // Mx x
+        stiff_axis(A, AK, 1, ih[1]); // Ky Mx x
+        mass_axis(A, 1, h[1]);       // My Mx x
+        mass_axis(B, 1, h[1]);       // My Kx x
+        double S[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) S[l] = A[l] + g.dt_alpha * (B[l] + AK[l]);
+        mass_axis(S, 2, h[2]);
+        double KA[8];
+        stiff_axis(A, KA, 2, ih[2]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) y[l] = S[l] + g.dt_alpha * KA[l];
+      }
+      // ---- facets ----
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int e1 = (k == 0) ? 1 : 0, e2 = (k == 2) ? 1 : 2;  // tangential axes
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          const int nbi = ci[k] + (side ? 1 : -1);
+          const bool interior = valid && nbi >= 0 && nbi < cn[k];
+          double xn[8];
+          if (k == 0) {  // lane +- 1 (all lanes)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) xn[l] = side ? shl1(x[l]) : shr1(x[l]);
+          } else if (k == ra) {
+#pragma unroll
+            for (int l = 0; l < 8; ++l) xn[l] = sX[sb][wave + (side ? 1 : -1)][l][lane];
+          } else {
+#pragma unroll
+            for (int l = 0; l < 8; ++l) xn[l] = side ? xu[l] : xl[l];
+          }
+          if (interior) {
+            // SIPG facet rows, '+' = L = lower cell: with J = (0, 1, -1, 0) and
+            // G = (-gL, gL, -gR, gR), g = 1/(2h), the 4x4 normal matrix
+            // pen J J^T - G J^T - J G^T reduces per tangential dof pair to the
+            // jump j = x_L1 - x_R0 and the normal differences d = x_1 - x_0 of
+            // both cells; then the tangential masses (they commute)
+            const double hn = g.h[k][nbi];
+            const double gO = 0.5 * ih[k], gN = 0.5 / hn;
+            double U[8];
+            if (side) {  // upper facet: this cell is L, the neighbour R
+              const double pen = pen_up;
+#pragma unroll
+              for (int tt = 0; tt < 4; ++tt) {
+                const int l0 = ((tt & 1) << e1) | ((tt >> 1) << e2), l1 = l0 | (1 << k);
+                const double j = x[l1] - xn[l0], dO = x[l1] - x[l0], dN = xn[l1] - xn[l0];
+                U[l0] = gO * j;
+                U[l1] = (pen - gO) * j - gO * dO - gN * dN;
+              }
+            } else {  // lower facet: this cell is R, the neighbour L ('+', its lengths set the penalty)
+              const double pen = g.penalty / sqrt(hd2 - h[k] * h[k] + hn * hn);
+#pragma unroll
+              for (int tt = 0; tt < 4; ++tt) {
+                const int l0 = ((tt & 1) << e1) | ((tt >> 1) << e2), l1 = l0 | (1 << k);
+                const double j = xn[l1] - x[l0], dO = x[l1] - x[l0], dN = xn[l1] - xn[l0];
+                U[l1] = -gO * j;
+                U[l0] = (gO - pen) * j + gO * dO + gN * dN;
+              }
+            }
+            mass_axis(U, e1, h[e1]);
+            mass_axis(U, e2, h[e2]);
+#pragma unroll
+            for (int l = 0; l < 8; ++l) y[l] += g.dt_alpha * U[l];
+          } else if (valid && g.bnd[k][side]) {
+            // Robin facet Jacobian on the physical boundary (3x3 Gauss, as
+            // k_dg_cells): only the 4 dofs on the facet (bit k == side) are nonzero there
+            double Tf[4], Xf[4], acc[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+              const int l = (side << k) | ((f & 1) << e1) | ((f >> 1) << e2);
+              Tf[f] = T[(int64_t)l * ncell + cid];
+              Xf[f] = x[l];
+              acc[f] = 0.0;
+            }
+#pragma unroll
+            for (int qq = 0; qq < 9; ++qq) {
+              const double s1 = kGX[qq % 3], s2 = kGX[qq / 3];
+              const double w = (kGW[qq % 3] * h[e1]) * (kGW[qq / 3] * h[e2]);
+              const double phi[4] = {(1.0 - s1) * (1.0 - s2), s1 * (1.0 - s2), (1.0 - s1) * s2, s1 * s2};
+              double Th = 0.0, Ph = 0.0;
+#pragma unroll
+              for (int f = 0; f < 4; ++f) {
+                Th += phi[f] * Tf[f];
+                Ph += phi[f] * Xf[f];
+              }
+              const double gv = dgfun(g, Th) * Ph;
+#pragma unroll
+              for (int f = 0; f < 4; ++f) acc[f] += w * gv * phi[f];
+            }
+#pragma unroll
+            for (int f = 0; f < 4; ++f) y[(side << k) | ((f & 1) << e1) | ((f >> 1) << e2)] += g.dt * acc[f];
+          }
+        }
+      }
+      if (writer && ci[2] >= g.k_begin && ci[2] < g.k_end) {
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+          out[(int64_t)l * ncell + cid] = y[l];
+          dot += x[l] * y[l];
+        }
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      xl[l] = x[l];
+      x[l] = xu[l];
+    }
+    form(rz, ro, xu);
+  }
+  if (partials != nullptr) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) dot += __shfl_xor(dot, off, 64);
+    if (lane == 0) red[wave] = dot;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sacc = 0.0;
+      for (int w = 0; w < R + 2; ++w) sacc += red[w];
+      partials[blockIdx.x] = sacc;
+    }
+  }
+}
+
+struct DgTile {
+  int nseg, ra, qchunk, nch, blocks;
+};
+DgTile dg_tile_plan(const DgGrid& g) {
+  static int qmax = -1;  // TVFEM_DG_CHUNK: planes marched per workgroup (default 5)
+  if (qmax < 0) {
+    const char* e = getenv("TVFEM_DG_CHUNK");
+    qmax = e ? std::max(1, atoi(e)) : 5;
+  }
+  DgTile p{};
+  p.nseg = (g.c0 + kSeg - 1) / kSeg;
+  p.ra = (g.c2 >= g.c1) ? 2 : 1;  // rows along the longer of axes 1 / 2, march along the other
+  const int nr = (p.ra == 2) ? g.c2 : g.c1, npl = (p.ra == 2) ? g.c1 : g.c2;
+  const int nrb = (nr + kDgRows - 1) / kDgRows;
+  p.nch = (npl + qmax - 1) / qmax;
+  p.qchunk = (npl + p.nch - 1) / p.nch;
+  p.nch = (npl + p.qchunk - 1) / p.qchunk;
+  p.blocks = p.nseg * nrb * p.nch;
+  return p;
+}
+
 // diag(J) by applying the operator to unit vectors of the cell (NL applies).
 template <int DIM>
 __global__ __launch_bounds__(kBlock) void k_dg_diag(DgGrid g, const double* __restrict__ T,
@@ -346,13 +630,40 @@ void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, doub
   launch_cells<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, s, nullptr);
 }
 
+static bool dg_tiled(const DgGrid& g) {  // 3D Jacobian: k_dg_tile (TVFEM_DG_TILE=0: k_dg_cells)
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("TVFEM_DG_TILE");
+    on = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return on && dg_dim(g) == 3;
+}
+
+template <bool FUSEP>
+static void launch_tile(const DgGrid& g, const double* T, const double* in0, const double* in1, double* out,
+                        double* pout, const PcgState* st, double* partials, int* n_partials, hipStream_t s) {
+  const DgTile p = dg_tile_plan(g);
+  if (n_partials) *n_partials = p.blocks;
+  if (p.blocks <= 0) return;
+  hipLaunchKernelGGL((k_dg_tile<FUSEP>), dim3(p.blocks), dim3((kDgRows + 2) * kWave), 0, s, g, T, in0, in1, out,
+                     pout, st, partials, p.nseg, p.ra, p.qchunk, p.nch);
+}
+
+int dg_num_blocks(const DgGrid& g) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int cells = (int)((ncell + kBlock - 1) / kBlock);
+  return std::max(cells, dg_tile_plan(g).blocks);
+}
+
 void launch_dg_japply(const DgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s) {
+  if (dg_tiled(g)) return launch_tile<false>(g, T, x, nullptr, y, nullptr, nullptr, partials, n_partials, s);
   launch_cells<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, nullptr, partials, s, n_partials);
 }
 
 void launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
                             const PcgState* st, double* partials, int* n_partials, hipStream_t s) {
+  if (dg_tiled(g)) return launch_tile<true>(g, T, z, pA, w, pB, st, partials, n_partials, s);
   launch_cells<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, s, n_partials);
 }
 

@@ -133,6 +133,7 @@ void launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, d
                             double* w, const PcgState* st, double* partials, int* n_partials,
                             hipStream_t s);
 void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
+int dg_num_blocks(const DgGrid& g);  // partial records of the largest DG launch
 
 void launch_visco(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
 void launch_visco_Tpass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
