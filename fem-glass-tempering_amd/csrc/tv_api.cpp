@@ -596,8 +596,7 @@ static void op_japply(Ctx* c, const double* T, const double* x, double* y, doubl
 static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr, int it = 0) {
   if (c->fam_T == TV_CG)
     return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail, it);
-  launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream);
-  return false;
+  return launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail);
 }
 
 // --------------------------------------------------------------------------------------

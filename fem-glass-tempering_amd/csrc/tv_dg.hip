@@ -277,7 +277,8 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
                                                                   const double* in1, double* __restrict__ out,
                                                                   double* pout, const PcgState* __restrict__ st,
                                                                   double* __restrict__ partials, int nseg, int ra,
-                                                                  int qchunk, int nch) {
+                                                                  int qchunk, int nch, RedTail rt) {
+  stamp_start(rt);
   constexpr int R = kDgRows;
   __shared__ double sX[2][R + 2][8][kWave];  // double-buffered plane slab: one barrier per plane
   __shared__ double red[R + 2];
@@ -484,8 +485,9 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
     if (threadIdx.x == 0) {
       double sacc = 0.0;
       for (int w = 0; w < R + 2; ++w) sacc += red[w];
-      partials[blockIdx.x] = sacc;
+      store_partial(&partials[blockIdx.x], sacc);
     }
+    fused_reduce_tail<1>(rt, (int)gridDim.x);  // p.w over all tiles (+ KSPCG logic)
   }
 }
 
@@ -640,13 +642,17 @@ static bool dg_tiled(const DgGrid& g) {  // 3D Jacobian: k_dg_tile (TVFEM_DG_TIL
 }
 
 template <bool FUSEP>
-static void launch_tile(const DgGrid& g, const double* T, const double* in0, const double* in1, double* out,
-                        double* pout, const PcgState* st, double* partials, int* n_partials, hipStream_t s) {
+static bool launch_tile(const DgGrid& g, const double* T, const double* in0, const double* in1, double* out,
+                        double* pout, const PcgState* st, double* partials, int* n_partials, hipStream_t s,
+                        const RedTail* tail = nullptr) {
   const DgTile p = dg_tile_plan(g);
   if (n_partials) *n_partials = p.blocks;
-  if (p.blocks <= 0) return;
+  if (p.blocks <= 0) return false;
+  RedTail rt{};
+  if (tail && partials) rt = *tail;
   hipLaunchKernelGGL((k_dg_tile<FUSEP>), dim3(p.blocks), dim3((kDgRows + 2) * kWave), 0, s, g, T, in0, in1, out,
-                     pout, st, partials, p.nseg, p.ra, p.qchunk, p.nch);
+                     pout, st, partials, p.nseg, p.ra, p.qchunk, p.nch, rt);
+  return rt.counter != nullptr;
 }
 
 int dg_num_blocks(const DgGrid& g) {
@@ -657,14 +663,19 @@ int dg_num_blocks(const DgGrid& g) {
 
 void launch_dg_japply(const DgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s) {
-  if (dg_tiled(g)) return launch_tile<false>(g, T, x, nullptr, y, nullptr, nullptr, partials, n_partials, s);
+  if (dg_tiled(g)) {
+    launch_tile<false>(g, T, x, nullptr, y, nullptr, nullptr, partials, n_partials, s);
+    return;
+  }
   launch_cells<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, nullptr, partials, s, n_partials);
 }
 
-void launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
-                            const PcgState* st, double* partials, int* n_partials, hipStream_t s) {
-  if (dg_tiled(g)) return launch_tile<true>(g, T, z, pA, w, pB, st, partials, n_partials, s);
+bool launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
+                            const PcgState* st, double* partials, int* n_partials, hipStream_t s,
+                            const RedTail* tail) {
+  if (dg_tiled(g)) return launch_tile<true>(g, T, z, pA, w, pB, st, partials, n_partials, s, tail);
   launch_cells<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, s, n_partials);
+  return false;
 }
 
 void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {

@@ -129,9 +129,10 @@ int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_dg_japply(const DgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s);
-void launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB,
+// 3D: k_dg_tile, with the reduction tail when `tail` is given (returns true)
+bool launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
-                            hipStream_t s);
+                            hipStream_t s, const RedTail* tail = nullptr);
 void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
 int dg_num_blocks(const DgGrid& g);  // partial records of the largest DG launch
 
