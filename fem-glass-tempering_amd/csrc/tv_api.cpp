@@ -310,6 +310,10 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     g.bnd[0][0] = g.bnd[0][1] = 1;
     g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
     g.bnd[2][0] = g.bnd[2][1] = g.deg2 ? 0 : 1;
+    const char* et = getenv("TVFEM_DG_TILE");
+    const char* ec = getenv("TVFEM_DG_CHUNK");
+    g.tile = (et && atoi(et) == 0) ? 0 : 1;
+    g.tile_chunk = ec ? std::max(1, atoi(ec)) : 5;
     for (int s = 0; s < 3; ++s) {
       const std::vector<double>& X = storage_coords(c, s, tmp);
       std::vector<double> h;

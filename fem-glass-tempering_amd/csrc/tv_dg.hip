@@ -495,11 +495,7 @@ struct DgTile {
   int nseg, ra, qchunk, nch, blocks;
 };
 DgTile dg_tile_plan(const DgGrid& g) {
-  static int qmax = -1;  // TVFEM_DG_CHUNK: planes marched per workgroup (default 5)
-  if (qmax < 0) {
-    const char* e = getenv("TVFEM_DG_CHUNK");
-    qmax = e ? std::max(1, atoi(e)) : 5;
-  }
+  const int qmax = std::max(1, g.tile_chunk);  // planes marched per workgroup (default 5)
   DgTile p{};
   p.nseg = (g.c0 + kSeg - 1) / kSeg;
   p.ra = (g.c2 >= g.c1) ? 2 : 1;  // rows along the longer of axes 1 / 2, march along the other
@@ -632,14 +628,7 @@ void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, doub
   launch_cells<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, s, nullptr);
 }
 
-static bool dg_tiled(const DgGrid& g) {  // 3D Jacobian: k_dg_tile (TVFEM_DG_TILE=0: k_dg_cells)
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("TVFEM_DG_TILE");
-    on = (e && atoi(e) == 0) ? 0 : 1;
-  }
-  return on && dg_dim(g) == 3;
-}
+static bool dg_tiled(const DgGrid& g) { return g.tile && dg_dim(g) == 3; }  // 3D Jacobian: k_dg_tile
 
 template <bool FUSEP>
 static bool launch_tile(const DgGrid& g, const double* T, const double* in0, const double* in1, double* out,

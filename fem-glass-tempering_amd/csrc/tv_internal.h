@@ -56,6 +56,10 @@ struct DgGrid {
   double a_rad, a_conv;
   double T_amb, T_amb4;
   double penalty;             // SIPG penalty (ThermoViscoProblem.py:313)
+  // 3D Jacobian kernel: 1 = marching tiles (k_dg_tile) of `tile_chunk` planes,
+  // 0 = one thread per cell (k_dg_cells); from TVFEM_DG_TILE / TVFEM_DG_CHUNK
+  // when the context is created
+  int tile, tile_chunk;
 };
 
 // Device-resident scalars of one PCG solve (PETSc KSPCG restated, preconditioned norm).

@@ -320,3 +320,44 @@ def test_in_solve_kernel_timing():
     assert st[1][1] == 2
     for kid in (3, 4, 1):
         assert 0.0 < st[kid][0] < 50.0, st
+
+
+def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
+    """The marching DG1 Jacobian (k_dg_tile) against the one-thread-per-cell
+    kernel (k_dg_cells, itself pinned to the oracle above) on a grid large
+    enough for two x segments, several row tiles (13 rows, 6 per tile) and
+    several march chunks (7 planes in chunks of 2 and 5): J x at a random T
+    (1e-12) and one coupled time step through the fused PCG matvec (T 1e-10).
+    The oracle itself is too slow to assemble DG1 at this size."""
+    torch = _torch()
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    axes = [np.linspace(0.0, 6.4, 65), np.concatenate([np.linspace(0.0, 0.4, 5), np.linspace(0.4, 1.3, 10)[1:]]),
+            np.linspace(0.0, 0.7, 8)]
+    cfg = {"T": DG, "sigma": DG}
+    rng = np.random.default_rng(3)
+    out = {}
+    for tile, chunk in ((0, 5), (1, 2), (1, 5)):
+        monkeypatch.setenv("TVFEM_DG_TILE", str(tile))
+        monkeypatch.setenv("TVFEM_DG_CHUNK", str(chunk))
+        p = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                               part_axis=2, materialize=False, verbose=False)
+        p.setup()
+        p.solve_timestep()
+        T1 = p.get_field("T")
+        n = T1.size
+        r = np.random.default_rng(3)
+        T = 700.0 + r.uniform(0.0, 150.0, n)
+        x = r.standard_normal(n)
+        p.set_field("T", T)
+        p._flush()
+        xd = torch.tensor(device_layout(p, x, "DG"), dtype=torch.float64, device="cuda")
+        yd = torch.zeros_like(xd)
+        assert p._lib.tv_jacobian_apply(p._ctx, xd.data_ptr(), yd.data_ptr()) == 0
+        out[(tile, chunk)] = (T1, host_layout(p, yd.cpu().numpy(), "DG"))
+        p.close()
+    T_ref, y_ref = out[(0, 5)]
+    for key in ((1, 2), (1, 5)):
+        T1, y = out[key]
+        assert relerr(y, y_ref) < 1e-12, key
+        assert relerr(T1, T_ref) < 1e-10, key
