@@ -331,12 +331,15 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
   };
   double xl[8], x[8], xu[8];  // planes L - 1, L, L + 1
   double rz[8], ro[8];        // raw loads of plane L + 2, in flight during step L
-  fetch(q0 - 1, rz, ro);
-  form(rz, ro, xl);
-  fetch(q0, rz, ro);
-  form(rz, ro, x);
-  fetch(q0 + 1, rz, ro);
-  form(rz, ro, xu);
+  {  // prologue: the loads of the first three planes in flight together
+    double az[8], ao[8], bz[8], bo[8];
+    fetch(q0 - 1, az, ao);
+    fetch(q0, bz, bo);
+    fetch(q0 + 1, rz, ro);
+    form(az, ao, xl);
+    form(bz, bo, x);
+    form(rz, ro, xu);
+  }
   double dot = 0.0;
   for (int L = q0; L < q1; ++L) {
     fetch(L + 2, rz, ro);
