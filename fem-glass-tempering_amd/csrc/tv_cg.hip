@@ -755,11 +755,12 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const uint32_t vo_own = lane_off(r), vo_halo = (halo && !(exp & 2)) ? lane_off(hrow) : kBadOff;
   const uint32_t vo_wr = writer ? vo_own : kBadOff;  // stores of the own row
   auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? (uint32_t)(sQ * L) * 8u : kBadOff; };
-  const bool ntl = (exp & 64) != 0;  // experiment: streaming policy for the plane loads
+  // (a streaming policy for these loads, bload_nt, measured no gain; a runtime
+  // switch between the two costs a scalar branch per load in the march)
   auto fetch = [&](uint32_t vo, int L, double& a0, double& a1) {
     const uint32_t o = vo + plane_off(L);
-    a0 = ntl ? bload_nt(rs0, o) : bload(rs0, o);
-    a1 = TWO ? (ntl ? bload_nt(rs1, o) : bload(rs1, o)) : 0.0;
+    a0 = bload(rs0, o);
+    a1 = TWO ? bload(rs1, o) : 0.0;
   };
 
   auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
