@@ -691,7 +691,15 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipEventRecord(c->evp[k], c->stream));
     return TV_OK;
   };
-  const int small = std::max(1, c->O.pcg_batch / 4);  // batches queued behind the first: 2 iterations
+  // batches queued behind the first: pcg_batch / 8 iterations (1 by default);
+  // the host's turnaround (~30 us) is well inside one iteration (~130 us at C4),
+  // and every iteration queued past convergence costs two early-exit launches
+  static int div = -1;
+  if (div < 0) {
+    const char* e = getenv("TVFEM_PCG_SMALL_DIV");
+    div = e ? std::max(1, atoi(e)) : 8;
+  }
+  const int small = std::max(1, c->O.pcg_batch / div);
   if (int e = enqueue(std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
   for (;;) {
     if (int e = enqueue(small, slot ^ 1)) return e;
