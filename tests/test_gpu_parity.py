@@ -361,3 +361,53 @@ def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
         T1, y = out[key]
         assert relerr(y, y_ref) < 1e-12, key
         assert relerr(T1, T_ref) < 1e-10, key
+
+
+EDGE_GRIDS = {
+    # two x segments (62 outputs per wave), a single cell across y
+    "x71_y1cell": [np.linspace(0.0, 7.0, 71), np.linspace(0.0, 0.1, 2), np.linspace(0.0, 0.3, 4)],
+    # one cell thick (two node planes along the partition axis), long rows
+    "z1cell": [np.linspace(0.0, 1.3, 14), np.linspace(0.0, 7.0, 71), np.linspace(0.0, 0.1, 2)],
+    # partial row tile (14 rows = 8 + 6), march split into two chunks (13 planes), graded x
+    "chunks": [np.concatenate([np.linspace(0.0, 1.0, 30), np.linspace(1.0, 6.6, 38)[1:]]),
+               np.linspace(0.0, 1.2, 13), np.linspace(0.0, 1.3, 14)],
+}
+
+
+@pytest.mark.parametrize("case", list(EDGE_GRIDS))
+def test_march_edge_grids(case):
+    """CG1 marching kernels on grids that exercise segment / row-tile / chunk
+    edges and one-cell-thick directions: F, J x, diag J (1e-12) and two coupled
+    time steps (T 1e-10) against the oracle."""
+    torch = _torch()
+    axes = EDGE_GRIDS[case]
+    dev, ref = make_pair(axes, {"T": CG, "sigma": CG})
+    rng = np.random.default_rng(11)
+    n = ref.VT.n
+    X = ref.VT.dof_coordinates()
+    T = 700.0 + 100.0 * np.cos(X[:, 0] / 3.0) + rng.uniform(-5, 5, n)
+    Tp = T + rng.uniform(-3, 3, n)
+    for fld, v in (("T", T), ("T_prev", Tp)):
+        dev.set_field(fld, v)
+    lib, ctx = dev._lib, dev._ctx
+    Td = torch.tensor(T, dtype=torch.float64, device="cuda")
+    Fd = torch.zeros_like(Td)
+    assert lib.tv_residual(ctx, Td.data_ptr(), Fd.data_ptr()) == 0
+    assert relerr(Fd.cpu().numpy(), ref.form.residual(T, Tp)) < 1e-12
+    x = rng.standard_normal(n)
+    xd = torch.tensor(x, dtype=torch.float64, device="cuda")
+    yd = torch.zeros_like(xd)
+    assert lib.tv_jacobian_apply(ctx, xd.data_ptr(), yd.data_ptr()) == 0
+    J = ref.form.jacobian(T)
+    assert relerr(yd.cpu().numpy(), J @ x) < 1e-12
+    dd = torch.zeros_like(xd)
+    assert lib.tv_jacobian_diag(ctx, dd.data_ptr()) == 0
+    assert relerr(dd.cpu().numpy(), J.diagonal()) < 1e-12
+    dev.close()
+    dev, ref = make_pair(axes, {"T": CG, "sigma": CG})
+    for s in range(2):
+        dev.solve_timestep()
+        ref.solve_timestep()
+        eT = relerr(dev.functions_current["T"].x.array, ref.functions_current["T"])
+        assert eT < 1e-10, (s, eT)
+    dev.close()
