@@ -431,7 +431,7 @@ static int setup_fields(Ctx* c) {
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv}) HIPC(hipMemsetAsync(p, 0, nb, c->stream));
   c->f[TV_F_RESIDUAL].ptr = c->r; c->f[TV_F_RESIDUAL].bs = 1; c->f[TV_F_RESIDUAL].space = 0;
   if (int e = alloc_field(c, TV_F_DX, 0, 1)) return e;
-  int np = std::max(kVecBlocks, 1);
+  int np = kVecBlocksMax;
   if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
   else np = std::max(np, dg_num_blocks(c->dg));
   c->n_partials_cap = np;

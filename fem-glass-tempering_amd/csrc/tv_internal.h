@@ -146,6 +146,7 @@ void launch_visco_Spass(int dim, int all, const ViscoConst& c, const ViscoFields
 
 // PCG vector kernels over the owned range [0, n) of already-offset pointers
 constexpr int kVecBlocks = 1024;
+constexpr int kVecBlocksMax = 8192;  // partial-record capacity of the vector kernels
 void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx,
                      double* partials, hipStream_t s);
 // PCG update of iteration it_host: w += facet terms, r <- r - a w, z <- B r

@@ -9,6 +9,7 @@
 // once converged every kernel of the batch exits at its first instruction.
 // Reductions: per-block partial sums (fixed order) -> one-block reduce, so the
 // result is bitwise reproducible run to run.
+#include <algorithm>
 #include <cstdlib>
 
 #include "tv_device.h"
@@ -212,8 +213,13 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ d, const d
 }
 
 int vec_blocks(int64_t n) {
+  static int cap = 0;  // TVFEM_VEC_BLOCKS (experiment): grid cap of the vector kernels
+  if (!cap) {
+    const char* e = getenv("TVFEM_VEC_BLOCKS");
+    cap = e ? std::min(kVecBlocksMax, std::max(64, atoi(e))) : kVecBlocks;
+  }
   int64_t b = (n + kBlock - 1) / kBlock;
-  if (b > kVecBlocks) b = kVecBlocks;
+  if (b > cap) b = cap;
   return b < 1 ? 1 : (int)b;
 }
 
