@@ -1298,6 +1298,15 @@ static int march_minblk() {  // workgroups the march grid is chunked up to (TVFE
   return v;
 }
 
+static int march_minq() {  // fewest planes per marching chunk when splitting for occupancy (TVFEM_MARCH_MINQ)
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("TVFEM_MARCH_MINQ");
+    v = (e && atoi(e) >= 2) ? atoi(e) : 6;
+  }
+  return v;
+}
+
 static int march_wpe() {  // TVFEM_MARCH_WPE=8: register budget for 8 waves / SIMD
   static int v = -1;
   if (v < 0) {
@@ -1385,7 +1394,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
     // enough workgroups to fill 256 CUs x ~4: split the march into chunks
     int nchunks = 1;
     const int minblk = march_minblk();
-    while ((int64_t)L.nseg * nrb * nchunks < minblk && nQ / (nchunks * 2) >= 6) nchunks *= 2;
+    while ((int64_t)L.nseg * nrb * nchunks < minblk && nQ / (nchunks * 2) >= march_minq()) nchunks *= 2;
     while ((nQ + nchunks - 1) / nchunks > kFaceChunk) ++nchunks;  // LDS coefficient stage bound
     L.qchunk = (nQ + nchunks - 1) / nchunks;
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;

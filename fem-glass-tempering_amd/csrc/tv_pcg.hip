@@ -213,13 +213,21 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ d, const d
 }
 
 int vec_blocks(int64_t n) {
-  static int cap = 0;  // TVFEM_VEC_BLOCKS (experiment): grid cap of the vector kernels
-  if (!cap) {
+  static int cap = -1;  // TVFEM_VEC_BLOCKS (experiment): fixed grid cap of the vector kernels
+  if (cap < 0) {
     const char* e = getenv("TVFEM_VEC_BLOCKS");
-    cap = e ? std::min(kVecBlocksMax, std::max(64, atoi(e))) : kVecBlocks;
+    cap = e ? std::min(kVecBlocksMax, std::max(64, atoi(e))) : 0;
   }
   int64_t b = (n + kBlock - 1) / kBlock;
-  if (b > cap) b = cap;
+  // default: at least kVecNodesPerThread nodes per thread (two 4-node rounds of
+  // the PCG update), between kVecBlocksMin and kVecBlocks workgroups.  Fewer
+  // workgroups than one node per thread halve the partial records the reduction
+  // tail walks: 20.5 -> 15.4 us per update at 1M nodes (the per-GPU share of C4
+  // on 8 GPUs); at C4 on one GPU the cap of 1024 still holds.
+  const int64_t lim = cap ? cap
+                          : std::min<int64_t>(kVecBlocks, std::max<int64_t>(kVecBlocksMin,
+                                (n + (int64_t)kBlock * kVecNodesPerThread - 1) / ((int64_t)kBlock * kVecNodesPerThread)));
+  if (b > lim) b = lim;
   return b < 1 ? 1 : (int)b;
 }
 
