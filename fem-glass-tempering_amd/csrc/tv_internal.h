@@ -147,7 +147,7 @@ void launch_visco_Spass(int dim, int all, const ViscoConst& c, const ViscoFields
 // PCG vector kernels over the owned range [0, n) of already-offset pointers
 constexpr int kVecBlocks = 1024;        // grid cap of the vector kernels
 constexpr int kVecBlocksMin = 256;      // below this the grid no longer shrinks with n
-constexpr int kVecNodesPerThread = 8;
+constexpr int kVecNodesPerThread = 16;
 constexpr int kVecBlocksMax = 8192;  // partial-record capacity of the vector kernels
 void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx,
                      double* partials, hipStream_t s);

@@ -219,11 +219,13 @@ int vec_blocks(int64_t n) {
     cap = e ? std::min(kVecBlocksMax, std::max(64, atoi(e))) : 0;
   }
   int64_t b = (n + kBlock - 1) / kBlock;
-  // default: at least kVecNodesPerThread nodes per thread (two 4-node rounds of
+  // default: at least kVecNodesPerThread nodes per thread (four 4-node rounds of
   // the PCG update), between kVecBlocksMin and kVecBlocks workgroups.  Fewer
-  // workgroups than one node per thread halve the partial records the reduction
-  // tail walks: 20.5 -> 15.4 us per update at 1M nodes (the per-GPU share of C4
-  // on 8 GPUs); at C4 on one GPU the cap of 1024 still holds.
+  // workgroups than one node per thread cut the partial records the reduction
+  // tail walks: 19-20 -> 15.5 us per update at 1M nodes (the per-GPU share of C4
+  // on 8 GPUs; 256 workgroups measured at or below 512 on every box, 128 worse);
+  // at C4 on one GPU the cap of 1024 still holds.  (8 nodes per thread and load
+  // round instead of 4: no gain at 1M nodes or at C4.)
   const int64_t lim = cap ? cap
                           : std::min<int64_t>(kVecBlocks, std::max<int64_t>(kVecBlocksMin,
                                 (n + (int64_t)kBlock * kVecNodesPerThread - 1) / ((int64_t)kBlock * kVecNodesPerThread)));
