@@ -332,6 +332,24 @@ __global__ __launch_bounds__(kBlock) void k_cg_rows(CgGrid g, const double* __re
   }
 }
 
+// local node index -> (i, j, k); 32-bit unsigned division whenever the local
+// grid fits (64-bit division is a long software sequence: k_cg_diag spent most
+// of its 63 us at C4 in it)
+__device__ __forceinline__ void decode_node(int64_t n, const CgGrid& g, int& i, int& j, int& k) {
+  if ((int64_t)g.n0 * g.n1 * g.n2 < (int64_t)0x7fffffff) {
+    const uint32_t u = (uint32_t)n, n0 = (uint32_t)g.n0, n1 = (uint32_t)g.n1;
+    const uint32_t q = u / n0;
+    const uint32_t kk = q / n1;
+    i = (int)(u - q * n0);
+    j = (int)(q - kk * n1);
+    k = (int)kk;
+  } else {
+    i = (int)(n % g.n0);
+    j = (int)((n / g.n0) % g.n1);
+    k = (int)(n / ((int64_t)g.n0 * g.n1));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // diag(J): pointwise, facet terms with directly loaded patches.
 // ---------------------------------------------------------------------------
@@ -346,9 +364,8 @@ __global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __re
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nown;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t n = base + t;
-    const int i = (int)(n % g.n0);
-    const int j = (int)((n / g.n0) % g.n1);
-    const int k = (int)(n / plane);
+    int i, j, k;
+    decode_node(n, g, i, j, k);
     const double* cx = g.coef[0] + (int64_t)i * C_NCOEF;
     const double* cy = g.coef[1] + (int64_t)j * C_NCOEF;
     const double* cz = g.coef[2] + (int64_t)k * C_NCOEF;
@@ -1252,11 +1269,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t*
   if (FUSEP && st->done) return;
   const double* x = in0;
   if (FUSEP) x = (st->it & 1) ? pB : in0;
-  const int64_t plane = (int64_t)g.n0 * g.n1;
   double dot = 0.0;
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nb; t += (int64_t)gridDim.x * kBlock) {
     const int64_t n = bnodes[t];
-    const int i = (int)(n % g.n0), j = (int)((n / g.n0) % g.n1), k = (int)(n / plane);
+    int i, j, k;
+    decode_node(n, g, i, j, k);
     const int c[3] = {i, j, k};
     const int nn[3] = {g.n0, g.n1, g.n2};
     double acc = 0.0;
