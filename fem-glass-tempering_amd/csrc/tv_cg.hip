@@ -353,50 +353,72 @@ __device__ __forceinline__ void decode_node(int64_t n, const CgGrid& g, int& i, 
 // ---------------------------------------------------------------------------
 // diag(J): pointwise, facet terms with directly loaded patches.
 // ---------------------------------------------------------------------------
-template <int DIM>
-__global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __restrict__ T,
-                                                    double* __restrict__ out, int invert) {
+// diag(J) at local node n; FACETS = false leaves out the Robin facet terms
+template <int DIM, bool FACETS>
+__device__ __forceinline__ double diag_value(const CgGrid& g, const double* __restrict__ T, int64_t n) {
   constexpr bool D1 = (DIM <= 2);
   constexpr bool D2 = (DIM == 1);
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  int i, j, k;
+  decode_node(n, g, i, j, k);
+  const double* cx = g.coef[0] + (int64_t)i * C_NCOEF;
+  const double* cy = g.coef[1] + (int64_t)j * C_NCOEF;
+  const double* cz = g.coef[2] + (int64_t)k * C_NCOEF;
+  double d = cx[C_MDI] * cy[C_MDI] * cz[C_MDI] +
+             g.dt_alpha * (cx[C_KDI] * cy[C_MDI] * cz[C_MDI] + cx[C_MDI] * cy[C_KDI] * cz[C_MDI] +
+                           cx[C_MDI] * cy[C_MDI] * cz[C_KDI]);
+  if (!FACETS) return d;
+  auto load_patch = [&](int64_t stride_a, int64_t stride_b, bool dega, bool degb, int ia, int na, int ib, int nb,
+                        double (&P)[3][3]) {
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const int aa = ia + u - 1, bb = ib + v - 1;
+        const bool ok = (dega ? u == 1 : (aa >= 0 && aa < na)) && (degb ? v == 1 : (bb >= 0 && bb < nb));
+        P[u][v] = ok ? T[n + (int64_t)(u - 1) * stride_a + (int64_t)(v - 1) * stride_b] : 0.0;
+      }
+  };
+  double P[3][3];
+  if ((i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1])) {
+    load_patch(g.n0, plane, D1, D2, j, g.n1, k, g.n2, P);
+    d += facet_sum<MODE_JAC, true, D1, D2>(g, cy[C_HLO], cy[C_HHI], cz[C_HLO], cz[C_HHI], P, P);
+  }
+  if (!D1 && ((j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]))) {
+    load_patch(1, plane, false, D2, i, g.n0, k, g.n2, P);
+    d += facet_sum<MODE_JAC, true, false, D2>(g, cx[C_HLO], cx[C_HHI], cz[C_HLO], cz[C_HHI], P, P);
+  }
+  if (!D2 && ((k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]))) {
+    load_patch(1, g.n0, false, D1, i, g.n0, j, g.n1, P);
+    d += facet_sum<MODE_JAC, true, false, D1>(g, cx[C_HLO], cx[C_HHI], cy[C_HLO], cy[C_HHI], P, P);
+  }
+  return d;
+}
+
+// all owned nodes; FACETS = false (3D marching path): the boundary nodes are
+// rewritten by k_cg_diag_bnd, so no wave runs the facet sum for its one or two
+// boundary lanes (every x-row has two)
+template <int DIM, bool FACETS>
+__global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __restrict__ T,
+                                                    double* __restrict__ out, int invert) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
   const int64_t nown = plane * (g.k_end - g.k_begin);
   const int64_t base = plane * g.k_begin;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nown;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t n = base + t;
-    int i, j, k;
-    decode_node(n, g, i, j, k);
-    const double* cx = g.coef[0] + (int64_t)i * C_NCOEF;
-    const double* cy = g.coef[1] + (int64_t)j * C_NCOEF;
-    const double* cz = g.coef[2] + (int64_t)k * C_NCOEF;
-    double d = cx[C_MDI] * cy[C_MDI] * cz[C_MDI] +
-               g.dt_alpha * (cx[C_KDI] * cy[C_MDI] * cz[C_MDI] + cx[C_MDI] * cy[C_KDI] * cz[C_MDI] +
-                             cx[C_MDI] * cy[C_MDI] * cz[C_KDI]);
-    auto load_patch = [&](int sa, int sb, int64_t stride_a, int64_t stride_b, bool dega, bool degb,
-                          int ia, int na, int ib, int nb, double (&P)[3][3]) {
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-#pragma unroll
-        for (int v = 0; v < 3; ++v) {
-          const int aa = ia + u - 1, bb = ib + v - 1;
-          const bool ok = (dega ? u == 1 : (aa >= 0 && aa < na)) && (degb ? v == 1 : (bb >= 0 && bb < nb));
-          P[u][v] = ok ? T[n + (int64_t)(u - 1) * stride_a + (int64_t)(v - 1) * stride_b] : 0.0;
-        }
-      (void)sa; (void)sb;
-    };
-    double P[3][3];
-    if ((i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1])) {
-      load_patch(1, 2, g.n0, plane, D1, D2, j, g.n1, k, g.n2, P);
-      d += facet_sum<MODE_JAC, true, D1, D2>(g, cy[C_HLO], cy[C_HHI], cz[C_HLO], cz[C_HHI], P, P);
-    }
-    if (!D1 && ((j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]))) {
-      load_patch(0, 2, 1, plane, false, D2, i, g.n0, k, g.n2, P);
-      d += facet_sum<MODE_JAC, true, false, D2>(g, cx[C_HLO], cx[C_HHI], cz[C_HLO], cz[C_HHI], P, P);
-    }
-    if (!D2 && ((k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]))) {
-      load_patch(0, 1, 1, g.n0, false, D1, i, g.n0, j, g.n1, P);
-      d += facet_sum<MODE_JAC, true, false, D1>(g, cx[C_HLO], cx[C_HHI], cy[C_HLO], cy[C_HHI], P, P);
-    }
+    const double d = diag_value<DIM, FACETS>(g, T, n);
+    out[n] = invert ? 1.0 / d : d;
+  }
+}
+
+// the owned physical-boundary nodes (g.bnodes), facet terms included
+__global__ __launch_bounds__(kBlock) void k_cg_diag_bnd(CgGrid g, const double* __restrict__ T,
+                                                        double* __restrict__ out, int invert) {
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < g.n_bnodes;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = g.bnodes[t];
+    const double d = diag_value<3, true>(g, T, n);
     out[n] = invert ? 1.0 / d : d;
   }
 }
@@ -1534,9 +1556,15 @@ void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, 
   int blocks = (int)std::min<int64_t>((nown + kBlock - 1) / kBlock, 4096);
   if (blocks <= 0) return;
   switch (dim_of(g)) {
-    case 1: hipLaunchKernelGGL(k_cg_diag<1>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
-    case 2: hipLaunchKernelGGL(k_cg_diag<2>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
-    default: hipLaunchKernelGGL(k_cg_diag<3>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
+    case 1: hipLaunchKernelGGL((k_cg_diag<1, true>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
+    case 2: hipLaunchKernelGGL((k_cg_diag<2, true>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
+    default:
+      if (use_march(g) && g.bnodes && g.n_bnodes > 0) {  // the boundary-node list of the marching path
+        hipLaunchKernelGGL((k_cg_diag<3, false>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
+        hipLaunchKernelGGL(k_cg_diag_bnd, dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, T, dinv, invert);
+      } else {
+        hipLaunchKernelGGL((k_cg_diag<3, true>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
+      }
   }
 }
 
