@@ -124,3 +124,24 @@ def test_partitioned_run_matches_single_partition(world):
     assert res["phi"] < 1e-11, res
     assert res["xi"] < 1e-6, res
     assert res["sigma"] < 1e-6, res
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal():
+    """bench.py's distributed flow (barriers, max-over-ranks timing, rank-0 JSON
+    line) at world size 2 with the host-staged transport, both ranks on GPU 0."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29711", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--comm", "host", "--cells", "40,40,10", "--steps", "2", "--warmup", "1",
+           "--kernel-reps", "2", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]  # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["steps"] == 2 and rec["value"] > 0
+    assert "host-staged" in rec["config"]["parallelism"]
+    assert rec["config"]["newton_its_per_step"] >= 2
