@@ -90,15 +90,15 @@ def main():
     lib, ctx = prob._lib, prob._ctx
     if world > 1:
         from tvfem.parallel import init_host_comm, init_rccl
-        if a.comm == "host":
+        if a.comm == "host":  # explicit opt-in only (rehearsal of several ranks on one GPU)
             init_host_comm(prob, rank, world, dist)
         else:
+            # production transport; no silent fallback: a failed RCCL init ends the run
             try:
                 init_rccl(prob, rank, world, dist)
-            except Exception as e:  # keep the scaling run alive: host-staged transport, reported in config
-                print(f"[bench rank {rank}] RCCL init failed ({e}); host-staged gloo transport", file=sys.stderr)
-                a.comm = "host"
-                init_host_comm(prob, rank, world, dist)
+            except Exception as e:
+                print(f"[bench rank {rank}] RCCL init failed: {e}", file=sys.stderr, flush=True)
+                raise SystemExit(3)
     prob.setup()
     n_owned, _ = prob.num_dofs(0)
     n_global = int(np.prod([n + 1 for n in nc])) if a.family == "CG" else 8 * int(np.prod(nc))
@@ -164,13 +164,18 @@ def main():
         kern[name] = rec
 
     dom = kern["pcg_matvec_fused"]
-    traffic = None
+    # traffic: HBM bytes per launch of this kernel from the rocprofv3 --pmc passes
+    # (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section) of this same
+    # bench command, committed under profiles/ (counters cannot be read inside
+    # the timed run); traffic_source names the file
+    traffic, traffic_src = None, None
     pmc_file = os.path.join(ROOT, "profiles", f"pmc_matvec_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
     if os.path.exists(pmc_file):
         with open(pmc_file) as fh:
             traffic = json.load(fh).get("hbm_bytes_per_launch")
+        traffic_src = "committed rocprofv3 --pmc record " + os.path.relpath(pmc_file, ROOT)
     roofline = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
+                "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)",
                 "bytes_per_launch": dom["bytes"], "ms_per_launch": dom["ms"],
                 "timing": "in-solve" if dom["launches_timed"] else "isolated"}
@@ -203,8 +208,9 @@ def main():
             "config": {"workload": f"{cname} 3D plate {a.family}1/{a.family}1 {nc[0]}x{nc[1]}x{nc[2]} hex "
                                    f"({n_global} T-dofs), dt 0.1, "
                                    + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
-                       "parallelism": f"mesh partition along y x{world} ("
-                                      + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")",
+                       "parallelism": ("single GPU, one partition (no communication)" if world == 1 else
+                                       f"mesh partition along y x{world} ("
+                                       + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")"),
                        "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},
             "roofline": roofline,

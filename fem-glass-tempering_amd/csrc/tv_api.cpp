@@ -32,6 +32,21 @@ static void set_global_error(const std::string& m) {
   g_err = m;
 }
 
+const char* experiment_env(const char* name) {
+  static std::mutex mu;
+  static std::vector<std::string> reported;
+  const char* gate = getenv("TVFEM_EXPERIMENTS");
+  if (!gate || std::strcmp(gate, "1") != 0) return nullptr;
+  const char* v = getenv(name);
+  if (!v) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (std::find(reported.begin(), reported.end(), name) == reported.end()) {
+    reported.emplace_back(name);
+    std::fprintf(stderr, "[tvfem] experiment switch %s=%s active (TVFEM_EXPERIMENTS=1)\n", name, v);
+  }
+  return v;
+}
+
 struct FieldInfo {
   double* ptr = nullptr;
   int bs = 1;       // components
@@ -310,8 +325,8 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     g.bnd[0][0] = g.bnd[0][1] = 1;
     g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
     g.bnd[2][0] = g.bnd[2][1] = g.deg2 ? 0 : 1;
-    const char* et = getenv("TVFEM_DG_TILE");
-    const char* ec = getenv("TVFEM_DG_CHUNK");
+    const char* et = experiment_env("TVFEM_DG_TILE");
+    const char* ec = experiment_env("TVFEM_DG_CHUNK");
     g.tile = (et && atoi(et) == 0) ? 0 : 1;
     g.tile_chunk = ec ? std::max(1, atoi(ec)) : 5;
     for (int s = 0; s < 3; ++s) {
@@ -696,7 +711,7 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   // and every iteration queued past convergence costs two early-exit launches
   static int div = -1;
   if (div < 0) {
-    const char* e = getenv("TVFEM_PCG_SMALL_DIV");
+    const char* e = experiment_env("TVFEM_PCG_SMALL_DIV");
     div = e ? std::max(1, atoi(e)) : 8;
   }
   const int small = std::max(1, c->O.pcg_batch / div);
@@ -736,6 +751,10 @@ static const char* reason_str(int r) {
 static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
   double* T = c->f[TV_F_T].ptr;
   const double* Tp = c->f[TV_F_T_PREV].ptr;
+  // NonlinearProblem.form: ghost update of the state before the first F
+  // (ThermoViscoProblem.py:351 scatter_forward); every rank enters it, every step
+  if (int e = halo(c, T)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
   const int64_t off = c->ownT_off, n = c->ownT_n;
   int its = 0, kits = 0;
   bool conv = false;
@@ -1071,8 +1090,10 @@ int tv_set_field(void* ctx, int field, const double* host, size_t n) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !host) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  // local only: no communication here (a host edit on some ranks must not make
+  // only those ranks enter an exchange); the ghost planes of T / T_prev are
+  // refreshed collectively at the start of every tv_step / tv_solve_T
   int rc = transfer(c, field, const_cast<double*>(host), n, 0);
-  if (rc == TV_OK && (field == TV_F_T || field == TV_F_T_PREV)) rc = halo(c, c->f[field].ptr);
   if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync");
   return rc;
 }

@@ -1322,7 +1322,7 @@ int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 static int march_rows() {
   static int rows = 0;
   if (!rows) {
-    const char* e = getenv("TVFEM_MARCH_ROWS");
+    const char* e = experiment_env("TVFEM_MARCH_ROWS");
     rows = (e && atoi(e) == 16) ? 16 : kRows;
   }
   return rows;
@@ -1331,7 +1331,7 @@ static int march_rows() {
 static int march_minblk() {  // workgroups the march grid is chunked up to (TVFEM_MARCH_MINBLK)
   static int v = 0;
   if (!v) {
-    const char* e = getenv("TVFEM_MARCH_MINBLK");
+    const char* e = experiment_env("TVFEM_MARCH_MINBLK");
     v = (e && atoi(e) > 0) ? atoi(e) : 1024;
   }
   return v;
@@ -1340,7 +1340,7 @@ static int march_minblk() {  // workgroups the march grid is chunked up to (TVFE
 static int march_minq() {  // fewest planes per marching chunk when splitting for occupancy (TVFEM_MARCH_MINQ)
   static int v = 0;
   if (!v) {
-    const char* e = getenv("TVFEM_MARCH_MINQ");
+    const char* e = experiment_env("TVFEM_MARCH_MINQ");
     v = (e && atoi(e) >= 2) ? atoi(e) : 6;
   }
   return v;
@@ -1349,7 +1349,7 @@ static int march_minq() {  // fewest planes per marching chunk when splitting fo
 static int march_wpe() {  // TVFEM_MARCH_WPE=8: register budget for 8 waves / SIMD
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("TVFEM_MARCH_WPE");
+    const char* e = experiment_env("TVFEM_MARCH_WPE");
     v = (e && atoi(e) == 8) ? 8 : 1;
   }
   return v;
@@ -1358,7 +1358,7 @@ static int march_wpe() {  // TVFEM_MARCH_WPE=8: register budget for 8 waves / SI
 static int march_pf() {  // prefetch depth of the march (TVFEM_MARCH_PF = 2 | 3 | 4)
   static int v = 0;
   if (!v) {
-    const char* e = getenv("TVFEM_MARCH_PF");
+    const char* e = experiment_env("TVFEM_MARCH_PF");
     v = e ? atoi(e) : 2;  // 2 measured best: deeper rings cost occupancy (66 -> 89 VGPRs)
     if (v < 2 || v > 4) v = 2;
   }
@@ -1368,7 +1368,7 @@ static int march_pf() {  // prefetch depth of the march (TVFEM_MARCH_PF = 2 | 3 
 static int march_dma() {  // Jacobian march with the LDS-DMA plane ring (TVFEM_MARCH_DMA=0 selects k_cg_march)
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("TVFEM_MARCH_DMA");
+    const char* e = experiment_env("TVFEM_MARCH_DMA");
     v = e ? (atoi(e) != 0) : 0;  // off: measured 80 vs 70 us in the PCG iteration (register ring + cache policy)
   }
   return v;
@@ -1377,7 +1377,7 @@ static int march_dma() {  // Jacobian march with the LDS-DMA plane ring (TVFEM_M
 static int march_exp() {  // TVFEM_MARCH_EXP: timing-experiment bits (see k_cg_march); 0 in production
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("TVFEM_MARCH_EXP");
+    const char* e = experiment_env("TVFEM_MARCH_EXP");
     v = e ? atoi(e) : 0;
   }
   return v;
@@ -1386,7 +1386,7 @@ static int march_exp() {  // TVFEM_MARCH_EXP: timing-experiment bits (see k_cg_m
 static int face_first() {  // face workgroups ahead of the marching tiles (TVFEM_FACE_FIRST=0|1)
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("TVFEM_FACE_FIRST");
+    const char* e = experiment_env("TVFEM_FACE_FIRST");
     v = e ? atoi(e) : 0;
     if (v < 0 || v > 2) v = 0;
   }
@@ -1404,7 +1404,7 @@ static int g_force_rows = -1;  // TVFEM_CG_KERNEL=rows selects the row kernel (t
 
 bool use_march(const CgGrid& g) {
   if (g_force_rows < 0) {
-    const char* e = getenv("TVFEM_CG_KERNEL");
+    const char* e = experiment_env("TVFEM_CG_KERNEL");
     g_force_rows = (e && e[0] == 'r') ? 1 : 0;
   }
   // the marching kernel addresses the fields with 32-bit buffer offsets

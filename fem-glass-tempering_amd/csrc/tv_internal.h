@@ -10,6 +10,13 @@
 
 namespace tv {
 
+// Experiment switches (TVFEM_MARCH_*, TVFEM_NT, TVFEM_DG_TILE, ...) select
+// kernel variants for measurements only.  They take effect only when
+// TVFEM_EXPERIMENTS=1 is set as well, and the library reports every switch it
+// honours on stderr once; a stray variable alone never changes the solver path.
+// Returns the variable's value, or nullptr when unset or not enabled.
+const char* experiment_env(const char* name);
+
 constexpr int kWave = 64;         // CDNA wavefront
 constexpr int kSeg = kWave - 2;   // outputs per wave of the x-row stencil kernels
 constexpr int kBlock = 256;       // 4 waves

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ d, const d
 int vec_blocks(int64_t n) {
   static int cap = -1;  // TVFEM_VEC_BLOCKS (experiment): fixed grid cap of the vector kernels
   if (cap < 0) {
-    const char* e = getenv("TVFEM_VEC_BLOCKS");
+    const char* e = experiment_env("TVFEM_VEC_BLOCKS");
     cap = e ? std::min(kVecBlocksMax, std::max(64, atoi(e))) : 0;
   }
   int64_t b = (n + kBlock - 1) / kBlock;
@@ -249,7 +249,7 @@ void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* 
   if (tail) rt = *tail;
   static int nt = -1;  // TVFEM_NT: 7 (default) or 0 (every stream with the default policy)
   if (nt < 0) {
-    const char* e = getenv("TVFEM_NT");
+    const char* e = experiment_env("TVFEM_NT");
     nt = (e && atoi(e) == 0) ? 0 : 7;
   }
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};

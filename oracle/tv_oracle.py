@@ -203,12 +203,15 @@ def _local_facets(d):
     return out
 
 
-def facet_topology(mesh):
+def facet_topology(mesh, plus_side="lower"):
     """Exterior facets [(cell, lf)] and interior facet pairs [(c+, lf+, c-, lf-)].
 
-    '+' is the lower cell index of the pair (dolfinx orders the two cells of an
-    interior facet by its facet->cell connectivity; for the uniform meshes used
-    for parity the choice does not change the form).
+    '+' is the lower cell index of the pair by default (``plus_side="higher"``
+    flips it).  dolfinx orders the two cells of an interior facet by its
+    facet->cell connectivity after its own cell reordering [3P, unpinned]: on a
+    uniform mesh the choice does not change the form, on a graded one it moves
+    h('+') in the SIPG penalty p/h('+') (ThermoViscoProblem.py:313-325), which
+    tests/test_oracle_kat.py::test_sipg_plus_side_sensitivity measures.
     """
     d = mesh.dim
     lfs = _local_facets(d)
@@ -232,7 +235,7 @@ def facet_topology(mesh):
     for k in range(0, len(idx), 2):
         i0, i1 = order[idx[k]], order[idx[k + 1]]
         o0, o1 = owners[i0], owners[i1]
-        if o0[0] > o1[0]:
+        if (o0[0] > o1[0]) == (plus_side == "lower"):
             o0, o1 = o1, o0
         interior.append((o0[0], o0[1], o1[0], o1[1]))
     interior = np.array(interior, dtype=np.int64).reshape(-1, 4)
@@ -302,7 +305,7 @@ class HeatForm:
     """
 
     def __init__(self, space: Space, dt: float, params: ThermalParams, qdeg_cell=3, qdeg_facet=3,
-                 penalty=5.0):
+                 penalty=5.0, plus_side="lower"):
         self.V = space
         self.mesh = space.mesh
         self.dt = dt
@@ -327,7 +330,7 @@ class HeatForm:
         self.Ke = np.einsum("cq,cqia,cqja->cij", self.cw, gphi, gphi)
         self.be = np.einsum("cq,qi->ci", self.cw, phi)         # int phi_i
         # exterior facets
-        ext, inter = facet_topology(self.mesh)
+        ext, inter = facet_topology(self.mesh, plus_side)
         self.ext = ext
         self.inter = inter
         self._prep_exterior(qdeg_facet)
@@ -623,7 +626,7 @@ class OracleProblem:
     (ThermoViscoProblem.py:112-171).
     """
 
-    def __init__(self, mesh: Mesh, time, dt, config, model_parameters, linear="direct"):
+    def __init__(self, mesh: Mesh, time, dt, config, model_parameters, linear="direct", plus_side="lower"):
         assert all(v["element"] in ("CG", "DG") for v in config.values()), \
             "Only CG and DG elements are supported"
         self.mesh = mesh
@@ -638,7 +641,7 @@ class OracleProblem:
         self.linear = linear
         self.VT = Space(mesh, config["T"]["element"], config["T"]["degree"])
         self.VS = Space(mesh, config["sigma"]["element"], config["sigma"]["degree"])
-        self.form = HeatForm(self.VT, dt, self.tp)
+        self.form = HeatForm(self.VT, dt, self.tp, plus_side=plus_side)
         d = self.dim
         nT, nS = self.VT.n, self.VS.n
         z = np.zeros

@@ -25,29 +25,19 @@ def _torch():
     return torch
 
 
-def relerr(a, b, mask=None):
-    """relative L2 error; NaN positions must coincide.  ``mask`` (per entry)
-    restricts the comparison to well-conditioned entries (see cond_mask)."""
-    a = np.asarray(a, dtype=np.float64)
-    b = np.asarray(b, dtype=np.float64)
-    if mask is not None:
-        a, b = a[mask], b[mask]
-    na, nb = np.isnan(a), np.isnan(b)
-    assert np.array_equal(na, nb), f"NaN pattern differs: {na.sum()} vs {nb.sum()}"
-    a, b = a[~na], b[~nb]
-    den = np.linalg.norm(b)
-    if den == 0.0:
-        return np.linalg.norm(a - b)
-    return np.linalg.norm(a - b) / den
+from parity_util import check_field, relerr  # noqa: E402
 
 
-def make_pair(axes, cfg, mp=None, materialize=True, dt=0.1):
+def make_pair(axes, cfg, mp=None, materialize=True, dt=0.1, linear="pcg"):
+    """device problem + oracle on the same mesh; the oracle's linear solver is
+    its PETSc KSPCG + Jacobi restatement (``linear="pcg"``) so that Krylov
+    iteration counts can be compared, or a direct solve."""
     from tvfem import RectilinearMesh
     from tvfem.problem import ThermoViscoProblem
     mp = dict(O.MAIN_MODEL_PARAMS if mp is None else mp)
     dev = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), dt, cfg, mp, part_axis=len(axes) - 1 if len(axes) == 3 else -1,
                              materialize=materialize, verbose=False)
-    ref = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), dt, cfg, mp)
+    ref = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), dt, cfg, mp, linear=linear)
     dev.setup()
     ref.setup()
     return dev, ref
@@ -175,32 +165,41 @@ STEP_CASES = [
 ]
 
 
+def check_counts(dev_its, ref_hist):
+    """Newton iterations equal per step; Krylov iterations of the step within
+    max(one per Newton solve, 5 %) of the oracle's PETSc-KSPCG restatement
+    (oracle/tv_oracle.py:510-548): the device recurrences round differently,
+    and CG's iteration count on the long 1D bars (~70 per solve) moves by a
+    few under rounding alone."""
+    assert len(dev_its) == len(ref_hist)
+    for (n_d, k_d), (n_r, k_r) in zip(dev_its, ref_hist):
+        assert n_d == n_r, (dev_its, ref_hist)
+        assert abs(k_d - k_r) <= max(n_r, int(np.ceil(0.05 * k_r))), (dev_its, ref_hist)
+
+
 @pytest.mark.parametrize("name,axes,tf,sf,steps", STEP_CASES, ids=[c[0] for c in STEP_CASES])
 def test_time_steps_match_oracle(name, axes, tf, sf, steps):
     _torch()
     dev, ref = make_pair(axes, {"T": tf, "sigma": sf})
+    its = []
     for s in range(steps):
         dev.solve_timestep()
         ref.solve_timestep()
+        its.append((dev.last_newton_iterations, dev.last_krylov_iterations))
         eT = relerr(dev.functions_current["T"].x.array, ref.functions_current["T"])
         assert eT < 1e-10, (s, eT)
+    check_counts(its, ref.newton_history)
     # xi == 0 (quirk Q5, NaN stress) happens where T - T_prev rounds to ~0; at
     # |T - T_prev| below 1e-6 K the reference's own stress is rounding noise
-    # (1 - E cancellation), so the comparison is restricted to
-    # well-conditioned dofs there (NaN positions must agree on them).
+    # (1 - E cancellation, SURVEY.md H2/H3): split comparison (parity_util)
     mT, mS = cond_mask(ref)
     d2 = dev.dim ** 2
-    checks = [
-        (dev.functions["phi"].x.array, ref.functions["phi"], 1e-9, None),
-        (dev.functions["xi"].x.array, ref.functions["xi"], 1e-6, mT),
-        (dev.functions_current["Tf"].x.array, ref.functions_current["Tf"], 1e-10, None),
-        (dev.functions_next["sigma"].x.array, ref.functions_next["sigma"], 1e-6, np.repeat(mS, d2)),
-    ]
-    for got, want, tol, m in checks:
-        e = relerr(got, want, m)
-        assert e < tol, (e, tol)
-    # the ill-conditioned remainder is a small minority of dofs
-    assert mT.mean() > 0.5 or dev.dim == 1
+    assert relerr(dev.functions["phi"].x.array, ref.functions["phi"]) < 1e-9
+    assert relerr(dev.functions_current["Tf"].x.array, ref.functions_current["Tf"]) < 1e-10
+    min_frac = 0.9 if dev.dim == 3 else None
+    check_field("xi", dev.functions["xi"].x.array, ref.functions["xi"], mT, 1, min_frac=min_frac)
+    check_field("sigma", dev.functions_next["sigma"].x.array, ref.functions_next["sigma"], mS, d2,
+                min_frac=min_frac)
     assert dev.last_newton_iterations >= 2
     dev.close()
 
@@ -337,6 +336,7 @@ def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
     cfg = {"T": DG, "sigma": DG}
     rng = np.random.default_rng(3)
     out = {}
+    monkeypatch.setenv("TVFEM_EXPERIMENTS", "1")  # the kernel-variant switches below are gated by it
     for tile, chunk in ((0, 5), (1, 2), (1, 5)):
         monkeypatch.setenv("TVFEM_DG_TILE", str(tile))
         monkeypatch.setenv("TVFEM_DG_CHUNK", str(chunk))

@@ -209,3 +209,31 @@ def test_petsc_cg_restatement_matches_direct():
     x, its = O.pcg_jacobi(A, b, rtol=1e-12)
     assert its > 0
     assert np.linalg.norm(x - x_direct) <= 1e-9 * np.linalg.norm(x_direct)
+
+
+def test_sipg_plus_side_sensitivity():
+    """[3P, unpinned] Which cell of an interior facet is '+' in the SIPG terms
+    (ThermoViscoProblem.py:313-325: penalty / h('+'), alpha('+')) follows
+    dolfinx's facet->cell order after its own cell reordering, which no fixture
+    pins.  The oracle and the HIP kernels take the lower cell index.  On a
+    uniform mesh the choice cannot matter; on the graded bar of the reference's
+    default config (main.py: DG temperature) it does, and this test records by
+    how much: T changes by ~4e-6 relative after one step, i.e.
+    the reference itself is only defined to that level there."""
+    cfg = {"T": {"element": "DG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+    from geometry import graded_bar  # the main.py mesh (continuously graded 0.1 .. 3)
+    graded = [graded_bar().axes[0]]
+    uniform = [np.linspace(0.0, 50.0, 41)]
+    out = {}
+    for name, axes in (("uniform", uniform), ("graded", graded)):
+        T = {}
+        for side in ("lower", "higher"):
+            r = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                                plus_side=side)
+            r.setup()
+            for _ in range(3):
+                r.solve_timestep()
+            T[side] = r.functions_current["T"].copy()
+        out[name] = np.linalg.norm(T["lower"] - T["higher"]) / np.linalg.norm(T["lower"])
+    assert out["uniform"] < 1e-14, out
+    assert 1e-7 < out["graded"] < 1e-4, out

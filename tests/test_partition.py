@@ -107,15 +107,10 @@ def test_gloo_two_rank_halo_exchange_cpu():
     assert all(ok for _, ok in res), res
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_partitioned_run_matches_single_partition(world):
-    import torch
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    port = 29700 + world
+def _partition_check(world, comm, port, extra=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "partition_check.py")]
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "partition_check.py"),
+           "--comm", comm, *extra]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("PARTITION_CHECK ")]
     assert line, out.stdout[-2000:] + out.stderr[-2000:]
@@ -124,6 +119,34 @@ def test_partitioned_run_matches_single_partition(world):
     assert res["phi"] < 1e-11, res
     assert res["xi"] < 1e-6, res
     assert res["sigma"] < 1e-6, res
+    # the global reductions make the partitioned solve take the same iterations
+    for (n1, k1), (n2, k2) in zip(res["its_parts"], res["its_single"]):
+        assert n1 == n2 and abs(k1 - k2) <= n1, res
+    return res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_run_matches_single_partition(world):
+    """P partitions on one GPU (host-staged transport) vs one partition."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _partition_check(world, "host", 29700 + world)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_rccl_partitioned_run_matches_single_partition(world):
+    """The production transport: one rank per GPU, RCCL grouped send/recv of the
+    ghost planes and ncclAllReduce of the PCG / Newton sums over xGMI (replaces
+    dolfinx scatter_forward, ThermoViscoProblem.py:351, and PETSc's MPI
+    reductions).  Needs `world` GPUs; skipped on smaller boxes."""
+    import torch
+    n = torch.cuda.device_count()  # does not initialise the GPU in this process
+    if n < world:
+        pytest.skip(f"{world} GPUs needed, {n} visible")
+    _partition_check(world, "rccl", 29720 + world, ("--cells", "12,48,6"))
 
 
 @pytest.mark.gpu

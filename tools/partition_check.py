@@ -1,6 +1,12 @@
-"""Partitioned run on one GPU (host-staged comm over gloo) vs the single-partition
-run of the same mesh: T, phi, xi and sigma must agree.  Launched by
-tests/test_partition.py as `torch.distributed.run --nproc-per-node P`."""
+"""Partitioned run vs the single-partition run of the same mesh: T, phi, xi and
+sigma must agree, and the Newton / Krylov iteration counts too.  Launched by
+tests/test_partition.py as `torch.distributed.run --nproc-per-node P`.
+
+    --comm host   every rank on GPU 0, host-staged transport over gloo (one GPU)
+    --comm rccl   rank r on GPU r (LOCAL_RANK), RCCL send/recv + allreduce over
+                  xGMI: the production transport (needs P GPUs)
+"""
+import argparse
 import json
 import os
 import sys
@@ -15,7 +21,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from tvfem import box_mesh  # noqa: E402
-from tvfem.parallel import init_host_comm  # noqa: E402
+from tvfem.parallel import init_host_comm, init_rccl  # noqa: E402
 from tvfem.problem import ThermoViscoProblem  # noqa: E402
 
 MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0, "htc": 280.1,
@@ -24,8 +30,8 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
 
-def run(mesh, n_parts, part, steps, comm=None):
-    p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=0, n_parts=n_parts, part=part, part_axis=1,
+def run(mesh, n_parts, part, steps, comm=None, device=0):
+    p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
                            verbose=False)
     if comm is not None:
         comm(p)
@@ -40,17 +46,29 @@ def run(mesh, n_parts, part, steps, comm=None):
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--comm", choices=["host", "rccl"], default="host")
+    ap.add_argument("--cells", default="10,30,5")
+    ap.add_argument("--steps", type=int, default=4)
+    a = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
     dist.init_process_group("gloo")
-    mesh = box_mesh([2.0, 6.0, 1.0], [10, 30, 5])
-    steps = 4
-    loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world))
+    nc = [int(v) for v in a.cells.split(",")]
+    mesh = box_mesh([2.0, 6.0, 1.0], nc)
+    steps = a.steps
+    if a.comm == "rccl":
+        if torch.cuda.device_count() < world:
+            raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
+        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local)
+    else:
+        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world))
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
         ref, its_ref = run(mesh, 1, 0, steps)
-        res = {"its_parts": its, "its_single": its_ref}
+        res = {"comm": a.comm, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             full = np.concatenate([np.asarray(g[k]) for g in gathered])
             e = np.linalg.norm(full - ref[k]) / np.linalg.norm(ref[k])
