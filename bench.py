@@ -49,6 +49,8 @@ def parse():
                     help="rccl (production) or host-staged gloo transport (rehearsal on one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the hot kernels inside the timed steps")
+    ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto",
+                    help="Krylov form: single-reduction (Chronopoulos-Gear, 3D CG) or PETSc KSPCG as written")
     return ap.parse_args()
 
 
@@ -86,7 +88,8 @@ def main():
         import torch
         device = local_rank % max(1, torch.cuda.device_count())
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
-                              n_parts=world, part=rank, part_axis=1, verbose=False)
+                              n_parts=world, part=rank, part_axis=1, verbose=False, pcg_variant=a.pcg)
+    single = prob.pcg_variant == "single"
     lib, ctx = prob._lib, prob._ctx
     if world > 1:
         from tvfem.parallel import init_host_comm, init_rccl
@@ -144,6 +147,8 @@ def main():
     # resident, so faster than in the solve; reported for reference only)
     kern = {}
     names = {3: "pcg_matvec_fused", 4: "pcg_update", 0: "jacobian_apply", 2: "residual"}
+    if single:  # one fused launch per Krylov iteration, no separate update
+        names = {3: "pcg_iteration_single_reduction", 0: "jacobian_apply", 2: "residual"}
     if not a.thermal_only:
         names[1] = "visco_update"
     for kid, name in names.items():
@@ -163,7 +168,7 @@ def main():
         rec["GBps"] = by.value / (rec["ms"] * 1e-3) / 1e9
         kern[name] = rec
 
-    dom = kern["pcg_matvec_fused"]
+    dom = kern[names[3]]
     # traffic: HBM bytes per launch of this kernel from the rocprofv3 --pmc passes
     # (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section) of this same
     # bench command, committed under profiles/ (counters cannot be read inside
@@ -176,7 +181,8 @@ def main():
         traffic_src = "committed rocprofv3 --pmc record " + os.path.relpath(pmc_file, ROOT)
     roofline = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)",
+                "kernel": ("pcg_iteration_single_reduction (s, p, x, r, z updates; w <- J(T) z; (r,z), (z,w), (z,z))"
+                           if single else "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)"),
                 "bytes_per_launch": dom["bytes"], "ms_per_launch": dom["ms"],
                 "timing": "in-solve" if dom["launches_timed"] else "isolated"}
 
@@ -212,6 +218,8 @@ def main():
                                        f"mesh partition along y x{world} ("
                                        + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")"),
                        "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,
+                       "krylov_form": ("single-reduction (Chronopoulos-Gear) Jacobi-PCG" if single
+                                       else "PETSc KSPCG Jacobi-PCG"),
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},
             "roofline": roofline,
             "kernels": kern,

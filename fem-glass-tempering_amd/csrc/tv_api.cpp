@@ -82,9 +82,15 @@ struct Ctx {
   double* dgh[3] = {nullptr, nullptr, nullptr};
   int* map = nullptr;
   int64_t* bnodes = nullptr;
-  double* fface[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  double* ffbuf[2] = {nullptr, nullptr};  // Robin facet-term face arrays (CgGrid::ffbuf)
   // PCG work (T space, local size)
   double *r = nullptr, *z = nullptr, *pA = nullptr, *pB = nullptr, *w = nullptr, *dinv = nullptr;
+  // single-reduction PCG (k_cgs_march): r, s, w in two parities (w[0] = w);
+  // p = pA, x = the dx field; wsend: the two packed boundary planes of w + facet
+  // terms sent to the neighbours (multi-rank)
+  bool cgs = false;
+  double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
+  double* wsend = nullptr;
   double* partials = nullptr;
   int n_partials_cap = 0;
   double* sums = nullptr;
@@ -274,6 +280,7 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       g.coef[s] = c->coef[s];
     }
     const int64_t plane = (int64_t)g.n0 * g.n1;
+    for (int f = 0; f < 6; ++f) g.ffoff[f] = -1;
     if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
       std::vector<int64_t> bn;
       for (int k = g.k_begin; k < g.k_end; ++k)
@@ -290,21 +297,29 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       }
       g.bnodes = c->bnodes;
       g.n_bnodes = (int64_t)bn.size();
-      // facet-Jacobian terms: one value per node of every physical boundary face
+      // facet-Jacobian terms: one value per node of every physical boundary
+      // face, the six faces in one contiguous buffer, two parities
       const int nn[3] = {g.n0, g.n1, g.n2};
+      int64_t tot = 0;
       for (int f = 0; f < 6; ++f) {
         const int ax = f >> 1, side = f & 1;
         g.fface[f] = nullptr;
         g.fn1[f] = g.fn2[f] = 0;
+        g.ffoff[f] = -1;
         if (!g.bnd[ax][side]) continue;
         const int t1 = (ax == 0) ? 1 : 0, t2 = (ax == 2) ? 1 : 2;
         g.fn1[f] = nn[t1];
         g.fn2[f] = nn[t2];
-        const size_t bytes = sizeof(double) * (size_t)nn[t1] * nn[t2];
-        HIPC(hipMalloc(&c->fface[f], bytes));
-        HIPC(hipMemsetAsync(c->fface[f], 0, bytes, c->stream));
-        g.fface[f] = c->fface[f];
+        g.ffoff[f] = tot;
+        tot += (int64_t)nn[t1] * nn[t2];
       }
+      g.ffsize = tot;
+      for (int q = 0; q < 2; ++q) {
+        HIPC(hipMalloc(&c->ffbuf[q], sizeof(double) * (size_t)std::max<int64_t>(1, tot)));
+        HIPC(hipMemsetAsync(c->ffbuf[q], 0, sizeof(double) * (size_t)std::max<int64_t>(1, tot), c->stream));
+        g.ffbuf[q] = c->ffbuf[q];
+      }
+      for (int f = 0; f < 6; ++f) g.fface[f] = (g.ffoff[f] >= 0) ? c->ffbuf[0] + g.ffoff[f] : nullptr;
     }
     c->nT = plane * g.n2;
     // the CG kernels index local nodes with 32-bit integers (68 M nodes = 290 GB
@@ -450,16 +465,35 @@ static int setup_fields(Ctx* c) {
   if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
   else np = std::max(np, dg_num_blocks(c->dg));
   c->n_partials_cap = np;
-  HIPC(hipMalloc(&c->partials, sizeof(double) * 2 * (size_t)np));
+  // records of width <= 3 per workgroup + the shard records of the two-level tail
+  HIPC(hipMalloc(&c->partials, sizeof(double) * 3 * ((size_t)np + 2 * kShards)));
   HIPC(hipMalloc(&c->sums, sizeof(double) * 8));
-  HIPC(hipMalloc(&c->counters, sizeof(unsigned) * 4));
-  HIPC(hipMemsetAsync(c->counters, 0, sizeof(unsigned) * 4, c->stream));
+  HIPC(hipMalloc(&c->counters, sizeof(unsigned) * kCounterWords));
+  HIPC(hipMemsetAsync(c->counters, 0, sizeof(unsigned) * kCounterWords, c->stream));
   HIPC(hipMalloc(&c->st, sizeof(PcgState)));
   HIPC(hipMalloc(&c->tflag, sizeof(int)));
   HIPC(hipMemsetAsync(c->tflag, 0, sizeof(int), c->stream));  // the tilde fields start at +0.0
   HIPC(hipHostMalloc(&c->h_st, 2 * sizeof(PcgState)));
   for (int k = 0; k < 2; ++k) HIPC(hipEventCreateWithFlags(&c->evp[k], hipEventDisableTiming));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
+  const int var = c->O.pcg_variant;
+  const bool can = c->fam_T == TV_CG && cg_cgs_supported(c->cg);
+  if (var == TV_PCG_SINGLE_REDUCTION && !can)
+    return c->fail(TV_ERR_ARG, "pcg_variant SINGLE_REDUCTION needs a 3D CG1 temperature space");
+  // AUTO: the single-reduction form where the mesh is partitioned (one RCCL
+  // group per iteration instead of two all-reduces + a halo + two logic
+  // launches); on one partition KSPCG's two lighter launches are faster
+  // (measured, DESIGN.md §5: 32 vs 37 us per iteration at 1M nodes, 130 vs
+  // 217 us at C4)
+  c->cgs = can && (var == TV_PCG_SINGLE_REDUCTION || (var == TV_PCG_AUTO && c->n_parts > 1));
+  if (c->cgs) {
+    for (double** q : {&c->cr[0], &c->cr[1], &c->cs[0], &c->cs[1], &c->cw1}) {
+      HIPC(hipMalloc(q, nb));
+      HIPC(hipMemsetAsync(*q, 0, nb, c->stream));
+    }
+    const size_t plane = (size_t)c->cg.n0 * c->cg.n1;
+    HIPC(hipMalloc(&c->wsend, sizeof(double) * 2 * plane));
+  }
   return TV_OK;
 }
 
@@ -666,7 +700,7 @@ static int pcg_iteration(Ctx* c, const double* T, int it) {
     if (int e = allreduce(c, c->sums, 1)) return e;
     launch_logic(c->st, c->sums, 2, c->stream);
   }
-  RedTail t2{c->counters + 1, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
+  RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
   const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
                     c->z + off, c->partials, c->stream, &t2, &fa, it);
@@ -736,6 +770,148 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   return TV_OK;
 }
 
+// ---- single-reduction PCG (Chronopoulos-Gear form, k_cgs_march) -------------
+// w of the owned boundary planes + the face-workgroup facet terms (the value a
+// neighbour's ghost plane must hold), packed for the halo
+__global__ __launch_bounds__(kBlock) void k_cgs_pack(CgGrid g, const double* __restrict__ w,
+                                                     const double* __restrict__ ff, int raxis,
+                                                     double* __restrict__ out) {
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < 2 * plane; t += (int64_t)gridDim.x * kBlock) {
+    const int side = (int)(t / plane);
+    const int64_t e = t - side * plane;
+    const int k = side ? g.k_end - 1 : g.k_begin;
+    const int i = (int)(e % g.n0), j = (int)(e / g.n0);
+    // facet terms in the order of k_cgs_march: x face, then the row-axis face
+    double fx = 0.0, fr = 0.0;
+    const int fxi = (i == 0) ? 0 : (i == g.n0 - 1 ? 1 : -1);
+    if (fxi >= 0 && g.ffoff[fxi] >= 0) fx = ff[g.ffoff[fxi] + j + (int64_t)g.n1 * k];
+    const int c = (raxis == 1) ? j : k, n = (raxis == 1) ? g.n1 : g.n2;
+    const int sd = (c == 0) ? 0 : (c == n - 1 ? 1 : -1);
+    if (sd >= 0 && g.ffoff[2 * raxis + sd] >= 0) fr = ff[g.ffoff[2 * raxis + sd] + i + (int64_t)g.n0 * ((raxis == 1) ? k : j)];
+    out[t] = w[e + plane * k] + (fx + fr);
+  }
+}
+
+static int cgs_raxis(const Ctx* c) { return (c->cg.n2 >= c->cg.n1) ? 2 : 1; }  // = plan(g).raxis
+
+// ghost planes of w_i: neighbours' packed boundary planes (RCCL group with
+// the all-reduce of the iteration's sums, or the host-staged transport)
+static int cgs_exchange(Ctx* c, double* wout, const double* fout) {
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  const int blocks = (int)std::min<int64_t>(1024, (2 * plane + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_cgs_pack, dim3(blocks), dim3(kBlock), 0, c->stream, g, wout, fout, cgs_raxis(c), c->wsend);
+  if (c->host_sendrecv) {
+    if (int e = allreduce(c, c->sums, 3)) return e;
+    double* s_lo = c->h_halo;
+    double* s_hi = c->h_halo + plane;
+    double* r_lo = c->h_halo + 2 * plane;
+    double* r_hi = c->h_halo + 3 * plane;
+    HIPC(hipMemcpyAsync(s_lo, c->wsend, 2 * plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (g.g_lo && c->host_sendrecv(s_lo, (size_t)plane, c->rank - 1, r_lo, (size_t)plane, c->rank - 1, c->host_user))
+      return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (g.g_hi && c->host_sendrecv(s_hi, (size_t)plane, c->rank + 1, r_hi, (size_t)plane, c->rank + 1, c->host_user))
+      return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (g.g_lo) HIPC(hipMemcpyAsync(wout, r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (g.g_hi) HIPC(hipMemcpyAsync(wout + plane * g.k_end, r_hi, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return TV_OK;
+  }
+  // one group: the 3-scalar all-reduce and the ghost planes of w (<= 2 peers)
+  NCCLC(ncclGroupStart());
+  NCCLC(ncclAllReduce(c->sums, c->sums, 3, ncclDouble, ncclSum, c->comm, c->stream));
+  if (g.g_lo) {
+    NCCLC(ncclSend(c->wsend, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclRecv(wout, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+  }
+  if (g.g_hi) {
+    NCCLC(ncclSend(c->wsend + plane, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclRecv(wout + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
+static CgsBuffers cgs_buffers(Ctx* c, const double* T, int it) {
+  // iteration it reads parity (it - 1) & 1 and writes it & 1; r_0 is the Newton
+  // residual (c->r), read by iterations 0 and 1
+  CgsBuffers v{};
+  const int o = (it + 1) & 1, w = it & 1;
+  double* W[2] = {c->w, c->cw1};
+  v.T = T;
+  v.rin = (it <= 1) ? c->r : c->cr[o];
+  v.rout = c->cr[w];
+  v.sin = c->cs[o];
+  v.sout = c->cs[w];
+  v.win = W[o];
+  v.wout = W[w];
+  v.fin = c->cg.ffbuf[o];
+  v.fout = c->cg.ffbuf[w];
+  v.p = c->pA;
+  v.x = c->f[TV_F_DX].ptr;
+  v.dinv = c->dinv;
+  return v;
+}
+
+static int cgs_iteration(Ctx* c, const double* T, int it) {
+  const bool multi = multi_rank(c);
+  const int slot = c->ts_next + it;
+  uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
+  const int kind = multi ? 0 : (it == 0 ? 4 : 5);
+  RedTail rt{c->counters, c->partials, c->sums, c->st, kind, ts};
+  const CgsBuffers v = cgs_buffers(c, T, it);
+  launch_cg_cgs(c->cg, it == 0, v, c->st, c->partials, c->stream, &rt, it, (multi && it > 0) ? c->sums : nullptr);
+  if (multi)
+    if (int e = cgs_exchange(c, v.wout, v.fout)) return e;
+  return TV_OK;
+}
+
+static int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  // ghost planes of r_0 and diag^-1 (the halo rows recompute z there)
+  if (int e = halo(c, c->r)) return e;
+  if (int e = halo(c, c->dinv)) return e;
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 4 * c->O.pcg_batch + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
+  int launched = 0, slot = 0;
+  auto enqueue = [&](int nb, int k) -> int {
+    for (int b = 0; b < nb; ++b)
+      if (int e = cgs_iteration(c, T, launched + b)) return e;
+    launched += nb;
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[k], c->stream));
+    return TV_OK;
+  };
+  // iteration 0 and the first batch, then one more iteration queued behind
+  // every poll (see pcg_solve); multi-rank the state lags one launch
+  const int lag = multi_rank(c) ? 1 : 0;
+  const int small = 1 + lag;
+  if (int e = enqueue(1 + std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
+  for (;;) {
+    if (int e = enqueue(small, slot ^ 1)) return e;
+    HIPC(hipEventSynchronize(c->evp[slot]));
+    if (c->h_st[slot].done) break;
+    if (launched > c->O.ksp_max_it + 2 * small + 4) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    slot ^= 1;
+  }
+  *its = c->h_st[slot].it;
+  *reason = c->h_st[slot].reason;
+  c->pcg_hint = *its;
+  if (c->ktime) {
+    for (int it = 1; it <= *its; it += c->kstride)  // productive iterations (iteration 0 is the init launch)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
+  }
+  return TV_OK;
+}
+
 static const char* reason_str(int r) {
   switch (r) {
     case R_DIV_ITS: return "DIVERGED_ITS";
@@ -763,7 +939,7 @@ static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
   while (!conv && its < c->O.newton_max_it) {
     op_diag(c, T, c->dinv, 1);  // J(u) (matrix-free) + Jacobi PC setup
     int k = 0, reason = 0;
-    if (int e = pcg_solve(c, T, &k, &reason)) return e;
+    if (int e = (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))) return e;
     kits += k;
     if (reason < 0)
       return c->fail(TV_ERR_KSP, std::string("Krylov solver did not converge (") + reason_str(reason) + ")");
@@ -889,6 +1065,7 @@ void tv_default_options(tv_options* o) {
   o->materialize = 1;
   o->use_graphs = 0;
   o->pcg_batch = 8;
+  o->pcg_variant = TV_PCG_AUTO;
 }
 
 void tv_default_params(tv_params* p) {
@@ -997,6 +1174,8 @@ int tv_destroy(void* ctx) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (int i = 0; i < TV_NUM_FIELDS; ++i)
     if (c->f[i].alloc && c->f[i].ptr) hipFree(c->f[i].ptr);
+  for (double* p : {c->cr[0], c->cr[1], c->cs[0], c->cs[1], c->cw1, c->wsend})
+    if (p) hipFree(p);
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
     if (p) hipFree(p);
   for (int s = 0; s < 3; ++s) {
@@ -1005,8 +1184,8 @@ int tv_destroy(void* ctx) {
   }
   if (c->map) hipFree(c->map);
   if (c->bnodes) hipFree(c->bnodes);
-  for (int f = 0; f < 6; ++f)
-    if (c->fface[f]) hipFree(c->fface[f]);
+  for (int q = 0; q < 2; ++q)
+    if (c->ffbuf[q]) hipFree(c->ffbuf[q]);
   if (c->st) hipFree(c->st);
   if (c->tflag) hipFree(c->tflag);
   if (c->counters) hipFree(c->counters);
@@ -1292,11 +1471,16 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       *bytes = 24.0 * n;
       break;
     case 3:  // fused PCG matvec: read z, p_old, write p, w (T on boundary nodes only)
+      // single-reduction iteration: read r, s, w, diag^-1, p, x; write r, s, p, x, w
+      *bytes = (c->cgs ? 88.0 : 32.0) * n;
+      break;
     case 5:
     case 7:
       *bytes = 32.0 * n;
       break;
     case 4:  // PCG update, mean of an even / odd pair: read w, dinv, z, write z (+ odd: read p_prev, p, dx, write dx)
+      *bytes = c->cgs ? 0.0 : 48.0 * n;
+      break;
     case 6:
     case 8:
       *bytes = 48.0 * n;
@@ -1311,9 +1495,11 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !ms || reps < 1) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  if (kernel == 4 && c->cgs) return c->fail(TV_ERR_ARG, "kernel 4: no separate update in the single-reduction PCG");
   if (kernel >= 3 && kernel <= 8) {  // PCG kernels need a running solver state
     PcgState h{};
     h.beta = 1.0; h.betaold = 2.0; h.a = 1e-3; h.it = 1; h.done = 0; h.max_it = 1 << 30;
+    h.gamma = 1.0; h.eta = 1.0;
     HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
   }
   int upd_it = 0;
@@ -1323,7 +1509,15 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       case 0: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); return TV_OK;
       case 1: return visco(c, false);
       case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;
-      case 3: op_japply_fused(c, c->f[TV_F_T].ptr, &np, nullptr, 1); return TV_OK;  // st->it = 1 below
+      case 3:
+        if (c->cgs) {  // the single-reduction iteration, parities alternating, no tail
+          const int it = 2 + (upd_it++);
+          const CgsBuffers v = cgs_buffers(c, c->f[TV_F_T].ptr, it);
+          launch_cg_cgs(c->cg, false, v, c->st, c->partials, c->stream, nullptr, it, nullptr);
+          return TV_OK;
+        }
+        op_japply_fused(c, c->f[TV_F_T].ptr, &np, nullptr, 1);  // st->it = 1 below
+        return TV_OK;
       case 4: {
         const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, c->ownT_off) : FaceAdd{};
         launch_pcg_update(c->ownT_n, c->st, c->pA + c->ownT_off, c->pB + c->ownT_off, c->w + c->ownT_off,
@@ -1347,7 +1541,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     int np = 0;
     for (int i = 0; i <= reps; ++i) {
       RedTail t1{tails ? c->counters : nullptr, c->partials, c->sums, c->st, 0};
-      RedTail t2{tails ? c->counters + 1 : nullptr, c->partials, c->sums, c->st, 0};
+      RedTail t2{tails ? c->counters + kTailCounters : nullptr, c->partials, c->sums, c->st, 0};
       HIPC(hipEventRecord(ev[3 * i], c->stream));
       op_japply_fused(c, c->f[TV_F_T].ptr, &np, &t1, i + 1);  // both parities, as in the solve
       HIPC(hipEventRecord(ev[3 * i + 1], c->stream));
@@ -1413,6 +1607,13 @@ int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches) {
   if (int e = ts_flush(c)) return e;
   *ms_avg = c->kcnt[k] ? c->ksum[k] / (double)c->kcnt[k] : 0.0;
   if (launches) *launches = c->kcnt[k];
+  return TV_OK;
+}
+
+int tv_pcg_variant(void* ctx, int* variant) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !variant) return TV_ERR_ARG;
+  *variant = c->cgs ? TV_PCG_SINGLE_REDUCTION : TV_PCG_KSPCG;
   return TV_OK;
 }
 

@@ -1277,6 +1277,494 @@ __global__ __launch_bounds__(R * kWave) void k_cg_march_dma(CgGrid g, const doub
   }
 }
 
+// ---------------------------------------------------------------------------
+// Single-reduction Jacobi-PCG iteration fused with the marching Jacobian: the
+// Chronopoulos-Gear form of CG, ONE launch and ONE reduction per iteration
+// (PETSc KSPCG, which the reference runs at ThermoViscoProblem.py:339-346,
+// needs two: p.w for alpha, then z.r and z.z for beta and the norm test).
+//
+// Iteration i (i >= 1) with alpha = alpha_{i-1}, beta = beta_{i-1}, per node:
+//     w_full = w_{i-1} + facet terms        (face workgroups' faces, f_{i-1})
+//     s_{i-1} = w_full + beta s_{i-2}       (= A p_{i-1} by recurrence)
+//     p_{i-1} = z_{i-1} + beta p_{i-2},  z_{i-1} = B r_{i-1}
+//     x_i = x_{i-1} + alpha p_{i-1}
+//     r_i = r_{i-1} - alpha s_{i-1},  z_i = B r_i      (B = diag(J)^-1)
+//     w_i = J z_i                            (the march below)
+//     partial sums (r_i, z_i), (z_i, w_i + facet terms), (z_i, z_i)
+// and the tail turns the sums into gamma_i = (r, z), eta_i = delta_i -
+// beta_i gamma_i / alpha_{i-1} (= (p_i, A p_i)), alpha_i, beta_i and PETSc's
+// convergence test on ||z_i|| (KSPConvergedDefault, preconditioned norm): the
+// same iterates as KSPCG in exact arithmetic.  i = 0 (INIT): z_0 = B r_0,
+// w_0 = J z_0, x = 0.  At i = 1 p and s start as z_0 and w_0 (no beta term).
+//
+// z at the halo rows of a tile is recomputed from r, s, w (+ facet terms) and
+// diag^-1 of the previous iteration, so r, s and w ping-pong between two
+// buffers (neighbouring tiles read the old values while this launch writes
+// the new ones); p and x are touched at owned nodes only, in place.  Loads,
+// LDS exchange, sliding window, coefficient staging and the in-tile faces
+// normal to the march axis follow k_cg_march.
+// ---------------------------------------------------------------------------
+
+// byte offset of the facet term of node (i, j, k) on the x faces / on the
+// faces normal to storage axis ra (1 or 2) in the face buffer, or kBadOff
+__device__ __forceinline__ uint32_t ff_off_x(const CgGrid& g, int i, int j, int k) {
+  const int f = (i == 0) ? 0 : (i == g.n0 - 1 ? 1 : -1);
+  if (f < 0 || g.ffoff[f] < 0) return kBadOff;
+  return (uint32_t)(g.ffoff[f] + j + (int64_t)g.n1 * k) * 8u;
+}
+__device__ __forceinline__ uint32_t ff_off_r(const CgGrid& g, int ra, int i, int j, int k) {
+  const int c = (ra == 1) ? j : k, n = (ra == 1) ? g.n1 : g.n2;
+  const int side = (c == 0) ? 0 : (c == n - 1 ? 1 : -1);
+  if (side < 0 || i < 0 || i >= g.n0) return kBadOff;
+  const int f = 2 * ra + side;
+  if (g.ffoff[f] < 0) return kBadOff;
+  return (uint32_t)(g.ffoff[f] + i + (int64_t)g.n0 * ((ra == 1) ? k : j)) * 8u;
+}
+
+// the single-reduction scalars of iteration it (alpha_{i-1}, beta_{i-1})
+struct CgsScal {
+  double a, b;
+  bool first;
+};
+
+// node update (see above); own = the node's p and x are updated too
+template <bool INIT>
+__device__ __forceinline__ void cgs_node(const CgsScal& k, double R, double S, double W, double D, double ff,
+                                         double& s, double& r, double& u) {
+  if (INIT) {
+    s = 0.0;
+    r = R;
+  } else {
+    const double wf = W + ff;
+    s = k.first ? wf : wf + k.b * S;
+    r = R - k.a * s;
+  }
+  u = D * r;
+}
+
+// Face workgroup of the single-reduction iteration: as face_block, with z_i
+// recomputed at the staged face nodes from (r, s, w + f, diag^-1) of the
+// previous iteration; writes f_i and the (0, z.f, 0) partial record.
+template <bool INIT, int R>
+__device__ void face_block_cgs(const CgGrid& g, const CgsBuffers& v, const CgsScal& ks, int raxis,
+                               double* __restrict__ partials, int fb, const FaceOff& fo, double* sm,
+                               double (*red)[R]) {
+  double (*sT)[kWave] = reinterpret_cast<double (*)[kWave]>(sm);
+  double (*sP)[kWave] = reinterpret_cast<double (*)[kWave]>(sm + (R + 1) * kWave);
+  double (*sCD)[R][kWave] = reinterpret_cast<double (*)[R][kWave]>(sm + 2 * (R + 1) * kWave);
+  int f = 0;
+  while (f < 5 && fb >= fo.off[f + 1]) ++f;
+  const int a = f >> 1, side = f & 1;
+  const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
+  const int n[3] = {g.n0, g.n1, g.n2};
+  const int n1 = n[t1], n2 = n[t2];
+  const int nseg1 = (n1 + kSeg - 1) / kSeg;
+  const int tile = fb - fo.off[f];
+  const int seg = tile % nseg1, tb = tile / nseg1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c1 = seg * kSeg - 1 + lane;
+  const int r0 = tb * (R - 1);
+  const bool ok1 = c1 >= 0 && c1 < n1;
+  // T and z_i of one staged node; z_i from the previous iteration's r, s,
+  // w + facet terms (x face, then row face: the order of the march's loads)
+  auto stage = [&](int row, int cc2) {
+    const bool ok = ok1 && cc2 >= 0 && cc2 < n2;
+    int c[3];
+    c[t1] = ok ? c1 : 0;
+    c[t2] = ok ? cc2 : 0;
+    c[a] = side ? n[a] - 1 : 0;
+    const int64_t o = c[0] + (int64_t)g.n0 * c[1] + (int64_t)g.n0 * g.n1 * c[2];
+    const double tt = v.T[o], R_ = v.rin[o], D = v.dinv[o];
+    double S = 0.0, W = 0.0, ff = 0.0;
+    if (!INIT) {
+      S = ks.first ? 0.0 : v.sin[o];
+      W = v.win[o];
+      const uint32_t ox = ff_off_x(g, c[0], c[1], c[2]);
+      const uint32_t orr = ff_off_r(g, raxis, c[0], c[1], c[2]);
+      const double fx = (ox != kBadOff) ? v.fin[ox / 8u] : 0.0;
+      const double fr = (orr != kBadOff) ? v.fin[orr / 8u] : 0.0;
+      ff = fx + fr;
+    }
+    double s, r, u;
+    cgs_node<INIT>(ks, R_, S, W, D, ff, s, r, u);
+    sT[row][lane] = ok ? tt : 0.0;
+    sP[row][lane] = ok ? u : 0.0;
+  };
+  const int fr = r0 - 1 + wave;
+  const bool facet_ok = c1 >= 0 && c1 < n1 - 1 && fr >= 0 && fr < n2 - 1;
+  const double h1 = g.coef[t1][(int64_t)(facet_ok ? c1 : 0) * C_NCOEF + C_HHI];
+  const double h2 = g.coef[t2][(int64_t)(facet_ok ? fr : 0) * C_NCOEF + C_HHI];
+  stage(wave, r0 - 1 + wave);
+  if (wave == R - 1) stage(R, r0 + R - 1);
+  __syncthreads();
+  const double Pa = sP[wave][lane];
+  double ya, yb, yc, yd;
+  facet_corners(g, facet_ok, h1, h2, sT[wave][lane], sT[wave + 1][lane], Pa, sP[wave + 1][lane], ya, yb, yc, yd);
+  sCD[0][wave][lane] = yc;
+  sCD[1][wave][lane] = yd;
+  const double ybl = shr1(yb);
+  __syncthreads();
+  double dot = 0.0;
+  const int c2 = r0 - 1 + wave;
+  const bool wr = wave >= 1 && ok1 && lane >= 1 && lane <= kSeg && c2 < n2;
+  if (wr) {
+    const double acc = (ya + ybl) + (sCD[0][wave - 1][lane] + sCD[1][wave - 1][lane - 1]);
+    int c[3];
+    c[t1] = c1;
+    c[t2] = c2;
+    c[a] = side ? n[a] - 1 : 0;
+    const bool owned = c[2] >= g.k_begin && c[2] < g.k_end;
+    v.fout[g.ffoff[f] + c1 + (int64_t)n1 * c2] = owned ? acc : 0.0;
+    dot = owned ? Pa * acc : 0.0;
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) red[1][wave] = dot;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s2 = 0.0;
+#pragma unroll
+    for (int w = 0; w < R; ++w) s2 += red[1][w];
+    store_partial(&partials[(int64_t)blockIdx.x * 3 + 0], 0.0);
+    store_partial(&partials[(int64_t)blockIdx.x * 3 + 1], s2);
+    store_partial(&partials[(int64_t)blockIdx.x * 3 + 2], 0.0);
+  }
+}
+
+template <bool INIT, int R, int PF>
+__global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v, PcgState* __restrict__ st,
+                                                         double* __restrict__ partials, int nseg, int raxis,
+                                                         int qchunk, RedTail rt, int nrec, int nmarch, FaceOff fo,
+                                                         int it_host, const double* __restrict__ lag_sums) {
+  stamp_start(rt);
+  __shared__ double lds[2][R + 2][kWave];  // double-buffered plane slab of z
+  __shared__ double red[3][R];
+  constexpr int kFaceLds = (8 * R + 8) * kWave;
+  __shared__ double fsm[kFaceLds];
+  __shared__ PcgState sst;  // lagged mode: this launch's view of the state
+  // ---- scalars: alpha_{i-1}, beta_{i-1} ----------------------------------------
+  CgsScal ks{0.0, 0.0, it_host == 1};
+  if (lag_sums != nullptr) {
+    // multi-rank: the state after the previous iteration is formed here from
+    // the all-reduced sums (identically in every workgroup); committed by WG 0
+    // when it ends the solve, else by this launch's tail
+    if (threadIdx.x == 0) {
+      sst = *st;
+      apply_logic(&sst, lag_sums, it_host == 1 ? 4 : 5);
+    }
+    __syncthreads();
+    if (sst.done) {
+      if (blockIdx.x == 0 && threadIdx.x == 0 && !st->done) *st = sst;
+      return;
+    }
+    ks.a = sst.a;
+    ks.b = sst.beta;
+  } else if (!INIT) {
+    if (st->done) return;  // converged: every launch queued behind exits here
+    ks.a = st->a;
+    ks.b = st->beta;
+  }
+  const int nface = (int)gridDim.x - nmarch;
+  if ((int)blockIdx.x >= nmarch && nface > 0) {
+    face_block_cgs<INIT, R>(g, v, ks, raxis, partials, (int)blockIdx.x - nmarch, fo, fsm, red);
+    cgs_tail(rt, nrec, st, lag_sums != nullptr ? &sst : nullptr);
+    return;
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n0 = g.n0;
+  const int nR = (raxis == 1) ? g.n1 : g.n2;
+  const int nQ = (raxis == 1) ? g.n2 : g.n1;
+  const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
+  const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
+  const int qaxis = 3 - raxis;
+  const int nch = (nQ + qchunk - 1) / qchunk;
+  const int b = xcd_remap((int)blockIdx.x, nmarch);
+  const int chunk = b % nch;
+  const int t = b / nch;
+  const int seg = t % nseg;
+  const int rb = t / nseg;
+  const int r0 = rb * R;
+  const int r = r0 + wave;
+  const bool row_ok = r < nR;
+  const int q0 = chunk * qchunk;
+  const int q1 = min(q0 + qchunk, nQ);
+  const int i = seg * kSeg - 1 + lane;
+  const bool col_ok = (i >= 0) && (i < n0);
+  const bool writer = col_ok && lane >= 1 && lane <= kSeg;
+  const int kb = g.k_begin, ke = g.k_end;
+  const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
+
+  const bool fq0 = q0 == 0 && g.bnd[qaxis][0];
+  const bool fq1 = q1 == nQ && g.bnd[qaxis][1];
+  double (*sFq)[2][R + 2][kWave] = reinterpret_cast<double (*)[2][R + 2][kWave]>(fsm);
+  double (*sCD)[2][R][kWave] = reinterpret_cast<double (*)[2][R][kWave]>(fsm + 4 * (R + 2) * kWave);
+  double yq0 = 0.0, yq1 = 0.0;
+  const double hq_own = uniform(g.coef[raxis][(int64_t)(row_ok ? r : 0) * C_NCOEF + C_HHI]);
+  const double hq_low = uniform(g.coef[raxis][(int64_t)(r0 >= 1 ? r0 - 1 : 0) * C_NCOEF + C_HHI]);
+  const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
+  const double My0 = uniform(cr[C_MLO]), My1 = uniform(cr[C_MDI]), My2 = uniform(cr[C_MUP]);
+  const double Ky0 = uniform(cr[C_KLO]), Ky1 = uniform(cr[C_KDI]), Ky2 = uniform(cr[C_KUP]);
+  const double da = g.dt_alpha;
+
+  // ---- buffer descriptors (out-of-range offsets read 0 / drop the store) -----
+  const uint32_t nbytes = (uint32_t)g.n0 * (uint32_t)g.n1 * (uint32_t)g.n2 * 8u;
+  const buf_t rsR = mk_rsrc(v.rin, nbytes);
+  const buf_t rsD = mk_rsrc(v.dinv, nbytes);
+  const buf_t rsS = mk_rsrc(v.sin, (INIT || ks.first) ? 0u : nbytes);
+  const buf_t rsW = mk_rsrc(v.win, INIT ? 0u : nbytes);
+  const buf_t rsF = mk_rsrc(v.fin, INIT ? 0u : (uint32_t)g.ffsize * 8u);
+  const buf_t rsP = mk_rsrc(v.p, (INIT || ks.first) ? 0u : nbytes);
+  const buf_t rsX = mk_rsrc(v.x, (INIT || ks.first) ? 0u : nbytes);
+  const buf_t wsR = mk_rsrc(v.rout, INIT ? 0u : nbytes);
+  const buf_t wsS = mk_rsrc(v.sout, INIT ? 0u : nbytes);
+  const buf_t wsP = mk_rsrc(v.p, INIT ? 0u : nbytes);
+  const buf_t wsX = mk_rsrc(v.x, nbytes);  // INIT: x = 0
+  const buf_t wsW = mk_rsrc(v.wout, nbytes);
+  const buf_t rsT = mk_rsrc(v.T, (fq0 || fq1) ? nbytes : 0u);
+  const bool halo = (wave == 0) || (wave == R - 1);
+  const int hrow = (wave == 0) ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
+  const int hslot = (wave == 0) ? 0 : R + 1;
+  auto lane_off = [&](int rr) -> uint32_t {
+    return (col_ok && rr >= 0 && rr < nR) ? (uint32_t)(i + sR * rr) * 8u : kBadOff;
+  };
+  const uint32_t vo_own = lane_off(r), vo_halo = halo ? lane_off(hrow) : kBadOff;
+  const uint32_t vo_wr = writer ? vo_own : kBadOff;
+  auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? (uint32_t)(sQ * L) * 8u : kBadOff; };
+  // facet terms of the face-workgroup faces at (i, row rr, plane L): x face,
+  // then the face normal to the row axis (base offsets per row, per lane)
+  auto xf_base = [&](int rr) -> int64_t {
+    if (!col_ok || rr < 0 || rr >= nR) return -1;
+    const int f = (i == 0) ? 0 : (i == n0 - 1 ? 1 : -1);
+    return (f < 0) ? -1 : g.ffoff[f];
+  };
+  auto rf_base = [&](int rr) -> int64_t {
+    if (!col_ok) return -1;
+    const int f = (rr == 0) ? 2 * raxis : (rr == nR - 1 ? 2 * raxis + 1 : -1);
+    return (f < 0) ? -1 : g.ffoff[f];
+  };
+  const int64_t xb_own = xf_base(r), rb_own = rf_base(r);
+  const int64_t xb_hal = halo ? xf_base(hrow) : -1, rb_hal = halo ? rf_base(hrow) : -1;
+  auto ff_offs = [&](int64_t xb, int64_t rbse, int rr, int L, uint32_t& ox, uint32_t& orr) {
+    const bool okL = L >= 0 && L < nQ;
+    const int64_t ix = (raxis == 2) ? ((int64_t)L + (int64_t)g.n1 * rr) : ((int64_t)rr + (int64_t)g.n1 * L);
+    ox = (xb >= 0 && okL) ? (uint32_t)(xb + ix) * 8u : kBadOff;
+    orr = (rbse >= 0 && okL) ? (uint32_t)(rbse + i + (int64_t)n0 * L) * 8u : kBadOff;
+  };
+
+  // raw loads of one (row, plane): r, s, w, diag^-1, facet terms (x, row)
+  struct Raw { double Rv, Sv, Wv, Dv, FX, FR, Pv, Xv; };
+  auto fetch = [&](uint32_t vo, int64_t xb, int64_t rbse, int rr, int L, Raw& a, bool own) {
+    const uint32_t o = vo + plane_off(L);
+    a.Rv = bload(rsR, o);
+    a.Dv = bload(rsD, o);
+    a.Pv = a.Xv = 0.0;
+    if (!INIT && own) {
+      a.Pv = bload(rsP, o);
+      a.Xv = bload(rsX, o);
+    }
+    if (!INIT) {
+      a.Sv = bload(rsS, o);
+      a.Wv = bload(rsW, o);
+      uint32_t ox, orr;
+      ff_offs(xb, rbse, rr, L, ox, orr);
+      a.FX = bload(rsF, ox);
+      a.FR = bload(rsF, orr);
+    } else {
+      a.Sv = a.Wv = a.FX = a.FR = 0.0;
+    }
+  };
+  Raw ra[PF + 1], rh[PF + 1] = {};
+#pragma unroll
+  for (int sI = 0; sI < PF; ++sI) {
+    fetch(vo_own, xb_own, rb_own, r, q0 - 1 + sI, ra[sI], true);
+    if (halo) fetch(vo_halo, xb_hal, rb_hal, hrow, q0 - 1 + sI, rh[sI], false);
+  }
+  // face planes normal to the march axis: T and z of the own and halo rows
+  double fT[2][2], fU[2][2];
+  if (fq0 || fq1) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int Lf = f == 0 ? (fq0 ? 0 : -1) : (fq1 ? nQ - 1 : -1);
+      const uint32_t po = plane_off(Lf);
+      fT[f][0] = bload(rsT, vo_own + po);
+      fT[f][1] = bload(rsT, vo_halo + po);
+      Raw a0, a1;
+      fetch(vo_own, xb_own, rb_own, r, Lf, a0, false);
+      fetch(vo_halo, xb_hal, rb_hal, hrow, Lf, a1, false);
+      double s_, r_;
+      cgs_node<INIT>(ks, a0.Rv, a0.Sv, a0.Wv, a0.Dv, a0.FX + a0.FR, s_, r_, fU[f][0]);
+      cgs_node<INIT>(ks, a1.Rv, a1.Sv, a1.Wv, a1.Dv, a1.FX + a1.FR, s_, r_, fU[f][1]);
+    }
+  }
+  // march-axis coefficients of the chunk and x coefficients (as k_cg_march)
+  __shared__ double2 cql[kFaceChunk + 2][5];
+  __shared__ double2 cxl[4][kWave];
+  const int nqs = q1 - q0 + 2;
+  const bool st_q = (int)threadIdx.x < nqs * 6;
+  const bool st_x = (int)threadIdx.x < 8 * kWave;
+  double cqv, cxv;
+  {
+    const int e = threadIdx.x;
+    const int qq = q0 - 1 + e / 6;
+    const bool okq = st_q && qq >= 0 && qq < nQ;
+    cqv = g.coef[qaxis][okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
+    cqv = okq ? cqv : 0.0;
+    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
+    const bool okx = st_x && ii >= 0 && ii < n0;
+    const int k = e >> 6;
+    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
+    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
+    cxv = (okx && k < 7) ? cxv : 0.0;
+  }
+  if (st_q) {
+    const int qs = threadIdx.x / 6, c = threadIdx.x % 6;
+    double* row = reinterpret_cast<double*>(cql[qs]);
+    if (c < 3) {
+      row[c] = cqv;
+      row[6 + c] = da * cqv;
+    } else {
+      row[c] = da * cqv;
+    }
+    if (c == 0) row[9] = 0.0;
+  }
+  if (st_x) reinterpret_cast<double*>(cxl[(threadIdx.x >> 6) >> 1])[2 * (threadIdx.x & (kWave - 1)) + ((threadIdx.x >> 6) & 1)] = cxv;
+  if (fq0 || fq1) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      sFq[f][0][wave + 1][lane] = fT[f][0];
+      sFq[f][1][wave + 1][lane] = fU[f][0];
+      if (halo) {
+        sFq[f][0][hslot][lane] = fT[f][1];
+        sFq[f][1][hslot][lane] = fU[f][1];
+      }
+    }
+  }
+  __syncthreads();
+  if (fq0 || fq1) {
+    const bool cok = i >= 0 && i < n0 - 1;
+    const double h1 = cxl[3][lane].x;
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      if (!(f == 0 ? fq0 : fq1)) continue;
+      double ya, yb, yc, yd;
+      facet_corners(g, cok && r < nR - 1, h1, hq_own, sFq[f][0][wave + 1][lane], sFq[f][0][wave + 2][lane],
+                    sFq[f][1][wave + 1][lane], sFq[f][1][wave + 2][lane], ya, yb, yc, yd);
+      double yq = ya + shr1(yb);
+      sCD[f][0][wave][lane] = yc;
+      sCD[f][1][wave][lane] = yd;
+      if (wave == 0) {
+        facet_corners(g, cok && r0 >= 1 && r0 - 1 < nR - 1, h1, hq_low, sFq[f][0][0][lane], sFq[f][0][1][lane],
+                      sFq[f][1][0][lane], sFq[f][1][1][lane], ya, yb, yc, yd);
+        yq += yc + shr1(yd);
+      }
+      if (f == 0) yq0 = yq; else yq1 = yq;
+    }
+    __syncthreads();
+    if (wave >= 1) {
+      const int lm = lane >= 1 ? lane - 1 : 0;
+      yq0 += sCD[0][0][wave - 1][lane] + sCD[0][1][wave - 1][lm];
+      yq1 += sCD[1][0][wave - 1][lane] + sCD[1][1][wave - 1][lm];
+    }
+  }
+
+  // ---- the march ----------------------------------------------------------------
+  double us_m = 0.0, us_c = 0.0, t_m = 0.0, t_c = 0.0;
+  double uc = 0.0, rc = 0.0;  // z_i and r_i of the centre plane (output node)
+  double dg = 0.0, dd = 0.0, dn = 0.0;  // partial (r, z), (z, w), (z, z)
+  auto step = [&](int L, const Raw& a, const Raw& h) {
+    const int buf = L & 1;
+    const bool qin = (L >= q0 && L < q1);
+    const uint32_t po = qin ? plane_off(L) : kBadOff;
+    double s, rr, u;
+    cgs_node<INIT>(ks, a.Rv, a.Sv, a.Wv, a.Dv, a.FX + a.FR, s, rr, u);
+    // own row: r, s (every local node incl. ghost planes), p, x (owned nodes)
+    const bool own_n = row_owned && ((raxis == 2) ? true : (L >= kb && L < ke));
+    if (!INIT) {
+      bstore(wsR, vo_wr + po, rr);
+      bstore(wsS, vo_wr + po, s);
+    }
+    {
+      const uint32_t o = vo_wr + (own_n ? po : kBadOff);
+      if (INIT) {
+        bstore(wsX, o, 0.0);
+      } else {
+        const double uo = a.Dv * a.Rv;  // z_{i-1}
+        const double Pv = ks.first ? uo : uo + ks.b * a.Pv;
+        const double Xv = ks.first ? ks.a * Pv : a.Xv + ks.a * Pv;
+        bstore(wsP, o, Pv);
+        bstore(wsX, o, Xv);
+      }
+    }
+    lds[buf][wave + 1][lane] = u;
+    if (halo) {
+      double hs, hr, hu;
+      cgs_node<INIT>(ks, h.Rv, h.Sv, h.Wv, h.Dv, h.FX + h.FR, hs, hr, hu);
+      lds[buf][hslot][lane] = hu;
+    }
+    __syncthreads();
+    const double x0 = lds[buf][wave][lane], x1 = u, x2 = lds[buf][wave + 2][lane];
+    const double us_p = My0 * x0 + My1 * x1 + My2 * x2;
+    const double vs_p = Ky0 * x0 + Ky1 * x1 + Ky2 * x2;
+    const double t_p = us_p + da * vs_p;
+    if (L >= q0 + 1 && L <= q1) {
+      const int q = L - 1;
+      const double2* cq = cql[q - q0 + 1];
+      const double2 c01 = cq[0], c23 = cq[1], c45 = cq[2], c67 = cq[3], c89 = cq[4];
+      const double S1 = c01.x * t_m + c01.y * t_c + c23.x * t_p + (c23.y * us_m + c45.x * us_c + c45.y * us_p);
+      const double S2 = c67.x * us_m + c67.y * us_c + c89.x * us_p;
+      const double2 xlo = cxl[0][lane], xdi = cxl[1][lane], xup = cxl[2][lane];
+      const double Lt = xup.x * S1 + xup.y * S2;
+      const double Rt = xlo.x * S1 + xlo.y * S2;
+      const double y = (xdi.x * S1 + xdi.y * S2) + (shr1(Lt) + shl1(Rt));
+      const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
+      const bool wr = writer && row_ok && row_owned && q_owned;
+      double yb = y;
+      if (fq0 && q == 0) yb += yq0;
+      if (fq1 && q == nQ - 1) yb += yq1;
+      bstore(wsW, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, yb);
+      if (wr) {
+        dg += rc * uc;
+        dd += uc * yb;
+        dn += uc * uc;
+      }
+    }
+    uc = u;
+    rc = rr;
+    us_m = us_c; us_c = us_p;
+    t_m = t_c; t_c = t_p;
+  };
+  for (int L = q0 - 1; L <= q1; L += PF + 1) {
+#pragma unroll
+    for (int sI = 0; sI <= PF; ++sI) {
+      const int sf = (sI + PF) % (PF + 1);
+      fetch(vo_own, xb_own, rb_own, r, L + sI + PF, ra[sf], true);
+      if (halo) fetch(vo_halo, xb_hal, rb_hal, hrow, L + sI + PF, rh[sf], false);  // waves 0 and R-1 only
+      step(L + sI, ra[sI], rh[sI]);
+    }
+  }
+  // ---- partial record (r.z, z.w, z.z) + tail ------------------------------------
+  dg = wave_sum(dg);
+  dd = wave_sum(dd);
+  dn = wave_sum(dn);
+  if (lane == 0) {
+    red[0][wave] = dg;
+    red[1][wave] = dd;
+    red[2][wave] = dn;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w3 = 0; w3 < 3; ++w3) {
+      double s3 = 0.0;
+#pragma unroll
+      for (int w = 0; w < R; ++w) s3 += red[w3][w];
+      store_partial(&partials[(int64_t)blockIdx.x * 3 + w3], s3);
+    }
+  }
+  cgs_tail(rt, nrec, st, lag_sums != nullptr ? &sst : nullptr);
+}
+
 // Robin facet terms of the owned boundary nodes (list built at context
 // creation), added after the marching kernel: out[n] += dt * sum_f int_f ...,
 // and the matching p.w correction for the PCG dot product.  For the fused PCG
@@ -1550,6 +2038,30 @@ bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, d
   if (n_partials) *n_partials = plan(g, true).nparts;
   return fused;
 }
+
+bool launch_cg_cgs(const CgGrid& g, bool init, const CgsBuffers& v, PcgState* st, double* partials,
+                   hipStream_t s, const RedTail* tail, int it_host, const double* lag_sums) {
+  if (!use_march(g)) return false;
+  const Launch L = plan(g, true);
+  const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
+  const int grid = L.blocks + fo.off[6];
+  RedTail rt{};
+  if (tail) rt = *tail;
+  if (init)
+    hipLaunchKernelGGL((k_cgs_march<true, 8, 1>), dim3(grid), dim3(8 * kWave), 0, s, g, v, st, partials, L.nseg,
+                       L.raxis, L.qchunk, rt, grid, L.blocks, fo, it_host, lag_sums);
+  else
+    hipLaunchKernelGGL((k_cgs_march<false, 8, 1>), dim3(grid), dim3(8 * kWave), 0, s, g, v, st, partials, L.nseg,
+                       L.raxis, L.qchunk, rt, grid, L.blocks, fo, it_host, lag_sums);
+  return true;
+}
+
+int cg_cgs_records(const CgGrid& g) {
+  const Launch L = plan(g, true);
+  return L.blocks + face_offsets(g, L.rows, 3 - L.raxis).off[6];
+}
+
+bool cg_cgs_supported(const CgGrid& g) { return use_march(g); }
 
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {
   const int64_t nown = (int64_t)g.n0 * g.n1 * (g.k_end - g.k_begin);

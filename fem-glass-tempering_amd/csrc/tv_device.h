@@ -62,26 +62,29 @@ __device__ __forceinline__ bool last_block_arrived(unsigned* counter, unsigned n
   return amlast != 0;
 }
 
-// Fixed-order reduction of n records of width W (<= 2) by one workgroup; the
-// result is in sums[] of thread 0.
+// Fixed-order reduction of the records first, first + stride, ... (< n) of
+// width W (<= 3) by one workgroup; the result is in sums[] of thread 0.
 template <int W>
-__device__ __forceinline__ void block_reduce_records(const double* partials, int n, double (&sums)[2]) {
-  __shared__ double red[W][16];
+__device__ __forceinline__ void block_reduce_records(const double* partials, int first, int stride, int n,
+                                                     double (&sums)[3]) {
+  __shared__ double red[3][16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) acc[w] = 0.0;
   // U records per thread in flight at once (the loads are independent; a
-  // one-record loop would serialise n / blockDim HBM latencies), summed in a
+  // one-record loop would serialise n / blockDim latencies), summed in a
   // fixed order so the result stays bitwise reproducible.
   constexpr int U = 8;
-  for (int base = threadIdx.x; base < n; base += blockDim.x * U) {
+  const int cnt = (n > first) ? (n - first + stride - 1) / stride : 0;
+  for (int base = threadIdx.x; base < cnt; base += blockDim.x * U) {
     double v[U][W];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = base + u * (int)blockDim.x;
+      const int k = base + u * (int)blockDim.x;
+      const int64_t t = (int64_t)first + (int64_t)k * stride;
 #pragma unroll
-      for (int w = 0; w < W; ++w) v[u][w] = (t < n) ? load_partial(&partials[(int64_t)t * W + w]) : 0.0;
+      for (int w = 0; w < W; ++w) v[u][w] = (k < cnt) ? load_partial(&partials[t * W + w]) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -151,23 +154,100 @@ __device__ __forceinline__ void logic_update(PcgState* st, const double* sums) {
   st->beta = beta;
 }
 
+// ---- the same logic for the single-reduction form (k_cgs_march) -------------
+// sums = (gamma_i, delta_i, nu_i) = ((r_i, z_i), (z_i, J z_i), (z_i, z_i)).
+// Iteration 0: PETSc's first pass up to alpha (dp test on ||z_0||, beta =
+// (z, r) == 0 test, dpi = (p, A p) with p = z_0: delta_0).
+__device__ __forceinline__ void logic_cgs_init(PcgState* st, const double* s) {
+  const double dp = sqrt(s[2]);
+  st->dp = dp;
+  st->rnorm0 = dp;
+  st->ttol = fmax(st->rtol * dp, st->atol);
+  st->it = 0;
+  st->done = 0;
+  st->reason = R_RUNNING;
+  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
+  const double gamma = s[0];
+  if (gamma == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
+  const double dpi = s[1];
+  if (!isfinite(dpi)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dpi == 0.0) { st->done = 1; st->reason = R_DIV_INDEF_MAT; return; }
+  st->gamma = gamma;
+  st->eta = dpi;
+  st->beta = 0.0;
+  st->a = gamma / dpi;
+}
+
+// Iteration i >= 1: the tests of logic_update on ||z_i|| and gamma_i, then
+// beta_i = gamma_i / gamma_{i-1}, PETSc's dpi as eta_i = delta_i - beta_i
+// gamma_i / alpha_{i-1} (= (p_i, A p_i) in exact arithmetic) with the tests of
+// logic_dpi, alpha_i = gamma_i / eta_i.
+__device__ __forceinline__ void logic_cgs(PcgState* st, const double* s) {
+  if (st->done) return;
+  const double dp = sqrt(s[2]);
+  st->it += 1;
+  st->dp = dp;
+  if (!isfinite(dp)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (dp <= st->ttol) { st->done = 1; st->reason = (dp <= st->atol) ? R_CONV_ATOL : R_CONV_RTOL; return; }
+  if (dp >= st->dtol * st->rnorm0) { st->done = 1; st->reason = R_DIV_DTOL; return; }
+  if (st->it >= st->max_it) { st->done = 1; st->reason = R_DIV_ITS; return; }
+  const double gamma = s[0];
+  if (gamma == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
+  if (gamma * st->gamma < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
+  const double beta = gamma / st->gamma;
+  const double eta = s[1] - beta * gamma / st->a;
+  if (!isfinite(eta)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
+  if (eta == 0.0 || ((eta > 0.0) != (st->eta > 0.0))) { st->done = 1; st->reason = R_DIV_INDEF_MAT; return; }
+  st->beta = beta;
+  st->gamma = gamma;
+  st->eta = eta;
+  st->a = gamma / eta;
+}
+
 __device__ __forceinline__ void apply_logic(PcgState* st, const double* sums, int kind) {
   if (kind == 1) logic_init(st, sums);
   else if (kind == 2) logic_dpi(st, sums);
   else if (kind == 3) logic_update(st, sums);
+  else if (kind == 4) logic_cgs_init(st, sums);
+  else if (kind == 5) logic_cgs(st, sums);
 }
 
-// Tail of a kernel that produced per-workgroup partial records: the last
-// workgroup reduces all `n` records into `out` and (kind > 0) runs the PCG logic.
+// Tail of a kernel that produced one partial record (width W) per workgroup:
+// the last workgroup to arrive reduces all n records in a fixed order into
+// rt.out and (kind > 0) runs the PCG logic on the sums.  Measured alternative,
+// not kept: a two-level tail with 8 shard counters (blockIdx % 8) and a top
+// counter, against the ~12 ns per arrival that serialise on one counter
+// (MI355X_MICROARCH.md price list "fanin"): 1-2 us SLOWER per launch at 0.1M,
+// 1M and 8M nodes (the arrivals are spread out by the march's own skew; the
+// extra hop is not).  Counters: rt.counter[0].
 template <int W>
 __device__ __forceinline__ void fused_reduce_tail(const RedTail& rt, int n) {
   if (rt.counter == nullptr) return;
   if (!last_block_arrived(rt.counter, gridDim.x)) return;
-  double sums[2] = {0.0, 0.0};
-  block_reduce_records<W>(rt.partials, n, sums);
+  double sums[3] = {0.0, 0.0, 0.0};
+  block_reduce_records<W>(rt.partials, 0, 1, n, sums);
   if (threadIdx.x == 0) {
     for (int w = 0; w < W; ++w) rt.out[w] = sums[w];
     apply_logic(rt.st, sums, rt.kind);
+    if (rt.ts) rt.ts[1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// Tail of the single-reduction iteration (records of width 3).  lag != nullptr
+// (multi-rank, lagged logic): the sums are only reduced (RCCL all-reduces them
+// next) and the tail workgroup commits the state this launch formed from the
+// previous sums -- every workgroup has read the old state by the time the last
+// one arrives.
+__device__ __forceinline__ void cgs_tail(const RedTail& rt, int n, PcgState* st, const PcgState* lag) {
+  if (rt.counter == nullptr) return;
+  if (!last_block_arrived(rt.counter, gridDim.x)) return;
+  double sums[3] = {0.0, 0.0, 0.0};
+  block_reduce_records<3>(rt.partials, 0, 1, n, sums);
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < 3; ++w) rt.out[w] = sums[w];
+    if (lag) *st = *lag;
+    else apply_logic(rt.st, sums, rt.kind);
     if (rt.ts) rt.ts[1] = __builtin_amdgcn_s_memrealtime();
   }
 }

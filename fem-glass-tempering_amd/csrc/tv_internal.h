@@ -48,6 +48,13 @@ struct CgGrid {
   // axes t1 < t2), rewritten by k_cg_faces before every Jacobian application
   double* fface[6];
   int fn1[6], fn2[6];
+  // the six face arrays are one contiguous buffer per parity (ffbuf[0] holds
+  // fface[] above; ffbuf[1] is the second set of the single-reduction PCG,
+  // which reads one set while it writes the other); ffoff[f] = offset of face
+  // f in doubles, -1 where face f is not a physical boundary of this partition
+  double* ffbuf[2];
+  int64_t ffoff[6];
+  int64_t ffsize;
 };
 
 // Grid of the DG1 temperature space: cells per storage axis; dof layout is
@@ -69,6 +76,13 @@ struct DgGrid {
   int tile, tile_chunk;
 };
 
+// two-level in-kernel reduction tails (tv_device.h fused_reduce_tail): kShards
+// shard counters + 1 top counter per tail; two tails per context (matvec,
+// update), rounded up
+constexpr int kShards = 8;
+constexpr int kTailCounters = kShards + 1;
+constexpr int kCounterWords = 32;
+
 // Device-resident scalars of one PCG solve (PETSc KSPCG restated, preconditioned norm).
 struct PcgState {
   double beta, betaold, dpi, dpiold, a, dp, rnorm0, ttol;
@@ -76,7 +90,9 @@ struct PcgState {
   int it, done, reason, max_it;
   double dx_norm2;            // ||dx||^2 of the last Newton update
   double a_prev;              // step length of the previous iteration (dx is updated every 2nd)
-  double pad[2];
+  // single-reduction form (k_cgs_march): gamma = (r, z) and eta = (p, A p) of
+  // the last iteration (PETSc's beta and dpi); a, beta as above
+  double gamma, eta;
 };
 
 // In-kernel reduction tail (last-arriving workgroup reduces the partial records
@@ -86,7 +102,7 @@ struct RedTail {
   const double* partials;
   double* out;                // reduced sums (read by RCCL allreduce on multi-GPU)
   PcgState* st;
-  int kind;                   // 0 none, 1 init, 2 p.w, 3 update
+  int kind;                   // 0 none, 1 init, 2 p.w, 3 update, 4 / 5 single-reduction init / iteration
   // in-solve kernel timing (tv_kernel_timing), or nullptr: ts[0] = REALTIME
   // clock when workgroup 0 starts, ts[1] = when the tail workgroup finishes
   uint64_t* ts;
@@ -134,6 +150,33 @@ void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double*
 bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
                             hipStream_t s, const RedTail* tail = nullptr, int it_host = 0);
+// Vectors of the single-reduction PCG iteration (k_cgs_march, tv_cg.hip); the
+// in / out pairs are the two parities of ping-pong buffers.
+struct CgsBuffers {
+  const double* T;     // temperature (facet terms)
+  const double* rin;   // r_{i-1} (i = 1: the Newton residual F; INIT: r_0 = F)
+  double* rout;        // r_i
+  const double* sin;   // s_{i-2}
+  double* sout;        // s_{i-1}
+  const double* win;   // w_{i-1} without the face-workgroup facet terms
+  double* wout;        // w_i (march part)
+  const double* fin;   // facet terms f_{i-1} (CgGrid::ffbuf layout)
+  double* fout;        // f_i
+  double* p;           // p (owned nodes, in place)
+  double* x;           // dx (owned nodes, in place)
+  const double* dinv;  // B = diag(J)^-1
+};
+
+// One single-reduction PCG iteration (Chronopoulos-Gear CG) fused with the
+// marching Jacobian, 3D CG1 path only (cg_cgs_supported): init = iteration 0
+// (z_0 = B r_0, w_0 = J z_0, x = 0); tail->kind 4 / 5 runs the logic in the
+// tail, or lag_sums != nullptr (multi-rank) makes every workgroup apply the
+// logic of the previous iteration's all-reduced sums first.  Records: width 3,
+// cg_cgs_records of them.
+bool launch_cg_cgs(const CgGrid& g, bool init, const CgsBuffers& v, PcgState* st, double* partials,
+                   hipStream_t s, const RedTail* tail, int it_host, const double* lag_sums);
+int cg_cgs_records(const CgGrid& g);
+bool cg_cgs_supported(const CgGrid& g);
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 

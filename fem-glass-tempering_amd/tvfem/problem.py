@@ -100,7 +100,7 @@ class ThermoViscoProblem:
     def __init__(self, mesh_path, time: tuple, dt: float, config: dict, model_parameters: dict,
                  jit_options: dict | None = None, *, device: int = 0, materialize: bool = True,
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
-                 verbose: bool = True) -> None:
+                 verbose: bool = True, pcg_variant: str = "auto") -> None:
         if isinstance(mesh_path, RectilinearMesh):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -121,7 +121,7 @@ class ThermoViscoProblem:
         self.last_newton_iterations = 0
         self.last_krylov_iterations = 0
         self.__init_function_spaces(config=config)
-        self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis)
+        self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
                                               functions_current=self.functions_current,
@@ -147,7 +147,7 @@ class ThermoViscoProblem:
             "sigma_partial": FunctionSpaceInfo(self, 1, config["sigma"]["element"], 1, 6 * d * d),
         }
 
-    def __init_native(self, mp, device, materialize, ksp_rtol, n_parts, part, part_axis):
+    def __init_native(self, mp, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant):
         lib = N.load_library()
         self._lib = lib
         desc = N.MeshDesc()
@@ -169,6 +169,8 @@ class ThermoViscoProblem:
         opts = N.default_options()
         opts.materialize = 1 if materialize else 0
         opts.ksp_rtol = ksp_rtol
+        opts.pcg_variant = {"auto": N.TV_PCG_AUTO, "kspcg": N.TV_PCG_KSPCG,
+                            "single": N.TV_PCG_SINGLE_REDUCTION}[pcg_variant]
         ctx = C.c_void_p()
         N.check(lib.tv_create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
         self._ctx = ctx
@@ -208,6 +210,14 @@ class ThermoViscoProblem:
         }
 
     # ---- host mirrors of device fields -------------------------------------------------
+    @property
+    def pcg_variant(self) -> str:
+        """Krylov form in use: "kspcg" (PETSc KSPSolve_CG as written, two
+        reductions per iteration) or "single" (Chronopoulos-Gear, one)."""
+        v = C.c_int()
+        N.check(self._lib.tv_pcg_variant(self._ctx, C.byref(v)), self._ctx)
+        return "single" if v.value == N.TV_PCG_SINGLE_REDUCTION else "kspcg"
+
     def num_dofs(self, space=0):
         n = C.c_int64()
         off = C.c_int64()

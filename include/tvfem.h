@@ -110,9 +110,21 @@ typedef struct {
   double ksp_rtol, ksp_atol, ksp_dtol;
   int ksp_max_it;
   int materialize;        /* 0: state fields only, 1: every reference field  */
-  int use_graphs;         /* capture PCG iteration batches in hipGraphs      */
+  int use_graphs;         /* reserved (no effect)                            */
   int pcg_batch;          /* iterations launched between convergence polls  */
+  int pcg_variant;        /* TV_PCG_AUTO / TV_PCG_KSPCG / TV_PCG_SINGLE_REDUCTION */
 } tv_options;
+
+/* Krylov iteration form (same Jacobi-PCG iterates in exact arithmetic):
+ *   KSPCG             PETSc KSPSolve_CG as written: two reductions per iteration
+ *                     (p.w, then z.z and z.r), a fused matvec and an update launch;
+ *   SINGLE_REDUCTION  Chronopoulos-Gear form: one launch and one reduction per
+ *                     iteration (3D CG1 temperature only);
+ *   AUTO              SINGLE_REDUCTION on partitioned 3D CG1 meshes (one
+ *                     communication round per iteration), else KSPCG. */
+#define TV_PCG_AUTO 0
+#define TV_PCG_KSPCG 1
+#define TV_PCG_SINGLE_REDUCTION 2
 
 /* field ids (the reference's Function objects) */
 enum {
@@ -222,6 +234,10 @@ int tv_kernel_timing(void* ctx, int on);
 int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches);
 /* counters of the last tv_step / tv_solve_T */
 int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm);
+/* the Krylov iteration form in use (TV_PCG_KSPCG or TV_PCG_SINGLE_REDUCTION);
+ * with SINGLE_REDUCTION, kernel id 3 of tv_time_kernel / tv_kernel_bytes /
+ * tv_kernel_stats is the fused single-reduction iteration and id 4 is unused */
+int tv_pcg_variant(void* ctx, int* variant);
 
 #ifdef __cplusplus
 }
