@@ -168,13 +168,23 @@ def main():
         rec["GBps"] = by.value / (rec["ms"] * 1e-3) / 1e9
         kern[name] = rec
 
+    # the plain J x behind the C-ABI (tv_jacobian_apply) with the Infinity Cache
+    # flushed before every launch: the HBM figure, next to
+    # the effective in-solve figure of the roofline kernel
+    fl_ms, fl_by = C.c_double(), C.c_double()
+    N.check(lib.tv_time_kernel(ctx, 10, max(3, a.kernel_reps // 2), C.byref(fl_ms)), ctx)
+    N.check(lib.tv_kernel_bytes(ctx, 10, C.byref(fl_by)), ctx)
+    flushed = {"kernel": "jacobian_apply (J(T) x, tv_jacobian_apply)", "bytes_per_launch": fl_by.value,
+               "ms_per_launch": fl_ms.value, "achieved": fl_by.value / (fl_ms.value * 1e-3) / 1e9,
+               "unit": "GB/s", "frac": fl_by.value / (fl_ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS,
+               "timing": "HBM (flushed): 512 MiB write before each launch, HIP events around the launch"}
     dom = kern[names[3]]
     # traffic: HBM bytes per launch of this kernel from the rocprofv3 --pmc passes
     # (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section) of this same
     # bench command, committed under profiles/ (counters cannot be read inside
     # the timed run); traffic_source names the file
     traffic, traffic_src = None, None
-    pmc_file = os.path.join(ROOT, "profiles", f"pmc_matvec_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
+    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{names[3]}_{a.family}_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
     if os.path.exists(pmc_file):
         with open(pmc_file) as fh:
             traffic = json.load(fh).get("hbm_bytes_per_launch")
@@ -184,7 +194,9 @@ def main():
                 "kernel": ("pcg_iteration_single_reduction (s, p, x, r, z updates; w <- J(T) z; (r,z), (z,w), (z,z))"
                            if single else "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)"),
                 "bytes_per_launch": dom["bytes"], "ms_per_launch": dom["ms"],
-                "timing": "in-solve" if dom["launches_timed"] else "isolated"}
+                "timing": ("effective (in-solve, Infinity-Cache assisted)" if dom["launches_timed"]
+                           else "isolated"),
+                "hbm_flushed": flushed}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -118,6 +118,8 @@ enum PcgReason {
 struct ViscoConst {
   double H_over_Rg, inv_Tb, dt, half_dt, alpha_s, dalpha, inv_dim;
   double lambda_m[6], m_n[6], lambda_g[6], g_n[6], lambda_k[6], k_n[6];
+  double chi;   // ViscoelasticModel.py:15 (Eq. 25, paper mode only)
+  int paper;    // model_mode: 0 reference semantics (quirks Q1-Q4 kept), 1 paper
 };
 
 // Pointers of the viscoelastic state (component-major, stride = n_local).
@@ -133,6 +135,7 @@ struct ViscoFields {
   double* st; double* sgt;                       // s_tilde, sigma_tilde (state)
   double* sp; double* sgp;                       // s, sigma partial (materialize=all)
   double* sigma;                                 // total stress (state)
+  double* Tfo;                                   // paper mode, mixed families: previous Tf per T dof (work)
   int copy_Tprev;             // fuse T_prev <- T (same family, single pass)
   // device word: 0 = s_tilde and sigma_tilde hold +0.0 at every dof (quirk Q3
   // keeps them there), so the update neither reads nor rewrites them; 1 = general

@@ -116,7 +116,8 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
     if (DXU) stc<NT2>(&dx[q], (v[3] + ap * v[4]) + a * v[5]);  // x <- (x + a_prev p_prev) + a p
     double wt = v[0];
     if (FACES) wt += face_terms(fa, q);  // w = J p incl. the Robin facet terms
-    const double rr = v[2] / v[1] - a * wt;  // r <- r - a w, r = B^-1 z
+    // r <- r - a w, r = B^-1 z; B = 0 on Dirichlet-constrained nodes (z stays 0)
+    const double rr = (v[1] != 0.0 ? v[2] / v[1] : 0.0) - a * wt;
     const double zz = v[1] * rr;             // z <- B r
     z[q] = zz;
     acc[0] += zz * zz;

@@ -45,40 +45,46 @@ __device__ __forceinline__ double taylor_E(double xi, double lam) {
 }
 
 struct TState {
-  double T, Tp, Tf, xi;
+  double T, Tp, Tf, Tfo, xi;  // Tfo: Tf of the previous step (paper mode's strain)
 };
 
 // T-family part: phi, Tf_partial, Tf, T_next, phi_next, xi at T-dof t.
-template <bool ALL>
+// PAPER (opt-in model_mode, never the default): Eq. 25 drives Eq. 24, the
+// thermal strain sees Tf - Tf_prev of the previous step, and xi takes the
+// trapezoidal "+" (the fixes of SURVEY.md A.3 Q1, Q2, Q4).
+template <bool ALL, bool PAPER>
 __device__ __forceinline__ TState t_part(const ViscoConst& c, const ViscoFields& f, int64_t t) {
   TState o;
   const double T = f.T[t];
   const double Tp = f.Tp[t];
+  const double Tfo = PAPER ? f.Tf[t] : 0.0;
   // Eq. 5 (VEM:156-161)
   const double phi = exp(c.H_over_Rg * (c.inv_Tb - 1.0 / T));
+  // Eq. 25 (VEM:100-108), overwritten by Eq. 5 in the reference (Q1)
+  const double phi_tf = PAPER ? exp(c.H_over_Rg * ((c.inv_Tb - c.chi / T) - (1.0 - c.chi) / Tfo)) : phi;
   // Eq. 24 (VEM:111-119), Tf_partial_prev -> Tf_partial (alias: TVP:469-470)
   double Tf = 0.0;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const double prev = f.Tfp[i * f.sT + t];
-    const double cur = (c.lambda_m[i] * prev + T * c.dt * phi) / (c.lambda_m[i] + c.dt * phi);
+    const double cur = (c.lambda_m[i] * prev + T * c.dt * phi_tf) / (c.lambda_m[i] + c.dt * phi_tf);
     f.Tfp[i * f.sT + t] = cur;
     Tf = Tf + c.m_n[i] * cur;  // Eq. 26 inner(m, Tf_partial) (VEM:122-125)
   }
-  f.Tf[t] = Tf;  // Tf_prev <- Tf (alias: TVP:481-482)
+  f.Tf[t] = Tf;  // Tf_prev <- Tf (alias: TVP:481-482; PAPER: the strain keeps Tfo)
   // extrapolation (VEM:150-153)
   const double Tn = T + (T - Tp);
   // phi again (identical, VEM:156) and phi_next (VEM:162-167)
   const double phin = exp(c.H_over_Rg * (c.inv_Tb - 1.0 / Tn));
-  // Eq. 19 with "-" (VEM:170-173)
-  const double xi = c.half_dt * (phin - phi);
+  // Eq. 19 with "-" (VEM:170-173, Q4), PAPER: "+"
+  const double xi = PAPER ? c.half_dt * (phin + phi) : c.half_dt * (phin - phi);
   f.phi[t] = phi;
   f.xi[t] = xi;
   if (ALL) {
     f.Tn[t] = Tn;
     f.phin[t] = phin;
   }
-  o.T = T; o.Tp = Tp; o.Tf = Tf; o.xi = xi;
+  o.T = T; o.Tp = Tp; o.Tf = Tf; o.Tfo = PAPER ? Tfo : Tf; o.xi = xi;
   return o;
 }
 
@@ -89,12 +95,15 @@ __device__ __forceinline__ TState t_part(const ViscoConst& c, const ViscoFields&
 // them is not +0.0 (E not finite, e.g. xi = NaN) -- a single rare branch per
 // dof -- which also raises `dirty` so the next launches read the fields
 // again.  Memory therefore always holds the exact values, in both modes.
-template <int D, bool ALL, bool LEAN>
+// PAPER: Eq. 16 feeds s~ / sigma~ from the previous s / sigma partial stresses
+// (Q3 fixed), which are then state fields (never LEAN).
+template <int D, bool ALL, bool LEAN, bool PAPER = false>
 __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f, int64_t s, const TState& ts,
                                        bool& dirty) {
   constexpr int DD = D * D;
+  static_assert(!(LEAN && PAPER), "paper mode carries s / sigma partial state");
   // Eq. 9 (VEM:128-133): I*(alpha_s (T - T_prev) + (alpha_l - alpha_s)(Tf - Tf_prev)), Tf_prev == Tf (Q2)
-  const double scal = c.alpha_s * (ts.T - ts.Tp) + c.dalpha * (ts.Tf - ts.Tf);
+  const double scal = c.alpha_s * (ts.T - ts.Tp) + c.dalpha * (ts.Tf - ts.Tfo);
   double tot[DD];
 #pragma unroll
   for (int i = 0; i < D; ++i)
@@ -134,14 +143,14 @@ __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f
       // Eq. 15a + 20 (VEM:176-182)
       const double ds = (((twog * dev[q]) / xi) * c.lambda_g[n]) * omEg;
       // Eq. 16a (VEM:195-200)
-      const double st = (LEAN ? 0.0 : f.st[o]) * Eg;
+      const double st = (LEAN ? 0.0 : (PAPER ? f.sp[o] : f.st[o])) * Eg;
       if (LEAN) tz |= (uint64_t)__double_as_longlong(st);
       // Eq. 17a (VEM:212-215)
       const double sp = ds + st;
       // Eq. 15b + 20 (VEM:185-191)
       const double dsg = (((c.k_n[n] * (tr * (i == j ? 1.0 : 0.0))) / xi) * c.lambda_k[n]) * omEk;
       // Eq. 16b (VEM:203-209)
-      const double sgt = (LEAN ? 0.0 : f.sgt[o]) * Ek;
+      const double sgt = (LEAN ? 0.0 : (PAPER ? f.sgp[o] : f.sgt[o])) * Ek;
       if (LEAN) tz |= (uint64_t)__double_as_longlong(sgt);
       // Eq. 17b (VEM:218-221)
       const double sgp = dsg + sgt;
@@ -152,6 +161,8 @@ __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f
       if (ALL) {
         f.ds[o] = ds;
         f.dsig[o] = dsg;
+      }
+      if (ALL || PAPER) {
         f.sp[o] = sp;
         f.sgp[o] = sgp;
       }
@@ -184,13 +195,13 @@ __device__ __forceinline__ void s_part(const ViscoConst& c, const ViscoFields& f
   }
 }
 
-template <int D, bool ALL, bool LEAN>
+template <int D, bool ALL, bool LEAN, bool PAPER = false>
 __device__ __forceinline__ void fused_loop(const ViscoConst& c, const ViscoFields& f) {
   bool dirty = false;
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
     const int64_t dT = f.off_T + t;
-    const TState ts = t_part<ALL>(c, f, dT);
-    s_part<D, ALL, LEAN>(c, f, f.off_S + t, ts, dirty);
+    const TState ts = t_part<ALL, PAPER>(c, f, dT);
+    s_part<D, ALL, LEAN, PAPER>(c, f, f.off_S + t, ts, dirty);
     if (f.copy_Tprev) f.Tp[dT] = ts.T;  // TVP:378-379, T_prev is not read after this point
   }
   if (dirty) *f.tflag = 1;
@@ -198,21 +209,32 @@ __device__ __forceinline__ void fused_loop(const ViscoConst& c, const ViscoField
 
 template <int D, bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_fused(ViscoConst c, ViscoFields f) {
+  if (c.paper) {
+    fused_loop<D, ALL, false, true>(c, f);
+    return;
+  }
   // read once: a flag raised later in this launch changes nothing (see s_part)
   if (*f.tflag == 0) fused_loop<D, ALL, true>(c, f);
   else fused_loop<D, ALL, false>(c, f);
 }
 
+// mixed families, T pass; in paper mode it also keeps the previous step's Tf
+// per T dof (f.Tfo, a work array) for the sigma pass's thermal strain
 template <bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_T(ViscoConst c, ViscoFields f) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
-    (void)t_part<ALL>(c, f, f.off_T + t);
+    if (c.paper) {
+      const TState ts = t_part<ALL, true>(c, f, f.off_T + t);
+      f.Tfo[f.off_T + t] = ts.Tfo;
+    } else {
+      (void)t_part<ALL, false>(c, f, f.off_T + t);
+    }
   }
 }
 
 // mixed families: sigma dof s reads the T-family values of the dof that the
 // last cell written by fem::interpolate assigns to it (f.map).
-template <int D, bool ALL, bool LEAN>
+template <int D, bool ALL, bool LEAN, bool PAPER = false>
 __device__ __forceinline__ void s_loop(const ViscoConst& c, const ViscoFields& f) {
   bool dirty = false;
   for (int64_t s = blockIdx.x * (int64_t)kBlock + threadIdx.x; s < f.n; s += (int64_t)gridDim.x * kBlock) {
@@ -221,15 +243,17 @@ __device__ __forceinline__ void s_loop(const ViscoConst& c, const ViscoFields& f
     ts.T = f.T[t];
     ts.Tp = f.Tp[t];
     ts.Tf = f.Tf[t];
+    ts.Tfo = PAPER ? f.Tfo[t] : ts.Tf;
     ts.xi = f.xi[t];
-    s_part<D, ALL, LEAN>(c, f, f.off_S + s, ts, dirty);
+    s_part<D, ALL, LEAN, PAPER>(c, f, f.off_S + s, ts, dirty);
   }
   if (dirty) *f.tflag = 1;
 }
 
 template <int D, bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_S(ViscoConst c, ViscoFields f) {
-  if (*f.tflag == 0) s_loop<D, ALL, true>(c, f);
+  if (c.paper) s_loop<D, ALL, false, true>(c, f);
+  else if (*f.tflag == 0) s_loop<D, ALL, true>(c, f);
   else s_loop<D, ALL, false>(c, f);
 }
 

@@ -15,6 +15,7 @@ LIB_NAME = "libtvfem.so"
 TV_OK, TV_ERR_ARG, TV_ERR_HIP, TV_ERR_NOT_CONVERGED, TV_ERR_KSP, TV_ERR_STATE, TV_ERR_COMM = range(7)
 TV_CG, TV_DG = 0, 1
 TV_PCG_AUTO, TV_PCG_KSPCG, TV_PCG_SINGLE_REDUCTION = 0, 1, 2
+TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -33,6 +34,7 @@ EXPORTS = [
     "tv_jacobian_diag", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
     "tv_comm_get_unique_id", "tv_comm_init", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes", "tv_kernel_timing", "tv_kernel_stats",
     "tv_last_stats", "tv_comm_init_host", "tv_partition_layout", "tv_pcg_variant",
+    "tv_set_dirichlet",
 ]
 
 HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
@@ -70,7 +72,8 @@ class Options(C.Structure):
     _fields_ = [("newton_rtol", C.c_double), ("newton_atol", C.c_double), ("newton_max_it", C.c_int),
                 ("error_on_nonconvergence", C.c_int), ("ksp_rtol", C.c_double), ("ksp_atol", C.c_double),
                 ("ksp_dtol", C.c_double), ("ksp_max_it", C.c_int), ("materialize", C.c_int),
-                ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int)]
+                ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
+                ("model_mode", C.c_int)]
 
 
 _lib = None
@@ -128,6 +131,7 @@ def load_library():
         "tv_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, HOST_ALLREDUCE_FN, HOST_SENDRECV_FN, vp]),
         "tv_partition_layout": (C.c_int, [C.POINTER(MeshDesc), i64p]),
         "tv_pcg_variant": (C.c_int, [vp, ip]),
+        "tv_set_dirichlet": (C.c_int, [vp, C.c_int, C.c_double]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -100,7 +100,7 @@ class ThermoViscoProblem:
     def __init__(self, mesh_path, time: tuple, dt: float, config: dict, model_parameters: dict,
                  jit_options: dict | None = None, *, device: int = 0, materialize: bool = True,
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
-                 verbose: bool = True, pcg_variant: str = "auto") -> None:
+                 verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference") -> None:
         if isinstance(mesh_path, RectilinearMesh):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -121,6 +121,9 @@ class ThermoViscoProblem:
         self.last_newton_iterations = 0
         self.last_krylov_iterations = 0
         self.__init_function_spaces(config=config)
+        if model_mode not in ("reference", "paper"):
+            raise ValueError("model_mode must be 'reference' (the reference as it runs) or 'paper'")
+        self.model_mode = model_mode
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -171,6 +174,7 @@ class ThermoViscoProblem:
         opts.ksp_rtol = ksp_rtol
         opts.pcg_variant = {"auto": N.TV_PCG_AUTO, "kspcg": N.TV_PCG_KSPCG,
                             "single": N.TV_PCG_SINGLE_REDUCTION}[pcg_variant]
+        opts.model_mode = N.TV_MODEL_PAPER if self.model_mode == "paper" else N.TV_MODEL_REFERENCE
         ctx = C.c_void_p()
         N.check(lib.tv_create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
         self._ctx = ctx
@@ -266,10 +270,16 @@ class ThermoViscoProblem:
     def setup(self, dirichlet_bc: bool = False, outfile_name: str = "visco", outfile_name1: str = "stresses") -> None:
         self._set_initial_condition(temp_value=self.material_model.T_init)
         if dirichlet_bc:
-            # ThermoViscoProblem.py:236-243 references the undefined self.fs and the
-            # bc is never passed to the solver (:331): the reference cannot run this.
-            raise AttributeError("'ThermoViscoProblem' object has no attribute 'fs' "
-                                 "(Dirichlet path of the reference is broken; not supported)")
+            if self.model_mode != "paper":
+                # ThermoViscoProblem.py:180 reads material_model.T_ambient, which
+                # ViscoelasticModel does not have (nor self.fs, :241), and the bc
+                # never reaches NonlinearProblem (:331): the reference cannot run this
+                raise AttributeError("'ViscoelasticModel' object has no attribute 'T_ambient' "
+                                     "(Dirichlet path of the reference is broken; model_mode='paper' runs it)")
+            # paper mode: T = T_ambient on the exterior boundary, in the Newton
+            # solve as dolfinx NonlinearProblem(bcs=[bc]) applies it
+            N.check(self._lib.tv_set_dirichlet(self._ctx, 1, float(self.physical_model.T_ambient)), self._ctx)
+        self.dirichlet_bc = bool(dirichlet_bc)
 
     def _set_initial_condition(self, temp_value: float) -> None:
         self._cache.clear()

@@ -113,7 +113,19 @@ typedef struct {
   int use_graphs;         /* reserved (no effect)                            */
   int pcg_batch;          /* iterations launched between convergence polls  */
   int pcg_variant;        /* TV_PCG_AUTO / TV_PCG_KSPCG / TV_PCG_SINGLE_REDUCTION */
+  int model_mode;         /* TV_MODEL_REFERENCE (default) / TV_MODEL_PAPER       */
 } tv_options;
+
+/* Model semantics.  REFERENCE reproduces the reference as it runs, quirks
+ * included.  PAPER (opt-in, never the default) applies
+ * the fixes the reference's comments name: Eq. 25 drives the partial fictive
+ * temperatures (ViscoelasticModel.py:100-108), Tf_prev is updated after the
+ * thermal strain (ThermoViscoProblem.py:481 vs :492), xi takes the trapezoidal
+ * "+" (ViscoelasticModel.py:171), s~ / sigma~ are fed from the previous s /
+ * sigma partial stresses (Eq. 16, ViscoelasticModel.py:195-209), and a
+ * Dirichlet condition can be applied (tv_set_dirichlet). */
+#define TV_MODEL_REFERENCE 0
+#define TV_MODEL_PAPER 1
 
 /* Krylov iteration form (same Jacobi-PCG iterates in exact arithmetic):
  *   KSPCG             PETSc KSPSolve_CG as written: two reductions per iteration
@@ -188,6 +200,15 @@ int tv_get_field(void* ctx, int field, double* host, size_t n_values);
 int tv_field_device_ptr(void* ctx, int field, void** dev_ptr, int64_t* comp_stride);
 
 int tv_set_initial_condition(void* ctx, double T0);
+/* Dirichlet condition T = value on every dof of the exterior boundary, applied
+ * in the Newton solve as dolfinx's NonlinearProblem(bcs=...) does (lifted
+ * residual, constrained dofs moved to the value by the first update):
+ * _set_dirichlet_bc (ThermoViscoProblem.py:236-243) as the reference intends
+ * it -- its own code cannot run (:241 self.fs, :180 material_model.T_ambient,
+ * and the bc never reaches NonlinearProblem at :331).  Only with model_mode =
+ * TV_MODEL_PAPER (TV_ERR_STATE otherwise).  DG temperature: no dof belongs to
+ * a facet, so the constraint is empty (as locate_dofs_topological would find). */
+int tv_set_dirichlet(void* ctx, int enable, double value);
 int tv_sync(void* ctx);
 
 /* ---- operators (device pointers, owned T-dofs, length n_owned) ---------- */
@@ -219,7 +240,9 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
 /* time `reps` launches of one hot kernel on the context stream with HIP events;
  * kernel: 0 = Jacobian apply (matvec), 1 = fused viscoelastic update,
  * 2 = residual, 3 = fused PCG matvec (p <- z + b p; w <- J p; p.w),
- * 4 = PCG vector update.  Writes the mean duration per launch in ms. */
+ * 4 = PCG vector update, 10 = Jacobian apply with the 256 MiB Infinity Cache
+ * flushed (512 MiB write) before every launch, events around the launch alone.
+ * Writes the mean duration per launch in ms. */
 int tv_time_kernel(void* ctx, int kernel, int reps, double* ms_per_launch);
 /* algorithmic bytes moved by one launch of `kernel` */
 int tv_kernel_bytes(void* ctx, int kernel, double* bytes);

@@ -551,8 +551,26 @@ def pcg_jacobi(A, b, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000):
     raise RuntimeError("KSP did not converge (max_it)")
 
 
-def newton_solve(T, F_fn, J_fn, rtol=1e-12, atol=1e-10, max_it=50, linear="direct"):
-    """Returns (n_iterations, converged, krylov_its); updates T in place."""
+def _apply_dirichlet(A, b, T, bc):
+    """dolfinx NonlinearProblem with bcs [3P]: J gets identity rows / columns
+    at the constrained dofs, b is lifted (apply_lifting(b, [J], [bcs], x0=[x],
+    scale=-1)) and set (set_bc(b, bcs, x, -1)): b_i -= J_iB (x_B - g) on free
+    rows, b_B = x_B - g, so the Newton step x <- x - dx lands on g."""
+    dofs, g = bc
+    d = np.zeros(A.shape[0])
+    d[dofs] = T[dofs] - g
+    b = b - A @ d
+    b[dofs] = T[dofs] - g
+    keep = np.ones(A.shape[0])
+    keep[dofs] = 0.0
+    K = sp.diags(keep)
+    A = (K @ A @ K + sp.diags(1.0 - keep)).tocsr()
+    return A, b
+
+
+def newton_solve(T, F_fn, J_fn, rtol=1e-12, atol=1e-10, max_it=50, linear="direct", bc=None):
+    """Returns (n_iterations, converged, krylov_its); updates T in place.
+    ``bc`` = (dofs, value): Dirichlet constraint applied as dolfinx does."""
     b = F_fn(T)
     it = 0
     kits = 0
@@ -560,6 +578,8 @@ def newton_solve(T, F_fn, J_fn, rtol=1e-12, atol=1e-10, max_it=50, linear="direc
     r0 = 0.0
     while not converged and it < max_it:
         A = J_fn(T)
+        if bc is not None:
+            A, b = _apply_dirichlet(A, b, T, bc)
         if linear == "direct":
             dx = spla.spsolve(A.tocsc(), b)
         else:
@@ -626,7 +646,8 @@ class OracleProblem:
     (ThermoViscoProblem.py:112-171).
     """
 
-    def __init__(self, mesh: Mesh, time, dt, config, model_parameters, linear="direct", plus_side="lower"):
+    def __init__(self, mesh: Mesh, time, dt, config, model_parameters, linear="direct", plus_side="lower",
+                 model_mode="reference"):
         assert all(v["element"] in ("CG", "DG") for v in config.values()), \
             "Only CG and DG elements are supported"
         self.mesh = mesh
@@ -639,6 +660,9 @@ class OracleProblem:
         self.vp = ViscoParams(model_parameters)
         self.tp = ThermalParams.from_dict(model_parameters)
         self.linear = linear
+        assert model_mode in ("reference", "paper")
+        self.model_mode = model_mode
+        self.bc = None
         self.VT = Space(mesh, config["T"]["element"], config["T"]["degree"])
         self.VS = Space(mesh, config["sigma"]["element"], config["sigma"]["degree"])
         self.form = HeatForm(self.VT, dt, self.tp, plus_side=plus_side)
@@ -693,7 +717,20 @@ class OracleProblem:
     # -- setup --------------------------------------------------------------
     def setup(self, dirichlet_bc=False):
         if dirichlet_bc:
-            raise NotImplementedError("reference Dirichlet path is broken (ThermoViscoProblem.py:236-243)")
+            # the reference's own path cannot run (ThermoViscoProblem.py:236-243:
+            # material_model.T_ambient and self.fs do not exist, and the bc never
+            # reaches NonlinearProblem at :331); paper mode runs what it intends:
+            # T = T_ambient on every dof of the exterior boundary.  For DG the
+            # dofs belong to cells, not facets, so locate_dofs_topological finds
+            # none [3P] and the constraint is empty.
+            if self.model_mode != "paper":
+                raise AttributeError("'ViscoelasticModel' object has no attribute 'T_ambient' "
+                                     "(Dirichlet path of the reference is broken)")
+            if self.VT.family == "CG":
+                dofs = np.unique(self.VT.dofmap[self.form.ext[:, 0]][
+                    np.array([[((l >> (lf // 2)) & 1) == (lf % 2) for l in range(2 ** self.dim)]
+                              for lf in self.form.ext[:, 1]])])
+                self.bc = (dofs, float(self.tp.T_ambient))
         T0 = self.vp.T_init
         self.functions_previous["T"][:] = T0
         self.functions_current["T"][:] = T0
@@ -708,7 +745,7 @@ class OracleProblem:
         T = self.functions_current["T"]
         Tp = self.functions_previous["T"]
         it, conv, kits = newton_solve(T, lambda u: self.form.residual(u, Tp), self.form.jacobian,
-                                      linear=self.linear)
+                                      linear=self.linear, bc=self.bc)
         self.newton_history.append((it, kits))
         assert conv
 
@@ -718,7 +755,12 @@ class OracleProblem:
         I = np.eye(d)
         # --- _solve_Tf (TVP:393-407)
         T = fc["T"]
-        f["phi"][:] = shift_function(T, vp)                                  # VEM:156-161 (Eq.5)
+        paper = self.model_mode == "paper"
+        Tf_old = fp["Tf"].copy()                                             # Tf_prev of the last step
+        if paper:                                                            # VEM:100-108 (Eq.25) honoured
+            f["phi"][:] = np.exp(vp.H / vp.Rg * (1.0 / vp.Tb - vp.chi / T - (1.0 - vp.chi) / Tf_old))
+        else:
+            f["phi"][:] = shift_function(T, vp)                              # VEM:156-161 (Eq.5), Q1
         Tfp_prev = fp["Tf_partial"].reshape(-1, 6)
         phi = f["phi"]
         Tfp = np.empty_like(Tfp_prev)
@@ -731,7 +773,8 @@ class OracleProblem:
         for i in range(6):                                                   # VEM:122-125 inner(m, Tf_partial)
             Tf = Tf + vp.m_n[i] * Tfp[:, i]
         fc["Tf"][:] = Tf
-        fp["Tf"][:] = fc["Tf"]                                               # TVP:481-482
+        if not paper:
+            fp["Tf"][:] = fc["Tf"]                                           # TVP:481-482 (Q2: before the strains)
         # --- _solve_strains (TVP:409-423), evaluated on the sigma space
         Ts = self._src("S", "T", fc["T"])
         Tps = self._src("S", "T", fp["T"])
@@ -748,12 +791,17 @@ class OracleProblem:
             tr = tr + tot[:, i, i]
         dev = tot - (1 / self.dim) * I[None] * tr[:, None, None]            # VEM:142-146 (Eq.29)
         f["deviatoric_strain"][:] = dev.ravel()
+        if paper:
+            fp["Tf"][:] = fc["Tf"]                                           # Tf_prev <- Tf after the strains
         # --- _solve_shifted_time (TVP:426-435)
         Tp = fp["T"]
         fn["T"][:] = T + (T - Tp)                                            # VEM:150-153
         f["phi"][:] = shift_function(T, vp)                                  # VEM:156-161
         fn["phi"][:] = shift_function(fn["T"], vp)                           # VEM:162-167
-        f["xi"][:] = dt / 2 * (fn["phi"] - f["phi"])                        # VEM:170-173 (Eq.19, "-")
+        if paper:
+            f["xi"][:] = dt / 2 * (fn["phi"] + f["phi"])                    # Eq.19, trapezoidal "+"
+        else:
+            f["xi"][:] = dt / 2 * (fn["phi"] - f["phi"])                    # VEM:170-173 (Eq.19, "-"), Q4
         # --- _solve_stress (TVP:438-452), sigma space
         xi = self._src("S", "T", f["xi"])
         dev = f["deviatoric_strain"].reshape(-1, d, d)
@@ -765,7 +813,8 @@ class OracleProblem:
             E = taylor_exponential(xi, lam)
             ds[:, n] = 2.0 * g * dev / xi[:, None, None] * lam * (1.0 - E)[:, None, None]
         f["ds_partial"][:] = ds.ravel()
-        st_cur = fc["s_tilde_partial"].reshape(-1, 6, d, d)
+        # Eq.16: reference feeds s~ from itself (Q3); paper mode from s
+        st_cur = (fc["s_partial"] if paper else fc["s_tilde_partial"]).reshape(-1, 6, d, d)
         st_next = np.empty_like(st_cur)
         for n in range(6):                                                   # VEM:195-200 (Eq.16a)
             st_next[:, n] = st_cur[:, n] * taylor_exponential(xi, vp.lambda_g[n])[:, None, None]
@@ -782,7 +831,7 @@ class OracleProblem:
             E = taylor_exponential(xi, lam)
             dsig[:, n] = k * (trI[:, None, None] * I[None]) / xi[:, None, None] * lam * (1.0 - E)[:, None, None]
         f["dsigma_partial"][:] = dsig.ravel()
-        sg_cur = fc["sigma_tilde_partial"].reshape(-1, 6, d, d)
+        sg_cur = (fc["sigma_partial"] if paper else fc["sigma_tilde_partial"]).reshape(-1, 6, d, d)
         sg_next = np.empty_like(sg_cur)
         for n in range(6):                                                   # VEM:203-209 (Eq.16b)
             sg_next[:, n] = sg_cur[:, n] * taylor_exponential(xi, vp.lambda_k[n])[:, None, None]

@@ -1,0 +1,161 @@
+"""Opt-in paper-correct model mode and the Dirichlet condition (SURVEY.md
+section 8(f) rank 4).  Never the default: reference mode keeps the quirks.
+
+Paper mode (model_mode="paper") applies what the reference's comments and the
+paper it cites intend, where the code does otherwise:
+  Q1  Eq. 25 (ViscoelasticModel.py:100-108) drives the partial fictive
+      temperatures instead of being overwritten by Eq. 5 (:156);
+  Q2  Tf_prev is updated after the thermal strain reads it (TVP:481 vs :492);
+  Q4  xi = dt/2 (phi_next + phi), trapezoidal (VEM:171 has "-");
+  Q3  s~ / sigma~ are fed from the previous s / sigma partial stresses (Eq. 16,
+      VEM:195-209 feed them from themselves);
+and setup(dirichlet_bc=True) applies T = T_ambient on the exterior boundary
+the way dolfinx's NonlinearProblem(bcs=...) would (ThermoViscoProblem.py:236-243,
+which cannot run as written).  CPU: oracle known answers.  GPU: the HIP path
+against the oracle's paper mode (T <= 1e-10, stresses <= 1e-6 rel. L2).
+"""
+import numpy as np
+import pytest
+
+from oracle import tv_oracle as O
+from parity_util import check_field, relerr
+
+CG = {"element": "CG", "degree": 1}
+DG = {"element": "DG", "degree": 1}
+
+
+def _oracle(axes, cfg, mode, linear="direct"):
+    r = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), linear=linear,
+                        model_mode=mode)
+    return r
+
+
+def test_oracle_paper_mode_known_answers():
+    axes = [np.linspace(0.0, 50.0, 51)]
+    ref, pap = _oracle(axes, {"T": CG, "sigma": CG}, "reference"), _oracle(axes, {"T": CG, "sigma": CG}, "paper")
+    ref.setup()
+    pap.setup()
+    with np.errstate(all="ignore"):
+        for _ in range(3):
+            ref.solve_timestep()
+            pap.solve_timestep()
+    # the thermal problem does not see the model mode
+    assert np.array_equal(ref.functions_current["T"], pap.functions_current["T"])
+    # trapezoidal xi is a sum of positive shift factors: never 0, never NaN
+    assert np.all(pap.functions["xi"] > 0.0)
+    assert np.isnan(ref.functions_next["sigma"]).any() and not np.isnan(pap.functions_next["sigma"]).any()
+    # Eq. 25 with Tf_prev: the partial fictive temperatures differ from Eq. 5's
+    assert not np.allclose(ref.functions_current["Tf_partial"], pap.functions_current["Tf_partial"])
+    # Eq. 16: the stress has memory (s~ fed from s), unlike the reference (Q3: always 0)
+    assert np.all(ref.functions_current["s_tilde_partial"] == 0.0)
+    assert np.abs(pap.functions_current["sigma_tilde_partial"]).max() > 0.0
+
+
+def test_oracle_dirichlet_dolfinx_semantics():
+    """T = T_ambient on the boundary dofs after the first Newton update; the
+    interior solves the lifted system (compared with an explicit elimination)."""
+    axes = [np.linspace(0.0, 2.0, 9), np.linspace(0.0, 1.0, 5)]
+    p = _oracle(axes, {"T": CG, "sigma": CG}, "paper")
+    p.setup(dirichlet_bc=True)
+    dofs, g = p.bc
+    assert g == O.MAIN_MODEL_PARAMS["T_ambient"]
+    X = p.VT.dof_coordinates()
+    on_bnd = (np.isclose(X[:, 0], 0) | np.isclose(X[:, 0], 2) | np.isclose(X[:, 1], 0) | np.isclose(X[:, 1], 1))
+    assert set(dofs) == set(np.nonzero(on_bnd)[0])
+    Tp = p.functions_previous["T"].copy()
+    p.solve_timestep()
+    T = p.functions_current["T"]
+    assert np.all(T[dofs] == g)
+    # the free rows of F(T) vanish at the converged T (the constrained rows are replaced)
+    F = p.form.residual(T, Tp)
+    free = np.setdiff1d(np.arange(p.VT.n), dofs)
+    assert np.abs(F[free]).max() < 1e-9 * np.abs(p.form.residual(Tp, Tp)).max()
+    # reference mode cannot run it, as the reference itself
+    r = _oracle(axes, {"T": CG, "sigma": CG}, "reference")
+    with pytest.raises(AttributeError):
+        r.setup(dirichlet_bc=True)
+
+
+# ---------------------------------------------------------------- GPU -------
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+PAPER_CASES = [
+    ("1d_cg", [np.linspace(0.0, 50.0, 101)], CG, CG, 6),
+    ("1d_dg_cg", [np.concatenate([np.linspace(0, 5, 11), np.linspace(5, 45, 9)[1:], np.linspace(45, 50, 11)[1:]])],
+     DG, CG, 6),
+    ("3d_cg", [np.linspace(0.0, 2.0, 9), np.linspace(0.0, 2.0, 7), np.linspace(0.0, 1.0, 5)], CG, CG, 4),
+    ("3d_dg", [np.linspace(0.0, 1.0, 4), np.linspace(0.0, 1.0, 4), np.linspace(0.0, 0.5, 3)], DG, DG, 3),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("materialize", [True, False])
+@pytest.mark.parametrize("name,axes,tf,sf,steps", PAPER_CASES, ids=[c[0] for c in PAPER_CASES])
+def test_paper_mode_matches_oracle(name, axes, tf, sf, steps, materialize):
+    _torch()
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    cfg = {"T": tf, "sigma": sf}
+    dev = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                             part_axis=2 if len(axes) == 3 else -1, materialize=materialize, verbose=False,
+                             model_mode="paper")
+    ref = _oracle(axes, cfg, "paper", linear="pcg")
+    dev.setup()
+    ref.setup()
+    for s in range(steps):
+        T_before = ref.functions_current["T"].copy()
+        dev.solve_timestep()
+        ref.solve_timestep()
+        assert relerr(dev.functions_current["T"].x.array, ref.functions_current["T"]) < 1e-10, s
+    d2 = len(axes) ** 2
+    mT = np.abs(ref.functions_current["T"] - T_before) > 1e-6
+    mS = mT[ref._maps[("S", "T")]]
+    assert relerr(dev.functions_current["Tf_partial"].x.array, ref.functions_current["Tf_partial"]) < 1e-10
+    assert relerr(dev.functions_current["Tf"].x.array, ref.functions_current["Tf"]) < 1e-10
+    assert relerr(dev.functions["phi"].x.array, ref.functions["phi"]) < 1e-9
+    assert relerr(dev.functions["xi"].x.array, ref.functions["xi"]) < 1e-9  # "+": no cancellation
+    check_field("sigma[paper]", dev.functions_next["sigma"].x.array, ref.functions_next["sigma"], mS, d2)
+    for k in ("s_partial", "sigma_partial", "s_tilde_partial", "sigma_tilde_partial"):
+        # the deviatoric partial stresses are rounding noise (isotropic strain):
+        # measured against the volumetric scale, as tests/test_golden.py does
+        scale = float(np.linalg.norm(ref.functions_current["sigma_partial"])) if k.startswith("s_") else None
+        check_field(f"{k}[paper]", dev.functions_current[k].x.array, ref.functions_current[k], mS, 6 * d2,
+                    scale=scale)
+    dev.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pcg", ["kspcg", "single"])
+@pytest.mark.parametrize("case", ["1d", "2d", "3d"])
+def test_dirichlet_matches_oracle(case, pcg):
+    _torch()
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    axes = {"1d": [np.linspace(0.0, 5.0, 41)], "2d": [np.linspace(0.0, 3.0, 13), np.linspace(0.0, 1.0, 6)],
+            "3d": [np.linspace(0.0, 2.0, 9), np.linspace(0.0, 2.0, 7), np.linspace(0.0, 1.0, 6)]}[case]
+    if pcg == "single" and case != "3d":
+        pytest.skip("the single-reduction form is the 3D path")
+    cfg = {"T": CG, "sigma": CG}
+    dev = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                             part_axis=2 if len(axes) == 3 else -1, verbose=False, model_mode="paper",
+                             pcg_variant=pcg if case == "3d" else "auto")
+    ref = _oracle(axes, cfg, "paper")
+    dev.setup(dirichlet_bc=True)
+    ref.setup(dirichlet_bc=True)
+    dofs, g = ref.bc
+    for s in range(3):
+        dev.solve_timestep()
+        ref.solve_timestep()
+        T = dev.functions_current["T"].x.array
+        assert np.all(T[dofs] == g), s
+        assert relerr(T, ref.functions_current["T"]) < 1e-10, s
+        assert dev.last_newton_iterations == ref.newton_history[-1][0]
+    dev.close()
+    bad = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False)
+    with pytest.raises(AttributeError):
+        bad.setup(dirichlet_bc=True)
+    bad.close()

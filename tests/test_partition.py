@@ -126,13 +126,16 @@ def _partition_check(world, comm, port, extra=()):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pcg", ["single", "kspcg"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_partitioned_run_matches_single_partition(world):
-    """P partitions on one GPU (host-staged transport) vs one partition."""
+def test_partitioned_run_matches_single_partition(world, pcg):
+    """P partitions on one GPU (host-staged transport) vs one partition, with
+    the single-reduction iteration (the partitioned default: lagged logic, one
+    all-reduce + packed w halo per iteration) and with PETSc KSPCG as written."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _partition_check(world, "host", 29700 + world)
+    _partition_check(world, "host", 29700 + world + (10 if pcg == "kspcg" else 0), ("--pcg", pcg))
 
 
 @pytest.mark.gpu

@@ -30,9 +30,9 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
 
-def run(mesh, n_parts, part, steps, comm=None, device=0):
+def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto"):
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
-                           verbose=False)
+                           verbose=False, pcg_variant=pcg)
     if comm is not None:
         comm(p)
     p.setup()
@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--comm", choices=["host", "rccl"], default="host")
     ap.add_argument("--cells", default="10,30,5")
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -61,14 +62,15 @@ def main():
     if a.comm == "rccl":
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
-        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local)
+        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
+                       pcg=a.pcg)
     else:
-        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world))
+        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
         ref, its_ref = run(mesh, 1, 0, steps)
-        res = {"comm": a.comm, "its_parts": its, "its_single": its_ref}
+        res = {"comm": a.comm, "pcg": a.pcg, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             full = np.concatenate([np.asarray(g[k]) for g in gathered])
             e = np.linalg.norm(full - ref[k]) / np.linalg.norm(ref[k])

@@ -1,12 +1,13 @@
-"""Drive the C4 hot-path kernels for a rocprofv3 --pmc pass.
+"""Drive the hot-path kernels for a rocprofv3 --pmc pass.
 
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
-        python3 tools/pmc_kernels.py [--cells 400,400,50] [--reps 5]
+        python3 tools/pmc_kernels.py [--cells 400,400,50] [--family CG|DG] [--reps 5]
 
-One coupled step (realistic state), then `reps` whole PCG iterations (fused
-matvec + update alternating as in the solve, tv_time_kernel id 5) and `reps`
-viscoelastic updates (id 1), so the counters see the kernels in the cache state
-of the solve.
+One coupled step (realistic state), then `reps` whole PCG iterations (CG: fused
+matvec + update alternating as in the solve, tv_time_kernel id 5; DG: the
+fused DG matvec, id 3), `reps` viscoelastic updates (id 1) and `reps` plain
+J x launches with the Infinity Cache flushed before each (id 10), so the
+counters see the kernels in the cache state of the solve.
 """
 import argparse
 import ctypes as C
@@ -26,15 +27,16 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
 ap = argparse.ArgumentParser()
 ap.add_argument("--cells", default="400,400,50")
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--family", choices=["CG", "DG"], default="CG")
 a = ap.parse_args()
 nc = [int(v) for v in a.cells.split(",")]
-cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+cfg = {"T": {"element": a.family, "degree": 1}, "sigma": {"element": a.family, "degree": 1}}
 prob = ThermoViscoProblem(box_mesh([50.0, 50.0, 5.0], nc), (0.0, 1.0), 0.1, cfg, dict(MP),
                           materialize=False, part_axis=1, verbose=False)
 prob.setup()
 prob.solve_timestep()
 lib, ctx = prob._lib, prob._ctx
-for kid in (5, 1):
+for kid in ((5, 1, 10) if a.family == "CG" else (3, 1, 10)):
     ms = C.c_double()
     N.check(lib.tv_time_kernel(ctx, kid, a.reps, C.byref(ms)), ctx)
     print(kid, ms.value, flush=True)

@@ -4,7 +4,10 @@ per launch for the hot-path kernels, with the gfx950 correction of
 streaming reads: doubled here; WRITE_SIZE taken as is).  Counter values are in
 KB (rocprofv3 derived-counter unit) -> bytes x1024.
 
-    python tools/pmc_summarize.py FETCH_DIR WRITE_DIR OUT.json
+    python tools/pmc_summarize.py FETCH_DIR WRITE_DIR OUT.json [DOMINANT]
+
+DOMINANT (default pcg_matvec_fused) names the group whose per-launch bytes are
+the record's top-level hbm_bytes_per_launch (bench.py's roofline.traffic).
 """
 import csv
 import glob
@@ -17,6 +20,9 @@ GROUPS = {
     "pcg_matvec_fused": ("k_cg_march<1, true",),  # marching tiles + face workgroups, one launch
     "pcg_update": ("k_pcg_update",),
     "visco_update": ("k_visco_fused",),
+    "jacobian_apply": ("k_cg_march<1, false",),  # plain J x (+ k_cg_addfaces, a few KB)
+    "dg_matvec_fused": ("k_dg_tile<true",),
+    "pcg_iteration_single_reduction": ("k_cgs_march<false",),
 }
 
 
@@ -62,8 +68,10 @@ def main():
         wr = wb * 1024.0
         res["kernels"][name] = {"fetch_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
                                 "dispatches": ff}
-    if "pcg_matvec_fused" in res["kernels"]:
-        res["hbm_bytes_per_launch"] = res["kernels"]["pcg_matvec_fused"]["hbm_bytes_per_launch"]
+    dom = sys.argv[4] if len(sys.argv) > 4 else "pcg_matvec_fused"
+    if dom in res["kernels"]:
+        res["dominant"] = dom
+        res["hbm_bytes_per_launch"] = res["kernels"][dom]["hbm_bytes_per_launch"]
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
