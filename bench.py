@@ -49,6 +49,9 @@ def parse():
                     help="rccl (production) or host-staged gloo transport (rehearsal on one GPU)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the hot kernels inside the timed steps")
+    ap.add_argument("--output", default=None, metavar="DIR",
+                    help="write the reference's five output series (T, phi, Tf, xi, sigma) every step "
+                         "into DIR (asynchronous XDMF writer), to measure the step cost with output on")
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto",
                     help="Krylov form: single-reduction (Chronopoulos-Gear, 3D CG) or PETSc KSPCG as written")
     return ap.parse_args()
@@ -88,7 +91,8 @@ def main():
         import torch
         device = local_rank % max(1, torch.cuda.device_count())
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
-                              n_parts=world, part=rank, part_axis=1, verbose=False, pcg_variant=a.pcg)
+                              n_parts=world, part=rank, part_axis=1, verbose=False, pcg_variant=a.pcg,
+                              write_output=a.output is not None, output_dir=a.output or "output")
     single = prob.pcg_variant == "single"
     lib, ctx = prob._lib, prob._ctx
     if world > 1:
@@ -129,6 +133,8 @@ def main():
         step()
         nits += prob.last_newton_iterations
         kits += prob.last_krylov_iterations
+    if a.output is not None:  # the timed region includes draining the writer
+        prob._finalize()
     barrier_sync()
     dt_local = time.perf_counter() - t0
     if dist is not None:
@@ -230,6 +236,8 @@ def main():
                                        f"mesh partition along y x{world} ("
                                        + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")"),
                        "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,
+                       "output": (f"T, phi, Tf, xi, sigma written every step (async XDMF) to {a.output}"
+                                  if a.output else "none (reference writes VTX/XDMF every step)"),
                        "krylov_form": ("single-reduction (Chronopoulos-Gear) Jacobi-PCG" if single
                                        else "PETSc KSPCG Jacobi-PCG"),
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},

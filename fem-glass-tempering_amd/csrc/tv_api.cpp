@@ -94,6 +94,8 @@ struct Ctx {
   double dir_value = 0.0;
   double *dB = nullptr, *dtmp = nullptr;
   double* Tfo = nullptr;  // paper mode, mixed families: previous Tf per T dof
+  Output* out = nullptr;  // time-series output (tv_output_*)
+  std::vector<int> out_fields;
   double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
   double* wsend = nullptr;
   double* partials = nullptr;
@@ -1235,6 +1237,7 @@ int tv_destroy(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->out) output_destroy(c->out);
   for (int i = 0; i < TV_NUM_FIELDS; ++i)
     if (c->f[i].alloc && c->f[i].ptr) hipFree(c->f[i].ptr);
   for (double* p : {c->cr[0], c->cr[1], c->cs[0], c->cs[1], c->cw1, c->wsend, c->dB, c->dtmp, c->Tfo})
@@ -1367,6 +1370,94 @@ int tv_set_initial_condition(void* ctx, double T0) {
   launch_fill(c->f[TV_F_TF_PARTIAL].ptr, c->nT * 6, T0, c->stream);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+// ---- time-series output (ThermoViscoProblem.py:246-276, 357-364, 614-620) ----
+int tv_output_open(void* ctx, const char* dir, const int* field_ids, int n_fields) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !dir || !field_ids || n_fields < 1) return TV_ERR_ARG;
+  if (c->out) return c->fail(TV_ERR_STATE, "output already open");
+  hipSetDevice(c->device);
+  // mesh of the owned nodes (storage order; a partition keeps its owned planes)
+  std::vector<std::vector<double>> Xs(3);
+  int phys[3];
+  std::vector<double> tmp;
+  for (int sx = 0; sx < 3; ++sx) {
+    Xs[sx] = storage_coords(c, sx, tmp);
+    phys[sx] = c->perm[sx];
+  }
+  if (c->fam_T == TV_CG && c->n_parts > 1)
+    Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin, Xs[2].begin() + c->plane_end);
+  std::string err;
+  Output* o = output_create(dir, c->dim, Xs, phys, err);
+  if (!o) return c->fail(TV_ERR_STATE, "output: " + err);
+  static const char* names[TV_NUM_FIELDS] = {
+      "T", "T_prev", "T_next", "Tf", "Tf_prev", "Tf_partial", "Tf_partial_prev", "phi", "phi_next", "xi",
+      "thermal_strain", "total_strain", "deviatoric_strain", "ds_partial", "dsigma_partial", "s_tilde_partial",
+      "s_tilde_partial_next", "sigma_tilde_partial", "sigma_tilde_partial_next", "s_partial", "s_partial_next",
+      "sigma_partial", "sigma_partial_next", "sigma", "residual", "dx"};
+  for (int k = 0; k < n_fields; ++k) {
+    const int id = field_ids[k];
+    if (id < 0 || id >= TV_NUM_FIELDS || !c->f[id].ptr) {
+      output_destroy(o);
+      return c->fail(TV_ERR_ARG, "output: field not available");
+    }
+    const FieldInfo& fi = c->f[id];
+    const bool dg = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
+    const int64_t n = (fi.space == 0) ? c->ownT_n : c->ownS_n;
+    if (!output_add_field(o, names[id], fi.bs, dg, (size_t)n * fi.bs, err)) {
+      output_destroy(o);
+      return c->fail(TV_ERR_STATE, "output: " + err);
+    }
+  }
+  if (!output_start(o, c->device, err)) {
+    output_destroy(o);
+    return c->fail(TV_ERR_HIP, err);
+  }
+  c->out = o;
+  c->out_fields.assign(field_ids, field_ids + n_fields);
+  return TV_OK;
+}
+
+// gathers the fields in the reference's interleaved layout into a device
+// staging set on the compute stream and returns; copy and file writes overlap
+// the following steps (tv_output.cpp)
+int tv_output_write(void* ctx, double t) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (!c->out) return c->fail(TV_ERR_STATE, "output not open");
+  hipSetDevice(c->device);
+  int set = 0;
+  double* d = output_acquire(c->out, &set);
+  for (size_t k = 0; k < c->out_fields.size(); ++k) {
+    const FieldInfo& fi = c->f[c->out_fields[k]];
+    const int64_t ndof = (fi.space == 0) ? c->ownT_n : c->ownS_n;
+    const int64_t off = (fi.space == 0) ? c->ownT_off : c->ownS_off;
+    const int64_t stride = (fi.space == 0) ? c->nT : c->nS;
+    const bool dgsp = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
+    const int nl = dgsp ? (1 << c->dim) : 0;
+    const int64_t ncell = dgsp ? ndof / nl : 0;
+    const int64_t need = ndof * fi.bs;
+    const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, (need + 255) / 256), 16384);
+    hipLaunchKernelGGL(k_interleave, dim3(blocks), dim3(256), 0, c->stream, 1, d + output_offset(c->out, k), fi.ptr,
+                       ndof, fi.bs, stride, off, nl, ncell);
+  }
+  HIPC(hipGetLastError());
+  std::string err;
+  if (!output_submit(c->out, set, t, c->stream, err)) return c->fail(TV_ERR_STATE, "output: " + err);
+  return TV_OK;
+}
+
+int tv_output_close(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (!c->out) return TV_OK;
+  hipSetDevice(c->device);
+  const std::string e = output_destroy(c->out);
+  c->out = nullptr;
+  c->out_fields.clear();
+  if (!e.empty()) return c->fail(TV_ERR_STATE, "output: " + e);
   return TV_OK;
 }
 

@@ -235,6 +235,17 @@ void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s);
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s);
 int pcg_vec_blocks(int64_t n);
 void launch_fill(double* x, int64_t n, double v, hipStream_t s);
+
+// ---- time-series output (tv_output.cpp) ----
+struct Output;
+Output* output_create(const std::string& dir, int dim, const std::vector<std::vector<double>>& Xs, const int* phys,
+                      std::string& err);
+bool output_add_field(Output* o, const std::string& name, int ncomp, bool dg, size_t n_values, std::string& err);
+bool output_start(Output* o, int device, std::string& err);
+double* output_acquire(Output* o, int* set);
+size_t output_offset(const Output* o, size_t k);
+bool output_submit(Output* o, int set, double t, hipStream_t compute, std::string& err);
+std::string output_destroy(Output* o);
 void launch_copy(double* dst, const double* src, int64_t n, hipStream_t s);
 
 }  // namespace tv

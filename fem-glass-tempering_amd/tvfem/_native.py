@@ -34,7 +34,8 @@ EXPORTS = [
     "tv_jacobian_diag", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
     "tv_comm_get_unique_id", "tv_comm_init", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes", "tv_kernel_timing", "tv_kernel_stats",
     "tv_last_stats", "tv_comm_init_host", "tv_partition_layout", "tv_pcg_variant",
-    "tv_set_dirichlet",
+    "tv_set_dirichlet", "tv_output_open", "tv_output_write", "tv_output_close", "tv_xdmf_open",
+    "tv_xdmf_add_field", "tv_xdmf_append", "tv_xdmf_close",
 ]
 
 HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p)
@@ -132,6 +133,13 @@ def load_library():
         "tv_partition_layout": (C.c_int, [C.POINTER(MeshDesc), i64p]),
         "tv_pcg_variant": (C.c_int, [vp, ip]),
         "tv_set_dirichlet": (C.c_int, [vp, C.c_int, C.c_double]),
+        "tv_output_open": (C.c_int, [vp, C.c_char_p, ip, C.c_int]),
+        "tv_output_write": (C.c_int, [vp, C.c_double]),
+        "tv_output_close": (C.c_int, [vp]),
+        "tv_xdmf_open": (vp, [C.c_char_p, C.c_int, ip, C.POINTER(dp)]),
+        "tv_xdmf_add_field": (C.c_int, [vp, C.c_char_p, C.c_int, C.c_int]),
+        "tv_xdmf_append": (C.c_int, [vp, C.c_int, C.c_double, dp, C.c_size_t]),
+        "tv_xdmf_close": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -15,7 +15,8 @@ Differences that are part of the contract:
   * the linear solver is matrix-free Jacobi-PCG (reference: CG + GAMG); T and
     sigma agree with the CPU restatement within the tolerances stated in
     tests/;
-  * file output (VTX / XDMF, :246-276) is not written by default.
+  * file output (:246-276, VTX / XDMF there) is XDMF over raw binary here
+    and written only with ``write_output=True`` (into ``output_dir``).
 """
 from __future__ import annotations
 
@@ -100,7 +101,8 @@ class ThermoViscoProblem:
     def __init__(self, mesh_path, time: tuple, dt: float, config: dict, model_parameters: dict,
                  jit_options: dict | None = None, *, device: int = 0, materialize: bool = True,
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
-                 verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference") -> None:
+                 verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
+                 write_output: bool = False, output_dir: str = "output") -> None:
         if isinstance(mesh_path, RectilinearMesh):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -124,6 +126,9 @@ class ThermoViscoProblem:
         if model_mode not in ("reference", "paper"):
             raise ValueError("model_mode must be 'reference' (the reference as it runs) or 'paper'")
         self.model_mode = model_mode
+        self.write_output = write_output
+        self.output_dir = output_dir
+        self._output_open = False
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -167,6 +172,7 @@ class ThermoViscoProblem:
         desc.part_axis = part_axis
         desc.n_parts = n_parts
         desc.part = part
+        self._n_parts, self._part = n_parts, part
         fe = N.FeConfig(_FAMILIES[self._fam["T"]], 1, _FAMILIES[self._fam["sigma"]], 1)
         params = N.default_params(mp, self.dt)
         opts = N.default_options()
@@ -280,6 +286,34 @@ class ThermoViscoProblem:
             # solve as dolfinx NonlinearProblem(bcs=[bc]) applies it
             N.check(self._lib.tv_set_dirichlet(self._ctx, 1, float(self.physical_model.T_ambient)), self._ctx)
         self.dirichlet_bc = bool(dirichlet_bc)
+        if self.write_output:
+            self._write_initial_output(t=self.t)
+
+    # the reference's five series (ThermoViscoProblem.py:246-276): T, phi, Tf,
+    # xi and sigma, as XDMF over raw binary (tvfem.xdmf reads them back)
+    OUTPUT_FIELDS = ("T", "phi", "Tf", "xi", "sigma")
+
+    def _write_initial_output(self, t: float = 0.0) -> None:
+        import os
+        d = self.output_dir
+        n_parts = getattr(self, "_n_parts", 1)
+        if n_parts > 1:
+            d = os.path.join(d, f"part{self._part}")
+        os.makedirs(d, exist_ok=True)
+        ids = (C.c_int * len(self.OUTPUT_FIELDS))(*[N.FIELD_ID[f] for f in self.OUTPUT_FIELDS])
+        N.check(self._lib.tv_output_open(self._ctx, d.encode(), ids, len(self.OUTPUT_FIELDS)), self._ctx)
+        self._output_open = True
+        self._write_output(t)
+
+    def _write_output(self, t=None) -> None:
+        """Queue this step's fields; the copy and the file writes overlap the next steps."""
+        self._flush()
+        N.check(self._lib.tv_output_write(self._ctx, float(self.t if t is None else t)), self._ctx)
+
+    def _finalize(self) -> None:
+        if self._output_open:
+            self._output_open = False
+            N.check(self._lib.tv_output_close(self._ctx), self._ctx)
 
     def _set_initial_condition(self, temp_value: float) -> None:
         self._cache.clear()
@@ -300,6 +334,8 @@ class ThermoViscoProblem:
         N.check(rc, self._ctx)
         self.last_newton_iterations = nits.value
         self.last_krylov_iterations = kits.value
+        if self._output_open:  # ThermoViscoProblem.py:374
+            self._write_output()
 
     def _solve_T(self):
         self._flush()
@@ -319,11 +355,15 @@ class ThermoViscoProblem:
             self.solve_timestep(t=self.t)
         if self.verbose:
             print(f"Solve finished in {_time.time() - t_start} seconds.")
+        self._finalize()  # ThermoViscoProblem.py:614-620
 
     def close(self):
         if self._ctx is not None:
-            self._lib.tv_destroy(self._ctx)
-            self._ctx = None
+            try:
+                self._finalize()
+            finally:
+                self._lib.tv_destroy(self._ctx)
+                self._ctx = None
 
     def __del__(self):
         try:

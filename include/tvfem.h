@@ -221,6 +221,26 @@ int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged);
 int tv_visco_update(void* ctx);
 int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its);
 
+/* ---- time-series output -------------------------------------------------------
+ * The reference writes T, phi, Tf, xi (VTX/BP4) and sigma (XDMF/HDF5) every
+ * step (ThermoViscoProblem.py:246-276 _write_initial_output, :357-364
+ * _write_output, :614-620 _finalize).  Here: one XDMF 3 series per field
+ * (<dir>/<name>.xdmf over raw little-endian <name>.bin, mesh_*.bin), written
+ * asynchronously -- tv_output_write gathers the fields on the device, a copy
+ * stream moves them to pinned host memory and a writer thread appends them to
+ * the files while the next steps run; it blocks only when two writes are still
+ * in flight.  tv_output_close drains.  A partition writes its owned nodes. */
+int tv_output_open(void* ctx, const char* dir, const int* field_ids, int n_fields);
+int tv_output_write(void* ctx, double t);
+int tv_output_close(void* ctx);
+/* The file format without a GPU (tests, tools): a rectilinear mesh as
+ * tv_mesh_desc gives it (one partition), fields appended from host arrays in
+ * the reference's interleaved layout; discontinuous = DG (cell-major dofs). */
+void* tv_xdmf_open(const char* dir, int dim, const int* n_cells, const double* const* coords);
+int tv_xdmf_add_field(void* xdmf, const char* name, int ncomp, int discontinuous);
+int tv_xdmf_append(void* xdmf, int field, double t, const double* values, size_t n_values);
+void tv_xdmf_close(void* xdmf);
+
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---------------------- */
 int tv_comm_unique_id_size(void);
 int tv_comm_get_unique_id(char* id_out);   /* rank 0; broadcast it out-of-band */
