@@ -72,7 +72,18 @@ struct XdmfSeries {
     return false;
   }
 
+  // the discontinuous copy of the mesh, written when the first DG field opens
+  std::vector<double> dg_xyz;
+  std::vector<int64_t> dg_cells;
+  bool dg_written = false;
+
   bool open_field(const std::string& name, int ncomp, bool cell_nodes) {
+    if (cell_nodes && !dg_written) {
+      if (!write_mesh("mesh_dg", dg_xyz, dg_cells)) return false;
+      dg_written = true;
+      std::vector<double>().swap(dg_xyz);
+      std::vector<int64_t>().swap(dg_cells);
+    }
     XdmfField fl;
     fl.name = name;
     fl.ncomp = ncomp;
@@ -85,20 +96,32 @@ struct XdmfSeries {
   }
 
   bool append(size_t k, double t, const double* v, size_t n) {
+    std::string e;
+    if (!append_field(k, t, v, n, e)) return fail(e);
+    return true;
+  }
+  // touches field k's file and index only (fields are written concurrently)
+  bool append_field(size_t k, double t, const double* v, size_t n, std::string& e) {
     XdmfField& fl = fields[k];
     const long long off = (long long)std::ftell(fl.bin);
-    if (std::fwrite(v, sizeof(double), n, fl.bin) != n) return fail("short write of " + fl.name + ".bin");
+    if (std::fwrite(v, sizeof(double), n, fl.bin) != n) {
+      e = "short write of " + fl.name + ".bin";
+      return false;
+    }
     std::fflush(fl.bin);
     fl.steps.emplace_back(t, off);
-    return rewrite_index(fl);
+    return rewrite_index(fl, &e);
   }
 
   // the whole index is rewritten at every step, so the .xdmf file is valid
   // XML at any moment (a run stopped half-way leaves a readable series)
-  bool rewrite_index(const XdmfField& fl) {
+  bool rewrite_index(const XdmfField& fl, std::string* e = nullptr) {
     const std::string path = dir + "/" + fl.name + ".xdmf", tmp = path + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "w");
-    if (!f) return fail("cannot write " + tmp);
+    if (!f) {
+      if (e) *e = "cannot write " + tmp;
+      return e ? false : fail("cannot write " + tmp);
+    }
     const char* pre = fl.cell_nodes ? "mesh_dg" : "mesh";
     const int64_t nn = fl.cell_nodes ? n_dnodes : n_nodes;
     const int npc = 1 << dim;
@@ -125,7 +148,10 @@ struct XdmfSeries {
     }
     std::fprintf(f, "  </Grid>\n </Domain>\n</Xdmf>\n");
     std::fclose(f);
-    if (std::rename(tmp.c_str(), path.c_str()) != 0) return fail("cannot rename " + tmp);
+    if (std::rename(tmp.c_str(), path.c_str()) != 0) {
+      if (e) *e = "cannot rename " + tmp;
+      return e ? false : fail("cannot rename " + tmp);
+    }
     return true;
   }
 
@@ -214,10 +240,12 @@ void* tv_xdmf_open(const char* dir, int dim, const int* n_cells, const double* c
   h->s.n_nodes = (int64_t)xyz.size() / 3;
   h->s.n_cells = (int64_t)cells.size() >> dim;
   h->s.n_dnodes = (int64_t)dxyz.size() / 3;
-  if (!h->s.write_mesh("mesh", xyz, cells) || !h->s.write_mesh("mesh_dg", dxyz, dcells)) {
+  if (!h->s.write_mesh("mesh", xyz, cells)) {
     delete h;
     return nullptr;
   }
+  h->s.dg_xyz.swap(dxyz);
+  h->s.dg_cells.swap(dcells);
   return h;
 }
 
@@ -279,10 +307,18 @@ struct Output {
         q.pop_front();
       }
       hipEventSynchronize(copied[j.set]);
+      // one thread per field: the page-cache copy of one fwrite is single-threaded
+      std::vector<std::thread> ws;
+      std::vector<std::string> errs(field_n.size());
       for (size_t k = 0; k < field_n.size(); ++k)
-        if (!series.append(k, j.t, hstage[j.set] + field_off[k], field_n[k])) {
+        ws.emplace_back([&, k] {
+          if (!series.append_field(k, j.t, hstage[j.set] + field_off[k], field_n[k], errs[k])) return;
+        });
+      for (auto& w : ws) w.join();
+      for (const auto& e : errs)
+        if (!e.empty()) {
           std::lock_guard<std::mutex> lk(mu);
-          err = series.err;
+          if (err.empty()) err = e;
         }
       {
         std::lock_guard<std::mutex> lk(mu);
@@ -304,11 +340,13 @@ Output* output_create(const std::string& dir, int dim, const std::vector<std::ve
   o->series.n_nodes = (int64_t)xyz.size() / 3;
   o->series.n_cells = (int64_t)cells.size() >> dim;
   o->series.n_dnodes = (int64_t)dxyz.size() / 3;
-  if (!o->series.write_mesh("mesh", xyz, cells) || !o->series.write_mesh("mesh_dg", dxyz, dcells)) {
+  if (!o->series.write_mesh("mesh", xyz, cells)) {
     err = o->series.err;
     delete o;
     return nullptr;
   }
+  o->series.dg_xyz.swap(dxyz);
+  o->series.dg_cells.swap(dcells);
   return o;
 }
 
