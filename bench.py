@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--output", default=None, metavar="DIR",
                     help="write the reference's five output series (T, phi, Tf, xi, sigma) every step "
                          "into DIR (asynchronous XDMF writer), to measure the step cost with output on")
+    ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
+                    help="box: the rectilinear plate (tensor-product kernels); distorted: the same plate as a "
+                         "general hexahedral mesh (jittered, sheared, warped; element-local kernels, one GPU)")
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto",
                     help="Krylov form: single-reduction (Chronopoulos-Gear, 3D CG) or PETSc KSPCG as written")
     return ap.parse_args()
@@ -70,7 +73,7 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from tvfem import box_mesh
+    from tvfem import box_mesh, distorted_box_mesh
     from tvfem import _native as N
     from tvfem.problem import ThermoViscoProblem
 
@@ -79,7 +82,10 @@ def main():
     if a.scaling == "weak":
         nc[1] *= world
         L[1] *= world
-    mesh = box_mesh(L, nc)
+    um = a.mesh == "distorted"
+    if um and (world > 1 or a.family != "CG"):
+        raise SystemExit("--mesh distorted: one GPU, CG1 (unstructured meshes run on one partition)")
+    mesh = distorted_box_mesh(L, nc) if um else box_mesh(L, nc)
     mp = {
         "f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0,
         "htc": 280.1, "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0e0, "Rg": 8.314,
@@ -155,6 +161,8 @@ def main():
     names = {3: "pcg_matvec_fused", 4: "pcg_update", 0: "jacobian_apply", 2: "residual"}
     if single:  # one fused launch per Krylov iteration, no separate update
         names = {3: "pcg_iteration_single_reduction", 0: "jacobian_apply", 2: "residual"}
+    if um:  # element-local kernels: J x (coloured cell + facet launches) is the roofline kernel
+        names = {0: "jacobian_apply_unstructured", 3: "pcg_matvec_unstructured", 4: "pcg_update", 2: "residual"}
     if not a.thermal_only:
         names[1] = "visco_update"
     for kid, name in names.items():
@@ -184,20 +192,23 @@ def main():
                "ms_per_launch": fl_ms.value, "achieved": fl_by.value / (fl_ms.value * 1e-3) / 1e9,
                "unit": "GB/s", "frac": fl_by.value / (fl_ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS,
                "timing": "HBM (flushed): 512 MiB write before each launch, HIP events around the launch"}
-    dom = kern[names[3]]
+    dom = kern[names[0] if um else names[3]]
     # traffic: HBM bytes per launch of this kernel from the rocprofv3 --pmc passes
     # (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section) of this same
     # bench command, committed under profiles/ (counters cannot be read inside
     # the timed run); traffic_source names the file
     traffic, traffic_src = None, None
-    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{names[3]}_{a.family}_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
+    dname = names[0] if um else names[3]
+    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{dname}_{a.family}_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
     if os.path.exists(pmc_file):
         with open(pmc_file) as fh:
             traffic = json.load(fh).get("hbm_bytes_per_launch")
         traffic_src = "committed rocprofv3 --pmc record " + os.path.relpath(pmc_file, ROOT)
     roofline = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": ("pcg_iteration_single_reduction (s, p, x, r, z updates; w <- J(T) z; (r,z), (z,w), (z,z))"
+                "kernel": ("jacobian_apply_unstructured (y <- J(T) x, isoparametric 27-point cells, coloured "
+                           "scatter; algorithmic bytes 16/vertex (x, y) + 24/vertex (coords) + 32/cell (ids))" if um else
+                           "pcg_iteration_single_reduction (s, p, x, r, z updates; w <- J(T) z; (r,z), (z,w), (z,z))"
                            if single else "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)"),
                 "bytes_per_launch": dom["bytes"], "ms_per_launch": dom["ms"],
                 "timing": ("effective (in-solve, Infinity-Cache assisted)" if dom["launches_timed"]
@@ -206,7 +217,10 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        if a.family == "CG":
+        if um:
+            cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
+                   "sample": "no unstructured path in oracle/tv_cpu.c (the numpy oracle covers its parity only)"}
+        elif a.family == "CG":
             cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only)
         else:
             cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
@@ -229,7 +243,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (uniform T_0 = 800 K initial state, main.py parameters)",
-            "config": {"workload": f"{cname} 3D plate {a.family}1/{a.family}1 {nc[0]}x{nc[1]}x{nc[2]} hex "
+            "config": {"workload": ("distorted-hex " if um else "")
+                                   + f"{cname} 3D plate {a.family}1/{a.family}1 {nc[0]}x{nc[1]}x{nc[2]} hex "
                                    f"({n_global} T-dofs), dt 0.1, "
                                    + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
                        "parallelism": ("single GPU, one partition (no communication)" if world == 1 else

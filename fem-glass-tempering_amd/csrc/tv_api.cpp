@@ -95,6 +95,15 @@ struct Ctx {
   double *dB = nullptr, *dtmp = nullptr;
   double* Tfo = nullptr;  // paper mode, mixed families: previous Tf per T dof
   Output* out = nullptr;  // time-series output (tv_output_*)
+  // unstructured mesh (tv_create_unstructured, tv_um.hip)
+  bool um = false;
+  UmGrid umg{};
+  std::vector<double> um_xyz;        // host copy: 3 per vertex
+  std::vector<int64_t> um_cells;     // host copy: 2^dim per cell (input order)
+  double* um_X[3] = {nullptr, nullptr, nullptr};
+  int *um_cell = nullptr, *um_fcell = nullptr;
+  signed char* um_flf = nullptr;
+  unsigned char* um_bmask = nullptr;  // boundary vertices (Dirichlet mode)
   std::vector<int> out_fields;
   double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
   double* wsend = nullptr;
@@ -477,7 +486,8 @@ static int setup_fields(Ctx* c) {
   c->f[TV_F_RESIDUAL].ptr = c->r; c->f[TV_F_RESIDUAL].bs = 1; c->f[TV_F_RESIDUAL].space = 0;
   if (int e = alloc_field(c, TV_F_DX, 0, 1)) return e;
   int np = kVecBlocksMax;
-  if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
+  if (c->um) np = std::max(np, 1024);
+  else if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
   else np = std::max(np, dg_num_blocks(c->dg));
   c->n_partials_cap = np;
   // records of width <= 3 per workgroup + the shard records of the two-level tail
@@ -492,7 +502,7 @@ static int setup_fields(Ctx* c) {
   for (int k = 0; k < 2; ++k) HIPC(hipEventCreateWithFlags(&c->evp[k], hipEventDisableTiming));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
   const int var = c->O.pcg_variant;
-  const bool can = c->fam_T == TV_CG && cg_cgs_supported(c->cg);
+  const bool can = c->fam_T == TV_CG && !c->um && cg_cgs_supported(c->cg);
   if (var == TV_PCG_SINGLE_REDUCTION && !can)
     return c->fail(TV_ERR_ARG, "pcg_variant SINGLE_REDUCTION needs a 3D CG1 temperature space");
   // AUTO: the single-reduction form where the mesh is partitioned (one RCCL
@@ -649,19 +659,26 @@ static int reduce_logic(Ctx* c, int n, int W, int kind, int check_done) {
 // operators
 // --------------------------------------------------------------------------------------
 static void op_residual(Ctx* c, const double* T, const double* Tp, double* F) {
-  if (c->fam_T == TV_CG) launch_cg_residual(c->cg, T, Tp, F, c->stream);
+  if (c->um) launch_um_residual(c->umg, T, Tp, F, c->stream);
+  else if (c->fam_T == TV_CG) launch_cg_residual(c->cg, T, Tp, F, c->stream);
   else launch_dg_residual(c->dg, T, Tp, F, c->stream);
 }
 static void op_diag(Ctx* c, const double* T, double* d, int invert) {
   // Jacobian "assembly": the diagonal for the Jacobi PC (J(T) itself is matrix-free)
-  if (c->fam_T == TV_CG) launch_cg_diag(c->cg, T, d, invert, c->stream);
+  if (c->um) launch_um_diag(c->umg, T, d, invert, c->stream);
+  else if (c->fam_T == TV_CG) launch_cg_diag(c->cg, T, d, invert, c->stream);
   else launch_dg_diag(c->dg, T, d, invert, c->stream);
 }
 static void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
-  if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
+  if (c->um) launch_um_japply(c->umg, T, x, y, c->stream);
+  else if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
   else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
 }
 static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr, int it = 0) {
+  if (c->um) {  // separate p update, coloured J p, p.w records (reduced by the caller)
+    *np = launch_um_japply_fused(c->umg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, it, c->stream);
+    return false;
+  }
   if (c->fam_T == TV_CG)
     return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail, it);
   return launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail);
@@ -716,7 +733,7 @@ static int pcg_iteration(Ctx* c, const double* T, int it) {
     launch_logic(c->st, c->sums, 2, c->stream);
   }
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
-  const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, off) : FaceAdd{};
+  const FaceAdd fa = (c->fam_T == TV_CG && !c->um) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
                     c->z + off, c->partials, c->stream, &t2, &fa, it);
   if (multi) {  // dp, beta, convergence
@@ -939,6 +956,14 @@ static const char* reason_str(int r) {
 }
 
 // ---- Dirichlet mode ----------------------------------------------------------
+struct BndTest {
+  CgGrid g;
+  const unsigned char* mask;  // unstructured: boundary vertices (else nullptr)
+};
+__device__ __forceinline__ bool cg_on_boundary(const CgGrid& g, int64_t n);
+__device__ __forceinline__ bool on_boundary(const BndTest& b, int64_t n) {
+  return b.mask ? b.mask[n] != 0 : cg_on_boundary(b.g, n);
+}
 __device__ __forceinline__ bool cg_on_boundary(const CgGrid& g, int64_t n) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
   const int k = (int)(n / plane);
@@ -948,19 +973,19 @@ __device__ __forceinline__ bool cg_on_boundary(const CgGrid& g, int64_t n) {
          (j == g.n1 - 1 && g.bnd[1][1]) || (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
 }
 // dB = T - value on constrained nodes, 0 elsewhere (every local node)
-__global__ __launch_bounds__(kBlock) void k_bc_dvec(CgGrid g, const double* __restrict__ T, double value,
+__global__ __launch_bounds__(kBlock) void k_bc_dvec(BndTest b, const double* __restrict__ T, double value,
                                                     double* __restrict__ dB, int64_t n) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
-    dB[t] = cg_on_boundary(g, t) ? T[t] - value : 0.0;
+    dB[t] = on_boundary(b, t) ? T[t] - value : 0.0;
 }
 // F -= J dB (lifting; the constrained rows are never read: diag^-1 = 0 there)
 // and diag^-1 = 0 on constrained nodes, so z = B r and every Krylov vector
 // stay in the free subspace: PCG on P J P with the Jacobi preconditioner P B P
-__global__ __launch_bounds__(kBlock) void k_bc_lift(CgGrid g, double* __restrict__ F, const double* __restrict__ JdB,
+__global__ __launch_bounds__(kBlock) void k_bc_lift(BndTest b, double* __restrict__ F, const double* __restrict__ JdB,
                                                     double* __restrict__ dinv, int64_t n) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     F[t] -= JdB[t];
-    if (cg_on_boundary(g, t)) dinv[t] = 0.0;
+    if (on_boundary(b, t)) dinv[t] = 0.0;
   }
 }
 // dx += dB (the constrained part of the Newton step: x - dx lands on the value)
@@ -971,9 +996,10 @@ __global__ __launch_bounds__(kBlock) void k_bc_step(double* __restrict__ dx, con
 static int dirichlet_pre(Ctx* c, const double* T) {
   const int64_t n = c->nT;
   const int blocks = (int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_bc_dvec, dim3(blocks), dim3(kBlock), 0, c->stream, c->cg, T, c->dir_value, c->dB, n);
+  const BndTest bt{c->cg, c->um ? c->um_bmask : nullptr};
+  hipLaunchKernelGGL(k_bc_dvec, dim3(blocks), dim3(kBlock), 0, c->stream, bt, T, c->dir_value, c->dB, n);
   op_japply(c, T, c->dB, c->dtmp, nullptr, nullptr);
-  hipLaunchKernelGGL(k_bc_lift, dim3(blocks), dim3(kBlock), 0, c->stream, c->cg, c->r, c->dtmp, c->dinv, n);
+  hipLaunchKernelGGL(k_bc_lift, dim3(blocks), dim3(kBlock), 0, c->stream, bt, c->r, c->dtmp, c->dinv, n);
   HIPC(hipGetLastError());
   return TV_OK;
 }
@@ -1206,6 +1232,133 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
   return TV_OK;
 }
 
+static int setup_umesh(Ctx* c, const tv_umesh_desc* m) {
+  const int d = m->dim;
+  if (d != 2 && d != 3) return c->fail(TV_ERR_ARG, "unstructured meshes: dim 2 (quadrilaterals) or 3 (hexahedra)");
+  if (c->fam_T != TV_CG || c->fam_S != TV_CG)
+    return c->fail(TV_ERR_ARG, "unstructured meshes: CG temperature and stress spaces only");
+  if (m->n_vertices < 1 || m->n_cells < 1 || !m->coords || !m->cells) return c->fail(TV_ERR_ARG, "empty mesh");
+  if (m->n_vertices >= INT32_MAX) return c->fail(TV_ERR_ARG, "unstructured meshes: < 2^31 vertices");
+  const int nl = 1 << d;
+  for (int64_t k = 0; k < m->n_cells * nl; ++k)
+    if (m->cells[k] < 0 || m->cells[k] >= m->n_vertices) return c->fail(TV_ERR_ARG, "cell vertex index out of range");
+  c->um = true;
+  c->dim = d;
+  c->um_xyz.assign(m->coords, m->coords + 3 * m->n_vertices);
+  c->um_cells.assign(m->cells, m->cells + m->n_cells * nl);
+  UmHost hh;
+  std::string err;
+  if (um_build(d, m->n_vertices, m->n_cells, m->cells, hh, err) != 0) return c->fail(TV_ERR_ARG, err);
+  if ((int)hh.color_off.size() - 1 > 64 || (int)hh.fcolor_off.size() - 1 > 64)
+    return c->fail(TV_ERR_ARG, "too many colours");
+  UmGrid& g = c->umg;
+  g.dim = d;
+  g.nv = m->n_vertices;
+  g.nc = m->n_cells;
+  g.nf = (int64_t)hh.fcell.size();
+  for (int a = 0; a < 3; ++a) {
+    std::vector<double> xa((size_t)g.nv);
+    for (int64_t v = 0; v < g.nv; ++v) xa[v] = m->coords[3 * v + a];
+    HIPC(hipMalloc(&c->um_X[a], sizeof(double) * xa.size()));
+    HIPC(hipMemcpy(c->um_X[a], xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice));
+    g.X[a] = c->um_X[a];
+  }
+  HIPC(hipMalloc(&c->um_cell, sizeof(int) * hh.cell.size()));
+  HIPC(hipMemcpy(c->um_cell, hh.cell.data(), sizeof(int) * hh.cell.size(), hipMemcpyHostToDevice));
+  g.cell = c->um_cell;
+  HIPC(hipMalloc(&c->um_fcell, sizeof(int) * std::max<size_t>(1, hh.fcell.size())));
+  HIPC(hipMalloc(&c->um_flf, std::max<size_t>(1, hh.flf.size())));
+  if (!hh.fcell.empty()) {
+    HIPC(hipMemcpy(c->um_fcell, hh.fcell.data(), sizeof(int) * hh.fcell.size(), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(c->um_flf, hh.flf.data(), hh.flf.size(), hipMemcpyHostToDevice));
+  }
+  g.fcell = c->um_fcell;
+  g.flf = c->um_flf;
+  g.ncolor = (int)hh.color_off.size() - 1;
+  g.nfcolor = (int)hh.fcolor_off.size() - 1;
+  for (int k = 0; k <= g.ncolor; ++k) g.color_off[k] = hh.color_off[k];
+  for (int k = 0; k <= g.nfcolor; ++k) g.fcolor_off[k] = hh.fcolor_off[k];
+  // boundary vertices: the vertices of the boundary facets
+  std::vector<unsigned char> bm((size_t)g.nv, 0);
+  for (size_t f = 0; f < hh.fcell.size(); ++f) {
+    const int pos = hh.fcell[f], lf = hh.flf[f];
+    for (int l = 0; l < nl; ++l)
+      if (((l >> (lf >> 1)) & 1) == (lf & 1)) bm[(size_t)hh.cell[(size_t)l * g.nc + pos]] = 1;
+  }
+  HIPC(hipMalloc(&c->um_bmask, bm.size()));
+  HIPC(hipMemcpy(c->um_bmask, bm.data(), bm.size(), hipMemcpyHostToDevice));
+  const tv_params& P = c->P;
+  g.dt = P.dt; g.dt_alpha = P.dt * P.alpha; g.dt_f = P.dt * P.f;
+  g.a_rad = 0.001 * (P.sigma * P.epsilon); g.a_conv = 0.001 * P.htc;
+  g.T_amb = P.T_ambient; g.T_amb4 = P.T_ambient * P.T_ambient * P.T_ambient * P.T_ambient;
+  c->nT = c->nS = g.nv;
+  c->ownT_off = c->ownS_off = 0;
+  c->ownT_n = c->ownS_n = g.nv;
+  c->globT_off = c->globS_off = 0;
+  return TV_OK;
+}
+
+int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
+                           const tv_options* opts, int device, void** ctx_out) {
+  if (!mesh || !fe || !params || !ctx_out) {
+    set_global_error("tv_create_unstructured: null argument");
+    return TV_ERR_ARG;
+  }
+  *ctx_out = nullptr;
+  auto c = std::make_unique<Ctx>();
+  if (fe->T_degree != 1 || fe->sigma_degree != 1) {
+    set_global_error("only degree-1 Lagrange elements are implemented");
+    return TV_ERR_ARG;
+  }
+  if (!(params->dt > 0.0)) {
+    set_global_error("dt must be positive");
+    return TV_ERR_ARG;
+  }
+  c->fam_T = fe->T_family;
+  c->fam_S = fe->sigma_family;
+  c->P = *params;
+  if (opts) c->O = *opts;
+  else tv_default_options(&c->O);
+  c->device = device;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    set_global_error("no HIP device available: libtvfem requires an MI355X (gfx950) GPU");
+    return TV_ERR_HIP;
+  }
+  if (device < 0 || device >= ndev) {
+    set_global_error("device index out of range");
+    return TV_ERR_ARG;
+  }
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    set_global_error("HIP stream/event creation failed");
+    return TV_ERR_HIP;
+  }
+  int rc = setup_umesh(c.get(), mesh);
+  if (rc == TV_OK) rc = setup_fields(c.get());
+  if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
+  if (rc != TV_OK) {
+    set_global_error(c->err);
+    tv_destroy(c.release());
+    return rc;
+  }
+  *ctx_out = c.release();
+  return TV_OK;
+}
+
+int tv_partition_rcb(const tv_umesh_desc* m, int n_parts, int* part_out) {
+  if (!m || !part_out || !m->coords || !m->cells || (m->dim != 2 && m->dim != 3)) {
+    set_global_error("tv_partition_rcb: bad argument");
+    return TV_ERR_ARG;
+  }
+  std::string err;
+  if (um_rcb(m->dim, m->n_vertices, m->coords, m->n_cells, m->cells, n_parts, part_out, err)) {
+    set_global_error(err);
+    return TV_ERR_ARG;
+  }
+  return TV_OK;
+}
+
 int tv_partition_layout(const tv_mesh_desc* m, int64_t* out) {
   if (!m || !out || m->dim < 1 || m->dim > 3 || m->n_parts < 1 || m->part < 0 || m->part >= m->n_parts) {
     set_global_error("tv_partition_layout: invalid arguments");
@@ -1240,8 +1393,13 @@ int tv_destroy(void* ctx) {
   if (c->out) output_destroy(c->out);
   for (int i = 0; i < TV_NUM_FIELDS; ++i)
     if (c->f[i].alloc && c->f[i].ptr) hipFree(c->f[i].ptr);
-  for (double* p : {c->cr[0], c->cr[1], c->cs[0], c->cs[1], c->cw1, c->wsend, c->dB, c->dtmp, c->Tfo})
+  for (double* p : {c->cr[0], c->cr[1], c->cs[0], c->cs[1], c->cw1, c->wsend, c->dB, c->dtmp, c->Tfo, c->um_X[0],
+                    c->um_X[1], c->um_X[2]})
     if (p) hipFree(p);
+  if (c->um_cell) hipFree(c->um_cell);
+  if (c->um_fcell) hipFree(c->um_fcell);
+  if (c->um_flf) hipFree(c->um_flf);
+  if (c->um_bmask) hipFree(c->um_bmask);
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
     if (p) hipFree(p);
   for (int s = 0; s < 3; ++s) {
@@ -1295,6 +1453,10 @@ int tv_dof_coordinates(void* ctx, int space, double* xyz, size_t n_dofs) {
   const int fam = space == 0 ? c->fam_T : c->fam_S;
   const int64_t nown = space == 0 ? c->ownT_n : c->ownS_n;
   if ((int64_t)n_dofs != nown) return c->fail(TV_ERR_ARG, "n_dofs mismatch");
+  if (c->um) {
+    std::memcpy(xyz, c->um_xyz.data(), sizeof(double) * 3 * (size_t)nown);
+    return TV_OK;
+  }
   std::vector<double> tmp;
   const std::vector<double>* X[3];
   std::vector<double> deg(1, 0.0);
@@ -1383,14 +1545,15 @@ int tv_output_open(void* ctx, const char* dir, const int* field_ids, int n_field
   std::vector<std::vector<double>> Xs(3);
   int phys[3];
   std::vector<double> tmp;
-  for (int sx = 0; sx < 3; ++sx) {
+  for (int sx = 0; sx < 3 && !c->um; ++sx) {
     Xs[sx] = storage_coords(c, sx, tmp);
     phys[sx] = c->perm[sx];
   }
-  if (c->fam_T == TV_CG && c->n_parts > 1)
+  if (c->fam_T == TV_CG && c->n_parts > 1 && !c->um)
     Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin, Xs[2].begin() + c->plane_end);
   std::string err;
-  Output* o = output_create(dir, c->dim, Xs, phys, err);
+  Output* o = c->um ? output_create_unstructured(dir, c->dim, c->um_xyz, c->um_cells, err)
+                    : output_create(dir, c->dim, Xs, phys, err);
   if (!o) return c->fail(TV_ERR_STATE, "output: " + err);
   static const char* names[TV_NUM_FIELDS] = {
       "T", "T_prev", "T_next", "Tf", "Tf_prev", "Tf_partial", "Tf_partial_prev", "phi", "phi_next", "xi",
@@ -1629,7 +1792,8 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
   switch (kernel) {
     case 0:  // J(T) x : read x, write y (geometry implicit, T only on boundary nodes)
     case 10:  // the same, timed with the Infinity Cache flushed (tv_time_kernel)
-      *bytes = 16.0 * n;
+      // unstructured: + 32 B vertex ids per cell + 24 B coordinates per vertex
+      *bytes = c->um ? 16.0 * n + 32.0 * (double)c->umg.nc + 24.0 * n : 16.0 * n;
       break;
     case 1: {  // fused visco update, per dof
       int tf = 1;
@@ -1693,7 +1857,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
         op_japply_fused(c, c->f[TV_F_T].ptr, &np, nullptr, 1);  // st->it = 1 below
         return TV_OK;
       case 4: {
-        const FaceAdd fa = (c->fam_T == TV_CG) ? cg_face_add(c->cg, c->ownT_off) : FaceAdd{};
+        const FaceAdd fa = (c->fam_T == TV_CG && !c->um) ? cg_face_add(c->cg, c->ownT_off) : FaceAdd{};
         launch_pcg_update(c->ownT_n, c->st, c->pA + c->ownT_off, c->pB + c->ownT_off, c->w + c->ownT_off,
                           c->dinv + c->ownT_off, c->f[TV_F_DX].ptr + c->ownT_off, c->z + c->ownT_off,
                           c->partials, c->stream, nullptr, &fa, upd_it++);  // even / odd alternate
@@ -1706,7 +1870,8 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     // matvec / update timed inside whole PCG iterations (march then update,
     // alternating, as in the solve), with (5, 6) or without (7, 8) the
     // in-kernel reduction tails (kind 0: reduce only, the state is not touched)
-    if (c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "kernel ids 5-8: CG temperature space only");
+    if (c->fam_T != TV_CG || c->um)
+      return c->fail(TV_ERR_ARG, "kernel ids 5-8: CG temperature space on a rectilinear mesh only");
     const bool tails = kernel <= 6;
     std::vector<hipEvent_t> ev(3 * (size_t)(reps + 1));
     for (auto& e : ev) HIPC(hipEventCreate(&e));

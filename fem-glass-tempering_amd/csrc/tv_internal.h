@@ -142,6 +142,43 @@ struct ViscoFields {
   int* tflag;
 };
 
+// Unstructured CG1 mesh (quadrilaterals / hexahedra of any shape, tv_um.hip):
+// vertex coordinates SoA, cell vertex ids [l][cell] (int32) sorted into
+// colours (no two cells of a colour share a vertex), boundary facets (cell
+// position, local facet 2 * axis + side) sorted into colours likewise.
+struct UmGrid {
+  int dim;
+  int64_t nv, nc, nf;
+  const double* X[3];
+  const int* cell;
+  const int* fcell;
+  const signed char* flf;
+  int ncolor, nfcolor;
+  int64_t color_off[65], fcolor_off[65];
+  double dt, dt_alpha, dt_f;
+  double a_rad, a_conv;
+  double T_amb, T_amb4;
+};
+
+// host side of the colouring (tv_um.hip um_build)
+struct UmHost {
+  std::vector<int> cell;             // [l][cell], coloured order
+  std::vector<int64_t> color_off;    // ncolor + 1
+  std::vector<int> fcell;            // boundary facets: cell position in the coloured order
+  std::vector<signed char> flf;      // local facet
+  std::vector<int64_t> fcolor_off;   // nfcolor + 1
+};
+int um_build(int dim, int64_t nv, int64_t nc, const int64_t* cells, UmHost& out, std::string& err);
+int um_rcb(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* cells, int n_parts, int* part,
+           std::string& err);
+void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
+void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s);
+void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hipStream_t s);
+// p <- z + beta p (iteration it_host's parity buffer), w <- J p, p.w partial
+// records (returns their number; reduced by a separate launch)
+int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
+                           const PcgState* st, double* partials, int it_host, hipStream_t s);
+
 // ---- kernel launchers (tv_cg.hip, tv_dg.hip, tv_visco.hip, tv_pcg.hip) ----
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
@@ -240,6 +277,8 @@ void launch_fill(double* x, int64_t n, double v, hipStream_t s);
 struct Output;
 Output* output_create(const std::string& dir, int dim, const std::vector<std::vector<double>>& Xs, const int* phys,
                       std::string& err);
+Output* output_create_unstructured(const std::string& dir, int dim, const std::vector<double>& xyz,
+                                   const std::vector<int64_t>& cells, std::string& err);
 bool output_add_field(Output* o, const std::string& name, int ncomp, bool dg, size_t n_values, std::string& err);
 bool output_start(Output* o, int device, std::string& err);
 double* output_acquire(Output* o, int* set);

@@ -350,6 +350,29 @@ Output* output_create(const std::string& dir, int dim, const std::vector<std::ve
   return o;
 }
 
+// unstructured mesh: vertices (3 per vertex) and cells (2^dim per cell, tensor
+// order) as given; cells written in VTK vertex order
+Output* output_create_unstructured(const std::string& dir, int dim, const std::vector<double>& xyz,
+                                   const std::vector<int64_t>& cells, std::string& err) {
+  auto* o = new Output();
+  o->series.dir = dir;
+  o->series.dim = dim;
+  static const int vtk[8] = {0, 1, 3, 2, 4, 5, 7, 6};
+  const int npc = 1 << dim;
+  std::vector<int64_t> vc(cells.size());
+  for (size_t e = 0; e < cells.size() / npc; ++e)
+    for (int q = 0; q < npc; ++q) vc[e * npc + q] = cells[e * npc + vtk[q]];
+  o->series.n_nodes = (int64_t)xyz.size() / 3;
+  o->series.n_cells = (int64_t)(cells.size() / npc);
+  o->series.n_dnodes = 0;
+  if (!o->series.write_mesh("mesh", xyz, vc)) {
+    err = o->series.err;
+    delete o;
+    return nullptr;
+  }
+  return o;
+}
+
 bool output_add_field(Output* o, const std::string& name, int ncomp, bool dg, size_t n_values, std::string& err) {
   if (!o->series.open_field(name, ncomp, dg)) {
     err = o->series.err;

@@ -28,7 +28,7 @@ FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 
 # every C symbol include/tvfem.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "tv_abi_version", "tv_last_error", "tv_default_options", "tv_default_params", "tv_create", "tv_destroy",
+    "tv_abi_version", "tv_last_error", "tv_default_options", "tv_default_params", "tv_create", "tv_create_unstructured", "tv_partition_rcb", "tv_destroy",
     "tv_num_dofs", "tv_field_block_size", "tv_dof_coordinates", "tv_set_field", "tv_get_field",
     "tv_field_device_ptr", "tv_set_initial_condition", "tv_sync", "tv_residual", "tv_jacobian_apply",
     "tv_jacobian_diag", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
@@ -52,6 +52,11 @@ class NativeError(RuntimeError):
 class MeshDesc(C.Structure):
     _fields_ = [("dim", C.c_int), ("n_cells", C.c_int * 3), ("coords", C.POINTER(C.c_double) * 3),
                 ("part_axis", C.c_int), ("n_parts", C.c_int), ("part", C.c_int)]
+
+
+class UMeshDesc(C.Structure):
+    _fields_ = [("dim", C.c_int), ("n_vertices", C.c_int64), ("coords", C.POINTER(C.c_double)),
+                ("n_cells", C.c_int64), ("cells", C.POINTER(C.c_int64))]
 
 
 class FeConfig(C.Structure):
@@ -103,6 +108,9 @@ def load_library():
         "tv_last_error": (C.c_char_p, [vp]),
         "tv_default_options": (None, [C.POINTER(Options)]),
         "tv_default_params": (None, [C.POINTER(Params)]),
+        "tv_create_unstructured": (C.c_int, [C.POINTER(UMeshDesc), C.POINTER(FeConfig), C.POINTER(Params),
+                                             C.POINTER(Options), C.c_int, C.POINTER(C.c_void_p)]),
+        "tv_partition_rcb": (C.c_int, [C.POINTER(UMeshDesc), C.c_int, C.POINTER(C.c_int)]),
         "tv_create": (C.c_int, [C.POINTER(MeshDesc), C.POINTER(FeConfig), C.POINTER(Params), C.POINTER(Options),
                                 C.c_int, C.POINTER(vp)]),
         "tv_destroy": (C.c_int, [vp]),

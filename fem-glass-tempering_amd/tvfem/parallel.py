@@ -40,6 +40,51 @@ def partition_layout(mesh, n_parts: int, part: int, part_axis: int = -1) -> dict
             "n_local": v[10], "ghost_lo": bool(v[11]), "ghost_hi": bool(v[12])}
 
 
+def umesh_desc(mesh):
+    """(tv_umesh_desc, buffers to keep alive) of a tvfem.UnstructuredMesh."""
+    desc = N.UMeshDesc()
+    desc.dim = mesh.dim
+    xyz = np.ascontiguousarray(mesh.x, dtype=np.float64)
+    cells = np.ascontiguousarray(mesh.cells, dtype=np.int64)
+    desc.n_vertices = xyz.shape[0]
+    desc.coords = xyz.ctypes.data_as(C.POINTER(C.c_double))
+    desc.n_cells = cells.shape[0]
+    desc.cells = cells.ctypes.data_as(C.POINTER(C.c_int64))
+    return desc, (xyz, cells)
+
+
+def rcb_partition(mesh, n_parts: int) -> np.ndarray:
+    """Cell -> part ids (int32) of an unstructured mesh by recursive coordinate
+    bisection (tv_partition_rcb, host only).  Parts differ in size by at most
+    one cell per bisection level."""
+    lib = N.load_library()
+    desc, keep = umesh_desc(mesh)
+    part = np.empty(mesh.num_cells, dtype=np.int32)
+    N.check(lib.tv_partition_rcb(C.byref(desc), int(n_parts), part.ctypes.data_as(C.POINTER(C.c_int))))
+    del keep
+    return part
+
+
+def partition_submesh(mesh, part: np.ndarray, p: int):
+    """Local mesh of part ``p``: its cells, the vertices they touch (owned
+    vertices first, then ghosts) and the local -> global vertex map.  A vertex
+    is owned by the lowest part among the cells that touch it (the dolfinx
+    convention is the owner rank chosen by its distributed vertex numbering)."""
+    from .mesh import UnstructuredMesh
+    nv = mesh.num_vertices
+    owner = np.full(nv, np.iinfo(np.int32).max, dtype=np.int64)
+    np.minimum.at(owner, mesh.cells.ravel(), np.repeat(part.astype(np.int64), mesh.cells.shape[1]))
+    cells = mesh.cells[part == p]
+    used = np.unique(cells.ravel())
+    own = used[owner[used] == p]
+    ghost = used[owner[used] != p]
+    l2g = np.concatenate([own, ghost])
+    g2l = np.full(nv, -1, dtype=np.int64)
+    g2l[l2g] = np.arange(len(l2g))
+    sub = UnstructuredMesh(mesh.dim, mesh.x[l2g], g2l[cells])
+    return {"mesh": sub, "l2g": l2g, "n_owned": len(own), "ghost_owner": owner[ghost]}
+
+
 def init_rccl(problem, rank: int, world: int, dist=None):
     """Create the RCCL communicator of a partitioned problem (rank 0 makes the id)."""
     if dist is None:

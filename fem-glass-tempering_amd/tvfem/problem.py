@@ -32,7 +32,7 @@ except Exception:  # pragma: no cover
     _xxhash = None
 
 from . import _native as N
-from .mesh import RectilinearMesh, read_msh
+from .mesh import RectilinearMesh, UnstructuredMesh, read_msh
 from .models import ThermalModel, ViscoelasticModel
 
 _FAMILIES = {"CG": N.TV_CG, "DG": N.TV_DG}
@@ -103,12 +103,12 @@ class ThermoViscoProblem:
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
                  write_output: bool = False, output_dir: str = "output") -> None:
-        if isinstance(mesh_path, RectilinearMesh):
+        if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
             self.mesh = read_msh(mesh_path)
         else:
-            raise TypeError("mesh_path must be a .msh path or a tvfem.RectilinearMesh")
+            raise TypeError("mesh_path must be a .msh path, a tvfem.RectilinearMesh or a tvfem.UnstructuredMesh")
         self.dim = self.mesh.dim
         self.dt = dt
         self.time = time
@@ -158,20 +158,39 @@ class ThermoViscoProblem:
     def __init_native(self, mp, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant):
         lib = N.load_library()
         self._lib = lib
-        desc = N.MeshDesc()
-        desc.dim = self.dim
-        self._coord_bufs = []
-        for a in range(3):
-            if a < self.dim:
-                buf = np.ascontiguousarray(self.mesh.axes[a])
-                self._coord_bufs.append(buf)
-                desc.n_cells[a] = len(buf) - 1
-                desc.coords[a] = buf.ctypes.data_as(C.POINTER(C.c_double))
-            else:
-                desc.n_cells[a] = 0
-        desc.part_axis = part_axis
-        desc.n_parts = n_parts
-        desc.part = part
+        um = isinstance(self.mesh, UnstructuredMesh)
+        if um:
+            # general quadrilateral / hexahedral cells: element-local kernels
+            # (csrc/tv_um.hip), one partition, CG1 spaces
+            if n_parts != 1:
+                raise NotImplementedError("unstructured meshes run on one partition (see tvfem.parallel.rcb_partition)")
+            if self._fam["T"] != "CG" or self._fam["sigma"] != "CG":
+                raise NotImplementedError("unstructured meshes: CG temperature and stress spaces")
+            desc = N.UMeshDesc()
+            desc.dim = self.dim
+            xyz = np.zeros((self.mesh.num_vertices, 3))
+            xyz[:, :self.dim] = self.mesh.x[:, :self.dim]
+            cells = np.ascontiguousarray(self.mesh.cells, dtype=np.int64)
+            self._coord_bufs = [xyz, cells]
+            desc.n_vertices = xyz.shape[0]
+            desc.coords = xyz.ctypes.data_as(C.POINTER(C.c_double))
+            desc.n_cells = cells.shape[0]
+            desc.cells = cells.ctypes.data_as(C.POINTER(C.c_int64))
+        else:
+            desc = N.MeshDesc()
+            desc.dim = self.dim
+            self._coord_bufs = []
+            for a in range(3):
+                if a < self.dim:
+                    buf = np.ascontiguousarray(self.mesh.axes[a])
+                    self._coord_bufs.append(buf)
+                    desc.n_cells[a] = len(buf) - 1
+                    desc.coords[a] = buf.ctypes.data_as(C.POINTER(C.c_double))
+                else:
+                    desc.n_cells[a] = 0
+            desc.part_axis = part_axis
+            desc.n_parts = n_parts
+            desc.part = part
         self._n_parts, self._part = n_parts, part
         fe = N.FeConfig(_FAMILIES[self._fam["T"]], 1, _FAMILIES[self._fam["sigma"]], 1)
         params = N.default_params(mp, self.dt)
@@ -182,7 +201,8 @@ class ThermoViscoProblem:
                             "single": N.TV_PCG_SINGLE_REDUCTION}[pcg_variant]
         opts.model_mode = N.TV_MODEL_PAPER if self.model_mode == "paper" else N.TV_MODEL_REFERENCE
         ctx = C.c_void_p()
-        N.check(lib.tv_create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
+        create = lib.tv_create_unstructured if um else lib.tv_create
+        N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
         self._ctx = ctx
         self.materialize = materialize
         self._bs = {}

@@ -82,6 +82,20 @@ typedef struct {
   int part;
 } tv_mesh_desc;
 
+/* Unstructured mesh: quadrilaterals (dim 2) or hexahedra (dim 3) of any
+ * shape, as gmsh writes them (geometry.py / gmshio.read_from_msh at
+ * ThermoViscoProblem.py:27-28).  coords: 3 doubles per vertex; cells: 2^dim
+ * vertex ids per cell in the tensor local order l = a + 2b + 4c (basix /
+ * dolfinx order).  One partition, CG1 temperature and stress spaces;
+ * assembled by the element-local kernels (csrc/tv_um.hip). */
+typedef struct {
+  int dim;
+  int64_t n_vertices;
+  const double* coords;
+  int64_t n_cells;
+  const int64_t* cells;
+} tv_umesh_desc;
+
 typedef struct {
   int T_family;      /* TV_CG / TV_DG  (fe_config["T"]["element"])      */
   int T_degree;      /* must be 1                                        */
@@ -177,6 +191,8 @@ void tv_default_params(tv_params* p);            /* main.py:29-55 + tableaux */
 
 int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
               const tv_options* opts, int device, void** ctx_out);
+int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
+                           const tv_options* opts, int device, void** ctx_out);
 int tv_destroy(void* ctx);
 
 /* Host-only (no GPU needed): layout of partition `part` of a CG1 mesh —
@@ -184,6 +200,11 @@ int tv_destroy(void* ctx);
  * nodes per storage axis, out[6..7] owned node planes [b0, b1) along storage
  * axis 2, out[8] global offset of the first owned dof, out[9] owned dofs,
  * out[10] local dofs incl. ghost planes, out[11..12] ghost plane below/above. */
+/* Host only (no GPU): recursive coordinate bisection of the cells of an
+ * unstructured mesh into n_parts balanced parts (part_out: n_cells ids).
+ * Replaces the graph partitioner dolfinx applies when it distributes the mesh
+ * read at ThermoViscoProblem.py:27-28. */
+int tv_partition_rcb(const tv_umesh_desc* mesh, int n_parts, int* part_out);
 int tv_partition_layout(const tv_mesh_desc* mesh, int64_t* out13);
 
 /* sizes: owned dofs of the T space / sigma space on this partition; block
