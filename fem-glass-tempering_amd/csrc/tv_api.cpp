@@ -100,9 +100,7 @@ struct Ctx {
   UmGrid umg{};
   std::vector<double> um_xyz;        // host copy: 3 per vertex
   std::vector<int64_t> um_cells;     // host copy: 2^dim per cell (input order)
-  double* um_X[3] = {nullptr, nullptr, nullptr};
-  int *um_cell = nullptr, *um_fcell = nullptr;
-  signed char* um_flf = nullptr;
+  UmDevice* umd = nullptr;            // assembled operators, facet data (tv_um.hip)
   unsigned char* um_bmask = nullptr;  // boundary vertices (Dirichlet mode)
   std::vector<int> out_fields;
   double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
@@ -486,7 +484,7 @@ static int setup_fields(Ctx* c) {
   c->f[TV_F_RESIDUAL].ptr = c->r; c->f[TV_F_RESIDUAL].bs = 1; c->f[TV_F_RESIDUAL].space = 0;
   if (int e = alloc_field(c, TV_F_DX, 0, 1)) return e;
   int np = kVecBlocksMax;
-  if (c->um) np = std::max(np, 1024);
+  if (c->um) np = std::max(np, um_num_blocks(c->umg));
   else if (c->fam_T == TV_CG) np = std::max(np, cg_num_blocks(c->cg, true));
   else np = std::max(np, dg_num_blocks(c->dg));
   c->n_partials_cap = np;
@@ -675,9 +673,9 @@ static void op_japply(Ctx* c, const double* T, const double* x, double* y, doubl
   else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
 }
 static bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr, int it = 0) {
-  if (c->um) {  // separate p update, coloured J p, p.w records (reduced by the caller)
-    *np = launch_um_japply_fused(c->umg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, it, c->stream);
-    return false;
+  if (c->um) {  // p <- z + b p, w <- J p, p.w and the reduction tail in one launch
+    *np = launch_um_japply_fused(c->umg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, it, tail, c->stream);
+    return tail && tail->counter;
   }
   if (c->fam_T == TV_CG)
     return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail, it);
@@ -1246,51 +1244,18 @@ static int setup_umesh(Ctx* c, const tv_umesh_desc* m) {
   c->dim = d;
   c->um_xyz.assign(m->coords, m->coords + 3 * m->n_vertices);
   c->um_cells.assign(m->cells, m->cells + m->n_cells * nl);
-  UmHost hh;
-  std::string err;
-  if (um_build(d, m->n_vertices, m->n_cells, m->cells, hh, err) != 0) return c->fail(TV_ERR_ARG, err);
-  if ((int)hh.color_off.size() - 1 > 64 || (int)hh.fcolor_off.size() - 1 > 64)
-    return c->fail(TV_ERR_ARG, "too many colours");
-  UmGrid& g = c->umg;
-  g.dim = d;
-  g.nv = m->n_vertices;
-  g.nc = m->n_cells;
-  g.nf = (int64_t)hh.fcell.size();
-  for (int a = 0; a < 3; ++a) {
-    std::vector<double> xa((size_t)g.nv);
-    for (int64_t v = 0; v < g.nv; ++v) xa[v] = m->coords[3 * v + a];
-    HIPC(hipMalloc(&c->um_X[a], sizeof(double) * xa.size()));
-    HIPC(hipMemcpy(c->um_X[a], xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice));
-    g.X[a] = c->um_X[a];
-  }
-  HIPC(hipMalloc(&c->um_cell, sizeof(int) * hh.cell.size()));
-  HIPC(hipMemcpy(c->um_cell, hh.cell.data(), sizeof(int) * hh.cell.size(), hipMemcpyHostToDevice));
-  g.cell = c->um_cell;
-  HIPC(hipMalloc(&c->um_fcell, sizeof(int) * std::max<size_t>(1, hh.fcell.size())));
-  HIPC(hipMalloc(&c->um_flf, std::max<size_t>(1, hh.flf.size())));
-  if (!hh.fcell.empty()) {
-    HIPC(hipMemcpy(c->um_fcell, hh.fcell.data(), sizeof(int) * hh.fcell.size(), hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(c->um_flf, hh.flf.data(), hh.flf.size(), hipMemcpyHostToDevice));
-  }
-  g.fcell = c->um_fcell;
-  g.flf = c->um_flf;
-  g.ncolor = (int)hh.color_off.size() - 1;
-  g.nfcolor = (int)hh.fcolor_off.size() - 1;
-  for (int k = 0; k <= g.ncolor; ++k) g.color_off[k] = hh.color_off[k];
-  for (int k = 0; k <= g.nfcolor; ++k) g.fcolor_off[k] = hh.fcolor_off[k];
-  // boundary vertices: the vertices of the boundary facets
-  std::vector<unsigned char> bm((size_t)g.nv, 0);
-  for (size_t f = 0; f < hh.fcell.size(); ++f) {
-    const int pos = hh.fcell[f], lf = hh.flf[f];
-    for (int l = 0; l < nl; ++l)
-      if (((l >> (lf >> 1)) & 1) == (lf & 1)) bm[(size_t)hh.cell[(size_t)l * g.nc + pos]] = 1;
-  }
-  HIPC(hipMalloc(&c->um_bmask, bm.size()));
-  HIPC(hipMemcpy(c->um_bmask, bm.data(), bm.size(), hipMemcpyHostToDevice));
   const tv_params& P = c->P;
+  UmGrid& g = c->umg;
   g.dt = P.dt; g.dt_alpha = P.dt * P.alpha; g.dt_f = P.dt * P.f;
   g.a_rad = 0.001 * (P.sigma * P.epsilon); g.a_conv = 0.001 * P.htc;
   g.T_amb = P.T_ambient; g.T_amb4 = P.T_ambient * P.T_ambient * P.T_ambient * P.T_ambient;
+  std::string err;
+  if (um_setup(d, m->n_vertices, m->coords, m->n_cells, m->cells, g, c->umd, c->stream, err) != 0)
+    return c->fail(err.rfind("HIP", 0) == 0 ? TV_ERR_HIP : TV_ERR_ARG, err);
+  std::vector<unsigned char> bm;
+  um_boundary_vertices(c->umd, bm);
+  HIPC(hipMalloc(&c->um_bmask, bm.size()));
+  HIPC(hipMemcpy(c->um_bmask, bm.data(), bm.size(), hipMemcpyHostToDevice));
   c->nT = c->nS = g.nv;
   c->ownT_off = c->ownS_off = 0;
   c->ownT_n = c->ownS_n = g.nv;
@@ -1393,12 +1358,9 @@ int tv_destroy(void* ctx) {
   if (c->out) output_destroy(c->out);
   for (int i = 0; i < TV_NUM_FIELDS; ++i)
     if (c->f[i].alloc && c->f[i].ptr) hipFree(c->f[i].ptr);
-  for (double* p : {c->cr[0], c->cr[1], c->cs[0], c->cs[1], c->cw1, c->wsend, c->dB, c->dtmp, c->Tfo, c->um_X[0],
-                    c->um_X[1], c->um_X[2]})
+  for (double* p : {c->cr[0], c->cr[1], c->cs[0], c->cs[1], c->cw1, c->wsend, c->dB, c->dtmp, c->Tfo})
     if (p) hipFree(p);
-  if (c->um_cell) hipFree(c->um_cell);
-  if (c->um_fcell) hipFree(c->um_fcell);
-  if (c->um_flf) hipFree(c->um_flf);
+  um_free(c->umd);
   if (c->um_bmask) hipFree(c->um_bmask);
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
     if (p) hipFree(p);
@@ -1792,8 +1754,9 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
   switch (kernel) {
     case 0:  // J(T) x : read x, write y (geometry implicit, T only on boundary nodes)
     case 10:  // the same, timed with the Infinity Cache flushed (tv_time_kernel)
-      // unstructured: + 32 B vertex ids per cell + 24 B coordinates per vertex
-      *bytes = c->um ? 16.0 * n + 32.0 * (double)c->umg.nc + 24.0 * n : 16.0 * n;
+      // unstructured: + the assembled cell operator (8 B value + 4 B column per
+      // stored SELL entry, padding included) and the Robin data of the boundary
+      *bytes = c->um ? 16.0 * n + 12.0 * (double)um_nnz(c->umd) : 16.0 * n;
       break;
     case 1: {  // fused visco update, per dof
       int tf = 1;

@@ -142,42 +142,51 @@ struct ViscoFields {
   int* tflag;
 };
 
-// Unstructured CG1 mesh (quadrilaterals / hexahedra of any shape, tv_um.hip):
-// vertex coordinates SoA, cell vertex ids [l][cell] (int32) sorted into
-// colours (no two cells of a colour share a vertex), boundary facets (cell
-// position, local facet 2 * axis + side) sorted into colours likewise.
+// Unstructured CG1 mesh (quadrilaterals / hexahedra of any shape, tv_um.hip).
+// The cell part of J(T) = M + dt alpha K does not depend on T: it is assembled
+// once, at context creation, into SELL-64 (sliced ELLPACK, one 64-row slice
+// per wavefront, column-major inside a slice so a wave's loads are coalesced).
+// The T-dependent Robin terms are evaluated on the fly from per-facet
+// quadrature weights, row by row (boundary rows only).
 struct UmGrid {
   int dim;
-  int64_t nv, nc, nf;
-  const double* X[3];
-  const int* cell;
-  const int* fcell;
-  const signed char* flf;
-  int ncolor, nfcolor;
-  int64_t color_off[65], fcolor_off[65];
+  int64_t nv, nc, nf, nslice;
+  // assembled cell operators (entry k of row r: soff[r / 64] + 64 k + r % 64)
+  const int64_t* soff;   // nslice + 1
+  const int* cols;
+  const double* V;       // M + dt alpha K  (J x)
+  const double* M;       // mass            (residual)
+  const double* K;       // dt alpha K      (residual)
+  const double* bvec;    // int phi_i       (f term of the residual)
+  const double* vdiag;   // diag V
+  // Robin terms
+  const int* fv;         // [m][facet] facet vertex ids, facet-local tensor order
+  const double* fw;      // [q][facet] w_q |J_s|(q), 3^(d-1) points
+  const int* boff;       // nv + 1: boundary incidences of each row
+  const int* binc;       // 4 facet + m
   double dt, dt_alpha, dt_f;
   double a_rad, a_conv;
   double T_amb, T_amb4;
 };
 
-// host side of the colouring (tv_um.hip um_build)
-struct UmHost {
-  std::vector<int> cell;             // [l][cell], coloured order
-  std::vector<int64_t> color_off;    // ncolor + 1
-  std::vector<int> fcell;            // boundary facets: cell position in the coloured order
-  std::vector<signed char> flf;      // local facet
-  std::vector<int64_t> fcolor_off;   // nfcolor + 1
-};
-int um_build(int dim, int64_t nv, int64_t nc, const int64_t* cells, UmHost& out, std::string& err);
+struct UmDevice;  // device allocations of one unstructured mesh (tv_um.hip)
+// builds the operators on the device (stream s, synchronised before return)
+int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g, UmDevice*& dev,
+             hipStream_t s, std::string& err);
+void um_free(UmDevice* dev);
+int64_t um_boundary_vertices(const UmDevice* dev, std::vector<unsigned char>& mask);  // host mask, returns count
+int64_t um_nnz(const UmDevice* dev);                       // stored entries incl. SELL padding
+int um_num_blocks(const UmGrid& g);                        // partial records of the fused launch
 int um_rcb(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* cells, int n_parts, int* part,
            std::string& err);
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s);
 void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hipStream_t s);
-// p <- z + beta p (iteration it_host's parity buffer), w <- J p, p.w partial
-// records (returns their number; reduced by a separate launch)
+// p <- z + beta p (iteration it_host's parity buffer), w <- J p, p.w; the
+// reduction tail (rt.counter != nullptr) reduces the records and runs the
+// logic.  Returns the number of partial records.
 int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
-                           const PcgState* st, double* partials, int it_host, hipStream_t s);
+                           const PcgState* st, double* partials, int it_host, const RedTail* tail, hipStream_t s);
 
 // ---- kernel launchers (tv_cg.hip, tv_dg.hip, tv_visco.hip, tv_pcg.hip) ----
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);

@@ -1,37 +1,52 @@
 // CG1 (Q1 quadrilateral / hexahedral) operators on UNSTRUCTURED meshes, gfx950:
-// the element-local path for meshes that are not tensor-product grids (gmsh
-// .msh input, distorted cells).
+// the path for meshes that are not tensor-product grids (gmsh .msh input,
+// distorted cells).
 //
 // Replaces, for such meshes, the FFCx cell kernel of F dx and its Jacobian
-// (ThermoViscoProblem.py:295-300, ufl.derivative at :331) and the exterior-facet
-// kernels of the Robin terms (:302-304), with the dolfinx assembly loops around
-// them [3P]: gather the cell's vertex coordinates and dofs, evaluate the
-// isoparametric element integral, scatter-add into the global vector.
+// (ThermoViscoProblem.py:295-300, ufl.derivative at :331), the exterior-facet
+// kernels of the Robin terms (:302-304) and the assembled PETSc matrix that
+// dolfinx's NonlinearProblem hands to KSP (:331-343) [3P].
 //
-// * One thread per cell: 2^d vertex ids (int32, [l][cell] layout: coalesced),
-//   their coordinates and values gathered; the element integral with 3-point
-//   Gauss per direction and the isoparametric Jacobian at every point (the
-//   oracle's rule, oracle/tv_oracle.py HeatForm, so the two agree to rounding
-//   on distorted cells); the 2^d results are added into the output vector.
-// * Scatter without atomics: the cells are sorted into colours (no two cells of
-//   a colour share a vertex, greedy colouring at context creation) and each
-//   colour is one launch, so every add is a plain read-modify-write with no
-//   conflict and the summation order is fixed (bitwise reproducible).
-// * Robin facets: one thread per boundary facet (3-point Gauss per tangential
-//   direction, surface measure |det J| |J^-T e_n| as the oracle), coloured the
-//   same way.
-// Algorithmic bytes of J x: 8 N (x) + 8 N (y) + 32 per cell
-// (vertex ids) + 24 per vertex (coordinates) = ~72 B per cell on a hex mesh.
+// Design (measured).  A matrix-free isoparametric J x --
+// 27 Gauss points per hexahedron, the Jacobian, its inverse and the physical
+// gradients at each -- costs ~16 kflop per cell: fp64-FLOP bound, 2.6 ms per
+// J x at 8M cells (2 % of the HBM roofline of its 72 B per cell).  The cell
+// part of J(T) is M + dt alpha K, independent of T, so it is assembled ONCE at
+// context creation into SELL-64 (sliced ELLPACK: 64-row slices = one
+// wavefront, column-major inside a slice, so the value / column loads of a
+// wave are 512 B / 256 B coalesced) and J x streams 12 B per stored entry
+// (~27 per row) at HBM speed.  The T-dependent Robin terms are evaluated on
+// the fly, row by row, from per-facet quadrature weights w_q |J_s| stored at
+// setup (boundary rows only).  Every row is owned by one lane: no atomics, no
+// colouring, the summation order is fixed (bitwise reproducible).
+//  * J x  (japply / the fused PCG matvec): V = M + dt alpha K;
+//  * F(T) (residual): M (T - T_prev) + (dt alpha K) T - dt f int phi + Robin, with
+//    M and dt alpha K kept apart so T - T_prev is formed before the product
+//    (no cancellation at T ~ T_prev);
+//  * diag J: diag V + the Robin diagonal.
+// Assembly: one thread per row gathers the rows of the element matrices of the
+// cells around its vertex (3-point Gauss per direction and the isoparametric
+// Jacobian, the oracle's rule, oracle/tv_oracle.py HeatForm) in cell order.
 #include <algorithm>
 #include <cstdio>
+#include <thread>
 #include <vector>
 
 #include "tv_device.h"
 
 namespace tv {
+
+struct UmDevice {
+  std::vector<void*> bufs;            // freed by um_free
+  std::vector<unsigned char> bmask;   // host: vertices on the boundary
+  int64_t nnz = 0;                    // stored entries (incl. SELL padding)
+  int64_t nb = 0;                     // boundary vertices
+};
+
 namespace {
 
-enum { UM_RES = 0, UM_JAC = 1, UM_DIAG = 2 };
+enum { UM_RES = 0, UM_JAC = 1, UM_DIAG = 2, UM_FUSED = 3 };
+constexpr int kUmBlocksMax = 2048;  // grid cap of the row kernels (partial records of the fused launch)
 
 __device__ constexpr double kUX[3] = {0.11270166537925831148, 0.5, 0.88729833462074168852};
 __device__ constexpr double kUW[3] = {5.0 / 18.0, 8.0 / 18.0, 5.0 / 18.0};
@@ -101,29 +116,17 @@ __device__ __forceinline__ double inv_det(const double (&J)[D][D], double (&Ji)[
   }
 }
 
-// cell term of one colour: out[v] += element vector (RES: F dx part, JAC: J x,
-// DIAG: diag J) -- ThermoViscoProblem.py:295-300 and its derivative
-template <int D, int MODE>
-__global__ __launch_bounds__(kBlock) void k_um_cells(UmGrid g, const double* __restrict__ u,
-                                                     const double* __restrict__ up, double* __restrict__ out,
-                                                     int64_t c0, int64_t c1) {
+
+// ---- setup kernels -----------------------------------------------------------------
+// row l of the element matrices of a cell: Ml[j] = int phi_l phi_j,
+// Kl[j] = int grad phi_l . grad phi_j
+template <int D>
+__device__ __forceinline__ void elem_row(const double (&X)[1 << D][D], int l, double (&Ml)[1 << D],
+                                         double (&Kl)[1 << D]) {
   constexpr int NL = 1 << D;
-  const int64_t e = c0 + blockIdx.x * (int64_t)kBlock + threadIdx.x;
-  if (e >= c1) return;
-  int nd[NL];
-  double X[NL][D], val[NL], mv[NL];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) {
-    nd[l] = g.cell[(int64_t)l * g.nc + e];
-#pragma unroll
-    for (int a = 0; a < D; ++a) X[l][a] = g.X[a][nd[l]];
-    val[l] = (MODE == UM_DIAG) ? 0.0 : u[nd[l]];
-    mv[l] = (MODE == UM_RES) ? val[l] - up[nd[l]] : val[l];
-  }
-  double y[NL];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) y[l] = 0.0;
   constexpr int NQ = (D == 2) ? 9 : 27;
+#pragma unroll
+  for (int j = 0; j < NL; ++j) Ml[j] = Kl[j] = 0.0;
 #pragma unroll 1
   for (int q = 0; q < NQ; ++q) {
     const int qi[3] = {q % 3, (q / 3) % 3, q / 9};
@@ -142,79 +145,126 @@ __global__ __launch_bounds__(kBlock) void k_um_cells(UmGrid g, const double* __r
       for (int b = 0; b < D; ++b) {
         double s = 0.0;
 #pragma unroll
-        for (int l = 0; l < NL; ++l) s += X[l][a] * dphi[l][b];
+        for (int m = 0; m < NL; ++m) s += X[m][a] * dphi[m][b];
         J[a][b] = s;
       }
     double Ji[D][D];
     const double wd = w * fabs(inv_det<D>(J, Ji));
-    // physical gradients: grad phi_l = J^-T dphi_l
-    double gp[NL][D];
+    double gp[NL][D];  // grad phi = J^-T dphi
 #pragma unroll
-    for (int l = 0; l < NL; ++l)
+    for (int m = 0; m < NL; ++m)
 #pragma unroll
       for (int a = 0; a < D; ++a) {
         double s = 0.0;
 #pragma unroll
-        for (int b = 0; b < D; ++b) s += Ji[b][a] * dphi[l][b];
-        gp[l][a] = s;
+        for (int b = 0; b < D; ++b) s += Ji[b][a] * dphi[m][b];
+        gp[m][a] = s;
       }
-    if (MODE == UM_DIAG) {
+    double phil = 0.0, gl[D];
 #pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        double gg = 0.0;
+    for (int a = 0; a < D; ++a) gl[a] = 0.0;
 #pragma unroll
-        for (int a = 0; a < D; ++a) gg += gp[l][a] * gp[l][a];
-        y[l] += wd * (phi[l] * phi[l] + g.dt_alpha * gg);
+    for (int m = 0; m < NL; ++m)
+      if (m == l) {
+        phil = phi[m];
+#pragma unroll
+        for (int a = 0; a < D; ++a) gl[a] = gp[m][a];
       }
-    } else {
-      double mq = 0.0, gu[D];
 #pragma unroll
-      for (int a = 0; a < D; ++a) gu[a] = 0.0;
+    for (int j = 0; j < NL; ++j) {
+      double gg = 0.0;
 #pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        mq += phi[l] * mv[l];
-#pragma unroll
-        for (int a = 0; a < D; ++a) gu[a] += gp[l][a] * val[l];
-      }
-      if (MODE == UM_RES) mq -= g.dt_f;
-#pragma unroll
-      for (int l = 0; l < NL; ++l) {
-        double gg = 0.0;
-#pragma unroll
-        for (int a = 0; a < D; ++a) gg += gp[l][a] * gu[a];
-        y[l] += wd * (phi[l] * mq + g.dt_alpha * gg);
-      }
+      for (int a = 0; a < D; ++a) gg += gl[a] * gp[j][a];
+      Ml[j] += wd * (phil * phi[j]);
+      Kl[j] += wd * gg;
     }
   }
-#pragma unroll
-  for (int l = 0; l < NL; ++l) out[nd[l]] += y[l];
 }
 
-// Robin facets of one colour (ThermoViscoProblem.py:302-304 and derivative)
-template <int D, int MODE>
-__global__ __launch_bounds__(kBlock) void k_um_facets(UmGrid g, const double* __restrict__ T,
-                                                      const double* __restrict__ x, double* __restrict__ out,
-                                                      int64_t f0, int64_t f1) {
+// one thread per row: sums the element rows of the cells around the vertex
+// (incidences in cell order) into the row's SELL entries, then V = M + K,
+// diag V and int phi_r
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_um_assemble(int64_t nv, int64_t nc, const int* __restrict__ cell,
+                                                        const double* __restrict__ X0, const double* __restrict__ X1,
+                                                        const double* __restrict__ X2,
+                                                        const int64_t* __restrict__ inc_off,
+                                                        const int64_t* __restrict__ inc,
+                                                        const int64_t* __restrict__ soff, const int* __restrict__ cols,
+                                                        const int* __restrict__ rnnz, double dt_alpha,
+                                                        double* __restrict__ V, double* __restrict__ M,
+                                                        double* __restrict__ K, double* __restrict__ bvec,
+                                                        double* __restrict__ vdiag) {
   constexpr int NL = 1 << D;
-  const int64_t f = f0 + blockIdx.x * (int64_t)kBlock + threadIdx.x;
-  if (f >= f1) return;
-  const int64_t e = g.fcell[f];
-  const int lf = g.flf[f];
+  const int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (r >= nv) return;
+  const int64_t base = soff[r >> 6] + (r & 63);
+  const int nz = rnnz[r];
+  const double* Xa[3] = {X0, X1, X2};
+  for (int64_t t = inc_off[r]; t < inc_off[r + 1]; ++t) {
+    const int64_t e = inc[t] >> 3;
+    const int l = (int)(inc[t] & 7);
+    int nd[NL];
+    double X[NL][D];
+#pragma unroll
+    for (int m = 0; m < NL; ++m) {
+      nd[m] = cell[(int64_t)m * nc + e];
+#pragma unroll
+      for (int a = 0; a < D; ++a) X[m][a] = Xa[a][nd[m]];
+    }
+    double Ml[NL], Kl[NL];
+    elem_row<D>(X, l, Ml, Kl);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      int lo = 0, hi = nz;  // columns of the row are sorted
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cols[base + 64 * (int64_t)mid] < nd[j]) lo = mid + 1;
+        else hi = mid;
+      }
+      const int64_t idx = base + 64 * (int64_t)lo;
+      M[idx] += Ml[j];
+      K[idx] += dt_alpha * Kl[j];
+    }
+  }
+  double b = 0.0;
+  for (int k = 0; k < nz; ++k) {
+    const int64_t idx = base + 64 * (int64_t)k;
+    const double v = M[idx] + K[idx];
+    V[idx] = v;
+    b += M[idx];
+    if (cols[idx] == (int)r) vdiag[r] = v;
+  }
+  bvec[r] = b;
+}
+
+// one thread per boundary facet: its vertex ids in facet-local tensor order
+// and w_q |J_s|(q) = w_q |det J| |J^-T e_n| at its 3^(d-1) points (the
+// oracle's facet measure)
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_um_facet_setup(int64_t nf, int64_t nc, const int* __restrict__ fcell,
+                                                           const signed char* __restrict__ flf,
+                                                           const int* __restrict__ cell, const double* __restrict__ X0,
+                                                           const double* __restrict__ X1,
+                                                           const double* __restrict__ X2, int* __restrict__ fv,
+                                                           double* __restrict__ fw) {
+  constexpr int NL = 1 << D;
+  constexpr int NQ = (D == 2) ? 3 : 9;
+  const int64_t f = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  if (f >= nf) return;
+  const int64_t e = fcell[f];
+  const int lf = flf[f];
   const int ax = lf >> 1, side = lf & 1;
-  int nd[NL];
-  double X[NL][D], Tv[NL], xv[NL];
+  const double* Xa[3] = {X0, X1, X2};
+  double X[NL][D];
+  int m = 0;
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
-    nd[l] = g.cell[(int64_t)l * g.nc + e];
+    const int v = cell[(int64_t)l * nc + e];
 #pragma unroll
-    for (int a = 0; a < D; ++a) X[l][a] = g.X[a][nd[l]];
-    Tv[l] = T[nd[l]];
-    xv[l] = (MODE == UM_JAC) ? x[nd[l]] : 0.0;
+    for (int a = 0; a < D; ++a) X[l][a] = Xa[a][v];
+    if (((l >> ax) & 1) == side) fv[(int64_t)(m++) * nf + f] = v;
   }
-  double y[NL];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) y[l] = 0.0;
-  constexpr int NQ = (D == 2) ? 3 : 9;
 #pragma unroll 1
   for (int q = 0; q < NQ; ++q) {
     double xi[3] = {0.0, 0.0, 0.0}, w = 1.0;
@@ -247,39 +297,150 @@ __global__ __launch_bounds__(kBlock) void k_um_facets(UmGrid g, const double* __
     double gn = 0.0;  // |row ax of J^-1| = |grad xi_ax|
 #pragma unroll
     for (int b = 0; b < D; ++b) gn += Ji[ax][b] * Ji[ax][b];
-    const double wm = w * det * sqrt(gn);
-    double Tq = 0.0, xq = 0.0;
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      Tq += phi[l] * Tv[l];
-      xq += phi[l] * xv[l];
-    }
-#pragma unroll
-    for (int l = 0; l < NL; ++l) {
-      double v;
-      if (MODE == UM_RES) v = um_g(g, Tq) * phi[l];
-      else if (MODE == UM_JAC) v = um_dg(g, Tq) * xq * phi[l];
-      else v = um_dg(g, Tq) * phi[l] * phi[l];
-      y[l] += wm * v;
-    }
+    fw[(int64_t)q * nf + f] = w * det * sqrt(gn);
   }
-#pragma unroll
-  for (int l = 0; l < NL; ++l)
-    if (((l >> ax) & 1) == side) out[nd[l]] += g.dt * y[l];
 }
 
-__global__ __launch_bounds__(kBlock) void k_um_zero(double* __restrict__ x, int64_t n) {
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = 0.0;
+// ---- the row kernels ---------------------------------------------------------------
+// facet-local Q1 basis at facet point q: tangential axes in increasing order,
+// point index q = i0 + 3 i1 (the product order of q1<D> on the cell)
+__device__ __forceinline__ double fphi(int m, int q, int D) {
+  const double x0 = kUX[q % 3];
+  const double f0 = (m & 1) ? x0 : 1.0 - x0;
+  if (D == 2) return f0;
+  const double x1 = kUX[q / 3];
+  return f0 * ((m >> 1) ? x1 : 1.0 - x1);
 }
-__global__ __launch_bounds__(kBlock) void k_um_invert(double* __restrict__ d, int64_t n) {
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) d[t] = 1.0 / d[t];
+
+// Robin terms of row r (ThermoViscoProblem.py:302-304 and their derivative)
+template <int D, int MODE, class XGet>
+__device__ __forceinline__ double robin_row(const UmGrid& g, int64_t r, const double* __restrict__ T, XGet xget) {
+  constexpr int NF = 1 << (D - 1);
+  constexpr int NQ = (D == 2) ? 3 : 9;
+  double acc = 0.0;
+  const int t1 = g.boff[r + 1];
+  for (int t = g.boff[r]; t < t1; ++t) {
+    const int code = g.binc[t];
+    const int64_t f = code >> 2;
+    const int m = code & 3;
+    double Tn[NF], xn[NF];
+#pragma unroll
+    for (int n = 0; n < NF; ++n) {
+      const int v = g.fv[(int64_t)n * g.nf + f];
+      Tn[n] = T[v];
+      xn[n] = (MODE == UM_JAC || MODE == UM_FUSED) ? xget(v) : 0.0;
+    }
+    double y = 0.0;
+#pragma unroll 1
+    for (int q = 0; q < NQ; ++q) {
+      double Tq = 0.0, xq = 0.0, pm = 0.0;
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const double ph = fphi(n, q, D);
+        Tq += ph * Tn[n];
+        xq += ph * xn[n];
+        if (n == m) pm = ph;
+      }
+      double v;
+      if (MODE == UM_RES) v = um_g(g, Tq) * pm;
+      else if (MODE == UM_DIAG) v = um_dg(g, Tq) * pm * pm;
+      else v = um_dg(g, Tq) * xq * pm;
+      y += g.fw[(int64_t)q * g.nf + f] * v;
+    }
+    acc += g.dt * y;
+  }
+  return acc;
+}
+
+// One lane per row, one wave per 64-row slice, each wave a contiguous range of
+// slices (XCD-remapped blocks: a contiguous row range per XCD, so the x
+// gathers of neighbouring rows share one L2).
+//   UM_JAC:   out = V u + Robin'(T) u
+//   UM_FUSED: the same with u = p (formed by k_um_pvec), out = w, p.w records
+//             + the reduction tail (PETSc's dpi and alpha)
+//   UM_RES:   out = M (u - up) + K u - dt f b + Robin(u)      (u = T, up = T_prev)
+//   UM_DIAG:  out = diag V + Robin diagonal (inverted if `invert`)
+template <int D, int MODE>
+__global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __restrict__ T,
+                                                    const double* __restrict__ u, const double* __restrict__ up,
+                                                    double* __restrict__ out, const PcgState* __restrict__ st,
+                                                    double* __restrict__ partials, RedTail rt, int invert) {
+  if (MODE == UM_FUSED && st->done) return;
+  auto xget = [&](int64_t c) -> double { return u[c]; };
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int WPB = kBlock / 64;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  const int64_t gw = (int64_t)blk * WPB + wave;
+  const int64_t chunk = (g.nslice + nw - 1) / nw;
+  const int64_t s0 = gw * chunk, s1 = std::min<int64_t>(s0 + chunk, g.nslice);
+  double pw = 0.0;
+  for (int64_t s = s0; s < s1; ++s) {
+    const int64_t r = s * 64 + lane;
+    const int64_t so = g.soff[s];
+    const int wdt = (int)((g.soff[s + 1] - so) >> 6);
+    const int* __restrict__ cs = g.cols + so + lane;  // entry k of this row: cs[64 k]
+    double acc = 0.0, acc2 = 0.0;
+    if (MODE == UM_RES) {
+      const double* __restrict__ ms = g.M + so + lane;
+      const double* __restrict__ ks = g.K + so + lane;
+      for (int k = 0; k < wdt; ++k) {
+        const int c = __builtin_nontemporal_load(&cs[64 * k]);
+        const double xc = u[c];
+        acc += __builtin_nontemporal_load(&ms[64 * k]) * (xc - up[c]);
+        acc2 += __builtin_nontemporal_load(&ks[64 * k]) * xc;
+      }
+    } else if (MODE != UM_DIAG) {
+      const double* __restrict__ vs = g.V + so + lane;
+      // U entries in flight per lane and round, the last round masked (27
+      // entries per interior hexahedral row = 3 full rounds of 9).  The matrix
+      // stream is read once per product: non-temporal loads keep it from
+      // evicting the gathered vector from L2 / the Infinity Cache (measured at
+      // 8.2M rows: 598 vs 717 us per J x, 4.6 vs 3.8 TB/s)
+      constexpr int U = 9;
+      for (int k = 0; k < wdt; k += U) {
+        int c[U];
+        double a[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          const bool ok = k + j < wdt;
+          const int o = 64 * (ok ? k + j : 0);
+          c[j] = __builtin_nontemporal_load(&cs[o]);
+          a[j] = __builtin_nontemporal_load(&vs[o]);
+          if (!ok) a[j] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) acc += a[j] * u[c[j]];
+      }
+    }
+    if (r < g.nv) {
+      double val;
+      if (MODE == UM_DIAG) val = g.vdiag[r];
+      else if (MODE == UM_RES) val = (acc + acc2) - g.dt_f * g.bvec[r];
+      else val = acc;
+      val += robin_row<D, MODE>(g, r, (MODE == UM_RES) ? u : T, xget);
+      if (MODE == UM_DIAG && invert) val = 1.0 / val;
+      if (MODE == UM_FUSED) pw += u[r] * val;
+      out[r] = val;
+    }
+  }
+  if (MODE == UM_FUSED) {
+    __shared__ double red[WPB];
+    const double sw = wave_sum64(pw);
+    if (lane == 0) red[wave] = sw;
+    __syncthreads();
+    if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
+    fused_reduce_tail<1>(rt, gridDim.x);
+  }
 }
 
 // PETSc KSPCG "p <- z + (beta / betaold) p" (p = z at iteration 0) into the
-// buffer of this iteration's parity (the convention of k_pcg_update)
+// buffer of this iteration's parity (the convention of k_pcg_update); carries
+// the start stamp of the iteration's matvec
 __global__ __launch_bounds__(kBlock) void k_um_pvec(int64_t n, const PcgState* __restrict__ st,
                                                     const double* __restrict__ z, double* pA, double* pB,
-                                                    int it_host) {
+                                                    int it_host, RedTail rt) {
+  stamp_start(rt);
   if (st->done) return;
   const bool first = it_host == 0;
   const double b = first ? 0.0 : st->beta / st->betaold;
@@ -289,92 +450,92 @@ __global__ __launch_bounds__(kBlock) void k_um_pvec(int64_t n, const PcgState* _
     p[t] = first ? z[t] : z[t] + b * po[t];
 }
 
-// partial records of p.w (width 1, fixed order)
-__global__ __launch_bounds__(kBlock) void k_um_dot(int64_t n, const PcgState* __restrict__ st, const double* pA,
-                                                   const double* pB, const double* __restrict__ w,
-                                                   double* __restrict__ partials, int it_host) {
-  __shared__ double red[kBlock / kWave];
-  if (st->done) return;
-  const double* p = (it_host & 1) ? pB : pA;
-  double acc = 0.0;
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
-    acc += p[t] * w[t];
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
+int row_blocks(const UmGrid& g) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((g.nslice + 3) / 4, kUmBlocksMax));
 }
 
-int blocks_of(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 1 << 20)); }
-int vblocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 1024)); }
-
 template <int MODE>
-void apply(const UmGrid& g, const double* T, const double* u, const double* up, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_um_zero, dim3(vblocks(g.nv)), dim3(kBlock), 0, s, out, g.nv);
-  for (int k = 0; k < g.ncolor; ++k) {
-    const int64_t c0 = g.color_off[k], c1 = g.color_off[k + 1];
-    if (c1 <= c0) continue;
-    if (g.dim == 2)
-      hipLaunchKernelGGL((k_um_cells<2, MODE>), dim3(blocks_of(c1 - c0)), dim3(kBlock), 0, s, g, u, up, out, c0, c1);
-    else
-      hipLaunchKernelGGL((k_um_cells<3, MODE>), dim3(blocks_of(c1 - c0)), dim3(kBlock), 0, s, g, u, up, out, c0, c1);
-  }
-  for (int k = 0; k < g.nfcolor; ++k) {
-    const int64_t f0 = g.fcolor_off[k], f1 = g.fcolor_off[k + 1];
-    if (f1 <= f0) continue;
-    if (g.dim == 2)
-      hipLaunchKernelGGL((k_um_facets<2, MODE>), dim3(blocks_of(f1 - f0)), dim3(kBlock), 0, s, g, T, u, out, f0, f1);
-    else
-      hipLaunchKernelGGL((k_um_facets<3, MODE>), dim3(blocks_of(f1 - f0)), dim3(kBlock), 0, s, g, T, u, out, f0, f1);
-  }
+void launch_rows(const UmGrid& g, const double* T, const double* u, const double* up, double* out,
+                 const PcgState* st, double* partials, const RedTail& rt, int invert, hipStream_t s) {
+  const dim3 grid(row_blocks(g)), block(kBlock);
+  if (g.dim == 2)
+    hipLaunchKernelGGL((k_um_rows<2, MODE>), grid, block, 0, s, g, T, u, up, out, st, partials, rt, invert);
+  else
+    hipLaunchKernelGGL((k_um_rows<3, MODE>), grid, block, 0, s, g, T, u, up, out, st, partials, rt, invert);
 }
 
 }  // namespace
 
+int um_num_blocks(const UmGrid& g) { return row_blocks(g); }
+int64_t um_nnz(const UmDevice* d) { return d ? d->nnz : 0; }
+int64_t um_boundary_vertices(const UmDevice* d, std::vector<unsigned char>& mask) {
+  mask = d->bmask;
+  return d->nb;
+}
+
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
-  apply<UM_RES>(g, T, T, Tp, F, s);
+  launch_rows<UM_RES>(g, T, T, Tp, F, nullptr, nullptr, RedTail{}, 0, s);
 }
 
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s) {
-  apply<UM_JAC>(g, T, x, nullptr, y, s);
+  launch_rows<UM_JAC>(g, T, x, nullptr, y, nullptr, nullptr, RedTail{}, 0, s);
 }
 
 void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hipStream_t s) {
-  apply<UM_DIAG>(g, T, nullptr, nullptr, d, s);
-  if (invert) hipLaunchKernelGGL(k_um_invert, dim3(vblocks(g.nv)), dim3(kBlock), 0, s, d, g.nv);
+  launch_rows<UM_DIAG>(g, T, nullptr, nullptr, d, nullptr, nullptr, RedTail{}, invert, s);
 }
 
 int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
-                           const PcgState* st, double* partials, int it_host, hipStream_t s) {
-  hipLaunchKernelGGL(k_um_pvec, dim3(vblocks(g.nv)), dim3(kBlock), 0, s, g.nv, st, z, pA, pB, it_host);
-  apply<UM_JAC>(g, T, (it_host & 1) ? pB : pA, nullptr, w, s);
-  const int nb = vblocks(g.nv);
-  hipLaunchKernelGGL(k_um_dot, dim3(nb), dim3(kBlock), 0, s, g.nv, st, pA, pB, w, partials, it_host);
-  return nb;
+                           const PcgState* st, double* partials, int it_host, const RedTail* tail, hipStream_t s) {
+  const RedTail rt = tail ? *tail : RedTail{};
+  const int vb = (int)std::max<int64_t>(1, std::min<int64_t>((g.nv + kBlock - 1) / kBlock, 2048));
+  hipLaunchKernelGGL(k_um_pvec, dim3(vb), dim3(kBlock), 0, s, g.nv, st, z, pA, pB, it_host, rt);
+  const double* p = (it_host & 1) ? pB : pA;
+  launch_rows<UM_FUSED>(g, T, p, nullptr, w, st, partials, rt, 0, s);
+  return row_blocks(g);
 }
 
-// ---- host: boundary facets and colouring ------------------------------------------
-static int greedy_colour(const std::vector<std::vector<int64_t>>& items, int64_t nv, std::vector<int>& colour) {
-  std::vector<uint64_t> used((size_t)nv, 0);
-  colour.assign(items.size(), 0);
-  int nc = 0;
-  for (size_t e = 0; e < items.size(); ++e) {
-    uint64_t m = 0;
-    for (int64_t v : items[e]) m |= used[(size_t)v];
-    int c = 0;
-    while (c < 64 && ((m >> c) & 1)) ++c;
-    if (c == 64) return -1;
-    colour[e] = c;
-    nc = std::max(nc, c + 1);
-    for (int64_t v : items[e]) used[(size_t)v] |= (uint64_t)1 << c;
+// ---- host: mesh analysis and device setup ----------------------------------------
+#define UMC(x)                                                             \
+  do {                                                                     \
+    if ((x) != hipSuccess) {                                               \
+      err = std::string("HIP error in unstructured setup: ") + #x;         \
+      return 1;                                                            \
+    }                                                                      \
+  } while (0)
+
+template <class T>
+static int um_upload(UmDevice* d, const std::vector<T>& h, T** out, std::string& err) {
+  void* p = nullptr;
+  UMC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, h.size())));
+  d->bufs.push_back(p);
+  if (!h.empty()) UMC(hipMemcpy(p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  *out = static_cast<T*>(p);
+  return 0;
+}
+
+template <class T>
+static int um_alloc(UmDevice* d, size_t n, T** out, std::string& err) {
+  void* p = nullptr;
+  UMC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, n)));
+  d->bufs.push_back(p);
+  *out = static_cast<T*>(p);
+  return 0;
+}
+
+static void release(UmDevice* d, void* p) {
+  auto it = std::find(d->bufs.begin(), d->bufs.end(), p);
+  if (it != d->bufs.end()) {
+    hipFree(p);
+    d->bufs.erase(it);
   }
-  return nc;
 }
 
-int um_build(int dim, int64_t nv, int64_t nc, const int64_t* cells, UmHost& out, std::string& err) {
+// boundary facets: local facets whose sorted vertex set occurs once; (cell, lf)
+// in cell order
+static int boundary_facets(int dim, int64_t nc, const int64_t* cells, std::vector<std::pair<int64_t, int>>& bf,
+                           std::string& err) {
   const int nl = 1 << dim;
-  // boundary facets: local facets whose sorted vertex set occurs once
   struct F {
     int64_t v[4];
     int64_t cell;
@@ -407,67 +568,209 @@ int um_build(int dim, int64_t nv, int64_t nc, const int64_t* cells, UmHost& out,
     if (key_less(b, a)) return false;
     return a.cell < b.cell;
   });
-  std::vector<std::pair<int64_t, int>> bf;
+  bf.clear();
   for (size_t i = 0; i < fs.size();) {
     size_t j = i + 1;
     while (j < fs.size() && key_eq(fs[i], fs[j])) ++j;
     if (j - i == 1) bf.emplace_back(fs[i].cell, fs[i].lf);
     else if (j - i > 2) {
       err = "non-manifold mesh: a facet shared by more than two cells";
-      return -1;
+      return 1;
     }
     i = j;
   }
   std::sort(bf.begin(), bf.end());
-  // colour the cells and the boundary facets
-  std::vector<std::vector<int64_t>> items((size_t)nc);
-  for (int64_t e = 0; e < nc; ++e) items[e].assign(cells + e * nl, cells + (e + 1) * nl);
-  std::vector<int> col;
-  const int ncol = greedy_colour(items, nv, col);
-  if (ncol < 0) {
-    err = "more than 64 colours needed";
-    return -1;
-  }
-  std::vector<std::vector<int64_t>> fitems(bf.size());
-  for (size_t f = 0; f < bf.size(); ++f) {
-    const int64_t e = bf[f].first;
-    const int lf = bf[f].second;
-    for (int l = 0; l < nl; ++l)
-      if (((l >> (lf >> 1)) & 1) == (lf & 1)) fitems[f].push_back(cells[e * nl + l]);
-  }
-  std::vector<int> fcol;
-  const int nfcol = greedy_colour(fitems, nv, fcol);
-  if (nfcol < 0) {
-    err = "more than 64 facet colours needed";
-    return -1;
-  }
-  // cells sorted by colour (stable: cell order within a colour); [l][cell] layout
-  std::vector<int64_t> order((size_t)nc);
-  for (int64_t e = 0; e < nc; ++e) order[e] = e;
-  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return col[a] < col[b]; });
-  std::vector<int64_t> pos((size_t)nc);
-  for (int64_t k = 0; k < nc; ++k) pos[order[k]] = k;
-  out.cell.assign((size_t)nl * nc, 0);
-  for (int64_t k = 0; k < nc; ++k)
-    for (int l = 0; l < nl; ++l) out.cell[(size_t)l * nc + k] = (int)cells[order[k] * nl + l];
-  out.color_off.assign(ncol + 1, 0);
-  for (int64_t e = 0; e < nc; ++e) out.color_off[col[e] + 1]++;
-  for (int k = 0; k < ncol; ++k) out.color_off[k + 1] += out.color_off[k];
-  std::vector<int64_t> forder(bf.size());
-  for (size_t f = 0; f < bf.size(); ++f) forder[f] = (int64_t)f;
-  std::stable_sort(forder.begin(), forder.end(), [&](int64_t a, int64_t b) { return fcol[a] < fcol[b]; });
-  out.fcell.resize(bf.size());
-  out.flf.resize(bf.size());
-  for (size_t k = 0; k < bf.size(); ++k) {
-    out.fcell[k] = (int)pos[bf[forder[k]].first];  // the cell's position in the coloured order
-    out.flf[k] = (signed char)bf[forder[k]].second;
-  }
-  out.fcolor_off.assign(nfcol + 1, 0);
-  for (size_t f = 0; f < bf.size(); ++f) out.fcolor_off[fcol[f] + 1]++;
-  for (int k = 0; k < nfcol; ++k) out.fcolor_off[k + 1] += out.fcolor_off[k];
   return 0;
 }
 
+static int n_threads() {
+  const unsigned h = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(16u, h ? h : 1u));
+}
+
+void um_free(UmDevice* d) {
+  if (!d) return;
+  for (void* p : d->bufs) hipFree(p);
+  delete d;
+}
+
+int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g, UmDevice*& dev,
+             hipStream_t s, std::string& err) {
+  const int nl = 1 << dim;
+  dev = new UmDevice();
+  UmDevice* d = dev;
+  // -- boundary facets
+  std::vector<std::pair<int64_t, int>> bf;
+  if (boundary_facets(dim, nc, cells, bf, err)) return 1;
+  const int64_t nf = (int64_t)bf.size();
+  // -- vertex -> (cell, local vertex) incidences, cell order
+  std::vector<int64_t> inc_off((size_t)nv + 1, 0), inc((size_t)nc * nl);
+  for (int64_t k = 0; k < nc * nl; ++k) inc_off[(size_t)cells[k] + 1]++;
+  for (int64_t v = 0; v < nv; ++v) inc_off[v + 1] += inc_off[v];
+  {
+    std::vector<int64_t> fill(inc_off.begin(), inc_off.end() - 1);
+    for (int64_t e = 0; e < nc; ++e)
+      for (int l = 0; l < nl; ++l) inc[(size_t)fill[(size_t)cells[e * nl + l]]++] = (e << 3) | l;
+  }
+  // -- sparsity pattern: the vertices of the cells around each vertex (sorted)
+  const int nth = n_threads();
+  std::vector<int> rnnz((size_t)nv, 0);
+  std::vector<std::vector<int>> part((size_t)nth);
+  std::vector<int64_t> r0((size_t)nth + 1);
+  for (int t = 0; t <= nth; ++t) r0[t] = nv * t / nth;
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+      th.emplace_back([&, t]() {
+        std::vector<int> buf;
+        auto& out = part[(size_t)t];
+        for (int64_t r = r0[t]; r < r0[t + 1]; ++r) {
+          buf.clear();
+          for (int64_t q = inc_off[r]; q < inc_off[r + 1]; ++q) {
+            const int64_t e = inc[(size_t)q] >> 3;
+            for (int j = 0; j < nl; ++j) buf.push_back((int)cells[e * nl + j]);
+          }
+          std::sort(buf.begin(), buf.end());
+          buf.erase(std::unique(buf.begin(), buf.end()), buf.end());
+          rnnz[(size_t)r] = (int)buf.size();
+          out.insert(out.end(), buf.begin(), buf.end());
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  // -- SELL-64 layout
+  const int64_t nslice = (nv + 63) / 64;
+  std::vector<int64_t> soff((size_t)nslice + 1, 0);
+  for (int64_t sl = 0; sl < nslice; ++sl) {
+    int w = 0;
+    for (int64_t r = sl * 64; r < std::min(nv, sl * 64 + 64); ++r) w = std::max(w, rnnz[(size_t)r]);
+    soff[(size_t)sl + 1] = soff[(size_t)sl] + 64 * (int64_t)w;
+  }
+  const int64_t nnz = soff[(size_t)nslice];
+  std::vector<int> cols((size_t)nnz, 0);
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nth; ++t)
+      th.emplace_back([&, t]() {
+        size_t pos = 0;
+        const auto& src = part[(size_t)t];
+        for (int64_t r = r0[t]; r < r0[t + 1]; ++r) {
+          const int64_t sl = r >> 6, lane = r & 63;
+          const int w = (int)((soff[(size_t)sl + 1] - soff[(size_t)sl]) >> 6);
+          for (int k = 0; k < w; ++k)
+            cols[(size_t)(soff[(size_t)sl] + 64 * k + lane)] = k < rnnz[(size_t)r] ? src[pos + k] : (int)r;
+          pos += (size_t)rnnz[(size_t)r];
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  // padding lanes of the last slice (rows >= nv) keep column 0, value 0
+  std::vector<std::vector<int>>().swap(part);
+  d->nnz = nnz;
+  // -- boundary facet data (host): incidences of the boundary rows
+  const int nfv = nl / 2;
+  std::vector<int> fcell((size_t)nf);
+  std::vector<signed char> flf((size_t)nf);
+  std::vector<int> boff((size_t)nv + 1, 0);
+  for (int64_t f = 0; f < nf; ++f) {
+    fcell[(size_t)f] = (int)bf[(size_t)f].first;
+    flf[(size_t)f] = (signed char)bf[(size_t)f].second;
+    const int64_t e = bf[(size_t)f].first;
+    const int lf = bf[(size_t)f].second;
+    for (int l = 0; l < nl; ++l)
+      if (((l >> (lf >> 1)) & 1) == (lf & 1)) boff[(size_t)cells[e * nl + l] + 1]++;
+  }
+  for (int64_t v = 0; v < nv; ++v) boff[(size_t)v + 1] += boff[(size_t)v];
+  std::vector<int> binc((size_t)boff[(size_t)nv]);
+  {
+    std::vector<int> fill(boff.begin(), boff.end() - 1);
+    for (int64_t f = 0; f < nf; ++f) {
+      const int64_t e = bf[(size_t)f].first;
+      const int lf = bf[(size_t)f].second;
+      int m = 0;
+      for (int l = 0; l < nl; ++l)
+        if (((l >> (lf >> 1)) & 1) == (lf & 1)) binc[(size_t)fill[(size_t)cells[e * nl + l]]++] = (int)(4 * f + m++);
+    }
+  }
+  d->bmask.assign((size_t)nv, 0);
+  d->nb = 0;
+  for (int64_t v = 0; v < nv; ++v)
+    if (boff[(size_t)v + 1] > boff[(size_t)v]) {
+      d->bmask[(size_t)v] = 1;
+      d->nb++;
+    }
+  (void)nfv;
+  // -- uploads
+  std::vector<double> Xh[3];
+  double* Xd[3];
+  for (int a = 0; a < 3; ++a) {
+    Xh[a].resize((size_t)nv);
+    for (int64_t v = 0; v < nv; ++v) Xh[a][(size_t)v] = xyz[3 * v + a];
+    if (um_upload(d, Xh[a], &Xd[a], err)) return 1;
+    std::vector<double>().swap(Xh[a]);
+  }
+  std::vector<int> cell_h((size_t)nl * nc);
+  for (int64_t e = 0; e < nc; ++e)
+    for (int l = 0; l < nl; ++l) cell_h[(size_t)l * nc + e] = (int)cells[e * nl + l];
+  int *cell_d, *cols_d, *rnnz_d, *fcell_d, *fv_d, *boff_d, *binc_d;
+  int64_t *inc_off_d, *inc_d, *soff_d;
+  signed char* flf_d;
+  double *V, *M, *K, *bvec, *vdiag, *fw;
+  if (um_upload(d, cell_h, &cell_d, err) || um_upload(d, cols, &cols_d, err) || um_upload(d, rnnz, &rnnz_d, err) ||
+      um_upload(d, inc_off, &inc_off_d, err) || um_upload(d, inc, &inc_d, err) || um_upload(d, soff, &soff_d, err) ||
+      um_upload(d, fcell, &fcell_d, err) || um_upload(d, flf, &flf_d, err) || um_upload(d, boff, &boff_d, err) ||
+      um_upload(d, binc, &binc_d, err))
+    return 1;
+  std::vector<int>().swap(cell_h);
+  std::vector<int>().swap(cols);
+  std::vector<int64_t>().swap(inc);
+  if (um_alloc(d, (size_t)nnz, &V, err) || um_alloc(d, (size_t)nnz, &M, err) || um_alloc(d, (size_t)nnz, &K, err) ||
+      um_alloc(d, (size_t)nv, &bvec, err) || um_alloc(d, (size_t)nv, &vdiag, err) ||
+      um_alloc(d, (size_t)nfv * nf, &fv_d, err) || um_alloc(d, (size_t)(dim == 2 ? 3 : 9) * nf, &fw, err))
+    return 1;
+  UMC(hipMemsetAsync(V, 0, sizeof(double) * (size_t)std::max<int64_t>(1, nnz), s));
+  UMC(hipMemsetAsync(M, 0, sizeof(double) * (size_t)std::max<int64_t>(1, nnz), s));
+  UMC(hipMemsetAsync(K, 0, sizeof(double) * (size_t)std::max<int64_t>(1, nnz), s));
+  UMC(hipMemsetAsync(vdiag, 0, sizeof(double) * (size_t)nv, s));
+  const double dt_alpha = g.dt_alpha;
+  const dim3 bl(kBlock);
+  const dim3 gr_v((unsigned)((nv + kBlock - 1) / kBlock)), gr_f((unsigned)std::max<int64_t>(1, (nf + kBlock - 1) / kBlock));
+  if (dim == 2) {
+    hipLaunchKernelGGL((k_um_assemble<2>), gr_v, bl, 0, s, nv, nc, cell_d, Xd[0], Xd[1], Xd[2], inc_off_d, inc_d,
+                       soff_d, cols_d, rnnz_d, dt_alpha, V, M, K, bvec, vdiag);
+    if (nf) hipLaunchKernelGGL((k_um_facet_setup<2>), gr_f, bl, 0, s, nf, nc, fcell_d, flf_d, cell_d, Xd[0], Xd[1],
+                               Xd[2], fv_d, fw);
+  } else {
+    hipLaunchKernelGGL((k_um_assemble<3>), gr_v, bl, 0, s, nv, nc, cell_d, Xd[0], Xd[1], Xd[2], inc_off_d, inc_d,
+                       soff_d, cols_d, rnnz_d, dt_alpha, V, M, K, bvec, vdiag);
+    if (nf) hipLaunchKernelGGL((k_um_facet_setup<3>), gr_f, bl, 0, s, nf, nc, fcell_d, flf_d, cell_d, Xd[0], Xd[1],
+                               Xd[2], fv_d, fw);
+  }
+  UMC(hipGetLastError());
+  UMC(hipStreamSynchronize(s));
+  // setup-only arrays
+  for (void* p : {(void*)Xd[0], (void*)Xd[1], (void*)Xd[2], (void*)cell_d, (void*)rnnz_d, (void*)inc_off_d,
+                  (void*)inc_d, (void*)fcell_d, (void*)flf_d})
+    release(d, p);
+  g.dim = dim;
+  g.nv = nv;
+  g.nc = nc;
+  g.nf = nf;
+  g.nslice = nslice;
+  g.soff = soff_d;
+  g.cols = cols_d;
+  g.V = V;
+  g.M = M;
+  g.K = K;
+  g.bvec = bvec;
+  g.vdiag = vdiag;
+  g.fv = fv_d;
+  g.fw = fw;
+  g.boff = boff_d;
+  g.binc = binc_d;
+  return 0;
+}
+#undef UMC
 
 // ---- host: recursive coordinate bisection of the cells ----------------------------
 // Splits the cell set along the axis of largest centroid extent so that the two

@@ -22,6 +22,14 @@ for fam in CG DG; do
   python3 tools/pmc_summarize.py $OUT/pmc_${fam}_fetch $OUT/pmc_${fam}_write $OUT/pmc_${key}_${fam}_${cells//,/x}_n1.json $dom > $OUT/pmc_${fam}_summary.log 2>&1 || exit 1
   cp $OUT/pmc_${key}_${fam}_${cells//,/x}_n1.json profiles/
 done
+step "pmc distorted-hex fetch / write"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_UM_fetch -o run --output-format csv -- python3 tools/pmc_kernels.py --mesh distorted > $OUT/pmc_UM_fetch.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_UM_write -o run --output-format csv -- python3 tools/pmc_kernels.py --mesh distorted > $OUT/pmc_UM_write.log 2>&1 || exit 1
+python3 tools/pmc_summarize.py $OUT/pmc_UM_fetch $OUT/pmc_UM_write $OUT/pmc_jacobian_apply_unstructured_CG_400x400x50_n1.json jacobian_apply_unstructured > $OUT/pmc_UM_summary.log 2>&1 || exit 1
+cp $OUT/pmc_jacobian_apply_unstructured_CG_400x400x50_n1.json profiles/
+step "bench distorted-hex C4 under rocprofv3 --kernel-trace --stats"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_distorted -o run --output-format csv -- python3 bench.py --mesh distorted --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_distorted_prof.json 2> $OUT/bench_distorted_prof.err || { tail -5 $OUT/bench_distorted_prof.err; exit 1; }
+timeout -k 10 600 python3 bench.py --mesh distorted --steps 5 --warmup 1 > $OUT/bench_distorted.json 2> $OUT/bench_distorted.err || { tail -5 $OUT/bench_distorted.err; exit 1; }
 step "bench C4 under rocprofv3 --kernel-trace --stats"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o run --output-format csv -- python3 bench.py > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { tail -5 $OUT/bench_prof.err; exit 1; }
 python3 tools/profile_summary.py $OUT/prof_bench $OUT/bench_prof.json $OUT/profile_summary.json > $OUT/profile_summary.log 2>&1

@@ -1,13 +1,15 @@
 """Drive the hot-path kernels for a rocprofv3 --pmc pass.
 
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- \
-        python3 tools/pmc_kernels.py [--cells 400,400,50] [--family CG|DG] [--reps 5]
+        python3 tools/pmc_kernels.py [--cells 400,400,50] [--family CG|DG] [--mesh box|distorted] [--reps 5]
 
 One coupled step (realistic state), then `reps` whole PCG iterations (CG: fused
 matvec + update alternating as in the solve, tv_time_kernel id 5; DG: the
 fused DG matvec, id 3), `reps` viscoelastic updates (id 1) and `reps` plain
 J x launches with the Infinity Cache flushed before each (id 10), so the
-counters see the kernels in the cache state of the solve.
+counters see the kernels in the cache state of the solve.  ``--mesh
+distorted``: the plate as a general hexahedral mesh (tv_um.hip), plain J x
+(id 0) and the visco update.
 """
 import argparse
 import ctypes as C
@@ -17,7 +19,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "fem-glass-tempering_amd"), ROOT]
 
-from tvfem import _native as N, box_mesh  # noqa: E402
+from tvfem import _native as N, box_mesh, distorted_box_mesh  # noqa: E402
 from tvfem.problem import ThermoViscoProblem  # noqa: E402
 
 MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0,
@@ -28,15 +30,18 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--cells", default="400,400,50")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--family", choices=["CG", "DG"], default="CG")
+ap.add_argument("--mesh", choices=["box", "distorted"], default="box")
 a = ap.parse_args()
 nc = [int(v) for v in a.cells.split(",")]
 cfg = {"T": {"element": a.family, "degree": 1}, "sigma": {"element": a.family, "degree": 1}}
-prob = ThermoViscoProblem(box_mesh([50.0, 50.0, 5.0], nc), (0.0, 1.0), 0.1, cfg, dict(MP),
-                          materialize=False, part_axis=1, verbose=False)
+um = a.mesh == "distorted"
+mesh = (distorted_box_mesh if um else box_mesh)([50.0, 50.0, 5.0], nc)
+prob = ThermoViscoProblem(mesh, (0.0, 1.0), 0.1, cfg, dict(MP), materialize=False,
+                          verbose=False, **({} if um else {"part_axis": 1}))
 prob.setup()
 prob.solve_timestep()
 lib, ctx = prob._lib, prob._ctx
-for kid in ((5, 1, 10) if a.family == "CG" else (3, 1, 10)):
+for kid in ((0, 1) if um else (5, 1, 10) if a.family == "CG" else (3, 1, 10)):
     ms = C.c_double()
     N.check(lib.tv_time_kernel(ctx, kid, a.reps, C.byref(ms)), ctx)
     print(kid, ms.value, flush=True)

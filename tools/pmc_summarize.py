@@ -23,6 +23,7 @@ GROUPS = {
     "jacobian_apply": ("k_cg_march<1, false",),  # plain J x (+ k_cg_addfaces, a few KB)
     "dg_matvec_fused": ("k_dg_tile<true",),
     "pcg_iteration_single_reduction": ("k_cgs_march<false",),
+    "jacobian_apply_unstructured": ("k_um_rows<3, 1>",),  # SELL-64 J x of tv_um.hip
 }
 
 
