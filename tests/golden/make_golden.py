@@ -4,7 +4,7 @@ ThermoViscoProblem.py:349-379).
 
     python tests/golden/make_golden.py
 
-The reference itself (dolfinx 0.8 + PETSc) is not installed in this image, so
+The reference itself (dolfinx 0.7.3 + PETSc 3.20, as the reference pins them) is not installed in this image, so
 these vectors pin regressions of the oracle and give the GPU tests a fixed
 target that does not need the oracle at run time; they are not dolfinx output
 (parity to dolfinx is unpinned).  Each .npz holds the inputs
