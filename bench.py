@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
                     help="box: the rectilinear plate (tensor-product kernels); distorted: the same plate as a "
                          "general hexahedral mesh (jittered, sheared, warped; element-local kernels, one GPU)")
+    ap.add_argument("--pc", choices=["auto", "jacobi", "gmg"], default="auto",
+                    help="preconditioner: gmg (geometric multigrid on the box hierarchy; 3D CG1 box, one "
+                         "partition), jacobi, or auto (gmg where it applies)")
+    ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto",
                     help="Krylov form: single-reduction (Chronopoulos-Gear, 3D CG) or PETSc KSPCG as written")
     return ap.parse_args()
@@ -96,9 +100,13 @@ def main():
     if a.comm == "host":  # rehearsal of several ranks on fewer GPUs (host-staged transport)
         import torch
         device = local_rank % max(1, torch.cuda.device_count())
+    pc = a.pc
+    if pc == "auto":
+        pc = "gmg" if (not um and a.family == "CG" and world == 1 and a.pcg != "single") else "jacobi"
+    kw = {} if um else {"n_parts": world, "part": rank, "part_axis": 1}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
-                              n_parts=world, part=rank, part_axis=1, verbose=False, pcg_variant=a.pcg,
-                              write_output=a.output is not None, output_dir=a.output or "output")
+                              verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,
+                              write_output=a.output is not None, output_dir=a.output or "output", **kw)
     single = prob.pcg_variant == "single"
     lib, ctx = prob._lib, prob._ctx
     if world > 1:
@@ -161,6 +169,8 @@ def main():
     names = {3: "pcg_matvec_fused", 4: "pcg_update", 0: "jacobian_apply", 2: "residual"}
     if single:  # one fused launch per Krylov iteration, no separate update
         names = {3: "pcg_iteration_single_reduction", 0: "jacobian_apply", 2: "residual"}
+    if pc == "gmg":  # the update is k_mg_update (no stamps); the V-cycle is timed as a whole
+        names = {3: "pcg_matvec_fused", 11: "mg_vcycle", 0: "jacobian_apply", 2: "residual"}
     if um:  # element-local kernels: J x (coloured cell + facet launches) is the roofline kernel
         names = {0: "jacobian_apply_unstructured", 3: "pcg_matvec_unstructured", 4: "pcg_update", 2: "residual"}
     if not a.thermal_only:
@@ -254,7 +264,9 @@ def main():
                        "output": (f"T, phi, Tf, xi, sigma written every step (async XDMF) to {a.output}"
                                   if a.output else "none (reference writes VTX/XDMF every step)"),
                        "krylov_form": ("single-reduction (Chronopoulos-Gear) Jacobi-PCG" if single
-                                       else "PETSc KSPCG Jacobi-PCG"),
+                                       else "PETSc KSPCG Jacobi-PCG" if pc == "jacobi"
+                                       else "PETSc KSPCG, geometric-multigrid V-cycle preconditioner"),
+                       "preconditioner": pc,
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},
             "roofline": roofline,
             "kernels": kern,

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -52,6 +53,22 @@ struct FieldInfo {
   int bs = 1;       // components
   int space = 0;    // 0 T space, 1 sigma space
   bool alloc = false;
+};
+
+// One coarse level of the geometric-multigrid hierarchy (tv_mg.hip): a
+// single-partition CG grid of the box coarsened by two along the axes with an
+// even cell count, its transfer from the next finer level and its vectors.
+struct MgLevel {
+  CgGrid g{};
+  std::vector<double> X[3];  // storage-axis node coordinates
+  int64_t n = 0;
+  double omega = 0.0;        // damped-Jacobi weight 2 / (1.1 b), b >= lambda_max(D^-1 J)
+  double *T = nullptr, *b = nullptr, *x = nullptr, *w = nullptr, *dinv = nullptr;
+  MgXfer xf{};               // finer level -> this level
+  double* coef[3] = {nullptr, nullptr, nullptr};
+  int64_t* bnodes = nullptr;
+  double* ffbuf[2] = {nullptr, nullptr};
+  std::vector<void*> bufs;   // T, b, x, w, dinv and the transfer maps
 };
 
 struct Ctx {
@@ -95,6 +112,11 @@ struct Ctx {
   double *dB = nullptr, *dtmp = nullptr;
   double* Tfo = nullptr;  // paper mode, mixed families: previous Tf per T dof
   Output* out = nullptr;  // time-series output (tv_output_*)
+  // geometric multigrid (options.preconditioner = TV_PC_GMG): levels 1.. (level 0 = cg)
+  bool mg_on = false;
+  std::vector<MgLevel> mg;
+  double mg_omega0 = 0.0;
+  double* mgx = nullptr;    // level-0 V-cycle iterate
   // unstructured mesh (tv_create_unstructured, tv_um.hip)
   bool um = false;
   UmGrid umg{};
@@ -238,6 +260,80 @@ static void part_planes(int N2, int P, int p, int* b0, int* b1) {
   *b1 = (int)((int64_t)N2 * (p + 1) / P);
 }
 
+// CG grid of `n2` local planes starting at global plane `first2` of storage
+// axis 2 (ghost planes included: g_lo / g_hi of them), from the global node
+// coordinates X[s] of the storage axes (a single 0 for a degenerate axis);
+// bnd2lo / bnd2hi: the low / high face of axis 2 is a physical boundary here.
+// Device arrays go to coef[3], *bnodes and ffbuf[2] (owned by the caller).
+static int build_cg_grid(Ctx* c, int d, const std::vector<double> (&X)[3], int first2, int n2, int g_lo, int g_hi,
+                         bool bnd2lo, bool bnd2hi, CgGrid& g, double** coef, int64_t** bnodes, double** ffbuf) {
+  g.n0 = (int)X[0].size();
+  g.n1 = (int)X[1].size();
+  g.g_lo = g_lo;
+  g.g_hi = g_hi;
+  g.n2 = n2;
+  g.k_begin = g_lo;
+  g.k_end = n2 - g_hi;
+  g.deg1 = X[1].size() == 1;
+  g.deg2 = X[2].size() == 1;
+  g.bnd[0][0] = g.bnd[0][1] = 1;
+  g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
+  g.bnd[2][0] = (!g.deg2 && bnd2lo) ? 1 : 0;
+  g.bnd[2][1] = (!g.deg2 && bnd2hi) ? 1 : 0;
+  const int first[3] = {0, 0, first2};
+  const int cnt[3] = {g.n0, g.n1, g.n2};
+  for (int s = 0; s < 3; ++s) {
+    std::vector<double> cf;
+    axis_coefs(X[s], first[s], cnt[s], cf);
+    HIPC(hipMalloc(&coef[s], cf.size() * sizeof(double)));
+    HIPC(hipMemcpy(coef[s], cf.data(), cf.size() * sizeof(double), hipMemcpyHostToDevice));
+    g.coef[s] = coef[s];
+  }
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  for (int f = 0; f < 6; ++f) g.ffoff[f] = -1;
+  if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
+    std::vector<int64_t> bn;
+    for (int k = g.k_begin; k < g.k_end; ++k)
+      for (int j = 0; j < g.n1; ++j)
+        for (int i = 0; i < g.n0; ++i) {
+          const bool on = (i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1]) ||
+                          (j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]) ||
+                          (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
+          if (on) bn.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
+        }
+    if (!bn.empty()) {
+      HIPC(hipMalloc(bnodes, bn.size() * sizeof(int64_t)));
+      HIPC(hipMemcpy(*bnodes, bn.data(), bn.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+    g.bnodes = *bnodes;
+    g.n_bnodes = (int64_t)bn.size();
+    // facet-Jacobian terms: one value per node of every physical boundary
+    // face, the six faces in one contiguous buffer, two parities
+    const int nn[3] = {g.n0, g.n1, g.n2};
+    int64_t tot = 0;
+    for (int f = 0; f < 6; ++f) {
+      const int ax = f >> 1, side = f & 1;
+      g.fface[f] = nullptr;
+      g.fn1[f] = g.fn2[f] = 0;
+      g.ffoff[f] = -1;
+      if (!g.bnd[ax][side]) continue;
+      const int t1 = (ax == 0) ? 1 : 0, t2 = (ax == 2) ? 1 : 2;
+      g.fn1[f] = nn[t1];
+      g.fn2[f] = nn[t2];
+      g.ffoff[f] = tot;
+      tot += (int64_t)nn[t1] * nn[t2];
+    }
+    g.ffsize = tot;
+    for (int q = 0; q < 2; ++q) {
+      HIPC(hipMalloc(&ffbuf[q], sizeof(double) * (size_t)std::max<int64_t>(1, tot)));
+      HIPC(hipMemsetAsync(ffbuf[q], 0, sizeof(double) * (size_t)std::max<int64_t>(1, tot), c->stream));
+      g.ffbuf[q] = ffbuf[q];
+    }
+    for (int f = 0; f < 6; ++f) g.fface[f] = (g.ffoff[f] >= 0) ? ffbuf[0] + g.ffoff[f] : nullptr;
+  }
+  return TV_OK;
+}
+
 static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   const int d = m->dim;
   if (d < 1 || d > 3) return c->fail(TV_ERR_ARG, "mesh dim must be 1..3");
@@ -271,70 +367,13 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     c->plane_begin = b0;
     c->plane_end = b1;
     CgGrid& g = c->cg;
-    g.n0 = c->Nnode_glob[0];
-    g.n1 = c->Nnode_glob[1];
-    g.g_lo = (p > 0) ? 1 : 0;
-    g.g_hi = (p < P - 1) ? 1 : 0;
-    g.n2 = (b1 - b0) + g.g_lo + g.g_hi;
-    g.k_begin = g.g_lo;
-    g.k_end = g.g_lo + (b1 - b0);
-    g.deg1 = (c->perm[1] < 0);
-    g.deg2 = (c->perm[2] < 0);
-    g.bnd[0][0] = g.bnd[0][1] = 1;
-    g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
-    g.bnd[2][0] = (!g.deg2 && p == 0) ? 1 : 0;
-    g.bnd[2][1] = (!g.deg2 && p == P - 1) ? 1 : 0;
-    const int first[3] = {0, 0, b0 - g.g_lo};
-    const int cnt[3] = {g.n0, g.n1, g.n2};
-    for (int s = 0; s < 3; ++s) {
-      std::vector<double> cf;
-      axis_coefs(storage_coords(c, s, tmp), first[s], cnt[s], cf);
-      HIPC(hipMalloc(&c->coef[s], cf.size() * sizeof(double)));
-      HIPC(hipMemcpy(c->coef[s], cf.data(), cf.size() * sizeof(double), hipMemcpyHostToDevice));
-      g.coef[s] = c->coef[s];
-    }
+    std::vector<double> X[3];
+    for (int s = 0; s < 3; ++s) X[s] = storage_coords(c, s, tmp);
+    const int g_lo = (p > 0) ? 1 : 0, g_hi = (p < P - 1) ? 1 : 0;
+    if (int e = build_cg_grid(c, d, X, b0 - g_lo, (b1 - b0) + g_lo + g_hi, g_lo, g_hi, p == 0, p == P - 1, g, c->coef,
+                              &c->bnodes, c->ffbuf))
+      return e;
     const int64_t plane = (int64_t)g.n0 * g.n1;
-    for (int f = 0; f < 6; ++f) g.ffoff[f] = -1;
-    if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
-      std::vector<int64_t> bn;
-      for (int k = g.k_begin; k < g.k_end; ++k)
-        for (int j = 0; j < g.n1; ++j)
-          for (int i = 0; i < g.n0; ++i) {
-            const bool on = (i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1]) ||
-                            (j == 0 && g.bnd[1][0]) || (j == g.n1 - 1 && g.bnd[1][1]) ||
-                            (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
-            if (on) bn.push_back((int64_t)i + (int64_t)g.n0 * j + plane * k);
-          }
-      if (!bn.empty()) {
-        HIPC(hipMalloc(&c->bnodes, bn.size() * sizeof(int64_t)));
-        HIPC(hipMemcpy(c->bnodes, bn.data(), bn.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-      }
-      g.bnodes = c->bnodes;
-      g.n_bnodes = (int64_t)bn.size();
-      // facet-Jacobian terms: one value per node of every physical boundary
-      // face, the six faces in one contiguous buffer, two parities
-      const int nn[3] = {g.n0, g.n1, g.n2};
-      int64_t tot = 0;
-      for (int f = 0; f < 6; ++f) {
-        const int ax = f >> 1, side = f & 1;
-        g.fface[f] = nullptr;
-        g.fn1[f] = g.fn2[f] = 0;
-        g.ffoff[f] = -1;
-        if (!g.bnd[ax][side]) continue;
-        const int t1 = (ax == 0) ? 1 : 0, t2 = (ax == 2) ? 1 : 2;
-        g.fn1[f] = nn[t1];
-        g.fn2[f] = nn[t2];
-        g.ffoff[f] = tot;
-        tot += (int64_t)nn[t1] * nn[t2];
-      }
-      g.ffsize = tot;
-      for (int q = 0; q < 2; ++q) {
-        HIPC(hipMalloc(&c->ffbuf[q], sizeof(double) * (size_t)std::max<int64_t>(1, tot)));
-        HIPC(hipMemsetAsync(c->ffbuf[q], 0, sizeof(double) * (size_t)std::max<int64_t>(1, tot), c->stream));
-        g.ffbuf[q] = c->ffbuf[q];
-      }
-      for (int f = 0; f < 6; ++f) g.fface[f] = (g.ffoff[f] >= 0) ? c->ffbuf[0] + g.ffoff[f] : nullptr;
-    }
     c->nT = plane * g.n2;
     // the CG kernels index local nodes with 32-bit integers (68 M nodes = 290 GB
     // of state at materialize=1 would already exceed one MI355X)
@@ -800,6 +839,281 @@ static int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   return TV_OK;
 }
 
+// ---- geometric-multigrid preconditioned CG (options.preconditioner = GMG) ----
+// Gershgorin bound of D^-1 J on a rectilinear level: max over nodes of the
+// exact absolute row sum of the 27-point cell operator M + dt alpha K over its
+// diagonal (the tensor-product entries from the per-axis 1D rows), over the
+// distinct (row_x, row_y, row_z) combinations only.  The Robin facet rows are
+// facet masses (row sum / diagonal <= 2.25 for Q1 facets): floor 2.25, then 5 %.
+static double mg_gershgorin(const std::vector<double> (&X)[3], double dt_alpha) {
+  using Row = std::array<double, 6>;  // M lo / di / up, K lo / di / up
+  std::vector<Row> rows[3];
+  for (int s = 0; s < 3; ++s) {
+    std::vector<double> cf;
+    axis_coefs(X[s], 0, (int)X[s].size(), cf);
+    for (size_t i = 0; i < X[s].size(); ++i) {
+      const double* c = &cf[i * C_NCOEF];
+      rows[s].push_back({c[C_MLO], c[C_MDI], c[C_MUP], c[C_KLO], c[C_KDI], c[C_KUP]});
+    }
+    std::sort(rows[s].begin(), rows[s].end());
+    rows[s].erase(std::unique(rows[s].begin(), rows[s].end()), rows[s].end());
+  }
+  double b = 0.0;
+  for (const Row& r0 : rows[0])
+    for (const Row& r1 : rows[1])
+      for (const Row& r2 : rows[2]) {
+        double sum = 0.0, diag = 0.0;
+        for (int a = 0; a < 3; ++a)
+          for (int bb = 0; bb < 3; ++bb)
+            for (int cc = 0; cc < 3; ++cc) {
+              const double v = r0[a] * r1[bb] * r2[cc] +
+                               dt_alpha * (r0[3 + a] * r1[bb] * r2[cc] + r0[a] * r1[3 + bb] * r2[cc] +
+                                           r0[a] * r1[bb] * r2[3 + cc]);
+              sum += std::fabs(v);
+              if (a == 1 && bb == 1 && cc == 1) diag = v;
+            }
+        b = std::max(b, sum / diag);
+      }
+  return std::max(b, 2.25) * 1.05;
+}
+
+template <class T>
+static int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
+  void* p = nullptr;
+  HIPC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, h.size())));
+  L.bufs.push_back(p);
+  HIPC(hipMemcpy(p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  *out = static_cast<const T*>(p);
+  return TV_OK;
+}
+
+static double mg_omega(double b) { return 2.0 / (1.1 * b); }
+
+// the hierarchy below the fine grid (single partition, 3D CG1 marching path)
+static int mg_setup(Ctx* c) {
+  if (c->fam_T != TV_CG || c->dim != 3 || c->um || !cg_cgs_supported(c->cg))
+    return c->fail(TV_ERR_ARG, "preconditioner GMG: 3D CG1 temperature space on a rectilinear mesh only");
+  if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "preconditioner GMG: one partition (use TV_PC_JACOBI when partitioned)");
+  if (c->cgs) return c->fail(TV_ERR_ARG, "preconditioner GMG runs in the KSPCG form (pcg_variant KSPCG or AUTO)");
+  std::vector<double> tmp, Xf[3];
+  for (int s = 0; s < 3; ++s) Xf[s] = storage_coords(c, s, tmp);
+  const double da = c->P.dt * c->P.alpha;
+  c->mg_omega0 = mg_omega(mg_gershgorin(Xf, da));
+  HIPC(hipMalloc(&c->mgx, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
+  HIPC(hipMemsetAsync(c->mgx, 0, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT), c->stream));
+  const int max_levels = c->O.mg_levels > 0 ? c->O.mg_levels : 8;
+  const bool automatic = c->O.mg_levels <= 0;
+  std::vector<double> Xp[3] = {Xf[0], Xf[1], Xf[2]};
+  for (int lev = 1; lev < max_levels; ++lev) {
+    double h = 1e300;  // smallest mean cell length over the axes
+    bool coarsen[3], any = false;
+    for (int s = 0; s < 3; ++s) {
+      const int cells = (int)Xp[s].size() - 1;
+      coarsen[s] = cells >= 2;
+      any = any || coarsen[s];
+      if (cells >= 1) h = std::min(h, (Xp[s].back() - Xp[s].front()) / cells);
+    }
+    // stop where the operator is mass-dominated: a Jacobi step is then a good solve
+    if (!any || (automatic && da / (h * h) <= 0.5)) break;
+    c->mg.emplace_back();
+    MgLevel& L = c->mg.back();
+    std::vector<char> is_c[3];  // fine node kept on this level
+    for (int s = 0; s < 3; ++s) {
+      const int nf = (int)Xp[s].size();
+      is_c[s].assign(nf, 1);
+      if (!coarsen[s]) {
+        L.X[s] = Xp[s];
+        continue;
+      }
+      // every other node, and the last one (an odd cell count keeps one fine cell at the end)
+      for (int i = 0; i < nf; ++i) is_c[s][i] = (i % 2 == 0 || i == nf - 1) ? 1 : 0;
+      for (int i = 0; i < nf; ++i)
+        if (is_c[s][i]) L.X[s].push_back(Xp[s][i]);
+    }
+    if (int e = build_cg_grid(c, 3, L.X, 0, (int)L.X[2].size(), 0, 0, true, true, L.g, L.coef, &L.bnodes, L.ffbuf))
+      return e;
+    const CgGrid& f = c->cg;
+    L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
+    L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
+    L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+    for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
+      void* p = nullptr;
+      HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
+      HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)L.n, c->stream));
+      L.bufs.push_back(p);
+      *q = static_cast<double*>(p);
+    }
+    L.omega = mg_omega(mg_gershgorin(L.X, da));
+    // transfer maps (finer level Xp -> this level)
+    MgXfer& x = L.xf;
+    for (int s = 0; s < 3; ++s) {
+      const int nf = (int)Xp[s].size(), nc = (int)L.X[s].size();
+      std::vector<int> pi(2 * (size_t)nf), ri(3 * (size_t)nc), cpos(nf, -1), fpos;
+      std::vector<double> pw(2 * (size_t)nf, 0.0), rw(3 * (size_t)nc, 0.0);
+      for (int i = 0; i < nf; ++i)
+        if (is_c[s][i]) {
+          cpos[i] = (int)fpos.size();
+          fpos.push_back(i);
+        }
+      for (int i = 0; i < nf; ++i) {
+        if (is_c[s][i]) {
+          pi[2 * i] = pi[2 * i + 1] = cpos[i];
+          pw[2 * i] = 1.0;
+        } else {  // linear interpolation between the coarse neighbours i - 1 and i + 1
+          const double wl = (Xp[s][i + 1] - Xp[s][i]) / (Xp[s][i + 1] - Xp[s][i - 1]);
+          pi[2 * i] = cpos[i - 1];
+          pi[2 * i + 1] = cpos[i + 1];
+          pw[2 * i] = wl;
+          pw[2 * i + 1] = 1.0 - wl;
+        }
+      }
+      for (int I = 0; I < nc; ++I) {  // R = P^T: the fine nodes that interpolate from I
+        const int fc = fpos[I];
+        for (int q = 0; q < 3; ++q) ri[3 * I + q] = fc;
+        rw[3 * I + 1] = 1.0;
+        if (fc - 1 >= 0 && !is_c[s][fc - 1]) {
+          ri[3 * I] = fc - 1;
+          rw[3 * I] = pw[2 * (fc - 1) + 1];  // fine fc - 1: its right coarse neighbour is I
+        }
+        if (fc + 1 < nf && !is_c[s][fc + 1]) {
+          ri[3 * I + 2] = fc + 1;
+          rw[3 * I + 2] = pw[2 * (fc + 1)];  // fine fc + 1: its left coarse neighbour is I
+        }
+      }
+      if (int e = mg_upload(c, L, pi, &x.pi[s])) return e;
+      if (int e = mg_upload(c, L, pw, &x.pw[s])) return e;
+      if (int e = mg_upload(c, L, ri, &x.ri[s])) return e;
+      if (int e = mg_upload(c, L, rw, &x.rw[s])) return e;
+      x.fn[s] = nf;
+      x.cn[s] = nc;
+      x.coarse[s] = coarsen[s] ? 1 : 0;
+    }
+    x.f_kb = 0;
+    x.f_ke = x.fn[2];
+    x.c_kb = 0;
+    x.c_ke = x.cn[2];
+    for (int s = 0; s < 3; ++s) Xp[s] = L.X[s];
+  }
+  c->mg_on = true;
+  return TV_OK;
+}
+
+// per Newton iteration: T injected down the hierarchy, coarse Jacobi diagonals
+static void mg_prepare(Ctx* c, const double* T) {
+  const double* Tf = T;
+  for (MgLevel& L : c->mg) {
+    launch_mg_inject(L.xf, Tf, L.T, c->stream);
+    launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream);
+    Tf = L.T;
+  }
+}
+
+// V-cycle on coarse level l >= 1 (index l - 1 in c->mg): rhs b -> x; the
+// pre-smoothing step from 0 (x = omega D^-1 b) was formed by the restriction
+// that produced b.  The J x before the restriction is complete (k_cg_addfaces:
+// a per-node facet term inside the 27-point gather measured slower); the one
+// before the post-smoothing leaves the facet terms of the faces along the
+// march to that pointwise consumer (FaceAdd).
+static void mg_level(Ctx* c, size_t l) {
+  MgLevel& L = c->mg[l - 1];
+  hipStream_t s = c->stream;
+  if (l < c->mg.size()) {
+    MgLevel& C = c->mg[l];
+    const FaceAdd fa = cg_face_add(L.g, 0);
+    launch_cg_japply(L.g, L.T, L.x, L.w, nullptr, nullptr, s, c->st);
+    launch_mg_restrict(C.xf, c->st, L.b, L.w, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
+    mg_level(c, l + 1);
+    launch_mg_prolong(C.xf, c->st, L.x, C.x, nullptr, s);
+    launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
+    launch_mg_jacobi(L.n, c->st, L.b, L.w, &fa, L.dinv, L.omega, L.x, 1, s);  // post-smoothing
+  }
+}
+
+// level 0: x0 = omega dinv r is in c->mgx (k_mg_update); coarse correction,
+// post-smoothing into z with the (z.z, z.r) reduction tail
+static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
+  const int64_t n = c->nT;
+  hipStream_t s = c->stream;
+  const double* mask = c->dir_on ? c->dinv : nullptr;  // Dirichlet: the free subspace
+  const FaceAdd fa = cg_face_add(c->cg, 0);
+  if (!c->mg.empty()) {
+    MgLevel& C = c->mg[0];
+    launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+    launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
+    mg_level(c, 1);
+    launch_mg_prolong(C.xf, c->st, c->mgx, C.x, mask, s);
+  }
+  launch_cg_japply_partial(c->cg, T, c->mgx, c->w, c->st, s);
+  return launch_mg_post(n, c->st, c->mgx, c->r, c->w, &fa, c->dinv, c->mg_omega0, c->z, c->partials, tail, s);
+}
+
+static int mg_iteration(Ctx* c, const double* T, int it) {
+  const int64_t n = c->nT;
+  const int slot = c->ts_next + it;
+  uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
+  RedTail t1{c->counters, c->partials, c->sums, c->st, 2, ts};
+  int np = 0;
+  if (!op_japply_fused(c, T, &np, &t1, it))  // p <- z + b p ; w <- J p ; p.w ; alpha
+    if (int e = reduce_logic(c, np, 1, 2, 1)) return e;
+  const FaceAdd fa = cg_face_add(c->cg, 0);
+  launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
+                   c->stream);
+  RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 3, nullptr};
+  mg_apply0(c, T, &t2);  // z <- V(r); z.z, z.r; beta, convergence
+  return TV_OK;
+}
+
+static int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
+  const int64_t n = c->nT;
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  mg_prepare(c, T);
+  launch_mg_update(n, c->st, c->pA, c->pB, c->w, nullptr, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
+                   c->stream);  // dx <- 0, x0 <- omega dinv r
+  RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 1, nullptr};
+  mg_apply0(c, T, &t0);  // z <- V(r); dp, beta (KSPCG init)
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
+  // an MG iteration is ~30 launches: the first hint - 1 iterations are queued
+  // at once, then one at a time behind a poll (no look-ahead: an iteration
+  // queued past convergence still costs its launches)
+  int launched = 0;
+  auto enqueue = [&](int nb) -> int {
+    for (int b = 0; b < nb; ++b)
+      if (int e = mg_iteration(c, T, launched + b)) return e;
+    launched += nb;
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[0], c->stream));
+    return TV_OK;
+  };
+  HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipEventRecord(c->evp[0], c->stream));
+  HIPC(hipEventSynchronize(c->evp[0]));
+  if (!c->h_st[0].done) {
+    if (int e = enqueue(std::max(1, c->pcg_hint - 1))) return e;
+    for (;;) {
+      HIPC(hipEventSynchronize(c->evp[0]));
+      if (c->h_st[0].done) break;
+      if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+      if (int e = enqueue(1)) return e;
+    }
+  }
+  *its = c->h_st[0].it;
+  *reason = c->h_st[0].reason;
+  c->pcg_hint = std::max(1, c->h_st[0].it);
+  if (c->ktime) {
+    for (int it = 0; it < *its; it += c->kstride)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
+  }
+  return TV_OK;
+}
+
 // ---- single-reduction PCG (Chronopoulos-Gear form, k_cgs_march) -------------
 // w of the owned boundary planes + the face-workgroup facet terms (the value a
 // neighbour's ghost plane must hold), packed for the halo
@@ -1021,7 +1335,9 @@ static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;
     int k = 0, reason = 0;
-    if (int e = (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))) return e;
+    if (int e = (c->mg_on ? pcg_solve_mg(c, T, &k, &reason)
+                          : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
+      return e;
     kits += k;
     if (reason < 0)
       return c->fail(TV_ERR_KSP, std::string("Krylov solver did not converge (") + reason_str(reason) + ")");
@@ -1155,6 +1471,8 @@ void tv_default_options(tv_options* o) {
   o->pcg_batch = 8;
   o->pcg_variant = TV_PCG_AUTO;
   o->model_mode = TV_MODEL_REFERENCE;
+  o->preconditioner = TV_PC_JACOBI;
+  o->mg_levels = 0;
 }
 
 void tv_default_params(tv_params* p) {
@@ -1220,6 +1538,8 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
   }
   int rc = setup_mesh(c.get(), mesh);
   if (rc == TV_OK) rc = setup_fields(c.get());
+  if (rc == TV_OK && c->O.preconditioner == TV_PC_GMG) rc = mg_setup(c.get());
+  else if (rc == TV_OK && c->O.preconditioner != TV_PC_JACOBI) rc = c->fail(TV_ERR_ARG, "unknown preconditioner");
   if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
   if (rc != TV_OK) {
     set_global_error(c->err);
@@ -1299,6 +1619,10 @@ int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, co
     set_global_error("HIP stream/event creation failed");
     return TV_ERR_HIP;
   }
+  if (c->O.preconditioner != TV_PC_JACOBI) {
+    set_global_error("unstructured meshes: preconditioner TV_PC_JACOBI only");
+    return TV_ERR_ARG;
+  }
   int rc = setup_umesh(c.get(), mesh);
   if (rc == TV_OK) rc = setup_fields(c.get());
   if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
@@ -1362,6 +1686,15 @@ int tv_destroy(void* ctx) {
     if (p) hipFree(p);
   um_free(c->umd);
   if (c->um_bmask) hipFree(c->um_bmask);
+  for (MgLevel& L : c->mg) {
+    for (void* p : L.bufs) hipFree(p);
+    for (int s = 0; s < 3; ++s)
+      if (L.coef[s]) hipFree(L.coef[s]);
+    if (L.bnodes) hipFree(L.bnodes);
+    for (int q = 0; q < 2; ++q)
+      if (L.ffbuf[q]) hipFree(L.ffbuf[q]);
+  }
+  if (c->mgx) hipFree(c->mgx);
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
     if (p) hipFree(p);
   for (int s = 0; s < 3; ++s) {
@@ -1786,6 +2119,16 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
     case 8:
       *bytes = 48.0 * n;
       break;
+    case 11: {  // one multigrid V-cycle (level 0: 2 J x, restriction, prolongation, post-smoothing)
+      if (!c->mg_on) return c->fail(TV_ERR_ARG, "kernel 11: preconditioner GMG not enabled");
+      double b = (16.0 * 2 + 16 + 16 + 40) * n;
+      for (size_t l = 0; l < c->mg.size(); ++l) {
+        const double nl = (double)c->mg[l].n;
+        b += (l + 1 < c->mg.size()) ? (24.0 + 16 * 2 + 16 + 16 + 40) * nl + 8.0 * nl : 24.0 * nl + 8.0 * nl;
+      }
+      *bytes = b;
+      break;
+    }
     default:
       return c->fail(TV_ERR_ARG, "unknown kernel id");
   }
@@ -1804,9 +2147,17 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
   }
   int upd_it = 0;
+  if (kernel == 11) {  // V-cycles on the current state (solver state reset: not converged)
+    if (!c->mg_on) return c->fail(TV_ERR_ARG, "kernel 11: preconditioner GMG not enabled");
+    PcgState h{};
+    h.max_it = 1 << 30;
+    HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+    mg_prepare(c, c->f[TV_F_T].ptr);
+  }
   auto one = [&]() -> int {
     int np = 0;
     switch (kernel) {
+      case 11: mg_apply0(c, c->f[TV_F_T].ptr, nullptr); return TV_OK;
       case 0: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); return TV_OK;
       case 1: return visco(c, false);
       case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;

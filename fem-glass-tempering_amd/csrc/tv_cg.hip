@@ -638,7 +638,9 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
 // out[n] += sum of the facet terms of the owned boundary node n (every face
 // it lies on), for the non-fused J(T) x
 __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t* __restrict__ bnodes, int64_t nb,
-                                                        double* __restrict__ out, int qaxis) {
+                                                        double* __restrict__ out, int qaxis,
+                                                        const PcgState* __restrict__ st) {
+  if (st != nullptr && st->done) return;  // queued behind a converged solve (multigrid V-cycle)
   const int n[3] = {g.n0, g.n1, g.n2};
   for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < nb; e += (int64_t)gridDim.x * kBlock) {
     const int nd = (int)bnodes[e];
@@ -702,7 +704,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   }
   if (fidx >= 0) {
     if (exp & 16) return;  // timing experiment only (TVFEM_MARCH_EXP): no face work
-    if (FUSEP && st->done) return;
+    if (st != nullptr && st->done) return;
     face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec, fidx, fo, fsm, red, it_host);
     return;
   }
@@ -826,6 +828,8 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   if (FUSEP) {
     if (st->done) return;
     bcoef = first ? 0.0 : st->beta / st->betaold;
+  } else if (st != nullptr && st->done) {
+    return;  // plain J x inside a converged solve's queued V-cycle
   }
   // face planes: T, z (, p_old) of the own and halo rows
   double fT[2][2], fZ[2][2], fO[2][2];  // [face][own, halo]
@@ -1946,7 +1950,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
 template <int MODE, bool FUSEP>
 bool launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
                  double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s,
-                 const RedTail* tail = nullptr, int it_host = 0) {
+                 const RedTail* tail = nullptr, int it_host = 0, bool addfaces = true) {
   const Launch L = plan(g, ghosts);
   if (L.blocks <= 0) return false;
   if (L.march) {
@@ -1972,9 +1976,9 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     else if (pf == 3) TV_MARCH(8, 1, 3);
     else TV_MARCH(8, 1, 4);
 #undef TV_MARCH
-    if (folded && !FUSEP && fo.off[6] > 0) {  // complete J x (the fused PCG adds them in the update)
+    if (folded && !FUSEP && addfaces && fo.off[6] > 0) {  // complete J x (else the consumer adds them)
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.n_bnodes + kBlock - 1) / kBlock, 1024));
-      hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, g.bnodes, g.n_bnodes, out, 3 - L.raxis);
+      hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, g.bnodes, g.n_bnodes, out, 3 - L.raxis, st);
     }
     if (folded) return rt.counter != nullptr;
     if (g.n_bnodes > 0) {
@@ -2024,9 +2028,14 @@ void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, doub
 }
 
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
-                      int* n_partials, hipStream_t s) {
-  launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, nullptr, partials, false, s);
+                      int* n_partials, hipStream_t s, const PcgState* st) {
+  launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, st, partials, false, s);
   if (n_partials) *n_partials = plan(g, false).nparts;
+}
+
+void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
+                              hipStream_t s) {
+  launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, st, nullptr, false, s, nullptr, 0, false);
 }
 
 bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, double* pA, double* pB,

@@ -252,6 +252,41 @@ __device__ __forceinline__ void cgs_tail(const RedTail& rt, int n, PcgState* st,
   }
 }
 
+// Robin facet terms of node t (local index t + t_off) left out of w by the
+// fused CG matvec (marching path); 0 off the physical boundary faces
+__device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
+  const int nd = (int)(t + fa.t_off);
+  const int plane = fa.n0 * fa.n1;
+  int k = (int)((double)nd * fa.inv_plane);
+  k -= (k * plane > nd) ? 1 : 0;
+  k += ((k + 1) * plane <= nd) ? 1 : 0;
+  const int rem = nd - k * plane;
+  int j = (int)((double)rem * fa.inv_n0);
+  j -= (j * fa.n0 > rem) ? 1 : 0;
+  j += ((j + 1) * fa.n0 <= rem) ? 1 : 0;
+  const int i = rem - j * fa.n0;
+  double add = 0.0;
+  if (i == 0 && fa.ff[0]) add += fa.ff[0][j + fa.n1 * k];
+  if (i == fa.n0 - 1 && fa.ff[1]) add += fa.ff[1][j + fa.n1 * k];
+  if (j == 0 && fa.ff[2]) add += fa.ff[2][i + fa.n0 * k];
+  if (j == fa.n1 - 1 && fa.ff[3]) add += fa.ff[3][i + fa.n0 * k];
+  if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
+  if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
+  return add;
+}
+
+// the same at local node (i, j, k) (coordinates known)
+__device__ __forceinline__ double face_at(const FaceAdd& fa, int i, int j, int k) {
+  double add = 0.0;
+  if (i == 0 && fa.ff[0]) add += fa.ff[0][j + fa.n1 * k];
+  if (i == fa.n0 - 1 && fa.ff[1]) add += fa.ff[1][j + fa.n1 * k];
+  if (j == 0 && fa.ff[2]) add += fa.ff[2][i + fa.n0 * k];
+  if (j == fa.n1 - 1 && fa.ff[3]) add += fa.ff[3][i + fa.n0 * k];
+  if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
+  if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
+  return add;
+}
+
 // Start stamp of a launch with a timed reduction tail: workgroup 0 is the
 // first one the dispatcher places, so its entry time is the launch's start.
 __device__ __forceinline__ void stamp_start(const RedTail& rt) {

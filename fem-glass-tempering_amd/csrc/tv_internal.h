@@ -191,7 +191,7 @@ int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, do
 // ---- kernel launchers (tv_cg.hip, tv_dg.hip, tv_visco.hip, tv_pcg.hip) ----
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
-                      int* n_partials, hipStream_t s);
+                      int* n_partials, hipStream_t s, const PcgState* st = nullptr);
 // returns true when the launch ends with the in-kernel reduction tail (the
 // caller then skips the separate reduce launch)
 // it_host: the PCG iteration index the host launches (== st->it while the
@@ -265,6 +265,50 @@ struct FaceAdd {
   const double* ff[6];
 };
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off);
+
+// ---- geometric multigrid on the box hierarchy (tv_mg.hip, tv_pcg.hip) ----
+// Transfer between a level and the next coarser one (nested rectilinear grids:
+// along a coarsened axis fine node 2I is coarse node I, odd fine nodes
+// interpolate linearly between their two coarse neighbours).  Per storage
+// axis: prolongation = two (coarse index, weight) pairs per fine node,
+// restriction (its transpose) = three (fine index, weight) pairs per coarse
+// node; indices are local (ghost planes included).
+struct MgXfer {
+  int fn[3], cn[3];           // local node counts of the fine / coarse level
+  int coarse[3];              // axis coarsened (else identity along it)
+  int f_kb, f_ke, c_kb, c_ke; // owned planes (storage axis 2) of the fine / coarse level
+  const int* pi[3];           // [2 fn[a]]
+  const double* pw[3];
+  const int* ri[3];           // [3 cn[a]]
+  const double* rw[3];
+};
+// bc <- P^T (bf - (wf + facet terms fa)) on the coarse owned nodes (mask:
+// level-0 dinv, 0 = excluded node); xc != nullptr: also the coarse level's
+// pre-smoothing from 0, xc <- omega_c dinv_c bc
+void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, const double* wf, const FaceAdd* fa,
+                        const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
+                        hipStream_t s);
+// xf <- xf + P xc on the fine owned nodes (mask as above: x stays 0 on excluded nodes)
+void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
+                       hipStream_t s);
+// mode 0: x <- omega dinv b ; mode 1: x <- x + omega dinv (b - (w + facet terms fa))    (damped Jacobi)
+void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
+                      const double* dinv, double omega, double* x, int mode, hipStream_t s);
+void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t s);  // coarse T <- fine T
+// J x without the facet terms of the faces along the march (the FaceAdd the
+// consumer adds, cg_face_add); the whole J x where the row kernel runs
+void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
+                              hipStream_t s);
+// level 0 of the PCG (tv_pcg.hip): r <- r - a (w + facet terms), dx <- dx + a p,
+// x0 <- omega dinv r (the V-cycle's pre-smoothing from 0); init: dx <- 0, x0 <- omega dinv r
+void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
+                      const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
+                      int it_host, int init, hipStream_t s);
+// z <- x0 + omega dinv (r - (w + facet terms)) (post-smoothing), (z.z, z.r) records + reduction tail;
+// returns the record count
+int launch_mg_post(int64_t n, const PcgState* st, const double* x0, const double* r, const double* w,
+                   const FaceAdd* fa, const double* dinv, double omega, double* z, double* partials,
+                   const RedTail* tail, hipStream_t s);
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* dinv, double* dx, double* z, double* partials, hipStream_t s,

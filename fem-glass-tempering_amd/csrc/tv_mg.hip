@@ -1,0 +1,215 @@
+// Geometric multigrid on the box hierarchy: grid-transfer and smoothing
+// kernels of the V-cycle preconditioner (gfx950).
+//
+// Replaces, for 3D CG1 rectilinear meshes, the algebraic multigrid the
+// reference configures for its Krylov solve (PCGAMG, ThermoViscoProblem.py:
+// 343-346).  The hierarchy is the box itself, every other node kept along each
+// axis (plus the last node when the cell count is odd, so the coarse nodes are
+// always a subset of the fine ones: P is exact linear interpolation, R = P^T);
+// the coarse operators are the same matrix-free tensor-product Jacobian on the
+// coarse grid (tv_cg.hip), with T injected.  Smoother: damped Jacobi, omega =
+// 2 / (1.1 b) with b the Gershgorin bound of D^-1 J (exact row sums of the
+// 27-point stencil), the same polynomial before and after the coarse
+// correction, so the V-cycle is a fixed symmetric positive definite operator
+// (CG stays CG).
+//
+// Every kernel exits at once when the solve has converged (st->done), so the
+// V-cycles queued behind the converged iteration cost a launch each.
+// Bytes (algorithmic, per node of the level): restriction 16 (r, w of the fine
+// level) + 8 / 8 (coarse write), prolongation 16 (+ coarse reads, cached),
+// Jacobi step 24 / 40.
+#include <algorithm>
+
+#include "tv_device.h"
+
+namespace tv {
+namespace {
+
+// Index maps along one axis, in closed form so no gathered address depends on
+// a table load (the weights still come from the tables, independently): the
+// coarse nodes are the even fine nodes and, for an odd cell count, the last
+// one (fn - 1).
+__device__ __forceinline__ void pmap(const MgXfer& x, int a, int i, int& c0, int& c1) {
+  if (!x.coarse[a]) {
+    c0 = c1 = i;
+  } else if (!(i & 1)) {
+    c0 = c1 = i >> 1;
+  } else if (i == x.fn[a] - 1) {
+    c0 = c1 = (i + 1) >> 1;
+  } else {
+    c0 = (i - 1) >> 1;
+    c1 = (i + 1) >> 1;
+  }
+}
+// the fine centre of coarse node I and its two neighbours (clamped to the centre
+// where absent; their restriction weights are 0 there)
+__device__ __forceinline__ void rmap(const MgXfer& x, int a, int I, int& f0, int& f1, int& f2) {
+  if (!x.coarse[a]) {
+    f0 = f1 = f2 = I;
+    return;
+  }
+  const int nf = x.fn[a];
+  f1 = (I == x.cn[a] - 1 && ((nf - 1) & 1)) ? nf - 1 : 2 * I;
+  f0 = (f1 >= 1) ? f1 - 1 : f1;
+  f2 = (f1 + 1 < nf) ? f1 + 1 : f1;
+}
+
+// One thread per output node (flat index over the owned planes, 32-bit decode).
+// b_c(I) = sum over the 3 x 3 x 3 fine nodes f of w(f, I) (b_f - w_f)(f)
+template <bool FACES>
+__global__ __launch_bounds__(kBlock) void k_mg_restrict(MgXfer x, const PcgState* __restrict__ st,
+                                                        const double* __restrict__ bf,
+                                                        const double* __restrict__ wf, FaceAdd fa,
+                                                        const double* __restrict__ mask, double* __restrict__ bc,
+                                                        const double* __restrict__ dinv_c, double omega_c,
+                                                        double* __restrict__ xc) {
+  if (st != nullptr && st->done) return;
+  const int plane = x.cn[0] * x.cn[1];
+  const int n = plane * (x.c_ke - x.c_kb);
+  const int fpl = x.fn[0] * x.fn[1];
+  for (int t = blockIdx.x * kBlock + threadIdx.x; t < n; t += gridDim.x * kBlock) {
+    const int k = t / plane + x.c_kb;
+    const int rem = t - (k - x.c_kb) * plane;
+    const int j = rem / x.cn[0];
+    const int i = rem - j * x.cn[0];
+    int fi[3], fj[3], fk[3];
+    rmap(x, 0, i, fi[0], fi[1], fi[2]);
+    rmap(x, 1, j, fj[0], fj[1], fj[2]);
+    rmap(x, 2, k, fk[0], fk[1], fk[2]);
+    double wi[3], wj[3], wk[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      wi[q] = x.rw[0][3 * i + q];
+      wj[q] = x.rw[1][3 * j + q];
+      wk[q] = x.rw[2][3 * k + q];
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double pl = 0.0;
+#pragma unroll
+      for (int b = 0; b < 3; ++b) {
+        const int base = fj[b] * x.fn[0] + fpl * fk[c];
+        double row = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          const int f = base + fi[a];
+          double r = bf[f] - wf[f];
+          if (mask != nullptr && mask[f] == 0.0) r = 0.0;
+          row += wi[a] * r;
+        }
+        pl += wj[b] * row;
+      }
+      acc += wk[c] * pl;
+    }
+    const int o = t + plane * x.c_kb;
+    bc[o] = acc;
+    if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;  // the coarse pre-smoothing step from 0
+  }
+}
+
+// x_f(f) += sum over the 2 x 2 x 2 coarse nodes I of w(f, I) x_c(I)
+__global__ __launch_bounds__(kBlock) void k_mg_prolong(MgXfer x, const PcgState* __restrict__ st,
+                                                       double* __restrict__ xf, const double* __restrict__ xc,
+                                                       const double* __restrict__ mask) {
+  if (st != nullptr && st->done) return;
+  const int plane = x.fn[0] * x.fn[1];
+  const int n = plane * (x.f_ke - x.f_kb);
+  const int cpl = x.cn[0] * x.cn[1];
+  for (int t = blockIdx.x * kBlock + threadIdx.x; t < n; t += gridDim.x * kBlock) {
+    const int f = t + plane * x.f_kb;
+    const int k = f / plane;
+    const int rem = f - k * plane;
+    const int j = rem / x.fn[0];
+    const int i = rem - j * x.fn[0];
+    int ci[2], cj[2], ck[2];
+    pmap(x, 0, i, ci[0], ci[1]);
+    pmap(x, 1, j, cj[0], cj[1]);
+    pmap(x, 2, k, ck[0], ck[1]);
+    double v[2][2][2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) v[c][b][a] = xc[ci[a] + x.cn[0] * cj[b] + cpl * ck[c]];
+    const double wi0 = x.pw[0][2 * i], wi1 = x.pw[0][2 * i + 1];
+    const double wj0 = x.pw[1][2 * j], wj1 = x.pw[1][2 * j + 1];
+    const double wk0 = x.pw[2][2 * k], wk1 = x.pw[2][2 * k + 1];
+    const double p0 = wj0 * (wi0 * v[0][0][0] + wi1 * v[0][0][1]) + wj1 * (wi0 * v[0][1][0] + wi1 * v[0][1][1]);
+    const double p1 = wj0 * (wi0 * v[1][0][0] + wi1 * v[1][0][1]) + wj1 * (wi0 * v[1][1][0] + wi1 * v[1][1][1]);
+    const double acc = wk0 * p0 + wk1 * p1;
+    const bool off = mask != nullptr && mask[f] == 0.0;
+    xf[f] = off ? 0.0 : xf[f] + acc;
+  }
+}
+
+template <int MODE, bool FACES>
+__global__ __launch_bounds__(kBlock) void k_mg_jacobi(int64_t n, const PcgState* __restrict__ st,
+                                                      const double* __restrict__ b, const double* __restrict__ w,
+                                                      FaceAdd fa, const double* __restrict__ dinv, double omega,
+                                                      double* __restrict__ x) {
+  if (st != nullptr && st->done) return;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    if (MODE == 0) {
+      x[t] = omega * dinv[t] * b[t];
+    } else {
+      double wt = w[t];
+      if (FACES) wt += face_terms(fa, t);
+      x[t] += omega * dinv[t] * (b[t] - wt);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_mg_inject(MgXfer x, const double* __restrict__ Tf,
+                                                      double* __restrict__ Tc, int nxb) {
+  const int row = (int)blockIdx.x / nxb;
+  const int i = ((int)blockIdx.x - row * nxb) * kBlock + (int)threadIdx.x;
+  const int j = row % x.cn[1], k = row / x.cn[1];
+  if (i >= x.cn[0]) return;
+  // the fine node that coincides with coarse node (i, j, k): restriction entry 1 (weight 1)
+  const int64_t f = x.ri[0][3 * i + 1] + (int64_t)x.fn[0] * (x.ri[1][3 * j + 1] + (int64_t)x.fn[1] * x.ri[2][3 * k + 1]);
+  Tc[(int64_t)i + (int64_t)x.cn[0] * (j + (int64_t)x.cn[1] * k)] = Tf[f];
+}
+
+int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
+
+}  // namespace
+
+void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, const double* wf, const FaceAdd* fa,
+                        const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
+                        hipStream_t s) {
+  const int64_t n = (int64_t)x.cn[0] * x.cn[1] * (x.c_ke - x.c_kb);
+  if (n <= 0) return;
+  const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
+  if (f.on)
+    hipLaunchKernelGGL(k_mg_restrict<true>, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, st, bf, wf, f, mask, bc, dinv_c,
+                       omega_c, xc);
+  else
+    hipLaunchKernelGGL(k_mg_restrict<false>, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, st, bf, wf, f, mask, bc,
+                       dinv_c, omega_c, xc);
+}
+
+void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
+                       hipStream_t s) {
+  const int64_t n = (int64_t)x.fn[0] * x.fn[1] * (x.f_ke - x.f_kb);
+  if (n > 0) hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, st, xf, xc, mask);
+}
+
+void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
+                      const double* dinv, double omega, double* x, int mode, hipStream_t s) {
+  if (n <= 0) return;
+  const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
+  const dim3 g(blocks_for(n)), bl(kBlock);
+  if (mode == 0) hipLaunchKernelGGL((k_mg_jacobi<0, false>), g, bl, 0, s, n, st, b, w, f, dinv, omega, x);
+  else if (f.on) hipLaunchKernelGGL((k_mg_jacobi<1, true>), g, bl, 0, s, n, st, b, w, f, dinv, omega, x);
+  else hipLaunchKernelGGL((k_mg_jacobi<1, false>), g, bl, 0, s, n, st, b, w, f, dinv, omega, x);
+}
+
+void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t s) {
+  const int nxb = (x.cn[0] + kBlock - 1) / kBlock;
+  const int64_t rows = (int64_t)x.cn[1] * x.cn[2];
+  if (rows > 0) hipLaunchKernelGGL(k_mg_inject, dim3((unsigned)(rows * nxb)), dim3(kBlock), 0, s, x, Tf, Tc, nxb);
+}
+
+}  // namespace tv

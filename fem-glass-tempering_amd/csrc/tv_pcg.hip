@@ -54,29 +54,6 @@ __global__ __launch_bounds__(kBlock) void k_pcg_init(int64_t n, const double* __
   block_partials<2>(acc, partials);
 }
 
-// Robin facet terms of node t (local index t + t_off) left out of w by the
-// fused CG matvec (marching path); 0 off the physical boundary faces
-__device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
-  const int nd = (int)(t + fa.t_off);
-  const int plane = fa.n0 * fa.n1;
-  int k = (int)((double)nd * fa.inv_plane);
-  k -= (k * plane > nd) ? 1 : 0;
-  k += ((k + 1) * plane <= nd) ? 1 : 0;
-  const int rem = nd - k * plane;
-  int j = (int)((double)rem * fa.inv_n0);
-  j -= (j * fa.n0 > rem) ? 1 : 0;
-  j += ((j + 1) * fa.n0 <= rem) ? 1 : 0;
-  const int i = rem - j * fa.n0;
-  double add = 0.0;
-  if (i == 0 && fa.ff[0]) add += fa.ff[0][j + fa.n1 * k];
-  if (i == fa.n0 - 1 && fa.ff[1]) add += fa.ff[1][j + fa.n1 * k];
-  if (j == 0 && fa.ff[2]) add += fa.ff[2][i + fa.n0 * k];
-  if (j == fa.n1 - 1 && fa.ff[3]) add += fa.ff[3][i + fa.n0 * k];
-  if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
-  if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
-  return add;
-}
-
 // Cache policy of the update's streams (TVFEM_NT bits, default 7): 1 = w, dx,
 // p_prev loads non-temporal, 2 = dx stores non-temporal, 4 = dinv load
 // non-temporal.  Only p (the next matvec's p_old) and z (its input) are written
@@ -149,6 +126,59 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
     double v[6];
     load(t, v);
     node(t, v);
+  }
+  block_partials<2>(acc, partials);
+  fused_reduce_tail<2>(rt, gridDim.x);
+}
+
+// ---- multigrid-preconditioned CG: level-0 vector kernels --------------------
+// KSPCG update with an explicit residual (the V-cycle smooths against r):
+// r <- r - a (w + facet terms), dx <- dx + a p, and the V-cycle's first
+// pre-smoothing step from 0, x0 <- omega dinv r.  INIT: dx <- 0, x0 <- omega dinv r.
+template <bool FACES, bool INIT>
+__global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState* __restrict__ st,
+                                                      const double* __restrict__ pA, const double* __restrict__ pB,
+                                                      const double* __restrict__ w, FaceAdd fa,
+                                                      const double* __restrict__ dinv, double omega,
+                                                      double* __restrict__ r, double* __restrict__ dx,
+                                                      double* __restrict__ x0, int it_host) {
+  if (st->done) return;
+  const double a = INIT ? 0.0 : st->a;
+  const double* __restrict__ p = (it_host & 1) ? pB : pA;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    double rr = r[t];
+    if (INIT) {
+      dx[t] = 0.0;
+    } else {
+      double wt = ldc<true>(&w[t]);
+      if (FACES) wt += face_terms(fa, t);
+      rr -= a * wt;
+      r[t] = rr;
+      stc<true>(&dx[t], ldc<true>(&dx[t]) + a * ldc<true>(&p[t]));
+    }
+    x0[t] = omega * ldc<true>(&dinv[t]) * rr;
+  }
+}
+
+// post-smoothing of level 0: z <- x0 + omega dinv (r - w), w = J x0; (z.z,
+// z.r) records and the KSPCG logic in the reduction tail (init: kind 1)
+template <bool FACES>
+__global__ __launch_bounds__(kBlock) void k_mg_post(int64_t n, const PcgState* __restrict__ st,
+                                                    const double* __restrict__ x0, const double* __restrict__ r,
+                                                    const double* __restrict__ w, FaceAdd fa,
+                                                    const double* __restrict__ dinv, double omega,
+                                                    double* __restrict__ z, double* __restrict__ partials,
+                                                    RedTail rt) {
+  if (st->done) return;
+  double acc[2] = {0.0, 0.0};
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    const double rr = r[t];
+    double wt = w[t];
+    if (FACES) wt += face_terms(fa, t);
+    const double zz = x0[t] + omega * dinv[t] * (rr - wt);
+    z[t] = zz;
+    acc[0] += zz * zz;
+    acc[1] += zz * rr;
   }
   block_partials<2>(acc, partials);
   fused_reduce_tail<2>(rt, gridDim.x);
@@ -241,6 +271,32 @@ int pcg_vec_blocks(int64_t n) { return vec_blocks(n); }
 void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, double* dx, double* partials,
                      hipStream_t s) {
   hipLaunchKernelGGL(k_pcg_init, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, r, dinv, z, dx, partials);
+}
+
+void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
+                      const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
+                      int it_host, int init, hipStream_t s) {
+  const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
+  const dim3 g(vec_blocks(n)), b(kBlock);
+  if (init)
+    hipLaunchKernelGGL((k_mg_update<false, true>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host);
+  else if (f.on)
+    hipLaunchKernelGGL((k_mg_update<true, false>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host);
+  else
+    hipLaunchKernelGGL((k_mg_update<false, false>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host);
+}
+
+int launch_mg_post(int64_t n, const PcgState* st, const double* x0, const double* r, const double* w,
+                   const FaceAdd* fa, const double* dinv, double omega, double* z, double* partials,
+                   const RedTail* tail, hipStream_t s) {
+  const RedTail rt = tail ? *tail : RedTail{};
+  const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
+  const int nb = vec_blocks(n);
+  if (f.on)
+    hipLaunchKernelGGL(k_mg_post<true>, dim3(nb), dim3(kBlock), 0, s, n, st, x0, r, w, f, dinv, omega, z, partials, rt);
+  else
+    hipLaunchKernelGGL(k_mg_post<false>, dim3(nb), dim3(kBlock), 0, s, n, st, x0, r, w, f, dinv, omega, z, partials, rt);
+  return nb;
 }
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,

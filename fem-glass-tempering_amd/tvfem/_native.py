@@ -16,6 +16,7 @@ TV_OK, TV_ERR_ARG, TV_ERR_HIP, TV_ERR_NOT_CONVERGED, TV_ERR_KSP, TV_ERR_STATE, T
 TV_CG, TV_DG = 0, 1
 TV_PCG_AUTO, TV_PCG_KSPCG, TV_PCG_SINGLE_REDUCTION = 0, 1, 2
 TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
+TV_PC_JACOBI, TV_PC_GMG = 0, 1
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -79,7 +80,7 @@ class Options(C.Structure):
                 ("error_on_nonconvergence", C.c_int), ("ksp_rtol", C.c_double), ("ksp_atol", C.c_double),
                 ("ksp_dtol", C.c_double), ("ksp_max_it", C.c_int), ("materialize", C.c_int),
                 ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
-                ("model_mode", C.c_int)]
+                ("model_mode", C.c_int), ("preconditioner", C.c_int), ("mg_levels", C.c_int)]
 
 
 _lib = None
@@ -153,7 +154,7 @@ def load_library():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.tv_abi_version() != 1:
+    if lib.tv_abi_version() != 2:
         raise NativeError(TV_ERR_ARG, "libtvfem ABI version mismatch")
     _lib = lib
     return lib

@@ -102,7 +102,8 @@ class ThermoViscoProblem:
                  jit_options: dict | None = None, *, device: int = 0, materialize: bool = True,
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
-                 write_output: bool = False, output_dir: str = "output") -> None:
+                 write_output: bool = False, output_dir: str = "output", preconditioner: str = "jacobi",
+                 mg_levels: int = 0) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -129,6 +130,11 @@ class ThermoViscoProblem:
         self.write_output = write_output
         self.output_dir = output_dir
         self._output_open = False
+        if preconditioner not in ("jacobi", "gmg"):
+            raise ValueError("preconditioner must be 'jacobi' (PETSc PCJACOBI, the oracle's) or 'gmg' "
+                             "(geometric multigrid on the box hierarchy)")
+        self.preconditioner = preconditioner
+        self._mg_levels = int(mg_levels)
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -200,6 +206,8 @@ class ThermoViscoProblem:
         opts.pcg_variant = {"auto": N.TV_PCG_AUTO, "kspcg": N.TV_PCG_KSPCG,
                             "single": N.TV_PCG_SINGLE_REDUCTION}[pcg_variant]
         opts.model_mode = N.TV_MODEL_PAPER if self.model_mode == "paper" else N.TV_MODEL_REFERENCE
+        opts.preconditioner = N.TV_PC_GMG if self.preconditioner == "gmg" else N.TV_PC_JACOBI
+        opts.mg_levels = self._mg_levels
         ctx = C.c_void_p()
         create = lib.tv_create_unstructured if um else lib.tv_create
         N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))

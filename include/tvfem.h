@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 1
+#define TV_ABI_VERSION 2  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels */
 
 /* status codes */
 #define TV_OK 0
@@ -128,7 +128,24 @@ typedef struct {
   int pcg_batch;          /* iterations launched between convergence polls  */
   int pcg_variant;        /* TV_PCG_AUTO / TV_PCG_KSPCG / TV_PCG_SINGLE_REDUCTION */
   int model_mode;         /* TV_MODEL_REFERENCE (default) / TV_MODEL_PAPER       */
+  int preconditioner;     /* TV_PC_JACOBI (default) / TV_PC_GMG                  */
+  int mg_levels;          /* GMG: levels incl. the fine one (0: automatic)       */
 } tv_options;
+
+/* Preconditioner of the Krylov solve (the reference configures PCGAMG,
+ * ThermoViscoProblem.py:343-346; PETSc's GAMG is not reproducible here):
+ *   JACOBI  point Jacobi (the oracle's PETSc KSPCG + PCJACOBI restatement; the
+ *           Krylov iteration counts the parity tests compare);
+ *   GMG     geometric multigrid V-cycle on the box hierarchy (3D CG1
+ *           rectilinear meshes on one partition): the box coarsened by two
+ *           along every axis with an even cell count until the coarsest level
+ *           is mass-dominated (dt alpha / h^2 <= 0.5) or cannot coarsen, damped
+ *           Jacobi smoothing (Gershgorin-bounded weight), coarse operators
+ *           re-discretised with T injected.  Same Newton solution (the linear
+ *           solves reach the same relative tolerance), ~4 instead of ~33 Krylov
+ *           iterations per solve at C4. */
+#define TV_PC_JACOBI 0
+#define TV_PC_GMG 1
 
 /* Model semantics.  REFERENCE reproduces the reference as it runs, quirks
  * included.  PAPER (opt-in, never the default) applies

@@ -1,0 +1,156 @@
+"""Geometric-multigrid preconditioner (options.preconditioner = GMG, tv_mg.hip)
+on the box hierarchy -- SURVEY.md section 8(f) rank 3; the reference configures
+PCGAMG (ThermoViscoProblem.py:343-346).
+
+The preconditioner changes the Krylov iterates, not the Newton solution: every
+linear solve still reaches rtol 1e-5 and Newton still stops at
+||dx|| / ||dx_1|| < 1e-12, so T must match the oracle (its PETSc KSPCG + Jacobi
+restatement) to the same 1e-10 as the Jacobi path, with the same Newton
+iteration counts.  The Krylov count must drop (the point of the preconditioner).
+Stresses follow T (pointwise update), checked with parity_util.check_field.
+"""
+import numpy as np
+import pytest
+
+from oracle import tv_oracle as O
+from parity_util import check_field, relerr
+
+CG = {"element": "CG", "degree": 1}
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _pair(axes, mode="reference", **kw):
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    cfg = {"T": CG, "sigma": CG}
+    dev = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False,
+                             part_axis=2, model_mode=mode, **kw)
+    ref = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), linear="pcg",
+                          model_mode=mode)
+    return dev, ref
+
+
+CASES = {
+    # h = 0.125 as at C4 (dt alpha / h^2 = 6.4): three levels
+    "plate": [np.linspace(0.0, 4.0, 33), np.linspace(0.0, 3.0, 25), np.linspace(0.0, 1.0, 9)],
+    # graded axes (non-uniform interpolation weights), one odd axis (not coarsened)
+    "graded": [np.concatenate([np.linspace(0.0, 0.5, 9), np.linspace(0.5, 2.5, 9)[1:]]),
+               np.linspace(0.0, 2.0, 17), np.linspace(0.0, 0.75, 8)],
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(CASES))
+def test_gmg_steps_match_oracle(case):
+    _torch()
+    axes = CASES[case]
+    dev, ref = _pair(axes, preconditioner="gmg")
+    jac, _ = _pair(axes)
+    for p in (dev, ref, jac):
+        p.setup()
+    kd = kj = 0
+    for s in range(4):
+        T_before = ref.functions_current["T"].copy()
+        for p in (dev, ref, jac):
+            p.solve_timestep()
+        kd += dev.last_krylov_iterations
+        kj += jac.last_krylov_iterations
+        assert relerr(dev.functions_current["T"].x.array, ref.functions_current["T"]) < 1e-10, s
+        assert dev.last_newton_iterations == ref.newton_history[-1][0], s
+    print(f"[gmg] {case}: Krylov iterations over 4 steps: GMG {kd}, Jacobi {kj}")
+    assert kd * 3 <= kj, (kd, kj)
+    mT = np.abs(ref.functions_current["T"] - T_before) > 1e-6
+    check_field(f"sigma[gmg,{case}]", dev.functions_next["sigma"].x.array, ref.functions_next["sigma"], mT, 9,
+                min_frac=0.9)
+    for p in (dev, jac):
+        p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("levels", [1, 2, 3])
+def test_gmg_explicit_levels(levels):
+    """Any depth is a valid preconditioner (1 level = two damped-Jacobi steps)."""
+    _torch()
+    axes = CASES["plate"]
+    dev, ref = _pair(axes, preconditioner="gmg", mg_levels=levels)
+    dev.setup()
+    ref.setup()
+    for s in range(2):
+        dev.solve_timestep()
+        ref.solve_timestep()
+        assert relerr(dev.functions_current["T"].x.array, ref.functions_current["T"]) < 1e-10, (levels, s)
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_gmg_dirichlet_matches_oracle():
+    _torch()
+    axes = [np.linspace(0.0, 2.0, 17), np.linspace(0.0, 2.0, 17), np.linspace(0.0, 1.0, 9)]
+    dev, ref = _pair(axes, mode="paper", preconditioner="gmg")
+    dev.setup(dirichlet_bc=True)
+    ref.setup(dirichlet_bc=True)
+    dofs, g = ref.bc
+    for s in range(3):
+        dev.solve_timestep()
+        ref.solve_timestep()
+        T = dev.functions_current["T"].x.array
+        assert np.all(T[dofs] == g), s
+        assert relerr(T, ref.functions_current["T"]) < 1e-10, s
+        assert dev.last_newton_iterations == ref.newton_history[-1][0]
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_gmg_vcycle_timing_and_bytes():
+    """tv_time_kernel / tv_kernel_bytes id 11 (one V-cycle) run on a live context."""
+    import ctypes as C
+    _torch()
+    dev, _ = _pair(CASES["plate"], preconditioner="gmg")
+    dev.setup()
+    dev.solve_timestep()
+    ms, by = C.c_double(), C.c_double()
+    assert dev._lib.tv_time_kernel(dev._ctx, 11, 3, C.byref(ms)) == 0
+    assert dev._lib.tv_kernel_bytes(dev._ctx, 11, C.byref(by)) == 0
+    assert ms.value > 0.0 and by.value > 0.0
+    T = dev.functions_current["T"].x.array.copy()
+    dev.solve_timestep()  # the timing left the solver state consistent
+    assert np.all(np.isfinite(dev.functions_current["T"].x.array)) and not np.array_equal(T, dev.functions_current["T"].x.array)
+    dev.close()
+
+
+@pytest.mark.gpu
+def test_gmg_rejects_unsupported_meshes():
+    _torch()
+    from tvfem import RectilinearMesh, UnstructuredMesh
+    from tvfem._native import NativeError
+    from tvfem.problem import ThermoViscoProblem
+    cfg = {"T": CG, "sigma": CG}
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    axes2 = [np.linspace(0, 1, 9), np.linspace(0, 1, 9)]
+    with pytest.raises(NativeError):
+        ThermoViscoProblem(RectilinearMesh(axes2), (0, 1), 0.1, cfg, mp, verbose=False, preconditioner="gmg")
+    axes3 = CASES["plate"]
+    with pytest.raises(NativeError):
+        ThermoViscoProblem(RectilinearMesh(axes3), (0, 1), 0.1, cfg, mp, verbose=False, preconditioner="gmg",
+                           n_parts=2, part=0, part_axis=2)
+    with pytest.raises(NativeError):
+        ThermoViscoProblem(UnstructuredMesh.from_rectilinear(RectilinearMesh(axes3)), (0, 1), 0.1, cfg, mp,
+                           verbose=False, preconditioner="gmg")
+    with pytest.raises(NativeError):
+        ThermoViscoProblem(RectilinearMesh(axes3), (0, 1), 0.1, {"T": {"element": "DG", "degree": 1},
+                                                                  "sigma": CG}, mp, verbose=False,
+                           preconditioner="gmg")
+
+
+def test_preconditioner_argument_checked():
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    with pytest.raises(ValueError):
+        ThermoViscoProblem(RectilinearMesh(CASES["plate"]), (0, 1), 0.1, {"T": CG, "sigma": CG},
+                           dict(O.MAIN_MODEL_PARAMS), verbose=False, preconditioner="gamg")
