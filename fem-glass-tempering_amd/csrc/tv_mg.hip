@@ -67,11 +67,25 @@ __global__ __launch_bounds__(kBlock) void k_mg_restrict(MgXfer x, const PcgState
   const int plane = x.cn[0] * x.cn[1];
   const int n = plane * (x.c_ke - x.c_kb);
   const int fpl = x.fn[0] * x.fn[1];
-  for (int t = blockIdx.x * kBlock + threadIdx.x; t < n; t += gridDim.x * kBlock) {
-    const int k = t / plane + x.c_kb;
-    const int rem = t - (k - x.c_kb) * plane;
-    const int j = rem / x.cn[0];
-    const int i = rem - j * x.cn[0];
+  // a contiguous range of output nodes per block, contiguous block ranges per
+  // XCD (xcd_remap): the fine rows a range gathers stay in one L2
+  const int per = (n + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x) * per, t1 = min(n, t0 + per);
+  int k = (t0 + (int)threadIdx.x) / plane, j, i;
+  {
+    const int rem = t0 + (int)threadIdx.x - k * plane;
+    j = rem / x.cn[0];
+    i = rem - j * x.cn[0];
+  }
+  k += x.c_kb;
+  for (int t = t0 + (int)threadIdx.x; t < t1; t += kBlock, i += kBlock) {
+    while (i >= x.cn[0]) {  // advance (i, j, k) by kBlock nodes
+      i -= x.cn[0];
+      if (++j == x.cn[1]) {
+        j = 0;
+        ++k;
+      }
+    }
     int fi[3], fj[3], fk[3];
     rmap(x, 0, i, fi[0], fi[1], fi[2]);
     rmap(x, 1, j, fj[0], fj[1], fj[2]);
@@ -108,7 +122,11 @@ __global__ __launch_bounds__(kBlock) void k_mg_restrict(MgXfer x, const PcgState
   }
 }
 
-// x_f(f) += sum over the 2 x 2 x 2 coarse nodes I of w(f, I) x_c(I)
+// x_f(f) += sum over the 2 x 2 x 2 coarse nodes I of w(f, I) x_c(I).  A block
+// owns kPU x kBlock consecutive fine nodes; a thread decodes its kPU nodes
+// first and issues all their gathers before the first FMA (one node per
+// round left each wave waiting on its load chain: 54 us at 8.2M nodes).
+constexpr int kPU = 2;
 __global__ __launch_bounds__(kBlock) void k_mg_prolong(MgXfer x, const PcgState* __restrict__ st,
                                                        double* __restrict__ xf, const double* __restrict__ xc,
                                                        const double* __restrict__ mask) {
@@ -116,31 +134,57 @@ __global__ __launch_bounds__(kBlock) void k_mg_prolong(MgXfer x, const PcgState*
   const int plane = x.fn[0] * x.fn[1];
   const int n = plane * (x.f_ke - x.f_kb);
   const int cpl = x.cn[0] * x.cn[1];
-  for (int t = blockIdx.x * kBlock + threadIdx.x; t < n; t += gridDim.x * kBlock) {
-    const int f = t + plane * x.f_kb;
-    const int k = f / plane;
-    const int rem = f - k * plane;
-    const int j = rem / x.fn[0];
-    const int i = rem - j * x.fn[0];
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x) * (kPU * kBlock) + (int)threadIdx.x;
+  int k = t0 / plane, j, i;
+  {
+    const int rem = t0 - k * plane;
+    j = rem / x.fn[0];
+    i = rem - j * x.fn[0];
+  }
+  k += x.f_kb;
+  int f[kPU], o[kPU][8];
+  double w[kPU][6];
+#pragma unroll
+  for (int u = 0; u < kPU; ++u) {
+    if (u > 0) {
+      i += kBlock;
+      while (i >= x.fn[0]) {
+        i -= x.fn[0];
+        if (++j == x.fn[1]) {
+          j = 0;
+          ++k;
+        }
+      }
+    }
+    const int t = t0 + u * kBlock;
+    const bool ok = t < n;
+    const int ii = ok ? i : 0, jj = ok ? j : 0, kk = ok ? k : x.f_kb;
+    f[u] = ok ? t + plane * x.f_kb : -1;
     int ci[2], cj[2], ck[2];
-    pmap(x, 0, i, ci[0], ci[1]);
-    pmap(x, 1, j, cj[0], cj[1]);
-    pmap(x, 2, k, ck[0], ck[1]);
-    double v[2][2][2];
+    pmap(x, 0, ii, ci[0], ci[1]);
+    pmap(x, 1, jj, cj[0], cj[1]);
+    pmap(x, 2, kk, ck[0], ck[1]);
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+    for (int q = 0; q < 8; ++q) o[u][q] = ci[q & 1] + x.cn[0] * cj[(q >> 1) & 1] + cpl * ck[q >> 2];
+    w[u][0] = x.pw[0][2 * ii]; w[u][1] = x.pw[0][2 * ii + 1];
+    w[u][2] = x.pw[1][2 * jj]; w[u][3] = x.pw[1][2 * jj + 1];
+    w[u][4] = x.pw[2][2 * kk]; w[u][5] = x.pw[2][2 * kk + 1];
+  }
+  double v[kPU][8], xo[kPU];
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+  for (int u = 0; u < kPU; ++u) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a) v[c][b][a] = xc[ci[a] + x.cn[0] * cj[b] + cpl * ck[c]];
-    const double wi0 = x.pw[0][2 * i], wi1 = x.pw[0][2 * i + 1];
-    const double wj0 = x.pw[1][2 * j], wj1 = x.pw[1][2 * j + 1];
-    const double wk0 = x.pw[2][2 * k], wk1 = x.pw[2][2 * k + 1];
-    const double p0 = wj0 * (wi0 * v[0][0][0] + wi1 * v[0][0][1]) + wj1 * (wi0 * v[0][1][0] + wi1 * v[0][1][1]);
-    const double p1 = wj0 * (wi0 * v[1][0][0] + wi1 * v[1][0][1]) + wj1 * (wi0 * v[1][1][0] + wi1 * v[1][1][1]);
-    const double acc = wk0 * p0 + wk1 * p1;
-    const bool off = mask != nullptr && mask[f] == 0.0;
-    xf[f] = off ? 0.0 : xf[f] + acc;
+    for (int q = 0; q < 8; ++q) v[u][q] = xc[o[u][q]];
+    xo[u] = f[u] >= 0 ? xf[f[u]] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < kPU; ++u) {
+    if (f[u] < 0) continue;
+    const double p0 = w[u][2] * (w[u][0] * v[u][0] + w[u][1] * v[u][1]) + w[u][3] * (w[u][0] * v[u][2] + w[u][1] * v[u][3]);
+    const double p1 = w[u][2] * (w[u][0] * v[u][4] + w[u][1] * v[u][5]) + w[u][3] * (w[u][0] * v[u][6] + w[u][1] * v[u][7]);
+    const double acc = w[u][4] * p0 + w[u][5] * p1;
+    const bool off = mask != nullptr && mask[f[u]] == 0.0;
+    xf[f[u]] = off ? 0.0 : xo[u] + acc;
   }
 }
 
@@ -173,6 +217,8 @@ __global__ __launch_bounds__(kBlock) void k_mg_inject(MgXfer x, const double* __
 }
 
 int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
+// transfers: ~4 x kBlock nodes per block (a contiguous range), at least one node per thread
+int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + 4 * kBlock - 1) / (4 * kBlock)); }
 
 }  // namespace
 
@@ -183,17 +229,17 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
   if (n <= 0) return;
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
   if (f.on)
-    hipLaunchKernelGGL(k_mg_restrict<true>, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, st, bf, wf, f, mask, bc, dinv_c,
+    hipLaunchKernelGGL(k_mg_restrict<true>, dim3(xfer_blocks(n)), dim3(kBlock), 0, s, x, st, bf, wf, f, mask, bc, dinv_c,
                        omega_c, xc);
   else
-    hipLaunchKernelGGL(k_mg_restrict<false>, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, st, bf, wf, f, mask, bc,
+    hipLaunchKernelGGL(k_mg_restrict<false>, dim3(xfer_blocks(n)), dim3(kBlock), 0, s, x, st, bf, wf, f, mask, bc,
                        dinv_c, omega_c, xc);
 }
 
 void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
                        hipStream_t s) {
   const int64_t n = (int64_t)x.fn[0] * x.fn[1] * (x.f_ke - x.f_kb);
-  if (n > 0) hipLaunchKernelGGL(k_mg_prolong, dim3(blocks_for(n)), dim3(kBlock), 0, s, x, st, xf, xc, mask);
+  if (n > 0) hipLaunchKernelGGL(k_mg_prolong, dim3((unsigned)((n + kPU * kBlock - 1) / (kPU * kBlock))), dim3(kBlock), 0, s, x, st, xf, xc, mask);
 }
 
 void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
