@@ -217,8 +217,10 @@ __global__ __launch_bounds__(kBlock) void k_mg_inject(MgXfer x, const double* __
 }
 
 int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
-// transfers: ~4 x kBlock nodes per block (a contiguous range), at least one node per thread
-int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + 4 * kBlock - 1) / (4 * kBlock)); }
+// restriction: one coarse node per thread (27-point gathers: the coarse
+// levels' few hundred blocks must not serialise rounds -- 4 nodes per thread
+// measured 24 us at 143k coarse nodes)
+int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kBlock - 1) / kBlock); }
 
 }  // namespace
 

@@ -139,6 +139,19 @@ def test_partitioned_run_matches_single_partition(world, pcg):
 
 
 @pytest.mark.gpu
+def test_partitioned_host_edit_on_one_rank():
+    """A host-side in-place edit of T made by one rank only (a local hot spot
+    after setup()) must neither hang the other rank nor leave stale ghost
+    planes: tv_set_field is local, and every rank refreshes the T / T_prev
+    ghosts collectively at the start of the step (ThermoViscoProblem.py:351's
+    scatter_forward).  Compared with the same edit on one partition."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _partition_check(2, "host", 29745, ("--edit", "--steps", "3"))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_partitioned_run_matches_single_partition(world):
     """The production transport: one rank per GPU, RCCL grouped send/recv of the

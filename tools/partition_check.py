@@ -30,12 +30,19 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
 
-def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto"):
+def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False):
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
                            verbose=False, pcg_variant=pcg)
     if comm is not None:
         comm(p)
     p.setup()
+    if edit:
+        # a local hot spot written in place on the host by the ranks that own it
+        # (rank 0 only when partitioned): the ghost planes must still follow
+        X = p._dof_coordinates(0)
+        m = (X[:, 0] < 0.6) & (X[:, 1] < 0.6)
+        if m.any():
+            p.functions_current["T"].x.array[m] += 20.0
     its = []
     for _ in range(steps):
         p.solve_timestep()
@@ -51,6 +58,7 @@ def main():
     ap.add_argument("--cells", default="10,30,5")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
+    ap.add_argument("--edit", action="store_true", help="host edit of T on the owning rank only, after setup()")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -63,13 +71,14 @@ def main():
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
-                       pcg=a.pcg)
+                       pcg=a.pcg, edit=a.edit)
     else:
-        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg)
+        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
+                       edit=a.edit)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
-        ref, its_ref = run(mesh, 1, 0, steps)
+        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit)
         res = {"comm": a.comm, "pcg": a.pcg, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             full = np.concatenate([np.asarray(g[k]) for g in gathered])
