@@ -39,9 +39,12 @@ def _pair(axes, mode="reference", **kw):
 CASES = {
     # h = 0.125 as at C4 (dt alpha / h^2 = 6.4): three levels
     "plate": [np.linspace(0.0, 4.0, 33), np.linspace(0.0, 3.0, 25), np.linspace(0.0, 1.0, 9)],
-    # graded axes (non-uniform interpolation weights), one odd axis (not coarsened)
+    # graded axes (non-uniform interpolation weights), an odd cell count along z
     "graded": [np.concatenate([np.linspace(0.0, 0.5, 9), np.linspace(0.5, 2.5, 9)[1:]]),
                np.linspace(0.0, 2.0, 17), np.linspace(0.0, 0.75, 8)],
+    # odd cell counts along x and y (the last fine node kept on every level: odd-tail transfers
+    # of the row-wise prolongation), several 64-node x segments
+    "oddx": [np.linspace(0.0, 16.375, 132), np.linspace(0.0, 1.875, 16), np.linspace(0.0, 0.5, 5)],
 }
 
 
