@@ -102,7 +102,7 @@ def main():
         device = local_rank % max(1, torch.cuda.device_count())
     pc = a.pc
     if pc == "auto":
-        pc = "gmg" if (not um and a.family == "CG" and world == 1 and a.pcg != "single") else "jacobi"
+        pc = "gmg" if (not um and world == 1 and a.pcg != "single") else "jacobi"
     kw = {} if um else {"n_parts": world, "part": rank, "part_axis": 1}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
                               verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,

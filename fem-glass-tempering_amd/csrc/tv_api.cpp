@@ -114,6 +114,7 @@ struct Ctx {
   Output* out = nullptr;  // time-series output (tv_output_*)
   // geometric multigrid (options.preconditioner = TV_PC_GMG): levels 1.. (level 0 = cg)
   bool mg_on = false;
+  bool mg_dg = false;       // DG1 level 0 over the CG1 hierarchy of the same box
   std::vector<MgLevel> mg;
   double mg_omega0 = 0.0;
   double* mgx = nullptr;    // level-0 V-cycle iterate
@@ -890,21 +891,86 @@ static int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out)
 static double mg_omega(double b) { return 2.0 / (1.1 * b); }
 
 // the hierarchy below the fine grid (single partition, 3D CG1 marching path)
+// the CG1 level of the box given by X (single partition), its vectors and weight
+static int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da) {
+  c->mg.emplace_back();
+  MgLevel& L = c->mg.back();
+  for (int s = 0; s < 3; ++s) L.X[s] = X[s];
+  if (int e = build_cg_grid(c, 3, L.X, 0, (int)L.X[2].size(), 0, 0, true, true, L.g, L.coef, &L.bnodes, L.ffbuf))
+    return e;
+  const CgGrid& f = c->cg;  // thermal constants (set by setup_fields for both families)
+  L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
+  L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
+  L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+  for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
+    void* p = nullptr;
+    HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
+    HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)L.n, c->stream));
+    L.bufs.push_back(p);
+    *q = static_cast<double*>(p);
+  }
+  L.omega = mg_omega(mg_gershgorin(L.X, da));
+  return TV_OK;
+}
+
+// lambda_max(D^-1 J) of the DG1 operator by power iteration (SIPG rows have no
+// closed-form Gershgorin bound here); the smoother takes it with a 10 % margin
+static int mg_dg_lambda(Ctx* c, double* lam) {
+  const int64_t n = c->nT;
+  const double* T = c->f[TV_F_T].ptr;
+  std::vector<double> h((size_t)n);
+  uint64_t st = 0x9E3779B97F4A7C15ull;
+  double nrm = 0.0;
+  for (int64_t t = 0; t < n; ++t) {  // fixed-seed xorshift start vector in (0.5, 1.5)
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    h[(size_t)t] = 0.5 + (double)(st >> 11) * (1.0 / 9007199254740992.0);
+    nrm += h[(size_t)t] * h[(size_t)t];
+  }
+  for (double& v : h) v /= std::sqrt(nrm);
+  HIPC(hipMemcpyAsync(c->mgx, h.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
+  std::vector<double> part(1024);
+  double l = 0.0;
+  for (int it = 0; it < 30; ++it) {
+    op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
+    const int nb = launch_mg_pow(n, c->dinv, c->w, c->partials, c->stream);
+    HIPC(hipMemcpyAsync(part.data(), c->partials, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    double s2 = 0.0;
+    for (int b = 0; b < nb; ++b) s2 += part[(size_t)b];
+    l = std::sqrt(s2);  // ||D^-1 J x|| with ||x|| = 1
+    if (!(l > 0.0) || !std::isfinite(l)) return c->fail(TV_ERR_HIP, "GMG: DG eigenvalue estimate failed");
+    launch_mg_scale(n, c->w, 1.0 / l, c->mgx, c->stream);
+  }
+  *lam = l;
+  return TV_OK;
+}
+
 static int mg_setup(Ctx* c) {
-  if (c->fam_T != TV_CG || c->dim != 3 || c->um || !cg_cgs_supported(c->cg))
-    return c->fail(TV_ERR_ARG, "preconditioner GMG: 3D CG1 temperature space on a rectilinear mesh only");
+  const bool dg = c->fam_T == TV_DG;
+  if (c->dim != 3 || c->um || (!dg && !cg_cgs_supported(c->cg)) || (dg && (c->dg.deg1 || c->dg.deg2)))
+    return c->fail(TV_ERR_ARG, "preconditioner GMG: 3D CG1 or DG1 temperature space on a rectilinear mesh only");
   if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "preconditioner GMG: one partition (use TV_PC_JACOBI when partitioned)");
   if (c->cgs) return c->fail(TV_ERR_ARG, "preconditioner GMG runs in the KSPCG form (pcg_variant KSPCG or AUTO)");
   std::vector<double> tmp, Xf[3];
   for (int s = 0; s < 3; ++s) Xf[s] = storage_coords(c, s, tmp);
   const double da = c->P.dt * c->P.alpha;
-  c->mg_omega0 = mg_omega(mg_gershgorin(Xf, da));
   HIPC(hipMalloc(&c->mgx, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
   HIPC(hipMemsetAsync(c->mgx, 0, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT), c->stream));
+  if (dg) {
+    // level 1: the CG1 space of the same box (two-level DG -> CG, then the CG hierarchy)
+    c->mg_dg = true;
+    double lam = 0.0;
+    if (int e = mg_dg_lambda(c, &lam)) return e;
+    c->mg_omega0 = 2.0 / (1.1 * 1.1 * lam);
+    if (int e = mg_add_cg_level(c, Xf, da)) return e;
+  } else {
+    c->mg_omega0 = mg_omega(mg_gershgorin(Xf, da));
+  }
   const int max_levels = c->O.mg_levels > 0 ? c->O.mg_levels : 8;
   const bool automatic = c->O.mg_levels <= 0;
   std::vector<double> Xp[3] = {Xf[0], Xf[1], Xf[2]};
-  for (int lev = 1; lev < max_levels; ++lev) {
+  for (int lev = 1 + (dg ? 1 : 0); lev < max_levels; ++lev) {
     double h = 1e300;  // smallest mean cell length over the axes
     bool coarsen[3], any = false;
     for (int s = 0; s < 3; ++s) {
@@ -998,11 +1064,14 @@ static int mg_setup(Ctx* c) {
   return TV_OK;
 }
 
-// per Newton iteration: T injected down the hierarchy, coarse Jacobi diagonals
+// per Newton iteration: T injected down the hierarchy (DG: the vertex mean of
+// the cell-local values onto the CG level), coarse Jacobi diagonals
 static void mg_prepare(Ctx* c, const double* T) {
   const double* Tf = T;
-  for (MgLevel& L : c->mg) {
-    launch_mg_inject(L.xf, Tf, L.T, c->stream);
+  for (size_t l = 0; l < c->mg.size(); ++l) {
+    MgLevel& L = c->mg[l];
+    if (l == 0 && c->mg_dg) launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+    else launch_mg_inject(L.xf, Tf, L.T, c->stream);
     launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream);
     Tf = L.T;
   }
@@ -1035,6 +1104,16 @@ static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
   const int64_t n = c->nT;
   hipStream_t s = c->stream;
   const double* mask = c->dir_on ? c->dinv : nullptr;  // Dirichlet: the free subspace
+  if (c->mg_dg) {  // DG1 level 0: complete DG J x (Robin facets inline), vertex sums / injection to CG1
+    const DgGrid& d = c->dg;
+    MgLevel& C = c->mg[0];
+    op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
+    launch_mg_dg_restrict(d.c0, d.c1, d.c2, c->st, c->r, c->w, mask, C.b, C.dinv, C.omega, C.x, s);
+    mg_level(c, 1);
+    launch_mg_dg_prolong(d.c0, d.c1, d.c2, c->st, c->mgx, C.x, mask, s);
+    op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
+    return launch_mg_post(n, c->st, c->mgx, c->r, c->w, nullptr, c->dinv, c->mg_omega0, c->z, c->partials, tail, s);
+  }
   const FaceAdd fa = cg_face_add(c->cg, 0);
   if (!c->mg.empty()) {
     MgLevel& C = c->mg[0];
@@ -1055,7 +1134,7 @@ static int mg_iteration(Ctx* c, const double* T, int it) {
   int np = 0;
   if (!op_japply_fused(c, T, &np, &t1, it))  // p <- z + b p ; w <- J p ; p.w ; alpha
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;
-  const FaceAdd fa = cg_face_add(c->cg, 0);
+  const FaceAdd fa = c->mg_dg ? FaceAdd{} : cg_face_add(c->cg, 0);  // DG: w is complete
   launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
                    c->stream);
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 3, nullptr};

@@ -601,6 +601,236 @@ __global__ __launch_bounds__(kBlock) void k_dg_diag(DgGrid g, const double* __re
   }
 }
 
+// ---- cell-block Jacobi (the multigrid smoother of DG1 level 0) ----------------------
+// B_c = the 8 x 8 diagonal block of J(T) for cell c (its own dofs): the cell
+// term, the SIPG self-couplings of its interior facets and its Robin facets --
+// the rows of k_dg_cells restricted to the cell's columns.  Stored inverted,
+// packed symmetric (36 entries, component-major [e][cell]).
+constexpr int kBP = 36;
+__device__ __forceinline__ int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+__global__ __launch_bounds__(kBlock) void k_dg_block(DgGrid g, const double* __restrict__ T,
+                                                     double* __restrict__ binv) {
+  using A = Ax<3>;
+  constexpr int NL = 8;
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int64_t cid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (cid >= ncell) return;
+  const int ci[3] = {(int)(cid % g.c0), (int)((cid / g.c0) % g.c1), (int)(cid / ((int64_t)g.c0 * g.c1))};
+  const int cn[3] = {g.c0, g.c1, g.c2};
+  double h[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) h[k] = g.h[k][ci[k]];
+  const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
+  double Tl[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) Tl[l] = T[(int64_t)l * ncell + cid];
+  double a[kBP];
+#pragma unroll
+  for (int l = 0; l < NL; ++l)
+#pragma unroll
+    for (int q = 0; q <= l; ++q) {
+      double mm = 1.0, kk = 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int al = (l >> k) & 1, bq = (q >> k) & 1;
+        double prod = kloc(h[k], al, bq);
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if (e != k) prod *= mloc(h[e], (l >> e) & 1, (q >> e) & 1);
+        kk += prod;
+        mm *= mloc(h[k], al, bq);
+      }
+      double v = mm + g.dt_alpha * kk;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          const int nbi = ci[k] + (side ? 1 : -1);
+          double mt = 1.0;
+#pragma unroll
+          for (int e = 0; e < 3; ++e)
+            if (e != k) mt *= mloc(h[e], (l >> e) & 1, (q >> e) & 1);
+          if (nbi >= 0 && nbi < cn[k]) {
+            const double hL = side ? h[k] : g.h[k][nbi];
+            const double hR = side ? g.h[k][nbi] : h[k];
+            const double pen = g.penalty / sqrt(hd2 - h[k] * h[k] + hL * hL);
+            const double Jv[4] = {0.0, 1.0, -1.0, 0.0};
+            const double Gv[4] = {-0.5 / hL, 0.5 / hL, -0.5 / hR, 0.5 / hR};
+            const int row = side ? ((l >> k) & 1) : 2 + ((l >> k) & 1);
+            const int col = side ? ((q >> k) & 1) : 2 + ((q >> k) & 1);
+            v += g.dt_alpha * mt * (pen * Jv[row] * Jv[col] - Gv[row] * Jv[col] - Jv[row] * Gv[col]);
+          } else if (g.bnd[k][side] && ((l >> k) & 1) == side && ((q >> k) & 1) == side) {
+            double acc = 0.0;
+#pragma unroll 1
+            for (int qq = 0; qq < 9; ++qq) {
+              double w = 1.0, xi_t[3] = {0.0, 0.0, 0.0};
+              int t = 0;
+#pragma unroll
+              for (int e = 0; e < 3; ++e) {
+                if (e == k) continue;
+                const int qi = (t == 0) ? (qq % 3) : (qq / 3);
+                xi_t[e] = kGX[qi];
+                w *= kGW[qi] * h[e];
+                ++t;
+              }
+              double Th = 0.0, pl = 0.0, pq = 0.0;
+#pragma unroll
+              for (int m = 0; m < NL; ++m) {
+                double f = (((m >> k) & 1) == side) ? 1.0 : 0.0;
+#pragma unroll
+                for (int e = 0; e < 3; ++e)
+                  if (e != k) f *= ((m >> e) & 1) ? xi_t[e] : 1.0 - xi_t[e];
+                Th += f * Tl[m];
+                if (m == l) pl = f;
+                if (m == q) pq = f;
+              }
+              acc += w * dgfun(g, Th) * pl * pq;
+            }
+            v += g.dt * acc;
+          }
+        }
+      }
+      a[pk(l, q)] = v;
+    }
+  // Cholesky B = L L^T (packed lower, in place), L^-1, then B^-1 = L^-T L^-1
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      double sum = a[pk(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) sum -= a[pk(i, k)] * a[pk(j, k)];
+      a[pk(i, j)] = (i == j) ? sqrt(sum) : sum / a[pk(j, j)];
+    }
+  double li[kBP];  // L^-1, packed lower
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    li[pk(i, i)] = 1.0 / a[pk(i, i)];
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = j; k < i; ++k) sum += a[pk(i, k)] * li[pk(k, j)];
+      li[pk(i, j)] = -sum * li[pk(i, i)];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = i; k < NL; ++k) sum += li[pk(k, i)] * li[pk(k, j)];
+      binv[(int64_t)pk(i, j) * ncell + cid] = sum;
+    }
+}
+
+// y = B_c^-1 v for one cell (packed symmetric inverse, component-major)
+__device__ __forceinline__ void bmul(const double* __restrict__ binv, int64_t ncell, int64_t cid, const double (&v)[8],
+                                     double (&y)[8]) {
+  double b[kBP];
+#pragma unroll
+  for (int e = 0; e < kBP; ++e) b[e] = __builtin_nontemporal_load(&binv[(int64_t)e * ncell + cid]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sum += b[pk(i, j)] * v[j];
+    y[i] = sum;
+  }
+}
+
+// level >= 1 style smoothing step on DG: MODE 0 x = omega B^-1 b ; MODE 1 x += omega B^-1 (b - w)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_dg_bsmooth(int64_t ncell, const PcgState* __restrict__ st,
+                                                       const double* __restrict__ b, const double* __restrict__ w,
+                                                       const double* __restrict__ binv, double omega,
+                                                       double* __restrict__ x) {
+  if (st != nullptr && st->done) return;
+  for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
+    double v[8], y[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) v[l] = MODE ? b[l * ncell + c] - w[l * ncell + c] : b[l * ncell + c];
+    bmul(binv, ncell, c, v, y);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) x[l * ncell + c] = MODE ? x[l * ncell + c] + omega * y[l] : omega * y[l];
+  }
+}
+
+// KSPCG update with the explicit residual for the DG multigrid: r <- r - a w,
+// dx <- dx + a p, x0 <- omega B^-1 r (INIT: dx <- 0, x0 <- omega B^-1 r)
+template <bool INIT>
+__global__ __launch_bounds__(kBlock) void k_dg_bupdate(int64_t ncell, const PcgState* __restrict__ st,
+                                                       const double* __restrict__ pA, const double* __restrict__ pB,
+                                                       const double* __restrict__ w, const double* __restrict__ binv,
+                                                       double omega, double* __restrict__ r, double* __restrict__ dx,
+                                                       double* __restrict__ x0, int it_host) {
+  if (st->done) return;
+  const double a = INIT ? 0.0 : st->a;
+  const double* __restrict__ p = (it_host & 1) ? pB : pA;
+  for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
+    double v[8], y[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int64_t o = l * ncell + c;
+      double rr = r[o];
+      if (INIT) {
+        dx[o] = 0.0;
+      } else {
+        rr -= a * __builtin_nontemporal_load(&w[o]);
+        r[o] = rr;
+        __builtin_nontemporal_store(__builtin_nontemporal_load(&dx[o]) + a * __builtin_nontemporal_load(&p[o]), &dx[o]);
+      }
+      v[l] = rr;
+    }
+    bmul(binv, ncell, c, v, y);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) x0[l * ncell + c] = omega * y[l];
+  }
+}
+
+// post-smoothing of DG level 0: z <- x0 + omega B^-1 (r - w); (z.z, z.r)
+// records and the KSPCG logic in the reduction tail
+__global__ __launch_bounds__(kBlock) void k_dg_bpost(int64_t ncell, const PcgState* __restrict__ st,
+                                                     const double* __restrict__ x0, const double* __restrict__ r,
+                                                     const double* __restrict__ w, const double* __restrict__ binv,
+                                                     double omega, double* __restrict__ z,
+                                                     double* __restrict__ partials, RedTail rt) {
+  __shared__ double red[2][kBlock / kWave];
+  if (st->done) return;
+  double acc[2] = {0.0, 0.0};
+  for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
+    double v[8], y[8], rr[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      rr[l] = r[l * ncell + c];
+      v[l] = rr[l] - w[l * ncell + c];
+    }
+    bmul(binv, ncell, c, v, y);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const double zz = x0[l * ncell + c] + omega * y[l];
+      z[l * ncell + c] = zz;
+      acc[0] += zz * zz;
+      acc[1] += zz * rr[l];
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const double sw = wave_sum64(acc[q]);
+    if (lane == 0) red[q][wave] = sw;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2)
+    store_partial(&partials[(int64_t)blockIdx.x * 2 + threadIdx.x],
+                  (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]));
+  fused_reduce_tail<2>(rt, gridDim.x);
+}
+
+int dg_vblocks(int64_t ncell) { return (int)std::max<int64_t>(1, std::min<int64_t>((ncell + kBlock - 1) / kBlock, 1024)); }
+
 int dg_dim(const DgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 
 template <int MODE, bool FUSEP>
@@ -679,6 +909,39 @@ void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, 
     case 2: hipLaunchKernelGGL(k_dg_diag<2>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
     default: hipLaunchKernelGGL(k_dg_diag<3>, dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
   }
+}
+
+void launch_dg_block(const DgGrid& g, const double* T, double* binv, hipStream_t s) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  hipLaunchKernelGGL(k_dg_block, dim3((unsigned)((ncell + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, g, T, binv);
+}
+
+void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* binv,
+                       double omega, double* x, int mode, hipStream_t s) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  if (mode == 0) hipLaunchKernelGGL(k_dg_bsmooth<0>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, b, w, binv, omega, x);
+  else hipLaunchKernelGGL(k_dg_bsmooth<1>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, b, w, binv, omega, x);
+}
+
+void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, const double* pB, const double* w,
+                       const double* binv, double omega, double* r, double* dx, double* x0, int it_host, int init,
+                       hipStream_t s) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  if (init)
+    hipLaunchKernelGGL(k_dg_bupdate<true>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, pA, pB, w, binv,
+                       omega, r, dx, x0, it_host);
+  else
+    hipLaunchKernelGGL(k_dg_bupdate<false>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, pA, pB, w, binv,
+                       omega, r, dx, x0, it_host);
+}
+
+int launch_dg_bpost(const DgGrid& g, const PcgState* st, const double* x0, const double* r, const double* w,
+                    const double* binv, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const RedTail rt = tail ? *tail : RedTail{};
+  const int nb = dg_vblocks(ncell);
+  hipLaunchKernelGGL(k_dg_bpost, dim3(nb), dim3(kBlock), 0, s, ncell, st, x0, r, w, binv, omega, z, partials, rt);
+  return nb;
 }
 
 }  // namespace tv

@@ -238,6 +238,19 @@ bool launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, d
                             hipStream_t s, const RedTail* tail = nullptr);
 void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
 int dg_num_blocks(const DgGrid& g);  // partial records of the largest DG launch
+// cell-block Jacobi of 3D DG1 (the multigrid smoother): inverted 8 x 8 diagonal
+// blocks of J(T), packed symmetric, 36 x ncell doubles [e][cell]
+void launch_dg_block(const DgGrid& g, const double* T, double* binv, hipStream_t s);
+// mode 0: x <- omega B^-1 b ; mode 1: x <- x + omega B^-1 (b - w)
+void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* binv,
+                       double omega, double* x, int mode, hipStream_t s);
+// r <- r - a w, dx <- dx + a p, x0 <- omega B^-1 r (init: dx <- 0, x0 <- omega B^-1 r)
+void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, const double* pB, const double* w,
+                       const double* binv, double omega, double* r, double* dx, double* x0, int it_host, int init,
+                       hipStream_t s);
+// z <- x0 + omega B^-1 (r - w), (z.z, z.r) records + reduction tail; returns the record count
+int launch_dg_bpost(const DgGrid& g, const PcgState* st, const double* x0, const double* r, const double* w,
+                    const double* binv, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s);
 
 void launch_visco(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
 void launch_visco_Tpass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
@@ -295,6 +308,19 @@ void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const do
 void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
                       const double* dinv, double omega, double* x, int mode, hipStream_t s);
 void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t s);  // coarse T <- fine T
+// DG1 level 0 -> CG1 level 1 of the same box (3D; cells c0 x c1 x c2, DG dof
+// (l, cell) at l * ncell + cell, l = a + 2b + 4c over the storage axes):
+// restriction = sum of the cell-local copies at each vertex (P = injection of
+// the vertex value into every copy), with the CG level's pre-smoothing fused
+void launch_mg_dg_restrict(int c0, int c1, int c2, const PcgState* st, const double* bf, const double* wf,
+                           const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
+                           hipStream_t s);
+void launch_mg_dg_prolong(int c0, int c1, int c2, const PcgState* st, double* xf, const double* xc, const double* mask,
+                          hipStream_t s);
+void launch_mg_dg_T(int c0, int c1, int c2, const double* Tdg, double* Tcg, hipStream_t s);  // vertex mean
+// power-iteration step for lambda_max(D^-1 J): y <- dinv .* y, per-block sums of y^2 (returns the count)
+int launch_mg_pow(int64_t n, const double* dinv, double* y, double* partials, hipStream_t s);
+void launch_mg_scale(int64_t n, const double* y, double a, double* x, hipStream_t s);  // x <- a y
 // J x without the facet terms of the faces along the march (the FaceAdd the
 // consumer adds, cg_face_add); the whole J x where the row kernel runs
 void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,

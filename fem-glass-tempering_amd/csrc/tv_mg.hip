@@ -328,6 +328,91 @@ __global__ __launch_bounds__(kBlock) void k_mg_inject(MgXfer x, const double* __
   Tc[(int64_t)i + (int64_t)x.cn[0] * (j + (int64_t)x.cn[1] * k)] = Tf[f];
 }
 
+// ---- DG1 level 0 <-> CG1 level 1 ------------------------------------------------------
+// vertex (i, j, k) of the box: the cell-local copies (a, b, c) of the cells
+// (i - a, j - b, k - c) that exist
+__global__ __launch_bounds__(kBlock) void k_mg_dg_restrict(int c0, int c1, int c2, const PcgState* __restrict__ st,
+                                                           const double* __restrict__ bf,
+                                                           const double* __restrict__ wf,
+                                                           const double* __restrict__ mask, double* __restrict__ bc,
+                                                           const double* __restrict__ dinv_c, double omega_c,
+                                                           double* __restrict__ xc) {
+  if (st != nullptr && st->done) return;
+  const int n0 = c0 + 1, n1 = c1 + 1, n2 = c2 + 1;
+  const int64_t nv = (int64_t)n0 * n1 * n2, ncell = (int64_t)c0 * c1 * c2;
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
+    const int i = (int)(v % n0), j = (int)((v / n0) % n1), k = (int)(v / ((int64_t)n0 * n1));
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = k - (l >> 2);
+      if (ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < 0 || ck >= c2) continue;
+      const int64_t f = (int64_t)l * ncell + ci + (int64_t)c0 * (cj + (int64_t)c1 * ck);
+      if (mask != nullptr && mask[f] == 0.0) continue;
+      acc += bf[f] - wf[f];
+    }
+    bc[v] = acc;
+    if (xc != nullptr) xc[v] = omega_c * dinv_c[v] * acc;
+  }
+}
+
+// every cell-local copy takes its vertex value: x_dg(l, cell) += x_cg(vertex)
+__global__ __launch_bounds__(kBlock) void k_mg_dg_prolong(int c0, int c1, int c2, const PcgState* __restrict__ st,
+                                                          double* __restrict__ xf, const double* __restrict__ xc,
+                                                          const double* __restrict__ mask) {
+  if (st != nullptr && st->done) return;
+  const int n0 = c0 + 1, n1 = c1 + 1;
+  const int64_t ncell = (int64_t)c0 * c1 * c2;
+  for (int64_t cell = blockIdx.x * (int64_t)kBlock + threadIdx.x; cell < ncell; cell += (int64_t)gridDim.x * kBlock) {
+    const int i = (int)(cell % c0), j = (int)((cell / c0) % c1), k = (int)(cell / ((int64_t)c0 * c1));
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int64_t v = (i + (l & 1)) + (int64_t)n0 * ((j + ((l >> 1) & 1)) + (int64_t)n1 * (k + (l >> 2)));
+      const int64_t f = (int64_t)l * ncell + cell;
+      xf[f] = (mask != nullptr && mask[f] == 0.0) ? 0.0 : xf[f] + xc[v];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_mg_dg_T(int c0, int c1, int c2, const double* __restrict__ Tdg,
+                                                    double* __restrict__ Tcg) {
+  const int n0 = c0 + 1, n1 = c1 + 1, n2 = c2 + 1;
+  const int64_t nv = (int64_t)n0 * n1 * n2, ncell = (int64_t)c0 * c1 * c2;
+  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
+    const int i = (int)(v % n0), j = (int)((v / n0) % n1), k = (int)(v / ((int64_t)n0 * n1));
+    double s = 0.0;
+    int cnt = 0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = k - (l >> 2);
+      if (ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < 0 || ck >= c2) continue;
+      s += Tdg[(int64_t)l * ncell + ci + (int64_t)c0 * (cj + (int64_t)c1 * ck)];
+      ++cnt;
+    }
+    Tcg[v] = s / cnt;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_mg_pow(int64_t n, const double* __restrict__ dinv, double* __restrict__ y,
+                                                   double* __restrict__ partials) {
+  __shared__ double red[kBlock / kWave];
+  double acc = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    const double v = dinv[t] * y[t];
+    y[t] = v;
+    acc += v * v;
+  }
+  acc = wave_sum64(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_mg_scale(int64_t n, const double* __restrict__ y, double a,
+                                                     double* __restrict__ x) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = a * y[t];
+}
+
 int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
 // restriction: one coarse node per thread (27-point gathers: the coarse
 // levels' few hundred blocks must not serialise rounds -- 4 nodes per thread
@@ -388,6 +473,35 @@ void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t
   const int nxb = (x.cn[0] + kBlock - 1) / kBlock;
   const int64_t rows = (int64_t)x.cn[1] * x.cn[2];
   if (rows > 0) hipLaunchKernelGGL(k_mg_inject, dim3((unsigned)(rows * nxb)), dim3(kBlock), 0, s, x, Tf, Tc, nxb);
+}
+
+void launch_mg_dg_restrict(int c0, int c1, int c2, const PcgState* st, const double* bf, const double* wf,
+                           const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
+                           hipStream_t s) {
+  const int64_t nv = (int64_t)(c0 + 1) * (c1 + 1) * (c2 + 1);
+  hipLaunchKernelGGL(k_mg_dg_restrict, dim3(blocks_for(nv)), dim3(kBlock), 0, s, c0, c1, c2, st, bf, wf, mask, bc,
+                     dinv_c, omega_c, xc);
+}
+
+void launch_mg_dg_prolong(int c0, int c1, int c2, const PcgState* st, double* xf, const double* xc, const double* mask,
+                          hipStream_t s) {
+  const int64_t nc = (int64_t)c0 * c1 * c2;
+  hipLaunchKernelGGL(k_mg_dg_prolong, dim3(blocks_for(nc)), dim3(kBlock), 0, s, c0, c1, c2, st, xf, xc, mask);
+}
+
+void launch_mg_dg_T(int c0, int c1, int c2, const double* Tdg, double* Tcg, hipStream_t s) {
+  const int64_t nv = (int64_t)(c0 + 1) * (c1 + 1) * (c2 + 1);
+  hipLaunchKernelGGL(k_mg_dg_T, dim3(blocks_for(nv)), dim3(kBlock), 0, s, c0, c1, c2, Tdg, Tcg);
+}
+
+int launch_mg_pow(int64_t n, const double* dinv, double* y, double* partials, hipStream_t s) {
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 1024));
+  hipLaunchKernelGGL(k_mg_pow, dim3(nb), dim3(kBlock), 0, s, n, dinv, y, partials);
+  return nb;
+}
+
+void launch_mg_scale(int64_t n, const double* y, double a, double* x, hipStream_t s) {
+  hipLaunchKernelGGL(k_mg_scale, dim3(blocks_for(n)), dim3(kBlock), 0, s, n, y, a, x);
 }
 
 }  // namespace tv

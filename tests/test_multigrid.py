@@ -75,6 +75,41 @@ def test_gmg_steps_match_oracle(case):
         p.close()
 
 
+DG = {"element": "DG", "degree": 1}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sig", ["DG", "CG"])
+def test_gmg_dg_steps_match_oracle(sig):
+    """DG1 temperature (C5's family): damped-Jacobi smoothing of the SIPG
+    operator (weight from a power-iteration estimate of lambda_max(D^-1 J)),
+    coarse correction on the CG1 space of the same box (vertex sums / injection)
+    and the CG hierarchy below it."""
+    _torch()
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    axes = [np.linspace(0.0, 3.0, 13), np.linspace(0.0, 2.5, 11), np.linspace(0.0, 1.0, 6)]
+    cfg = {"T": DG, "sigma": DG if sig == "DG" else CG}
+    mk = lambda pc: ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),  # noqa: E731
+                                       verbose=False, part_axis=2, preconditioner=pc)
+    dev, jac = mk("gmg"), mk("jacobi")
+    ref = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), linear="pcg")
+    for p in (dev, jac, ref):
+        p.setup()
+    kd = kj = 0
+    for s in range(3):
+        for p in (dev, jac, ref):
+            p.solve_timestep()
+        kd += dev.last_krylov_iterations
+        kj += jac.last_krylov_iterations
+        assert relerr(dev.functions_current["T"].x.array, ref.functions_current["T"]) < 1e-10, s
+        assert dev.last_newton_iterations == ref.newton_history[-1][0], s
+    print(f"[gmg] DG/{sig}: Krylov iterations over 3 steps: GMG {kd}, Jacobi {kj}")
+    assert kd * 3 <= kj, (kd, kj)
+    for p in (dev, jac):
+        p.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("levels", [1, 2, 3])
 def test_gmg_explicit_levels(levels):
@@ -145,9 +180,8 @@ def test_gmg_rejects_unsupported_meshes():
     with pytest.raises(NativeError):
         ThermoViscoProblem(UnstructuredMesh.from_rectilinear(RectilinearMesh(axes3)), (0, 1), 0.1, cfg, mp,
                            verbose=False, preconditioner="gmg")
-    with pytest.raises(NativeError):
-        ThermoViscoProblem(RectilinearMesh(axes3), (0, 1), 0.1, {"T": {"element": "DG", "degree": 1},
-                                                                  "sigma": CG}, mp, verbose=False,
+    with pytest.raises(NativeError):  # DG1 in 2D
+        ThermoViscoProblem(RectilinearMesh(axes2), (0, 1), 0.1, {"T": DG, "sigma": CG}, mp, verbose=False,
                            preconditioner="gmg")
 
 
