@@ -118,6 +118,7 @@ struct Ctx {
   std::vector<MgLevel> mg;
   double mg_omega0 = 0.0;
   double* mgx = nullptr;    // level-0 V-cycle iterate
+  double* dggface = nullptr; // DG level 0: facet means of dg(T) for the cell-block Jacobi smoother
   // unstructured mesh (tv_create_unstructured, tv_um.hip)
   bool um = false;
   UmGrid umg{};
@@ -913,8 +914,9 @@ static int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da)
   return TV_OK;
 }
 
-// lambda_max(D^-1 J) of the DG1 operator by power iteration (SIPG rows have no
-// closed-form Gershgorin bound here); the smoother takes it with a 10 % margin
+// lambda_max(B^-1 J) of the DG1 operator by power iteration, B the cell blocks
+// (point Jacobi D under the experiment switch); SIPG rows have no closed-form
+// Gershgorin bound here.  The smoother takes it with a 21 % margin
 static int mg_dg_lambda(Ctx* c, double* lam) {
   const int64_t n = c->nT;
   const double* T = c->f[TV_F_T].ptr;
@@ -928,12 +930,14 @@ static int mg_dg_lambda(Ctx* c, double* lam) {
   }
   for (double& v : h) v /= std::sqrt(nrm);
   HIPC(hipMemcpyAsync(c->mgx, h.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
-  launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
+  if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
+  else launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
   std::vector<double> part(1024);
   double l = 0.0;
   for (int it = 0; it < 30; ++it) {
     op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
-    const int nb = launch_mg_pow(n, c->dinv, c->w, c->partials, c->stream);
+    if (c->dggface) launch_dg_bsmooth(c->dg, nullptr, c->w, nullptr, c->dggface, 1.0, c->w, 0, c->stream);  // in place, per cell
+    const int nb = launch_mg_pow(n, c->dggface ? nullptr : c->dinv, c->w, c->partials, c->stream);
     HIPC(hipMemcpyAsync(part.data(), c->partials, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     double s2 = 0.0;
@@ -960,6 +964,9 @@ static int mg_setup(Ctx* c) {
   if (dg) {
     // level 1: the CG1 space of the same box (two-level DG -> CG, then the CG hierarchy)
     c->mg_dg = true;
+    if (!experiment_env("TVFEM_MG_DG_POINT")) {
+      HIPC(hipMalloc(&c->dggface, sizeof(double) * (size_t)dg_gface_size(c->dg)));
+    }
     double lam = 0.0;
     if (int e = mg_dg_lambda(c, &lam)) return e;
     c->mg_omega0 = 2.0 / (1.1 * 1.1 * lam);
@@ -1070,7 +1077,10 @@ static void mg_prepare(Ctx* c, const double* T) {
   const double* Tf = T;
   for (size_t l = 0; l < c->mg.size(); ++l) {
     MgLevel& L = c->mg[l];
-    if (l == 0 && c->mg_dg) launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+    if (l == 0 && c->mg_dg) {
+      launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+      if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
+    }
     else launch_mg_inject(L.xf, Tf, L.T, c->stream);
     launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream);
     Tf = L.T;
@@ -1107,11 +1117,13 @@ static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
   if (c->mg_dg) {  // DG1 level 0: complete DG J x (Robin facets inline), vertex sums / injection to CG1
     const DgGrid& d = c->dg;
     MgLevel& C = c->mg[0];
-    op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
+    launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
     launch_mg_dg_restrict(d.c0, d.c1, d.c2, c->st, c->r, c->w, mask, C.b, C.dinv, C.omega, C.x, s);
     mg_level(c, 1);
     launch_mg_dg_prolong(d.c0, d.c1, d.c2, c->st, c->mgx, C.x, mask, s);
-    op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
+    launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+    if (c->dggface)
+      return launch_dg_bpost(d, c->st, c->mgx, c->r, c->w, c->dggface, c->mg_omega0, c->z, c->partials, tail, s);
     return launch_mg_post(n, c->st, c->mgx, c->r, c->w, nullptr, c->dinv, c->mg_omega0, c->z, c->partials, tail, s);
   }
   const FaceAdd fa = cg_face_add(c->cg, 0);
@@ -1135,8 +1147,12 @@ static int mg_iteration(Ctx* c, const double* T, int it) {
   if (!op_japply_fused(c, T, &np, &t1, it))  // p <- z + b p ; w <- J p ; p.w ; alpha
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;
   const FaceAdd fa = c->mg_dg ? FaceAdd{} : cg_face_add(c->cg, 0);  // DG: w is complete
-  launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
-                   c->stream);
+  if (c->dggface)
+    launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
+                      c->stream);
+  else
+    launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
+                     c->stream);
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 3, nullptr};
   mg_apply0(c, T, &t2);  // z <- V(r); z.z, z.r; beta, convergence
   return TV_OK;
@@ -1151,8 +1167,12 @@ static int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   h.max_it = c->O.ksp_max_it;
   HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
   mg_prepare(c, T);
-  launch_mg_update(n, c->st, c->pA, c->pB, c->w, nullptr, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
-                   c->stream);  // dx <- 0, x0 <- omega dinv r
+  if (c->dggface)
+    launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
+                      c->stream);  // dx <- 0, x0 <- omega B^-1 r
+  else
+    launch_mg_update(n, c->st, c->pA, c->pB, c->w, nullptr, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
+                     c->stream);  // dx <- 0, x0 <- omega dinv r
   RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 1, nullptr};
   mg_apply0(c, T, &t0);  // z <- V(r); dp, beta (KSPCG init)
   if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
@@ -1409,7 +1429,7 @@ static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
   double r0 = 0.0, rn = 0.0;
   op_residual(c, T, Tp, c->r);  // F(u)
   while (!conv && its < c->O.newton_max_it) {
-    op_diag(c, T, c->dinv, 1);  // J(u) (matrix-free) + Jacobi PC setup
+    if (!c->dggface) op_diag(c, T, c->dinv, 1);  // J(u) (matrix-free) + Jacobi PC setup (DG GMG: cell blocks)
     const bool dir = c->dir_on && c->fam_T == TV_CG;
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;
@@ -1774,6 +1794,7 @@ int tv_destroy(void* ctx) {
       if (L.ffbuf[q]) hipFree(L.ffbuf[q]);
   }
   if (c->mgx) hipFree(c->mgx);
+  if (c->dggface) hipFree(c->dggface);
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
     if (p) hipFree(p);
   for (int s = 0; s < 3; ++s) {

@@ -230,6 +230,143 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
 }
 
 
+// ---- cell-block Jacobi (the multigrid smoother of DG1 level 0) ----------------------
+// B_c = the 8 x 8 diagonal block of J(T) for cell c (its own dofs): the cell
+// term, the SIPG self-couplings of its interior facets and its Robin facets.
+// On a box cell every term is a Kronecker product of 1D 2 x 2 matrices,
+//   B_c = Mx (x) My (x) Mz + dt alpha (Ax (x) My (x) Mz + Mx (x) Ay (x) Mz + Mx (x) My (x) Az),
+// A_k = the 1D stiffness + the SIPG self terms of the two facets along k (+ the
+// Robin term on a boundary facet), so B_c^-1 is applied by fast diagonalisation:
+// A_k V_k = M_k V_k L_k per axis (2 x 2, closed form), B_c^-1 =
+// (Vx (x) Vy (x) Vz) (I + dt alpha (Lx + Ly + Lz))^-1 (Vx (x) Vy (x) Vz)^T -- no
+// per-cell storage.  The one approximation: the Robin facet weight dg(T) is
+// taken constant over a facet (the mean of its 4 nodal values, gface below; the
+// 3 x 3 Gauss sum of the operator varies it), which keeps the block separable.
+// The smoother only has to be symmetric positive definite and close to B_c.
+
+// per boundary facet: mean of dg(T) over its 4 nodes; layout per axis k (the two
+// other axes a < b): [side][i_a][i_b], axes concatenated (gface_offsets)
+__device__ __forceinline__ void gface_offsets(const DgGrid& g, int64_t (&off)[4]) {
+  off[0] = 0;
+  off[1] = off[0] + 2 * (int64_t)g.c1 * g.c2;
+  off[2] = off[1] + 2 * (int64_t)g.c0 * g.c2;
+  off[3] = off[2] + 2 * (int64_t)g.c0 * g.c1;
+}
+
+__global__ __launch_bounds__(kBlock) void k_dg_gface(DgGrid g, const double* __restrict__ T,
+                                                     double* __restrict__ gface) {
+  int64_t off[4];
+  gface_offsets(g, off);
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= off[3]) return;
+  const int k = t < off[1] ? 0 : (t < off[2] ? 1 : 2);
+  const int cn[3] = {g.c0, g.c1, g.c2};
+  const int ea = k == 0 ? 1 : 0, eb = k == 2 ? 1 : 2;
+  const int64_t r = t - off[k];
+  const int ib = (int)(r % cn[eb]), ia = (int)((r / cn[eb]) % cn[ea]), side = (int)(r / ((int64_t)cn[ea] * cn[eb]));
+  int ci[3];
+  ci[k] = side ? cn[k] - 1 : 0;
+  ci[ea] = ia;
+  ci[eb] = ib;
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int64_t cid = ci[0] + (int64_t)g.c0 * (ci[1] + (int64_t)g.c1 * ci[2]);
+  double acc = 0.0;
+#pragma unroll
+  for (int l = 0; l < 8; ++l)
+    if (((l >> k) & 1) == side) acc += dgfun(g, T[(int64_t)l * ncell + cid]);
+  gface[t] = 0.25 * acc;
+}
+
+// A v = lambda M v for M = h/6 [[2, 1], [1, 2]] and symmetric A: with S = M^-1/2
+// = [[p, q], [q, p]], one Jacobi rotation diagonalises C = S A S; V = S J
+__device__ __forceinline__ void fdm2(double h, double a00, double a01, double a11, double (&V)[4], double (&lam)[2]) {
+  const double s0 = sqrt(2.0 / h), s1 = sqrt(6.0 / h);
+  const double p = 0.5 * (s0 + s1), q = 0.5 * (s0 - s1);
+  const double b00 = a00 * p + a01 * q, b01 = a00 * q + a01 * p;
+  const double b10 = a01 * p + a11 * q, b11 = a01 * q + a11 * p;
+  const double c00 = p * b00 + q * b10, c01 = p * b01 + q * b11, c11 = q * b01 + p * b11;
+  double t = 0.0, cs = 1.0, sn = 0.0;
+  if (c01 != 0.0) {
+    const double tau = (c11 - c00) / (2.0 * c01);
+    t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+    cs = 1.0 / sqrt(1.0 + t * t);
+    sn = t * cs;
+  }
+  lam[0] = c00 - t * c01;
+  lam[1] = c11 + t * c01;
+  // V = S [[cs, sn], [-sn, cs]], row-major V[row * 2 + col]
+  V[0] = p * cs - q * sn;
+  V[1] = p * sn + q * cs;
+  V[2] = q * cs - p * sn;
+  V[3] = q * sn + p * cs;
+}
+
+// y = B_c^-1 v for cell cid (fast diagonalisation, see above)
+__device__ __forceinline__ void fdm_mul(const DgGrid& g, const double* __restrict__ gface, int64_t cid,
+                                        const double (&v)[8], double (&y)[8]) {
+  const int cn[3] = {g.c0, g.c1, g.c2};
+  const int ci[3] = {(int)(cid % g.c0), (int)((cid / g.c0) % g.c1), (int)(cid / ((int64_t)g.c0 * g.c1))};
+  double h[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) h[k] = g.h[k][ci[k]];
+  const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
+  int64_t off[4];
+  gface_offsets(g, off);
+  double V[3][4], lam[3][2];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double hk = h[k], ih = 1.0 / hk;
+    double a00 = ih, a01 = -ih, a11 = ih;  // 1D stiffness
+    const int ea = k == 0 ? 1 : 0, eb = k == 2 ? 1 : 2;
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int nbi = ci[k] + (side ? 1 : -1);
+      if (nbi >= 0 && nbi < cn[k]) {  // SIPG self terms of the facet (rows of k_dg_diag)
+        const double hn = g.h[k][nbi];
+        const double pen = g.penalty / sqrt(side ? hd2 : hd2 - hk * hk + hn * hn);
+        a01 += 0.5 * ih;
+        if (side) a11 += pen - ih;
+        else a00 += pen - ih;
+      } else if (g.bnd[k][side]) {  // Robin: dt dg e e^T (x) M (x) M = dt alpha (dg / alpha) ...
+        const double gw = gface[off[k] + ((int64_t)side * cn[ea] + ci[ea]) * cn[eb] + ci[eb]];
+        const double r = g.dt / g.dt_alpha * gw;
+        if (side) a11 += r;
+        else a00 += r;
+      }
+    }
+    fdm2(hk, a00, a01, a11, V[k], lam[k]);
+  }
+  double u[8];
+#pragma unroll
+  for (int l = 0; l < 8; ++l) u[l] = v[l];
+  // u <- (Vx (x) Vy (x) Vz)^T u
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int l = 0; l < 8; ++l)
+      if (!((l >> k) & 1)) {
+        const int m = l | (1 << k);
+        const double u0 = u[l], u1 = u[m];
+        u[l] = V[k][0] * u0 + V[k][2] * u1;
+        u[m] = V[k][1] * u0 + V[k][3] * u1;
+      }
+#pragma unroll
+  for (int l = 0; l < 8; ++l)
+    u[l] /= 1.0 + g.dt_alpha * (lam[0][l & 1] + lam[1][(l >> 1) & 1] + lam[2][(l >> 2) & 1]);
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int l = 0; l < 8; ++l)
+      if (!((l >> k) & 1)) {
+        const int m = l | (1 << k);
+        const double u0 = u[l], u1 = u[m];
+        u[l] = V[k][0] * u0 + V[k][1] * u1;
+        u[m] = V[k][2] * u0 + V[k][3] * u1;
+      }
+#pragma unroll
+  for (int l = 0; l < 8; ++l) y[l] = u[l];
+}
+
 // ---------------------------------------------------------------------------
 // 3D Jacobian apply on an (x-segment x rows) tile of cells marching through a
 // chunk of planes: the SIPG J x of k_dg_cells<3, MODE_JAC>, restructured for
@@ -246,6 +383,10 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
 //     matrix, then the two tangential 2x2 masses (~0.5 kflop per cell, not ~3).
 // FUSEP: x = p = z + beta/betaold p_old formed on the fly and stored (as
 // k_dg_cells); out = w on owned cells; one p.w partial per workgroup.
+// (Fusing the DG multigrid post-smoothing -- prolongation, J x, cell-block
+// solve and the (z.z, z.r) records -- into this kernel measured slower than the
+// three separate kernels at C5: 195 us vs 187 us; the epilogue runs at 2 waves
+// per SIMD with 254 VGPRs.)
 // ---------------------------------------------------------------------------
 constexpr int kDgRows = 6;  // + 2 halo waves: 512 threads, up to 256 VGPRs (no spills)
 
@@ -282,7 +423,7 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
   constexpr int R = kDgRows;
   __shared__ double sX[2][R + 2][8][kWave];  // double-buffered plane slab: one barrier per plane
   __shared__ double red[R + 2];
-  if (FUSEP && st->done) return;  // uniform over the grid
+  if (st != nullptr && st->done) return;  // uniform over the grid
   const int pa = 3 - ra;
   const int cn[3] = {g.c0, g.c1, g.c2};
   const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
@@ -601,158 +742,19 @@ __global__ __launch_bounds__(kBlock) void k_dg_diag(DgGrid g, const double* __re
   }
 }
 
-// ---- cell-block Jacobi (the multigrid smoother of DG1 level 0) ----------------------
-// B_c = the 8 x 8 diagonal block of J(T) for cell c (its own dofs): the cell
-// term, the SIPG self-couplings of its interior facets and its Robin facets --
-// the rows of k_dg_cells restricted to the cell's columns.  Stored inverted,
-// packed symmetric (36 entries, component-major [e][cell]).
-constexpr int kBP = 36;
-__device__ __forceinline__ int pk(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
-
-__global__ __launch_bounds__(kBlock) void k_dg_block(DgGrid g, const double* __restrict__ T,
-                                                     double* __restrict__ binv) {
-  using A = Ax<3>;
-  constexpr int NL = 8;
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
-  const int64_t cid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (cid >= ncell) return;
-  const int ci[3] = {(int)(cid % g.c0), (int)((cid / g.c0) % g.c1), (int)(cid / ((int64_t)g.c0 * g.c1))};
-  const int cn[3] = {g.c0, g.c1, g.c2};
-  double h[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) h[k] = g.h[k][ci[k]];
-  const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
-  double Tl[NL];
-#pragma unroll
-  for (int l = 0; l < NL; ++l) Tl[l] = T[(int64_t)l * ncell + cid];
-  double a[kBP];
-#pragma unroll
-  for (int l = 0; l < NL; ++l)
-#pragma unroll
-    for (int q = 0; q <= l; ++q) {
-      double mm = 1.0, kk = 0.0;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int al = (l >> k) & 1, bq = (q >> k) & 1;
-        double prod = kloc(h[k], al, bq);
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if (e != k) prod *= mloc(h[e], (l >> e) & 1, (q >> e) & 1);
-        kk += prod;
-        mm *= mloc(h[k], al, bq);
-      }
-      double v = mm + g.dt_alpha * kk;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-#pragma unroll
-        for (int side = 0; side < 2; ++side) {
-          const int nbi = ci[k] + (side ? 1 : -1);
-          double mt = 1.0;
-#pragma unroll
-          for (int e = 0; e < 3; ++e)
-            if (e != k) mt *= mloc(h[e], (l >> e) & 1, (q >> e) & 1);
-          if (nbi >= 0 && nbi < cn[k]) {
-            const double hL = side ? h[k] : g.h[k][nbi];
-            const double hR = side ? g.h[k][nbi] : h[k];
-            const double pen = g.penalty / sqrt(hd2 - h[k] * h[k] + hL * hL);
-            const double Jv[4] = {0.0, 1.0, -1.0, 0.0};
-            const double Gv[4] = {-0.5 / hL, 0.5 / hL, -0.5 / hR, 0.5 / hR};
-            const int row = side ? ((l >> k) & 1) : 2 + ((l >> k) & 1);
-            const int col = side ? ((q >> k) & 1) : 2 + ((q >> k) & 1);
-            v += g.dt_alpha * mt * (pen * Jv[row] * Jv[col] - Gv[row] * Jv[col] - Jv[row] * Gv[col]);
-          } else if (g.bnd[k][side] && ((l >> k) & 1) == side && ((q >> k) & 1) == side) {
-            double acc = 0.0;
-#pragma unroll 1
-            for (int qq = 0; qq < 9; ++qq) {
-              double w = 1.0, xi_t[3] = {0.0, 0.0, 0.0};
-              int t = 0;
-#pragma unroll
-              for (int e = 0; e < 3; ++e) {
-                if (e == k) continue;
-                const int qi = (t == 0) ? (qq % 3) : (qq / 3);
-                xi_t[e] = kGX[qi];
-                w *= kGW[qi] * h[e];
-                ++t;
-              }
-              double Th = 0.0, pl = 0.0, pq = 0.0;
-#pragma unroll
-              for (int m = 0; m < NL; ++m) {
-                double f = (((m >> k) & 1) == side) ? 1.0 : 0.0;
-#pragma unroll
-                for (int e = 0; e < 3; ++e)
-                  if (e != k) f *= ((m >> e) & 1) ? xi_t[e] : 1.0 - xi_t[e];
-                Th += f * Tl[m];
-                if (m == l) pl = f;
-                if (m == q) pq = f;
-              }
-              acc += w * dgfun(g, Th) * pl * pq;
-            }
-            v += g.dt * acc;
-          }
-        }
-      }
-      a[pk(l, q)] = v;
-    }
-  // Cholesky B = L L^T (packed lower, in place), L^-1, then B^-1 = L^-T L^-1
-#pragma unroll
-  for (int i = 0; i < NL; ++i)
-#pragma unroll
-    for (int j = 0; j <= i; ++j) {
-      double sum = a[pk(i, j)];
-#pragma unroll
-      for (int k = 0; k < j; ++k) sum -= a[pk(i, k)] * a[pk(j, k)];
-      a[pk(i, j)] = (i == j) ? sqrt(sum) : sum / a[pk(j, j)];
-    }
-  double li[kBP];  // L^-1, packed lower
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    li[pk(i, i)] = 1.0 / a[pk(i, i)];
-#pragma unroll
-    for (int j = 0; j < i; ++j) {
-      double sum = 0.0;
-#pragma unroll
-      for (int k = j; k < i; ++k) sum += a[pk(i, k)] * li[pk(k, j)];
-      li[pk(i, j)] = -sum * li[pk(i, i)];
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < NL; ++i)
-#pragma unroll
-    for (int j = 0; j <= i; ++j) {
-      double sum = 0.0;
-#pragma unroll
-      for (int k = i; k < NL; ++k) sum += li[pk(k, i)] * li[pk(k, j)];
-      binv[(int64_t)pk(i, j) * ncell + cid] = sum;
-    }
-}
-
-// y = B_c^-1 v for one cell (packed symmetric inverse, component-major)
-__device__ __forceinline__ void bmul(const double* __restrict__ binv, int64_t ncell, int64_t cid, const double (&v)[8],
-                                     double (&y)[8]) {
-  double b[kBP];
-#pragma unroll
-  for (int e = 0; e < kBP; ++e) b[e] = __builtin_nontemporal_load(&binv[(int64_t)e * ncell + cid]);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sum += b[pk(i, j)] * v[j];
-    y[i] = sum;
-  }
-}
-
 // level >= 1 style smoothing step on DG: MODE 0 x = omega B^-1 b ; MODE 1 x += omega B^-1 (b - w)
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_dg_bsmooth(int64_t ncell, const PcgState* __restrict__ st,
+__global__ __launch_bounds__(kBlock) void k_dg_bsmooth(DgGrid g, const PcgState* __restrict__ st,
                                                        const double* __restrict__ b, const double* __restrict__ w,
-                                                       const double* __restrict__ binv, double omega,
+                                                       const double* __restrict__ gface, double omega,
                                                        double* __restrict__ x) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
   if (st != nullptr && st->done) return;
   for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
     double v[8], y[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) v[l] = MODE ? b[l * ncell + c] - w[l * ncell + c] : b[l * ncell + c];
-    bmul(binv, ncell, c, v, y);
+    fdm_mul(g, gface, c, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) x[l * ncell + c] = MODE ? x[l * ncell + c] + omega * y[l] : omega * y[l];
   }
@@ -761,11 +763,12 @@ __global__ __launch_bounds__(kBlock) void k_dg_bsmooth(int64_t ncell, const PcgS
 // KSPCG update with the explicit residual for the DG multigrid: r <- r - a w,
 // dx <- dx + a p, x0 <- omega B^-1 r (INIT: dx <- 0, x0 <- omega B^-1 r)
 template <bool INIT>
-__global__ __launch_bounds__(kBlock) void k_dg_bupdate(int64_t ncell, const PcgState* __restrict__ st,
+__global__ __launch_bounds__(kBlock) void k_dg_bupdate(DgGrid g, const PcgState* __restrict__ st,
                                                        const double* __restrict__ pA, const double* __restrict__ pB,
-                                                       const double* __restrict__ w, const double* __restrict__ binv,
+                                                       const double* __restrict__ w, const double* __restrict__ gface,
                                                        double omega, double* __restrict__ r, double* __restrict__ dx,
                                                        double* __restrict__ x0, int it_host) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
   if (st->done) return;
   const double a = INIT ? 0.0 : st->a;
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
@@ -784,7 +787,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_bupdate(int64_t ncell, const PcgS
       }
       v[l] = rr;
     }
-    bmul(binv, ncell, c, v, y);
+    fdm_mul(g, gface, c, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) x0[l * ncell + c] = omega * y[l];
   }
@@ -792,11 +795,12 @@ __global__ __launch_bounds__(kBlock) void k_dg_bupdate(int64_t ncell, const PcgS
 
 // post-smoothing of DG level 0: z <- x0 + omega B^-1 (r - w); (z.z, z.r)
 // records and the KSPCG logic in the reduction tail
-__global__ __launch_bounds__(kBlock) void k_dg_bpost(int64_t ncell, const PcgState* __restrict__ st,
+__global__ __launch_bounds__(kBlock) void k_dg_bpost(DgGrid g, const PcgState* __restrict__ st,
                                                      const double* __restrict__ x0, const double* __restrict__ r,
-                                                     const double* __restrict__ w, const double* __restrict__ binv,
+                                                     const double* __restrict__ w, const double* __restrict__ gface,
                                                      double omega, double* __restrict__ z,
                                                      double* __restrict__ partials, RedTail rt) {
+  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
   __shared__ double red[2][kBlock / kWave];
   if (st->done) return;
   double acc[2] = {0.0, 0.0};
@@ -807,7 +811,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_bpost(int64_t ncell, const PcgSta
       rr[l] = r[l * ncell + c];
       v[l] = rr[l] - w[l * ncell + c];
     }
-    bmul(binv, ncell, c, v, y);
+    fdm_mul(g, gface, c, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       const double zz = x0[l * ncell + c] + omega * y[l];
@@ -884,9 +888,9 @@ int dg_num_blocks(const DgGrid& g) {
 }
 
 void launch_dg_japply(const DgGrid& g, const double* T, const double* x, double* y, double* partials,
-                      int* n_partials, hipStream_t s) {
+                      int* n_partials, hipStream_t s, const PcgState* st) {
   if (dg_tiled(g)) {
-    launch_tile<false>(g, T, x, nullptr, y, nullptr, nullptr, partials, n_partials, s);
+    launch_tile<false>(g, T, x, nullptr, y, nullptr, st, partials, n_partials, s);
     return;
   }
   launch_cells<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, nullptr, partials, s, n_partials);
@@ -911,36 +915,39 @@ void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, 
   }
 }
 
-void launch_dg_block(const DgGrid& g, const double* T, double* binv, hipStream_t s) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
-  hipLaunchKernelGGL(k_dg_block, dim3((unsigned)((ncell + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, g, T, binv);
+int64_t dg_gface_size(const DgGrid& g) {
+  return 2 * ((int64_t)g.c1 * g.c2 + (int64_t)g.c0 * g.c2 + (int64_t)g.c0 * g.c1);
 }
 
-void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* binv,
+void launch_dg_gface(const DgGrid& g, const double* T, double* gface, hipStream_t s) {
+  const int64_t n = dg_gface_size(g);
+  hipLaunchKernelGGL(k_dg_gface, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, g, T, gface);
+}
+
+void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* gface,
                        double omega, double* x, int mode, hipStream_t s) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
-  if (mode == 0) hipLaunchKernelGGL(k_dg_bsmooth<0>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, b, w, binv, omega, x);
-  else hipLaunchKernelGGL(k_dg_bsmooth<1>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, b, w, binv, omega, x);
+  const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
+  if (mode == 0) hipLaunchKernelGGL(k_dg_bsmooth<0>, dim3(nb), dim3(kBlock), 0, s, g, st, b, w, gface, omega, x);
+  else hipLaunchKernelGGL(k_dg_bsmooth<1>, dim3(nb), dim3(kBlock), 0, s, g, st, b, w, gface, omega, x);
 }
 
 void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, const double* pB, const double* w,
-                       const double* binv, double omega, double* r, double* dx, double* x0, int it_host, int init,
+                       const double* gface, double omega, double* r, double* dx, double* x0, int it_host, int init,
                        hipStream_t s) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
   if (init)
-    hipLaunchKernelGGL(k_dg_bupdate<true>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, pA, pB, w, binv,
-                       omega, r, dx, x0, it_host);
+    hipLaunchKernelGGL(k_dg_bupdate<true>, dim3(nb), dim3(kBlock), 0, s, g, st, pA, pB, w, gface, omega, r, dx, x0,
+                       it_host);
   else
-    hipLaunchKernelGGL(k_dg_bupdate<false>, dim3(dg_vblocks(ncell)), dim3(kBlock), 0, s, ncell, st, pA, pB, w, binv,
-                       omega, r, dx, x0, it_host);
+    hipLaunchKernelGGL(k_dg_bupdate<false>, dim3(nb), dim3(kBlock), 0, s, g, st, pA, pB, w, gface, omega, r, dx, x0,
+                       it_host);
 }
 
 int launch_dg_bpost(const DgGrid& g, const PcgState* st, const double* x0, const double* r, const double* w,
-                    const double* binv, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+                    const double* gface, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s) {
   const RedTail rt = tail ? *tail : RedTail{};
-  const int nb = dg_vblocks(ncell);
-  hipLaunchKernelGGL(k_dg_bpost, dim3(nb), dim3(kBlock), 0, s, ncell, st, x0, r, w, binv, omega, z, partials, rt);
+  const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
+  hipLaunchKernelGGL(k_dg_bpost, dim3(nb), dim3(kBlock), 0, s, g, st, x0, r, w, gface, omega, z, partials, rt);
   return nb;
 }
 

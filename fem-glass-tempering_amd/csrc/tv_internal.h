@@ -230,27 +230,30 @@ void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, 
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 
 void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
+// st: queued multigrid work exits once the solve has converged (3D tiles)
 void launch_dg_japply(const DgGrid& g, const double* T, const double* x, double* y, double* partials,
-                      int* n_partials, hipStream_t s);
+                      int* n_partials, hipStream_t s, const PcgState* st = nullptr);
 // 3D: k_dg_tile, with the reduction tail when `tail` is given (returns true)
 bool launch_dg_japply_fused(const DgGrid& g, const double* T, const double* z, double* pA, double* pB,
                             double* w, const PcgState* st, double* partials, int* n_partials,
                             hipStream_t s, const RedTail* tail = nullptr);
 void launch_dg_diag(const DgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
 int dg_num_blocks(const DgGrid& g);  // partial records of the largest DG launch
-// cell-block Jacobi of 3D DG1 (the multigrid smoother): inverted 8 x 8 diagonal
-// blocks of J(T), packed symmetric, 36 x ncell doubles [e][cell]
-void launch_dg_block(const DgGrid& g, const double* T, double* binv, hipStream_t s);
+// cell-block Jacobi of 3D DG1 (the multigrid smoother), applied by fast
+// diagonalisation of the 8 x 8 cell blocks of J(T); gface = per boundary facet
+// mean of dg(T) (dg_gface_size doubles, refreshed per Newton iteration)
+int64_t dg_gface_size(const DgGrid& g);
+void launch_dg_gface(const DgGrid& g, const double* T, double* gface, hipStream_t s);
 // mode 0: x <- omega B^-1 b ; mode 1: x <- x + omega B^-1 (b - w)
-void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* binv,
+void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* gface,
                        double omega, double* x, int mode, hipStream_t s);
 // r <- r - a w, dx <- dx + a p, x0 <- omega B^-1 r (init: dx <- 0, x0 <- omega B^-1 r)
 void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, const double* pB, const double* w,
-                       const double* binv, double omega, double* r, double* dx, double* x0, int it_host, int init,
+                       const double* gface, double omega, double* r, double* dx, double* x0, int it_host, int init,
                        hipStream_t s);
 // z <- x0 + omega B^-1 (r - w), (z.z, z.r) records + reduction tail; returns the record count
 int launch_dg_bpost(const DgGrid& g, const PcgState* st, const double* x0, const double* r, const double* w,
-                    const double* binv, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s);
+                    const double* gface, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s);
 
 void launch_visco(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);
 void launch_visco_Tpass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s);

@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_pow(int64_t n, const double* __re
   __shared__ double red[kBlock / kWave];
   double acc = 0.0;
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
-    const double v = dinv[t] * y[t];
+    const double v = dinv ? dinv[t] * y[t] : y[t];  // null: the norm only
     y[t] = v;
     acc += v * v;
   }
