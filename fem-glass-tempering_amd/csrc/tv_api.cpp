@@ -404,9 +404,12 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
       std::vector<double> h;
       if (X.size() == 1) h.assign(1, 1.0);
       else for (size_t i = 0; i + 1 < X.size(); ++i) h.push_back(X[i + 1] - X[i]);
+      const size_t nh = h.size();
+      for (size_t q = 0; q < nh; ++q) h.push_back(1.0 / h[q]);  // [h..., 1/h...]
       HIPC(hipMalloc(&c->dgh[s], h.size() * sizeof(double)));
       HIPC(hipMemcpy(c->dgh[s], h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
       g.h[s] = c->dgh[s];
+      g.ih[s] = c->dgh[s] + nh;
     }
     const int nl = 1 << d;
     c->nT = (int64_t)g.c0 * g.c1 * g.c2 * nl;

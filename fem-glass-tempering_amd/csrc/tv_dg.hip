@@ -44,6 +44,15 @@ __device__ __forceinline__ double dgfun(const DgGrid& g, double T) { return g.a_
 
 __device__ __forceinline__ double mloc(double h, int a, int b) { return h * (a == b ? (1.0 / 3.0) : (1.0 / 6.0)); }
 __device__ __forceinline__ double kloc(double h, int a, int b) { return (a == b ? 1.0 : -1.0) / h; }
+// SIPG penalty / sqrt(q) without the FP64 sqrt + divide sequences (~25
+// instructions each, a third of the tile kernels' per-cell VALU count): v_rsq_f64
+// refined by two Newton steps (relative error ~1e-16, not bitwise the IEEE quotient)
+__device__ __forceinline__ double pen_rsq(double penalty, double q) {
+  double r = __builtin_amdgcn_rsq(q);
+  r = r * (1.5 - (0.5 * q) * (r * r));
+  r = r * (1.5 - (0.5 * q) * (r * r));
+  return penalty * r;
+}
 
 template <int DIM, int MODE, bool FUSEP>
 __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __restrict__ T,
@@ -502,8 +511,8 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
 #pragma unroll
       for (int e = 0; e < 3; ++e) h[e] = g.h[e][ci[e]];
       const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
-      const double ih[3] = {1.0 / h[0], 1.0 / h[1], 1.0 / h[2]};
-      const double pen_up = g.penalty / sqrt(hd2);  // upper facets: this cell is '+'
+      const double ih[3] = {g.ih[0][ci[0]], g.ih[1][ci[1]], g.ih[2][ci[2]]};
+      const double pen_up = pen_rsq(g.penalty, hd2);  // upper facets: this cell is '+'
       double y[8];
       // ---- cell term: Mz(My Mx x + da (My Kx x + Ky Mx x)) + da Kz (My Mx x) ----
       {
@@ -528,6 +537,7 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const int e1 = (k == 0) ? 1 : 0, e2 = (k == 2) ? 1 : 2;  // tangential axes
+        double Us[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // both facets along k: one pair of tangential masses
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
           const int nbi = ci[k] + (side ? 1 : -1);
@@ -550,7 +560,7 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
             // jump j = x_L1 - x_R0 and the normal differences d = x_1 - x_0 of
             // both cells; then the tangential masses (they commute)
             const double hn = g.h[k][nbi];
-            const double gO = 0.5 * ih[k], gN = 0.5 / hn;
+            const double gO = 0.5 * ih[k], gN = 0.5 * g.ih[k][nbi];
             double U[8];
             if (side) {  // upper facet: this cell is L, the neighbour R
               const double pen = pen_up;
@@ -562,7 +572,7 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
                 U[l1] = (pen - gO) * j - gO * dO - gN * dN;
               }
             } else {  // lower facet: this cell is R, the neighbour L ('+', its lengths set the penalty)
-              const double pen = g.penalty / sqrt(hd2 - h[k] * h[k] + hn * hn);
+              const double pen = pen_rsq(g.penalty, hd2 - h[k] * h[k] + hn * hn);
 #pragma unroll
               for (int tt = 0; tt < 4; ++tt) {
                 const int l0 = ((tt & 1) << e1) | ((tt >> 1) << e2), l1 = l0 | (1 << k);
@@ -571,10 +581,8 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
                 U[l0] = (gO - pen) * j + gO * dO + gN * dN;
               }
             }
-            mass_axis(U, e1, h[e1]);
-            mass_axis(U, e2, h[e2]);
 #pragma unroll
-            for (int l = 0; l < 8; ++l) y[l] += g.dt_alpha * U[l];
+            for (int l = 0; l < 8; ++l) Us[l] += U[l];
           } else if (valid && g.bnd[k][side]) {
             // Robin facet Jacobian on the physical boundary (3x3 Gauss, as
             // k_dg_cells): only the 4 dofs on the facet (bit k == side) are nonzero there
@@ -605,6 +613,10 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
             for (int f = 0; f < 4; ++f) y[(side << k) | ((f & 1) << e1) | ((f >> 1) << e2)] += g.dt * acc[f];
           }
         }
+        mass_axis(Us, e1, h[e1]);
+        mass_axis(Us, e2, h[e2]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) y[l] += g.dt_alpha * Us[l];
       }
       if (writer && ci[2] >= g.k_begin && ci[2] < g.k_end) {
 #pragma unroll

@@ -65,6 +65,7 @@ struct DgGrid {
   int deg1, deg2;
   int bnd[3][2];
   const double* h[3];         // device: cell length per local cell per axis
+  const double* ih[3];        // device: 1 / h (the tile kernels: no FP64 divisions per cell)
   double hdiam_inv;           // unused for rectilinear non-uniform (per-cell below)
   double dt, dt_alpha, dt_f;
   double a_rad, a_conv;
