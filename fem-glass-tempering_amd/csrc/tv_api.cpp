@@ -1395,6 +1395,14 @@ __global__ __launch_bounds__(kBlock) void k_bc_dvec(BndTest b, const double* __r
 // F -= J dB (lifting; the constrained rows are never read: diag^-1 = 0 there)
 // and diag^-1 = 0 on constrained nodes, so z = B r and every Krylov vector
 // stay in the free subspace: PCG on P J P with the Jacobi preconditioner P B P
+// read-only sweep (cache state for the flushed timing of tv_time_kernel id 10):
+// one sum per workgroup into out[block] so the loads are not dead
+__global__ __launch_bounds__(kBlock) void k_read_sweep(const double* __restrict__ a, int64_t n, double* out) {
+  double acc = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) acc += a[t];
+  if (acc == 12345.678) out[blockIdx.x] = acc;  // practically never: keeps the loads
+}
+
 __global__ __launch_bounds__(kBlock) void k_bc_lift(BndTest b, double* __restrict__ F, const double* __restrict__ JdB,
                                                     double* __restrict__ dinv, int64_t n) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
@@ -2319,8 +2327,10 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
   }
   if (kernel == 10) {
     // J x with the Infinity Cache flushed before every launch: a 512 MiB write
-    // (2x the 256 MiB L3) between launches, HIP events around each launch
-    // alone (the HBM figure, not the cache-assisted one)
+    // (2x the 256 MiB L3) then a read sweep of the same buffer, so the cache
+    // holds clean lines (no write-backs of the flush competing with the timed
+    // launch), HIP events around each launch alone (SURVEY.md section 8(d) H7:
+    // the HBM figure, not the cache-assisted one)
     const size_t fl = (size_t)512 << 20;
     void* flush = nullptr;
     HIPC(hipMalloc(&flush, fl));
@@ -2329,6 +2339,8 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr);  // warm-up
     for (int i = 0; i < reps; ++i) {
       HIPC(hipMemsetAsync(flush, i & 0xff, fl, c->stream));
+      hipLaunchKernelGGL(k_read_sweep, dim3(1024), dim3(kBlock), 0, c->stream, static_cast<const double*>(flush),
+                         (int64_t)(fl / sizeof(double)), c->partials);
       HIPC(hipEventRecord(ev[2 * i], c->stream));
       op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr);
       HIPC(hipEventRecord(ev[2 * i + 1], c->stream));
