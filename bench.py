@@ -230,11 +230,8 @@ def main():
         if um:
             cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
                    "sample": "no unstructured path in oracle/tv_cpu.c (the numpy oracle covers its parity only)"}
-        elif a.family == "CG":
-            cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only)
         else:
-            cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
-                   "sample": "no DG1 path in oracle/tv_cpu.c (the numpy oracle covers DG1 parity only)"}
+            cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only, a.family)
 
     prob.close()
     if rank == 0:
@@ -275,7 +272,7 @@ def main():
         print(json.dumps(out))
 
 
-def cpu_baseline(nc, L, mp, seconds, thermal_only):
+def cpu_baseline(nc, L, mp, seconds, thermal_only, family="CG"):
     """Time the oracle's C/OpenMP restatement (oracle/tv_cpu.c, a port of the same
     algorithm) on a bounded sample of the same workload: the same mesh and
     physics, as many full time steps as fit ~`seconds` (at least one)."""
@@ -283,7 +280,7 @@ def cpu_baseline(nc, L, mp, seconds, thermal_only):
         from oracle import tv_cpu
     except Exception as e:  # the baseline is reported, never required
         return {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
-    return tv_cpu.time_baseline(nc, L, mp, seconds, thermal_only)
+    return tv_cpu.time_baseline(nc, L, mp, seconds, thermal_only, family)
 
 
 if __name__ == "__main__":

@@ -13,6 +13,10 @@
  *   PETSc KSPCG (:343) with a Jacobi preconditioner in place of GAMG (:344),
  *   the viscoelastic expressions ViscoelasticModel.py:100-228 in the call order
  *   of ThermoViscoProblem.py:393-595 (state fields only).
+ * DG1 (tvcpu_create_dg): the SIPG residual / Jacobian of
+ * ThermoViscoProblem.py:308-325 on the same rectilinear plates (cell-local
+ * dofs, '+' = the lower cell, h = the '+' cell's diameter, penalty 5), the
+ * same Newton / Jacobi-PCG / visco code on the 8 dofs of every cell.
  * Parity: unpinned against dolfinx (see oracle/tv_oracle.py); checked against
  * the numpy oracle in tests/test_cpu_port.py.
  */
@@ -38,6 +42,10 @@ typedef struct {
   /* work */
   double *r, *z, *p, *w, *dx, *dinv;
   int last_newton, last_krylov;
+  /* DG1: cell counts, cell lengths per axis; dof (l, cell) at l * ncell + cell */
+  int dg, nc[3];
+  long long ncell;
+  double* hc[3];
 } tvcpu;
 
 static const double GX[3] = {0.11270166537925831148, 0.5, 0.88729833462074168852};
@@ -193,6 +201,130 @@ static void diag_inv(tvcpu* h) {
       }
 }
 
+/* ---------------- DG1 (SIPG) ---------------- */
+static double mloc(double hh, int a, int b) { return hh * (a == b ? (1.0 / 3.0) : (1.0 / 6.0)); }
+static double kloc(double hh, int a, int b) { return (a == b ? 1.0 : -1.0) / hh; }
+
+/* mode 0: y = F(T; Tp) ; 1: y = J(T) x ; 2: y = diag J(T) */
+static void dg_apply(tvcpu* h, int mode, const double* x, double* y) {
+  const int c0 = h->nc[0], c1 = h->nc[1], c2 = h->nc[2];
+  const long long nce = h->ncell;
+  const double* T = h->T;
+  const long long cst[3] = {1, c0, (long long)c0 * c1};
+  const int cn[3] = {c0, c1, c2};
+  const double pen0 = 5.0;
+#pragma omp parallel for schedule(static)
+  for (long long cid = 0; cid < nce; ++cid) {
+    const int ci[3] = {(int)(cid % c0), (int)((cid / c0) % c1), (int)(cid / ((long long)c0 * c1))};
+    double hh[3], hd2 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+      hh[k] = h->hc[k][ci[k]];
+      hd2 += hh[k] * hh[k];
+    }
+    double u[8], m[8], yl[8];
+    for (int l = 0; l < 8; ++l) {
+      u[l] = mode == 0 ? T[l * nce + cid] : (mode == 1 ? x[l * nce + cid] : 0.0);
+      m[l] = mode == 0 ? u[l] - h->Tp[l * nce + cid] - h->dtf : u[l];
+    }
+    /* cell term */
+    for (int l = 0; l < 8; ++l) {
+      double acc = 0.0;
+      for (int q = 0; q < 8; ++q) {
+        if (mode == 2 && q != l) continue;
+        double mm = 1.0, kk = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          const int a = (l >> k) & 1, b = (q >> k) & 1;
+          double prod = kloc(hh[k], a, b);
+          for (int e = 0; e < 3; ++e)
+            if (e != k) prod *= mloc(hh[e], (l >> e) & 1, (q >> e) & 1);
+          kk += prod;
+          mm *= mloc(hh[k], a, b);
+        }
+        if (mode == 2) acc += mm + h->dta * kk;
+        else acc += mm * m[q] + h->dta * kk * u[q];
+      }
+      yl[l] = acc;
+    }
+    /* facets */
+    for (int k = 0; k < 3; ++k)
+      for (int side = 0; side < 2; ++side) {
+        const int nbi = ci[k] + (side ? 1 : -1);
+        if (nbi >= 0 && nbi < cn[k]) {
+          const long long nb = cid + (side ? cst[k] : -cst[k]);
+          double un[8];
+          for (int l = 0; l < 8; ++l) un[l] = mode == 0 ? T[l * nce + nb] : (mode == 1 ? x[l * nce + nb] : 0.0);
+          const double hL = side ? hh[k] : h->hc[k][nbi], hR = side ? h->hc[k][nbi] : hh[k];
+          const double pen = pen0 / sqrt(hd2 - hh[k] * hh[k] + hL * hL);
+          const double Jv[4] = {0.0, 1.0, -1.0, 0.0};
+          const double Gv[4] = {-0.5 / hL, 0.5 / hL, -0.5 / hR, 0.5 / hR};
+          for (int l = 0; l < 8; ++l) {
+            const int row = side ? ((l >> k) & 1) : 2 + ((l >> k) & 1);
+            double acc = 0.0;
+            for (int q = 0; q < 8; ++q) {
+              if (mode == 2 && q != l) continue;
+              const int bq = (q >> k) & 1;
+              double mt = 1.0;
+              for (int e = 0; e < 3; ++e)
+                if (e != k) mt *= mloc(hh[e], (l >> e) & 1, (q >> e) & 1);
+              const int co = side ? bq : 2 + bq, cb = side ? 2 + bq : bq;
+              const double ao = pen * Jv[row] * Jv[co] - Gv[row] * Jv[co] - Jv[row] * Gv[co];
+              const double an = pen * Jv[row] * Jv[cb] - Gv[row] * Jv[cb] - Jv[row] * Gv[cb];
+              acc += mode == 2 ? mt * ao : mt * (ao * u[q] + an * un[q]);
+            }
+            yl[l] += h->dta * acc;
+          }
+        } else {
+          /* Robin facet: 3 x 3 Gauss over the two tangential axes */
+          double Tl[8];
+          for (int l = 0; l < 8; ++l) Tl[l] = T[l * nce + cid];
+          double acc[8] = {0};
+          for (int qq = 0; qq < 9; ++qq) {
+            double w = 1.0, xt[3] = {0.0, 0.0, 0.0};
+            int t = 0;
+            for (int e = 0; e < 3; ++e) {
+              if (e == k) continue;
+              const int qi = t == 0 ? qq % 3 : qq / 3;
+              xt[e] = GX[qi];
+              w *= GW[qi] * hh[e];
+              ++t;
+            }
+            double phi[8], Th = 0.0, Ph = 0.0;
+            for (int l = 0; l < 8; ++l) {
+              double f = (((l >> k) & 1) == side) ? 1.0 : 0.0;
+              for (int e = 0; e < 3; ++e)
+                if (e != k) f *= ((l >> e) & 1) ? xt[e] : 1.0 - xt[e];
+              phi[l] = f;
+              Th += f * Tl[l];
+              Ph += f * u[l];
+            }
+            for (int l = 0; l < 8; ++l) {
+              if (mode == 0) acc[l] += w * gfun(h, Th) * phi[l];
+              else if (mode == 1) acc[l] += w * dgfun(h, Th) * Ph * phi[l];
+              else acc[l] += w * dgfun(h, Th) * phi[l] * phi[l];
+            }
+          }
+          for (int l = 0; l < 8; ++l) yl[l] += h->dt * acc[l];
+        }
+      }
+    for (int l = 0; l < 8; ++l) y[l * nce + cid] = yl[l];
+  }
+}
+
+static void op_apply(tvcpu* h, int mode, const double* x, double* y) {
+  if (h->dg) dg_apply(h, mode, x, y);
+  else apply(h, mode, x, y);
+}
+
+static void op_diag_inv(tvcpu* h) {
+  if (!h->dg) {
+    diag_inv(h);
+    return;
+  }
+  dg_apply(h, 2, NULL, h->dinv);
+#pragma omp parallel for
+  for (long long t = 0; t < h->N; ++t) h->dinv[t] = 1.0 / h->dinv[t];
+}
+
 static int pcg(tvcpu* h, double rtol) {
   const long long N = h->N;
   double zz = 0, zr = 0;
@@ -210,7 +342,7 @@ static int pcg(tvcpu* h, double rtol) {
     double b = it ? beta / betaold : 0.0;
 #pragma omp parallel for
     for (long long t = 0; t < N; ++t) h->p[t] = it ? h->z[t] + b * h->p[t] : h->z[t];
-    apply(h, 1, h->p, h->w);
+    op_apply(h, 1, h->p, h->w);
     double dpi = 0;
 #pragma omp parallel for reduction(+ : dpi)
     for (long long t = 0; t < N; ++t) dpi += h->p[t] * h->w[t];
@@ -239,9 +371,9 @@ static int newton(tvcpu* h) {
   const long long N = h->N;
   int its = 0, kits = 0, conv = 0;
   double r0 = 0.0;
-  apply(h, 0, NULL, h->r);
+  op_apply(h, 0, NULL, h->r);
   while (!conv && its < 50) {
-    diag_inv(h);
+    op_diag_inv(h);
     int k = pcg(h, 1e-5);
     if (k < 0) return -1;
     kits += k;
@@ -255,7 +387,7 @@ static int newton(tvcpu* h) {
     ++its;
     if (its == 1) r0 = rn;
     else conv = (rn / r0 < 1e-12) || (rn < 1e-10);
-    if (!conv) apply(h, 0, NULL, h->r);
+    if (!conv) op_apply(h, 0, NULL, h->r);
   }
   h->last_newton = its;
   h->last_krylov = kits;
@@ -311,16 +443,21 @@ static void visco(tvcpu* h) {
 }
 
 /* ---------------- C entry points (ctypes) ---------------- */
-void* tvcpu_create(const int* ncells, const double* x, const double* y, const double* z, const double* params /* f eps sigma Ta T0 alpha htc H Tb Rg as al dt */,
-                   const double* tabs /* 36: m lm g lg k lk */) {
+static void* create(int dg, const int* ncells, const double* x, const double* y, const double* z,
+                    const double* params, const double* tabs) {
   tvcpu* h = (tvcpu*)calloc(1, sizeof(tvcpu));
   const double* X[3] = {x, y, z};
+  h->dg = dg;
   for (int a = 0; a < 3; ++a) {
     h->n[a] = ncells[a] + 1;
     h->c[a] = (double*)malloc(sizeof(double) * NC * h->n[a]);
     coefs(X[a], h->n[a], h->c[a]);
+    h->nc[a] = ncells[a];
+    h->hc[a] = (double*)malloc(sizeof(double) * (size_t)ncells[a]);
+    for (int i = 0; i < ncells[a]; ++i) h->hc[a][i] = X[a][i + 1] - X[a][i];
   }
-  h->N = (long long)h->n[0] * h->n[1] * h->n[2];
+  h->ncell = (long long)ncells[0] * ncells[1] * ncells[2];
+  h->N = dg ? 8 * h->ncell : (long long)h->n[0] * h->n[1] * h->n[2];
   double f = params[0], eps = params[1], sg = params[2], Ta = params[3], T0 = params[4], al = params[5], htc = params[6];
   h->dt = params[12];
   h->dta = h->dt * al;
@@ -350,6 +487,19 @@ void* tvcpu_create(const int* ncells, const double* x, const double* y, const do
     for (int i = 0; i < 6; ++i) h->Tfp[i * N + t] = T0;
   }
   return h;
+}
+
+void* tvcpu_create(const int* ncells, const double* x, const double* y, const double* z,
+                   const double* params /* f eps sigma Ta T0 alpha htc H Tb Rg as al dt */,
+                   const double* tabs /* 36: m lm g lg k lk */) {
+  return create(0, ncells, x, y, z, params, tabs);
+}
+
+/* DG1 temperature and stress spaces; dofs (l, cell) at l * ncell + cell with
+ * l = bx + 2 by + 4 bz the cell corner */
+void* tvcpu_create_dg(const int* ncells, const double* x, const double* y, const double* z, const double* params,
+                      const double* tabs) {
+  return create(1, ncells, x, y, z, params, tabs);
 }
 
 int tvcpu_step(void* hp, int thermal_only, int* newton_its, int* krylov_its) {
@@ -392,7 +542,7 @@ void tvcpu_destroy(void* hp) {
   tvcpu* h = (tvcpu*)hp;
   if (!h) return;
   double* bufs[] = {h->T, h->Tp, h->Tf, h->phi, h->xi, h->r, h->z, h->p, h->w, h->dx, h->dinv, h->Tfp, h->st, h->sg, h->sig,
-                    h->c[0], h->c[1], h->c[2]};
+                    h->c[0], h->c[1], h->c[2], h->hc[0], h->hc[1], h->hc[2]};
   for (size_t q = 0; q < sizeof(bufs) / sizeof(bufs[0]); ++q) free(bufs[q]);
   free(h);
 }

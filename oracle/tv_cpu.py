@@ -24,6 +24,8 @@ def load():
         dp = C.POINTER(C.c_double)
         lib.tvcpu_create.restype = C.c_void_p
         lib.tvcpu_create.argtypes = [C.POINTER(C.c_int), dp, dp, dp, dp, dp]
+        lib.tvcpu_create_dg.restype = C.c_void_p
+        lib.tvcpu_create_dg.argtypes = [C.POINTER(C.c_int), dp, dp, dp, dp, dp]
         lib.tvcpu_step.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         lib.tvcpu_num_dofs.restype = C.c_longlong
         lib.tvcpu_num_dofs.argtypes = [C.c_void_p]
@@ -34,9 +36,10 @@ def load():
 
 
 class CpuProblem:
-    """Structured 3D CG1/CG1 plate on the CPU (axes: node coordinates per axis)."""
+    """Structured 3D plate on the CPU (axes: node coordinates per axis), CG1/CG1
+    or (family "DG") DG1/DG1 with cell-local dofs at l * ncell + cell."""
 
-    def __init__(self, axes, mp, dt):
+    def __init__(self, axes, mp, dt, family="CG"):
         lib = load()
         self.axes = [np.ascontiguousarray(a, dtype=np.float64) for a in axes]
         nc = (C.c_int * 3)(*[len(a) - 1 for a in self.axes])
@@ -45,7 +48,8 @@ class CpuProblem:
         tabs = np.concatenate([O.PRONY[k] for k in ("m_n", "lambda_m", "g_n", "lambda_g", "k_n", "lambda_k")])
         dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
         self._keep = (params, tabs)
-        self.h = lib.tvcpu_create(nc, dp(self.axes[0]), dp(self.axes[1]), dp(self.axes[2]), dp(params), dp(tabs))
+        create = lib.tvcpu_create_dg if family == "DG" else lib.tvcpu_create
+        self.h = create(nc, dp(self.axes[0]), dp(self.axes[1]), dp(self.axes[2]), dp(params), dp(tabs))
         self.n = lib.tvcpu_num_dofs(self.h)
         self.lib = lib
 
@@ -76,12 +80,12 @@ def cores():
         return os.cpu_count() or 1
 
 
-def time_baseline(nc, L, mp, seconds=15.0, thermal_only=False):
+def time_baseline(nc, L, mp, seconds=15.0, thermal_only=False, family="CG"):
     """Bounded sample of the bench workload: the full mesh, as many whole time
     steps as fit about `seconds` (at least one, at most 10).  Returns the
     cpu_baseline record of bench.py."""
     axes = [np.linspace(0.0, l, n + 1) for l, n in zip(L, nc)]
-    P = CpuProblem(axes, mp, 0.1)
+    P = CpuProblem(axes, mp, 0.1, family)
     t0 = time.perf_counter()
     steps = 0
     while True:
@@ -96,4 +100,4 @@ def time_baseline(nc, L, mp, seconds=15.0, thermal_only=False):
             "kind": "port",
             "sample": f"{steps} full time step(s) of the same {nc[0]}x{nc[1]}x{nc[2]} hex mesh "
                       f"({n} dofs, {'thermal-only' if thermal_only else 'coupled'}) in {el:.1f} s, "
-                      "oracle/tv_cpu.c (C/OpenMP port: matrix-free Jacobi-PCG Newton + visco update)"}
+                      f"oracle/tv_cpu.c (C/OpenMP port, {family}1: matrix-free Jacobi-PCG Newton + visco update)"}
