@@ -397,7 +397,7 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     g.bnd[2][0] = g.bnd[2][1] = g.deg2 ? 0 : 1;
     const char* et = experiment_env("TVFEM_DG_TILE");
     const char* ec = experiment_env("TVFEM_DG_CHUNK");
-    g.tile = (et && atoi(et) == 0) ? 0 : 1;
+    g.tile = et ? std::min(2, std::max(0, atoi(et))) : 2;  // 2: k_dg_tile with halo-loading edge waves
     g.tile_chunk = ec ? std::max(1, atoi(ec)) : 5;
     for (int s = 0; s < 3; ++s) {
       const std::vector<double>& X = storage_coords(c, s, tmp);

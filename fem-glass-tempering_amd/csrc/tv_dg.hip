@@ -414,6 +414,8 @@ __device__ __forceinline__ void fdm_mul(const DgGrid& g, const double* __restric
 // per SIMD with 254 VGPRs.)
 // ---------------------------------------------------------------------------
 constexpr int kDgRows = 6;  // + 2 halo waves: 512 threads, up to 256 VGPRs (no spills)
+constexpr int kDgRowsHL = 8;  // HL: 8 computing waves, the edge waves also load the halo rows
+constexpr int dg_rows(bool hl) { return hl ? kDgRowsHL : kDgRows; }
 
 // v <- (M_e (x) I) v along storage axis e (local bit e), M_e = h [1/3 1/6; 1/6 1/3]
 __device__ __forceinline__ void mass_axis(double (&v)[8], int e, double h) {
@@ -437,17 +439,21 @@ __device__ __forceinline__ void stiff_axis(const double (&v)[8], double (&out)[8
     }
 }
 
-template <bool FUSEP>
-__global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, const double* __restrict__ T,
-                                                                  const double* __restrict__ in0,
-                                                                  const double* in1, double* __restrict__ out,
-                                                                  double* pout, const PcgState* __restrict__ st,
-                                                                  double* __restrict__ partials, int nseg, int ra,
-                                                                  int qchunk, int nch, RedTail rt) {
+// HL (halo loads): no halo waves -- all 8 waves compute a row and waves 0 / 7
+// also load the rows above / below the tile (plane L + 1 in flight during step
+// L, formed into the slab's halo slots at the top of step L + 1): 8 output
+// rows per 8 waves instead of 6.
+template <bool FUSEP, bool HL>
+__global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restrict__ T,
+                                                 const double* __restrict__ in0, const double* in1,
+                                                 double* __restrict__ out, double* pout,
+                                                 const PcgState* __restrict__ st, double* __restrict__ partials,
+                                                 int nseg, int ra, int qchunk, int nch, RedTail rt) {
   stamp_start(rt);
-  constexpr int R = kDgRows;
+  constexpr int R = dg_rows(HL);
+  constexpr int NW = HL ? R : R + 2;  // waves per workgroup (512 threads either way)
   __shared__ double sX[2][R + 2][8][kWave];  // double-buffered plane slab: one barrier per plane
-  __shared__ double red[R + 2];
+  __shared__ double red[NW];
   if (st != nullptr && st->done) return;  // uniform over the grid
   const int pa = 3 - ra;
   const int cn[3] = {g.c0, g.c1, g.c2};
@@ -463,12 +469,18 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
   const int rb = t / nseg;
   const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, npl);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
-  const int r = rb * R - 1 + wave;  // row along ra (waves 0 and R + 1: halo rows)
+  const int r = HL ? rb * R + wave : rb * R - 1 + wave;  // row along ra (!HL: waves 0 and R + 1 are halo rows)
+  const int slot = HL ? wave + 1 : wave;                   // the row's slot in the slab
   const int i = seg * kSeg - 1 + lane;
   const bool valid = i >= 0 && i < g.c0 && r >= 0 && r < cn[ra];
-  const bool compute = wave >= 1 && wave <= R;
+  const bool compute = HL || (wave >= 1 && wave <= R);
   const bool writer = compute && valid && lane >= 1 && lane <= kSeg;
   const int64_t cbase = (valid ? i : 0) + cst[ra] * (valid ? r : 0);  // cell of plane 0
+  // HL: the halo row this wave loads (wave 0: the row below the tile, wave R - 1: above)
+  const int rh = wave == 0 ? r - 1 : r + 1;
+  const bool hvalid = HL && (wave == 0 || wave == R - 1) && i >= 0 && i < g.c0 && rh >= 0 && rh < cn[ra];
+  const int hslot = wave == 0 ? 0 : R + 1;
+  const int64_t hbase = (hvalid ? i : 0) + cst[ra] * (hvalid ? rh : 0);
 
   double bcoef = 0.0;
   bool first = false;
@@ -495,6 +507,18 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
 #pragma unroll
     for (int l = 0; l < 8; ++l) v[l] = FUSEP ? rz[l] + bcoef * ro[l] : rz[l];
   };
+  double hz[8], ho[8];  // HL: raw loads of the halo row of plane L + 1, in flight during step L
+  auto hfetch = [&](int L) {
+    const bool ok = hvalid && L >= 0 && L < npl;
+    const int64_t c = hbase + cst[pa] * (ok ? L : 0);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int64_t o = (int64_t)l * ncell + c;
+      hz[l] = ok ? in0[o] : 0.0;
+      ho[l] = (FUSEP && !first && ok) ? pold[o] : 0.0;
+    }
+  };
+  if (HL) hfetch(q0);
   double xl[8], x[8], xu[8];  // planes L - 1, L, L + 1
   double rz[8], ro[8];        // raw loads of plane L + 2, in flight during step L
   {  // prologue: the loads of the first three planes in flight together
@@ -511,7 +535,12 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
     fetch(L + 2, rz, ro);
     const int sb = L & 1;
 #pragma unroll
-    for (int l = 0; l < 8; ++l) sX[sb][wave][l][lane] = x[l];
+    for (int l = 0; l < 8; ++l) sX[sb][slot][l][lane] = x[l];
+    if (HL && (wave == 0 || wave == R - 1)) {  // wave-uniform
+#pragma unroll
+      for (int l = 0; l < 8; ++l) sX[sb][hslot][l][lane] = FUSEP ? hz[l] + bcoef * ho[l] : hz[l];
+      hfetch(L + 1);
+    }
     const int64_t cid = cbase + cst[pa] * L;
     if (FUSEP && writer) {
 #pragma unroll
@@ -564,7 +593,7 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
             for (int l = 0; l < 8; ++l) xn[l] = side ? shl1(x[l]) : shr1(x[l]);
           } else if (k == ra) {
 #pragma unroll
-            for (int l = 0; l < 8; ++l) xn[l] = sX[sb][wave + (side ? 1 : -1)][l][lane];
+            for (int l = 0; l < 8; ++l) xn[l] = sX[sb][slot + (side ? 1 : -1)][l][lane];
           } else {
 #pragma unroll
             for (int l = 0; l < 8; ++l) xn[l] = side ? xu[l] : xl[l];
@@ -656,7 +685,7 @@ __global__ __launch_bounds__((kDgRows + 2) * kWave) void k_dg_tile(DgGrid g, con
     __syncthreads();
     if (threadIdx.x == 0) {
       double sacc = 0.0;
-      for (int w = 0; w < R + 2; ++w) sacc += red[w];
+      for (int w = 0; w < NW; ++w) sacc += red[w];
       store_partial(&partials[blockIdx.x], sacc);
     }
     fused_reduce_tail<1>(rt, (int)gridDim.x);  // p.w over all tiles (+ KSPCG logic)
@@ -672,7 +701,8 @@ DgTile dg_tile_plan(const DgGrid& g) {
   p.nseg = (g.c0 + kSeg - 1) / kSeg;
   p.ra = (g.c2 >= g.c1) ? 2 : 1;  // rows along the longer of axes 1 / 2, march along the other
   const int nr = (p.ra == 2) ? g.c2 : g.c1, npl = (p.ra == 2) ? g.c1 : g.c2;
-  const int nrb = (nr + kDgRows - 1) / kDgRows;
+  const int rows = dg_rows(g.tile == 2);
+  const int nrb = (nr + rows - 1) / rows;
   p.nch = (npl + qmax - 1) / qmax;
   p.qchunk = (npl + p.nch - 1) / p.nch;
   p.nch = (npl + p.qchunk - 1) / p.qchunk;
@@ -904,8 +934,12 @@ static bool launch_tile(const DgGrid& g, const double* T, const double* in0, con
   if (p.blocks <= 0) return false;
   RedTail rt{};
   if (tail && partials) rt = *tail;
-  hipLaunchKernelGGL((k_dg_tile<FUSEP>), dim3(p.blocks), dim3((kDgRows + 2) * kWave), 0, s, g, T, in0, in1, out,
-                     pout, st, partials, p.nseg, p.ra, p.qchunk, p.nch, rt);
+  if (g.tile == 2)
+    hipLaunchKernelGGL((k_dg_tile<FUSEP, true>), dim3(p.blocks), dim3(512), 0, s, g, T, in0, in1, out, pout, st,
+                       partials, p.nseg, p.ra, p.qchunk, p.nch, rt);
+  else
+    hipLaunchKernelGGL((k_dg_tile<FUSEP, false>), dim3(p.blocks), dim3(512), 0, s, g, T, in0, in1, out, pout, st,
+                       partials, p.nseg, p.ra, p.qchunk, p.nch, rt);
   return rt.counter != nullptr;
 }
 

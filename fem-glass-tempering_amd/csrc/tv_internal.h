@@ -71,9 +71,10 @@ struct DgGrid {
   double a_rad, a_conv;
   double T_amb, T_amb4;
   double penalty;             // SIPG penalty (ThermoViscoProblem.py:313)
-  // 3D Jacobian kernel: 1 = marching tiles (k_dg_tile) of `tile_chunk` planes,
-  // 0 = one thread per cell (k_dg_cells); from TVFEM_DG_TILE / TVFEM_DG_CHUNK
-  // when the context is created
+  // 3D Jacobian kernel: 2 = marching tiles (k_dg_tile) of 8 computing waves whose
+  // edge waves load the halo rows (default), 1 = 6 computing + 2 halo waves,
+  // both of `tile_chunk` planes; 0 = one thread per cell (k_dg_cells); from
+  // TVFEM_DG_TILE / TVFEM_DG_CHUNK when the context is created
   int tile, tile_chunk;
 };
 

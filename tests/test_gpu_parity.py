@@ -325,12 +325,14 @@ def test_in_solve_kernel_timing():
 
 
 def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
-    """The marching DG1 Jacobian (k_dg_tile) against the one-thread-per-cell
-    kernel (k_dg_cells, itself pinned to the oracle above) on a grid large
-    enough for two x segments, several row tiles (13 rows, 6 per tile) and
-    several march chunks (7 planes in chunks of 2 and 5): J x at a random T
-    (1e-12) and one coupled time step through the fused PCG matvec (T 1e-10).
-    The oracle itself is too slow to assemble DG1 at this size."""
+    """The marching DG1 Jacobian (k_dg_tile; TVFEM_DG_TILE 1: 6 computing + 2
+    halo waves, 2 (default): 8 computing waves whose edge waves load the halo
+    rows) against the one-thread-per-cell kernel (k_dg_cells, itself pinned to
+    the oracle above) on a grid large enough for two x segments, several row
+    tiles (13 rows, 6 or 8 per tile) and several march chunks (7 planes in
+    chunks of 2 and 5): J x at a random T (1e-12) and one coupled time step
+    through the fused PCG matvec (T 1e-10).  The oracle itself is too slow to
+    assemble DG1 at this size."""
     torch = _torch()
     from tvfem import RectilinearMesh
     from tvfem.problem import ThermoViscoProblem
@@ -340,7 +342,7 @@ def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
     rng = np.random.default_rng(3)
     out = {}
     monkeypatch.setenv("TVFEM_EXPERIMENTS", "1")  # the kernel-variant switches below are gated by it
-    for tile, chunk in ((0, 5), (1, 2), (1, 5)):
+    for tile, chunk in ((0, 5), (1, 2), (1, 5), (2, 2), (2, 5)):
         monkeypatch.setenv("TVFEM_DG_TILE", str(tile))
         monkeypatch.setenv("TVFEM_DG_CHUNK", str(chunk))
         p = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
@@ -360,7 +362,7 @@ def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
         out[(tile, chunk)] = (T1, host_layout(p, yd.cpu().numpy(), "DG"))
         p.close()
     T_ref, y_ref = out[(0, 5)]
-    for key in ((1, 2), (1, 5)):
+    for key in ((1, 2), (1, 5), (2, 2), (2, 5)):
         T1, y = out[key]
         assert relerr(y, y_ref) < 1e-12, key
         assert relerr(T1, T_ref) < 1e-10, key
