@@ -443,12 +443,15 @@ __device__ __forceinline__ void stiff_axis(const double (&v)[8], double (&out)[8
 // also load the rows above / below the tile (plane L + 1 in flight during step
 // L, formed into the slab's halo slots at the top of step L + 1): 8 output
 // rows per 8 waves instead of 6.
-template <bool FUSEP, bool HL>
+// RA: the row axis (1 or 2) as a template parameter, so every k == ra / pa
+// test and ci[] / cn[] index in the unrolled facet loop resolves at compile time
+template <bool FUSEP, bool HL, int RA>
 __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restrict__ T,
                                                  const double* __restrict__ in0, const double* in1,
                                                  double* __restrict__ out, double* pout,
                                                  const PcgState* __restrict__ st, double* __restrict__ partials,
-                                                 int nseg, int ra, int qchunk, int nch, RedTail rt) {
+                                                 int nseg, int qchunk, int nch, RedTail rt) {
+  constexpr int ra = RA;
   stamp_start(rt);
   constexpr int R = dg_rows(HL);
   constexpr int NW = HL ? R : R + 2;  // waves per workgroup (512 threads either way)
@@ -934,12 +937,17 @@ static bool launch_tile(const DgGrid& g, const double* T, const double* in0, con
   if (p.blocks <= 0) return false;
   RedTail rt{};
   if (tail && partials) rt = *tail;
-  if (g.tile == 2)
-    hipLaunchKernelGGL((k_dg_tile<FUSEP, true>), dim3(p.blocks), dim3(512), 0, s, g, T, in0, in1, out, pout, st,
-                       partials, p.nseg, p.ra, p.qchunk, p.nch, rt);
-  else
-    hipLaunchKernelGGL((k_dg_tile<FUSEP, false>), dim3(p.blocks), dim3(512), 0, s, g, T, in0, in1, out, pout, st,
-                       partials, p.nseg, p.ra, p.qchunk, p.nch, rt);
+#define TV_DG_TILE(HLV, RAV)                                                                                  \
+  hipLaunchKernelGGL((k_dg_tile<FUSEP, HLV, RAV>), dim3(p.blocks), dim3(512), 0, s, g, T, in0, in1, out, pout, st, \
+                     partials, p.nseg, p.qchunk, p.nch, rt)
+  if (g.tile == 2) {
+    if (p.ra == 2) TV_DG_TILE(true, 2);
+    else TV_DG_TILE(true, 1);
+  } else {
+    if (p.ra == 2) TV_DG_TILE(false, 2);
+    else TV_DG_TILE(false, 1);
+  }
+#undef TV_DG_TILE
   return rt.counter != nullptr;
 }
 
