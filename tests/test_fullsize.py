@@ -1,0 +1,113 @@
+"""Parity at BASELINE.json's full sizes through size-independent properties
+(the oracle cannot assemble 8M dofs in a test's time).
+
+C4 (400 x 400 x 50 CG1 hex, 8.2M dofs) and C5 (200 x 200 x 25 DG1, 8M dofs) on
+the 50 x 50 x 5 plate of bench.py:
+  * J(T) is symmetric: y.(J x) = x.(J y) for random x, y (SIPG and the Robin
+    facet terms included);
+  * J(T0) 1 sums to |Omega| + dt dg(T0) |dOmega| at a uniform T0: the stiffness
+    and the SIPG terms annihilate constants, the mass and the boundary mass sum
+    to the volume and the area (ThermoViscoProblem.py:293-325 with
+    dg(T) = 0.001 (4 sigma eps T^3 + htc));
+  * one coupled step with the geometric-multigrid preconditioner and one with
+    Jacobi give the same T (Newton to 1e-12 either way, so only the Krylov
+    iterates differ) and the same Newton count, and the converged residual is
+    small against the first one.
+"""
+import numpy as np
+import pytest
+
+from oracle import tv_oracle as O
+
+L = (50.0, 50.0, 5.0)
+SIZES = {"C4": ("CG", (400, 400, 50)), "C5": ("DG", (200, 200, 25))}
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _problem(fam, nc, pc):
+    from tvfem import box_mesh
+    from tvfem.problem import ThermoViscoProblem
+    cfg = {"T": {"element": fam, "degree": 1}, "sigma": {"element": fam, "degree": 1}}
+    return ThermoViscoProblem(box_mesh(L, nc), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False,
+                              materialize=False, part_axis=1, preconditioner=pc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(SIZES))
+def test_fullsize_jacobian_symmetry_and_constants(case):
+    torch = _torch()
+    fam, nc = SIZES[case]
+    p = _problem(fam, nc, "jacobi")
+    p.setup()
+    lib, ctx = p._lib, p._ctx
+    n = p.get_field("T").size
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
+    y = torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
+    jx, jy = torch.empty_like(x), torch.empty_like(y)
+    assert lib.tv_jacobian_apply(ctx, x.data_ptr(), jx.data_ptr()) == 0
+    assert lib.tv_jacobian_apply(ctx, y.data_ptr(), jy.data_ptr()) == 0
+    a, b = float(torch.dot(y, jx)), float(torch.dot(x, jy))
+    assert abs(a - b) <= 1e-12 * (abs(a) + abs(b)), (case, a, b)
+    one = torch.ones(n, dtype=torch.float64, device="cuda")
+    j1 = torch.empty_like(one)
+    assert lib.tv_jacobian_apply(ctx, one.data_ptr(), j1.data_ptr()) == 0
+    mp = O.MAIN_MODEL_PARAMS
+    T0 = mp["T_0"]
+    dg = 0.001 * (4.0 * mp["sigma"] * mp["epsilon"] * T0 ** 3 + mp["htc"])
+    vol = L[0] * L[1] * L[2]
+    area = 2.0 * (L[0] * L[1] + L[0] * L[2] + L[1] * L[2])
+    want = vol + 0.1 * dg * area
+    got = float(j1.sum())
+    print(f"[fullsize] {case}: n {n}, sum J1 {got:.12e} vs {want:.12e}; symmetry {abs(a - b) / abs(a):.1e}")
+    assert abs(got - want) <= 1e-10 * want, (case, got, want)
+    p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(SIZES))
+def test_fullsize_gmg_step_matches_jacobi_step(case):
+    import ctypes as C
+    from tvfem import _native as N
+    torch = _torch()
+    fam, nc = SIZES[case]
+    out = {}
+    for pc in ("gmg", "jacobi"):
+        p = _problem(fam, nc, pc)
+        p.setup()
+        T0 = p.get_field("T")
+        lib, ctx = p._lib, p._ctx
+        n = T0.size
+        # residual at the start of the step (T = T_prev = T0: only the Robin and source terms)
+        Td = torch.tensor(T0, dtype=torch.float64, device="cuda")
+        F0 = torch.empty_like(Td)
+        assert lib.tv_residual(ctx, Td.data_ptr(), F0.data_ptr()) == 0
+        p.solve_timestep()
+        T1 = p.get_field("T")
+        # the converged step's residual, F(T1; T_prev = T0), against the initial one:
+        # T1 from the context's own device field (device layout), T_prev reset to the
+        # uniform T0 the visco update overwrote
+        p.set_field("T_prev", T0)
+        p._flush()
+        ptr, stride = C.c_void_p(), C.c_int64()
+        assert lib.tv_field_device_ptr(ctx, N.FIELD_ID["T"], C.byref(ptr), C.byref(stride)) == 0
+        F1 = torch.empty_like(Td)
+        assert lib.tv_residual(ctx, ptr.value, F1.data_ptr()) == 0
+        ratio = float(torch.linalg.norm(F1) / torch.linalg.norm(F0))
+        out[pc] = (T1, p.last_newton_iterations, p.last_krylov_iterations, ratio, n)
+        p.close()
+    Tg, ng, kg, rg, n = out["gmg"]
+    Tj, nj, kj, rj, _ = out["jacobi"]
+    rel = float(np.linalg.norm(Tg - Tj) / np.linalg.norm(Tj))
+    print(f"[fullsize] {case}: n {n}, T gmg vs jacobi {rel:.2e}; Newton {ng} / {nj}, Krylov {kg} / {kj}; "
+          f"|F(T1)| / |F(T0)| {rg:.1e} / {rj:.1e}")
+    assert rel < 1e-10, rel
+    assert ng == nj
+    assert kg * 3 <= kj
+    assert rg < 1e-6 and rj < 1e-6, (rg, rj)
