@@ -1180,9 +1180,12 @@ static int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   mg_apply0(c, T, &t0);  // z <- V(r); dp, beta (KSPCG init)
   if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
     if (int e = ts_flush(c)) return e;
-  // an MG iteration is ~30 launches: the first hint - 1 iterations are queued
-  // at once, then one at a time behind a poll (no look-ahead: an iteration
-  // queued past convergence still costs its launches)
+  // an MG iteration is ~25 launches: the previous solve's count (hint) is queued
+  // right behind the init, with no host wait in between (the GPU would idle
+  // while the host enqueues ~100 launches; an init that already converged
+  // makes every queued launch exit at once), then one iteration at a time
+  // behind a poll.  The Newton solves of a step take near-constant counts, so
+  // the hint usually ends the solve at the first poll.
   int launched = 0;
   auto enqueue = [&](int nb) -> int {
     for (int b = 0; b < nb; ++b)
@@ -1193,17 +1196,12 @@ static int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipEventRecord(c->evp[0], c->stream));
     return TV_OK;
   };
-  HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
-  HIPC(hipEventRecord(c->evp[0], c->stream));
-  HIPC(hipEventSynchronize(c->evp[0]));
-  if (!c->h_st[0].done) {
-    if (int e = enqueue(std::max(1, c->pcg_hint - 1))) return e;
-    for (;;) {
-      HIPC(hipEventSynchronize(c->evp[0]));
-      if (c->h_st[0].done) break;
-      if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
-      if (int e = enqueue(1)) return e;
-    }
+  if (int e = enqueue(std::max(1, c->pcg_hint))) return e;
+  for (;;) {
+    HIPC(hipEventSynchronize(c->evp[0]));
+    if (c->h_st[0].done) break;
+    if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    if (int e = enqueue(1)) return e;
   }
   *its = c->h_st[0].it;
   *reason = c->h_st[0].reason;
