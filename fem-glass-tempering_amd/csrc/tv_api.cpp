@@ -2058,6 +2058,7 @@ int tv_residual(void* ctx, const double* T_dev, double* F_dev) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !T_dev || !F_dev) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
   op_residual(c, T_dev, c->f[TV_F_T_PREV].ptr, F_dev);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));
@@ -2068,6 +2069,7 @@ int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !x_dev || !y_dev) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
   op_japply(c, c->f[TV_F_T].ptr, x_dev, y_dev, nullptr, nullptr);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));
@@ -2078,6 +2080,7 @@ int tv_jacobian_diag(void* ctx, double* d_dev) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !d_dev) return TV_ERR_ARG;
   hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
   op_diag(c, c->f[TV_F_T].ptr, d_dev, 0);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));

@@ -300,6 +300,133 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_rows(MgXfer x, const PcgS
   if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;  // the coarse pre-smoothing step from 0
 }
 
+// ---- x-pair transfers --------------------------------------------------------
+// A lane owns the fine pair (2I, 2I + 1) of coarse x node I and moves it with
+// ONE 16-byte load / store (rows of an odd node count start 8-byte aligned:
+// gfx950 buffer / global accesses need dword alignment only), so a wave's
+// access is one contiguous 1 KB run per row instead of two 8-byte-strided
+// ones (half the load instructions and half the L1 lines per fine node of the
+// row-per-wave kernels above).  The x neighbour across the pair boundary comes
+// from the adjacent lane (DPP wave shift); the segment's first (restriction)
+// or last (prolongation) lane only loads it for its neighbour.
+typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
+constexpr int kPairSeg = kWave - 1;  // outputs per wave
+
+__device__ __forceinline__ d2a8 ld_pair(const double* p) { return *reinterpret_cast<const d2a8*>(p); }
+
+// Restriction, one wave per (coarse row, 63-node x segment); lane l is coarse
+// node I = 63 seg - 1 + l (lane 0 = the halo lane whose right fine node is
+// lane 1's left neighbour).  A lane whose fine centre is the row's last node
+// (even cell count, or the odd tail) loads that node alone; its right weight is 0.
+template <bool MASK>
+__global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const PcgState* __restrict__ st,
+                                                             const double* __restrict__ bf,
+                                                             const double* __restrict__ wf,
+                                                             const double* __restrict__ mask, double* __restrict__ bc,
+                                                             const double* __restrict__ dinv_c, double omega_c,
+                                                             double* __restrict__ xc, int nseg) {
+  if (st != nullptr && st->done) return;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = bid / nseg;
+  const int seg = bid - row * nseg;
+  const int J = row % x.cn[1], K = row / x.cn[1] + x.c_kb;
+  const int lane = (int)threadIdx.x;
+  const int cn = x.cn[0], nf = x.fn[0];
+  const int I = seg * kPairSeg - 1 + lane;
+  const bool ok = lane > 0 && I < cn;
+  const int II = I < 0 ? 0 : (I < cn ? I : cn - 1);
+  const int f1 = (II == cn - 1 && ((nf - 1) & 1)) ? nf - 1 : 2 * II;
+  const bool pair = f1 + 1 < nf;
+  const double wl = x.rw[0][3 * II], wr = x.rw[0][3 * II + 2];
+  const int64_t fpl = (int64_t)nf * x.fn[1];
+  double dc[9], dr[9], wq[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int c = q / 3, b = q % 3;
+    wq[q] = x.rw[2][3 * K + c] * x.rw[1][3 * J + b];
+    const int64_t f = (int64_t)x.ri[1][3 * J + b] * nf + fpl * x.ri[2][3 * K + c] + f1;
+    if (pair) {
+      const d2a8 r = ld_pair(bf + f), w = ld_pair(wf + f);
+      dc[q] = r.x - w.x;
+      dr[q] = r.y - w.y;
+      if (MASK) {
+        const d2a8 m = ld_pair(mask + f);
+        if (m.x == 0.0) dc[q] = 0.0;
+        if (m.y == 0.0) dr[q] = 0.0;
+      }
+    } else {
+      double d = bf[f] - wf[f];
+      if (MASK && mask[f] == 0.0) d = 0.0;
+      dc[q] = dr[q] = d;
+    }
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const double dl = shr1(dr[q]);  // lane - 1's right fine node = 2I - 1 (weight 0 at I = 0 and the odd tail)
+    acc += wq[q] * ((wl * dl + dc[q]) + wr * dr[q]);
+  }
+  if (!ok) return;
+  const int64_t o = (int64_t)I + (int64_t)cn * (J + (int64_t)x.cn[1] * K);
+  bc[o] = acc;
+  if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;  // the coarse pre-smoothing step from 0
+}
+
+// Prolongation, one wave per (fine row, 63-pair segment); lane l owns the fine
+// pair (2c, 2c + 1), c = 63 seg + l; lane 63 only loads coarse c for lane 62.
+// Fine 2c is coarse c; fine 2c + 1 interpolates c and c + 1 (lane + 1), or is
+// the odd tail (coarse c + 1 itself).
+__global__ __launch_bounds__(kWave) void k_mg_prolong_pairs(MgXfer x, const PcgState* __restrict__ st,
+                                                            double* __restrict__ xf, const double* __restrict__ xc,
+                                                            const double* __restrict__ mask, int nseg) {
+  if (st != nullptr && st->done) return;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int row = bid / nseg;
+  const int seg = bid - row * nseg;
+  const int j = row % x.fn[1], k = row / x.fn[1] + x.f_kb;
+  const int nf = x.fn[0], cn = x.cn[0];
+  const int lane = (int)threadIdx.x;
+  const int c = seg * kPairSeg + lane;
+  const int cc = c < cn ? c : cn - 1;
+  const int i0 = 2 * c, i1 = 2 * c + 1;
+  const bool has0 = lane < kPairSeg && i0 < nf, has1 = lane < kPairSeg && i1 < nf;
+  const bool tail = i1 == nf - 1 && ((nf - 1) & 1);
+  const int i1c = has1 ? i1 : 0;
+  const double wl = x.pw[0][2 * i1c], wr = x.pw[0][2 * i1c + 1];
+  const int64_t cpl = (int64_t)cn * x.cn[1];
+  const int64_t f = (int64_t)i0 + (int64_t)nf * (j + (int64_t)x.fn[1] * k);
+  double v[4], w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int cz = q >> 1, b = q & 1;
+    w[q] = x.pw[2][2 * k + cz] * x.pw[1][2 * j + b];
+    v[q] = xc[cc + (int64_t)cn * x.pi[1][2 * j + b] + cpl * x.pi[2][2 * k + cz]];
+  }
+  d2a8 xo = {0.0, 0.0};
+  if (has1) xo = ld_pair(xf + f);
+  else if (has0) xo.x = xf[f];
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double vr = shl1(v[q]);  // coarse c + 1
+    a0 += w[q] * v[q];
+    a1 += w[q] * (tail ? vr : wl * v[q] + wr * vr);
+  }
+  if (!has0) return;
+  if (has1) {
+    d2a8 out = {xo.x + a0, xo.y + a1};
+    if (mask != nullptr) {
+      const d2a8 m = ld_pair(mask + f);
+      if (m.x == 0.0) out.x = 0.0;
+      if (m.y == 0.0) out.y = 0.0;
+    }
+    *reinterpret_cast<d2a8*>(xf + f) = out;
+  } else {
+    const bool off = mask != nullptr && mask[f] == 0.0;
+    xf[f] = off ? 0.0 : xo.x + a0;
+  }
+}
+
 template <int MODE, bool FACES>
 __global__ __launch_bounds__(kBlock) void k_mg_jacobi(int64_t n, const PcgState* __restrict__ st,
                                                       const double* __restrict__ b, const double* __restrict__ w,
@@ -413,6 +540,16 @@ __global__ __launch_bounds__(kBlock) void k_mg_scale(int64_t n, const double* __
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = a * y[t];
 }
 
+// TVFEM_MG_ROWS=1 (with TVFEM_EXPERIMENTS=1): the row-per-wave transfers of
+// one fine node per lane instead of the x-pair kernels (measurements only)
+bool mg_rows_experiment() {
+  static const bool on = [] {
+    const char* v = experiment_env("TVFEM_MG_ROWS");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
+}
+
 int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
 // restriction: one coarse node per thread (27-point gathers: the coarse
 // levels' few hundred blocks must not serialise rounds -- 4 nodes per thread
@@ -427,6 +564,17 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
   (void)fa;  // the restriction consumes a complete J x (k_cg_addfaces): see mg_level in tv_api.cpp
   const int64_t n = (int64_t)x.cn[0] * x.cn[1] * (x.c_ke - x.c_kb);
   if (n <= 0) return;
+  if (x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment()) {  // by rows, 16-byte fine pairs
+    const int nseg = (x.cn[0] + kPairSeg - 1) / kPairSeg;
+    const dim3 g((unsigned)((int64_t)x.cn[1] * (x.c_ke - x.c_kb) * nseg));
+    if (mask != nullptr)
+      hipLaunchKernelGGL(k_mg_restrict_pairs<true>, g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c,
+                         xc, nseg);
+    else
+      hipLaunchKernelGGL(k_mg_restrict_pairs<false>, g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c,
+                         xc, nseg);
+    return;
+  }
   if (x.coarse[0] && x.fn[0] >= 3) {  // by rows, lane-shared x gathers
     const int nseg = (x.cn[0] + kWave - 1) / kWave;
     const dim3 g((unsigned)((int64_t)x.cn[1] * (x.c_ke - x.c_kb) * nseg));
@@ -450,6 +598,12 @@ void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const do
                        hipStream_t s) {
   const int64_t n = (int64_t)x.fn[0] * x.fn[1] * (x.f_ke - x.f_kb);
   if (n <= 0) return;
+  if (x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment()) {  // by rows, 16-byte fine pairs
+    const int nseg = ((x.fn[0] + 1) / 2 + kPairSeg - 1) / kPairSeg;
+    const int64_t rows = (int64_t)x.fn[1] * (x.f_ke - x.f_kb);
+    hipLaunchKernelGGL(k_mg_prolong_pairs, dim3((unsigned)(rows * nseg)), dim3(kWave), 0, s, x, st, xf, xc, mask, nseg);
+    return;
+  }
   if (x.coarse[0] && x.fn[0] >= 3) {  // by rows, lane-shared x gathers
     const int nseg = (x.fn[0] + kWave - 1) / kWave;
     const int64_t rows = (int64_t)x.fn[1] * (x.f_ke - x.f_kb);

@@ -249,7 +249,10 @@ int tv_set_initial_condition(void* ctx, double T0);
 int tv_set_dirichlet(void* ctx, int enable, double value);
 int tv_sync(void* ctx);
 
-/* ---- operators (device pointers, owned T-dofs, length n_owned) ---------- */
+/* ---- operators (device pointers, owned T-dofs, length n_owned) ----------
+ * The context stream is non-blocking: these calls first wait for all work
+ * already queued on the device (hipDeviceSynchronize), so inputs written on
+ * another stream (e.g. torch's) before the call are complete when it reads them. */
 int tv_residual(void* ctx, const double* T_dev, double* F_dev);     /* F(T; T_prev) */
 int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev); /* J(T)·x      */
 int tv_jacobian_diag(void* ctx, double* d_dev);                       /* diag J(T)   */
