@@ -427,6 +427,105 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_pairs(MgXfer x, const PcgS
   }
 }
 
+// Prolongation by 2 x 2 blocks of fine rows (all three axes coarsened, one
+// partition): fine rows (2jb + a, 2kb + c) interpolate only from the coarse
+// rows (jb, jb + 1) x (kb, kb + 1) (the odd tail too), so a wave loads those
+// four coarse x-runs once for four fine rows -- 4 coarse loads per 4 x 128 fine
+// nodes instead of 16, and four 1 KB fine runs in flight per wave.
+__global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgState* __restrict__ st,
+                                                          double* __restrict__ xf, const double* __restrict__ xc,
+                                                          const double* __restrict__ mask, int nseg, int nbj) {
+  if (st != nullptr && st->done) return;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int blk = bid / nseg;
+  const int seg = bid - blk * nseg;
+  const int jb = blk % nbj, kb = blk / nbj;
+  const int nf = x.fn[0], cn = x.cn[0];
+  const int lane = (int)threadIdx.x;
+  const int c = seg * kPairSeg + lane;
+  const int cc = c < cn ? c : cn - 1;
+  const int i0 = 2 * c, i1 = 2 * c + 1;
+  const bool has0 = lane < kPairSeg && i0 < nf, has1 = lane < kPairSeg && i1 < nf;
+  const bool tail = i1 == nf - 1 && ((nf - 1) & 1);
+  const int i1c = has1 ? i1 : 0;
+  const double wl = x.pw[0][2 * i1c], wr = x.pw[0][2 * i1c + 1];
+  const int64_t cpl = (int64_t)cn * x.cn[1];
+  const int jc1 = min(jb + 1, x.cn[1] - 1), kc1 = min(kb + 1, x.cn[2] - 1);
+  double v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
+    v[q] = xc[cc + (int64_t)cn * jcq + cpl * kcq];
+  }
+  // per fine row of the block: its weights on coarse rows jb / jb + 1 (kb / kb + 1)
+  double wy[2][2], wz[2][2];
+  bool rj[2], rk[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int j = 2 * jb + a, k = 2 * kb + a;
+    rj[a] = j < x.fn[1];
+    rk[a] = k < x.f_ke;
+    wy[a][0] = wy[a][1] = wz[a][0] = wz[a][1] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      if (rj[a]) {
+        const int ci = x.pi[1][2 * j + e];
+        const double w = x.pw[1][2 * j + e];
+        wy[a][0] += ci == jb ? w : 0.0;
+        wy[a][1] += ci == jb + 1 ? w : 0.0;
+      }
+      if (rk[a]) {
+        const int ci = x.pi[2][2 * k + e];
+        const double w = x.pw[2][2 * k + e];
+        wz[a][0] += ci == kb ? w : 0.0;
+        wz[a][1] += ci == kb + 1 ? w : 0.0;
+      }
+    }
+  }
+  int64_t f[4];
+  d2a8 xo[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int a = r & 1, b = r >> 1;
+    f[r] = (int64_t)i0 + (int64_t)nf * ((2 * jb + a) + (int64_t)x.fn[1] * (2 * kb + b));
+    xo[r] = d2a8{0.0, 0.0};
+    if (rj[a] && rk[b]) {
+      if (has1) xo[r] = ld_pair(xf + f[r]);
+      else if (has0) xo[r].x = xf[f[r]];
+    }
+  }
+  // x-interpolated coarse values: even fine node (coarse c), odd (c, c + 1)
+  double e0[4], e1[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double vr = shl1(v[q]);
+    e0[q] = v[q];
+    e1[q] = tail ? vr : wl * v[q] + wr * vr;
+  }
+  if (!has0) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int a = r & 1, b = r >> 1;
+    if (!(rj[a] && rk[b])) continue;
+    const double w00 = wz[b][0] * wy[a][0], w01 = wz[b][0] * wy[a][1];
+    const double w10 = wz[b][1] * wy[a][0], w11 = wz[b][1] * wy[a][1];
+    const double a0 = (w00 * e0[0] + w01 * e0[1]) + (w10 * e0[2] + w11 * e0[3]);
+    const double a1 = (w00 * e1[0] + w01 * e1[1]) + (w10 * e1[2] + w11 * e1[3]);
+    if (has1) {
+      d2a8 out = {xo[r].x + a0, xo[r].y + a1};
+      if (mask != nullptr) {
+        const d2a8 m = ld_pair(mask + f[r]);
+        if (m.x == 0.0) out.x = 0.0;
+        if (m.y == 0.0) out.y = 0.0;
+      }
+      *reinterpret_cast<d2a8*>(xf + f[r]) = out;
+    } else {
+      const bool off = mask != nullptr && mask[f[r]] == 0.0;
+      xf[f[r]] = off ? 0.0 : xo[r].x + a0;
+    }
+  }
+}
+
 template <int MODE, bool FACES>
 __global__ __launch_bounds__(kBlock) void k_mg_jacobi(int64_t n, const PcgState* __restrict__ st,
                                                       const double* __restrict__ b, const double* __restrict__ w,
@@ -550,6 +649,15 @@ bool mg_rows_experiment() {
   return on;
 }
 
+// TVFEM_MG_PAIRS=1: the one-row-per-wave pair prolongation instead of the 2 x 2 row blocks
+bool mg_pairs_experiment() {
+  static const bool on = [] {
+    const char* v = experiment_env("TVFEM_MG_PAIRS");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
+}
+
 int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
 // restriction: one coarse node per thread (27-point gathers: the coarse
 // levels' few hundred blocks must not serialise rounds -- 4 nodes per thread
@@ -598,6 +706,14 @@ void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const do
                        hipStream_t s) {
   const int64_t n = (int64_t)x.fn[0] * x.fn[1] * (x.f_ke - x.f_kb);
   if (n <= 0) return;
+  if (x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0 && !mg_rows_experiment() &&
+      !mg_pairs_experiment()) {  // 2 x 2 blocks of fine rows, 16-byte fine pairs
+    const int nseg = ((x.fn[0] + 1) / 2 + kPairSeg - 1) / kPairSeg;
+    const int nbj = (x.fn[1] + 1) / 2, nbk = (x.f_ke + 1) / 2;
+    hipLaunchKernelGGL(k_mg_prolong_blk, dim3((unsigned)((int64_t)nbj * nbk * nseg)), dim3(kWave), 0, s, x, st, xf, xc,
+                       mask, nseg, nbj);
+    return;
+  }
   if (x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment()) {  // by rows, 16-byte fine pairs
     const int nseg = ((x.fn[0] + 1) / 2 + kPairSeg - 1) / kPairSeg;
     const int64_t rows = (int64_t)x.fn[1] * (x.f_ke - x.f_kb);
