@@ -5,8 +5,6 @@ tests/test_partition.py as `torch.distributed.run --nproc-per-node P`.
     --comm host   every rank on GPU 0, host-staged transport over gloo (one GPU)
     --comm rccl   rank r on GPU r (LOCAL_RANK), RCCL send/recv + allreduce over
                   xGMI: the production transport (needs P GPUs)
-    --comm rccl0  the RCCL transport with every rank on GPU 0 (one-GPU rehearsal
-                  of the RCCL code path, where RCCL accepts ranks sharing a device)
 """
 import argparse
 import json
@@ -56,7 +54,7 @@ def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--comm", choices=["host", "rccl", "rccl0"], default="host")
+    ap.add_argument("--comm", choices=["host", "rccl"], default="host")
     ap.add_argument("--cells", default="10,30,5")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
@@ -69,10 +67,7 @@ def main():
     nc = [int(v) for v in a.cells.split(",")]
     mesh = box_mesh([2.0, 6.0, 1.0], nc)
     steps = a.steps
-    if a.comm == "rccl0":
-        loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=0,
-                       pcg=a.pcg, edit=a.edit)
-    elif a.comm == "rccl":
+    if a.comm == "rccl":
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
