@@ -135,7 +135,12 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
 // KSPCG update with an explicit residual (the V-cycle smooths against r):
 // r <- r - a (w + facet terms), dx <- dx + a p, and the V-cycle's first
 // pre-smoothing step from 0, x0 <- omega dinv r.  INIT: dx <- 0, x0 <- omega dinv r.
-template <bool FACES, bool INIT>
+// DXU (odd iterations): dx <- (dx + a_prev p_prev) + a p, the steps of this
+// and the previous iteration (both p buffers are live until the next matvec),
+// so the dx stream moves every second iteration only: 40 B per node on even
+// iterations, 72 on odd ones (56 mean, was 64); a solve of odd length ends
+// with k_dx_tail.  U nodes per thread and round, every load issued first.
+template <bool FACES, bool INIT, bool DXU>
 __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState* __restrict__ st,
                                                       const double* __restrict__ pA, const double* __restrict__ pB,
                                                       const double* __restrict__ w, FaceAdd fa,
@@ -144,19 +149,47 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
                                                       double* __restrict__ x0, int it_host) {
   if (st->done) return;
   const double a = INIT ? 0.0 : st->a;
+  const double ap = DXU ? st->a_prev : 0.0;
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
-    double rr = r[t];
-    if (INIT) {
-      dx[t] = 0.0;
-    } else {
-      double wt = ldc<true>(&w[t]);
-      if (FACES) wt += face_terms(fa, t);
-      rr -= a * wt;
-      r[t] = rr;
-      stc<true>(&dx[t], ldc<true>(&dx[t]) + a * ldc<true>(&p[t]));
+  const double* __restrict__ pp = (it_host & 1) ? pA : pB;
+  // v = {r, w, dinv, dx, p_prev, p}
+  auto load = [&](int64_t q, double (&v)[6]) {
+    v[0] = r[q];
+    v[2] = ldc<true>(&dinv[q]);
+    if (!INIT) v[1] = ldc<true>(&w[q]);
+    if (DXU) {
+      v[3] = ldc<true>(&dx[q]);
+      v[4] = ldc<true>(&pp[q]);
+      v[5] = ldc<true>(&p[q]);
     }
-    x0[t] = omega * ldc<true>(&dinv[t]) * rr;
+  };
+  auto node = [&](int64_t q, const double (&v)[6]) {
+    double rr = v[0];
+    if (INIT) {
+      dx[q] = 0.0;
+    } else {
+      double wt = v[1];
+      if (FACES) wt += face_terms(fa, q);
+      rr -= a * wt;
+      r[q] = rr;
+      if (DXU) stc<true>(&dx[q], (v[3] + ap * v[4]) + a * v[5]);
+    }
+    x0[q] = omega * v[2] * rr;
+  };
+  constexpr int U = 4;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  for (; t + (U - 1) * stride < n; t += U * stride) {
+    double v[U][6];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load(t + u * stride, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) node(t + u * stride, v[u]);
+  }
+  for (; t < n; t += stride) {
+    double v[6];
+    load(t, v);
+    node(t, v);
   }
 }
 
@@ -278,12 +311,18 @@ void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const dou
                       int it_host, int init, hipStream_t s) {
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
   const dim3 g(vec_blocks(n)), b(kBlock);
-  if (init)
-    hipLaunchKernelGGL((k_mg_update<false, true>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host);
-  else if (f.on)
-    hipLaunchKernelGGL((k_mg_update<true, false>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host);
-  else
-    hipLaunchKernelGGL((k_mg_update<false, false>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host);
+  const bool odd = (it_host & 1) != 0;
+#define TV_MGU(F, I, D) \
+  hipLaunchKernelGGL((k_mg_update<F, I, D>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host)
+  if (init) TV_MGU(false, true, false);
+  else if (f.on) {
+    if (odd) TV_MGU(true, false, true);
+    else TV_MGU(true, false, false);
+  } else {
+    if (odd) TV_MGU(false, false, true);
+    else TV_MGU(false, false, false);
+  }
+#undef TV_MGU
 }
 
 int launch_mg_post(int64_t n, const PcgState* st, const double* x0, const double* r, const double* w,
