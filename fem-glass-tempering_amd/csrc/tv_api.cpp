@@ -1111,6 +1111,16 @@ static void mg_level(Ctx* c, size_t l) {
   }
 }
 
+// TVFEM_MG_POST=split (with TVFEM_EXPERIMENTS=1): level 0's last J x and the
+// post-smoothing as two launches (k_cg_march + k_mg_post) instead of the fused march
+static bool mg_post_split() {
+  static const bool on = [] {
+    const char* v = experiment_env("TVFEM_MG_POST");
+    return v != nullptr && v[0] == 's';
+  }();
+  return on;
+}
+
 // level 0: x0 = omega dinv r is in c->mgx (k_mg_update); coarse correction,
 // post-smoothing into z with the (z.z, z.r) reduction tail
 static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
@@ -1136,6 +1146,12 @@ static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
     launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
     mg_level(c, 1);
     launch_mg_prolong(C.xf, c->st, c->mgx, C.x, mask, s);
+  }
+  // J x, post-smoothing and (z.z, z.r) in the march epilogue (+ the side-face pass)
+  if (!mg_post_split()) {
+    const int nrec = launch_cg_japply_post(c->cg, T, c->mgx, c->r, c->dinv, c->mg_omega0, c->z, c->st, c->partials,
+                                           tail, s);
+    if (nrec >= 0) return nrec;
   }
   launch_cg_japply_partial(c->cg, T, c->mgx, c->w, c->st, s);
   return launch_mg_post(n, c->st, c->mgx, c->r, c->w, &fa, c->dinv, c->mg_omega0, c->z, c->partials, tail, s);

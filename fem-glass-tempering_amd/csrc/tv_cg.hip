@@ -663,14 +663,21 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, const int64_t*
 // WPE: minimum waves per SIMD the register allocation must allow (8: <= 64
 // VGPRs, four 8-wave tiles per CU, at the price of a few spills)
 // PF: prefetch depth (planes whose loads are in flight while one is computed)
-template <int MODE, bool FUSEP, int R, int WPE, int PF>
+// POST (MODE_JAC, !FUSEP): the multigrid's level-0 post-smoothing in the
+// epilogue -- out = z = x + omega dinv (r - J x) instead of J x, with r and dinv
+// of the output plane in the prefetch ring, and (z.z, z.r) per tile as records
+// 2 tile, 2 tile + 1; the facet terms of the face workgroups (faces along the
+// march) are applied afterwards by k_mg_post_faces, which also runs the tail.
+template <int MODE, bool FUSEP, int R, int WPE, int PF, bool POST = false>
 __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cg_march(CgGrid g, const double* __restrict__ T,
                                                         const double* __restrict__ in0, const double* in1,
                                                         double* __restrict__ out, double* pout,
                                                         const PcgState* __restrict__ st,
                                                         double* __restrict__ partials, int nseg, int raxis,
                                                         int qchunk, RedTail rt, int nrec, int nmarch,
-                                                        FaceOff fo, int ffirst, int exp, int it_host) {
+                                                        FaceOff fo, int ffirst, int exp, int it_host,
+                                                        PostArgs pa) {
+  static_assert(!POST || (MODE == MODE_JAC && !FUSEP), "POST: plain Jacobian march only");
   stamp_start(rt);
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
   __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
@@ -705,7 +712,8 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   if (fidx >= 0) {
     if (exp & 16) return;  // timing experiment only (TVFEM_MARCH_EXP): no face work
     if (st != nullptr && st->done) return;
-    face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec, fidx, fo, fsm, red, it_host);
+    face_block<FUSEP, R>(g, T, in0, in1, pout, st, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx, fo,
+                         fsm, red, it_host);
     return;
   }
   const int lane = threadIdx.x & (kWave - 1);
@@ -803,6 +811,15 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     a0 = bload(rs0, o);
     a1 = TWO ? bload(rs1, o) : 0.0;
   };
+  // POST: r and dinv of the own row at plane L - 1 (the output plane of step L)
+  const buf_t rsr = mk_rsrc(pa.r, POST ? nbytes : 0u);
+  const buf_t rsd = mk_rsrc(pa.dinv, POST ? nbytes : 0u);
+  auto fetch_post = [&](int L, double& a_r, double& a_d) {
+    if (!POST) return;
+    const uint32_t o = vo_wr + plane_off(L - 1);
+    a_r = bload(rsr, o);
+    a_d = bload(rsd, o);
+  };
 
   auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
     v = a0;
@@ -818,10 +835,12 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   // so PF planes of loads are in flight while a plane is combined, exchanged
   // and computed
   double ra0[PF + 1], ra1[PF + 1], rh0[PF + 1], rh1[PF + 1];
+  double rr[PF + 1], rd[PF + 1];  // POST: r, dinv of the output plane
 #pragma unroll
   for (int s = 0; s < PF; ++s) {
     fetch(vo_own, q0 - 1 + s, ra0[s], ra1[s]);
     fetch(vo_halo, q0 - 1 + s, rh0[s], rh1[s]);
+    fetch_post(q0 - 1 + s, rr[s], rd[s]);
   }
   // the solver state is read only now, so its latency overlaps the prefetch;
   // once the PCG has converged every launch of the batch exits here
@@ -922,8 +941,8 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   //   us = My . x (mass), t = My . m + da Ky . x (m = x, or T - Tp - dt f for RES)
   double us_m = 0.0, us_c = 0.0, t_m = 0.0, t_c = 0.0;
   double xc = 0.0;  // own-row value of the centre plane (p of the output node)
-  double dot = 0.0;
-  auto step = [&](int L, double c0, double c1, double h0, double h1) {
+  double dot = 0.0, zz = 0.0, zr = 0.0;
+  auto step = [&](int L, double c0, double c1, double h0, double h1, double pr, double pd) {
     const int buf = L & 1;
     double v, vm;
     combine(vo_own, L, c0, c1, v, vm);
@@ -964,8 +983,15 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       double yb = y;
       if (fq0 && q == 0) yb += yq0;
       if (fq1 && q == nQ - 1) yb += yq1;
-      bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, yb);
-      if (MODE == MODE_JAC) dot += wr ? xc * yb : 0.0;
+      if (POST) {  // z = x + omega dinv (r - J x): the post-smoothing step (facet terms of the side faces later)
+        const double zq = xc + pa.omega * pd * (pr - yb);
+        bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, zq);
+        zz += wr ? zq * zq : 0.0;
+        zr += wr ? zq * pr : 0.0;
+      } else {
+        bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, yb);
+      }
+      if (MODE == MODE_JAC && !POST) dot += wr ? xc * yb : 0.0;
     }
     xc = x1;
     us_m = us_c; us_c = us_p;
@@ -979,8 +1005,29 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       const int sf = (s + PF) % (PF + 1);  // the set consumed one step ago
       fetch(vo_own, L + s + PF, ra0[sf], ra1[sf]);
       fetch(vo_halo, L + s + PF, rh0[sf], rh1[sf]);
-      step(L + s, ra0[s], ra1[s], rh0[s], rh1[s]);
+      fetch_post(L + s + PF, rr[sf], rd[sf]);
+      step(L + s, ra0[s], ra1[s], rh0[s], rh1[s], POST ? rr[s] : 0.0, POST ? rd[s] : 0.0);
     }
+  }
+  if (POST) {  // (z.z, z.r) records of the tile; k_mg_post_faces reduces them
+    zz = wave_sum(zz);
+    zr = wave_sum(zr);
+    if (lane == 0) {
+      red[wave] = zz;
+      fsm[wave] = zr;  // the face LDS is free after the prologue
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double a = 0.0, c = 0.0;
+#pragma unroll
+      for (int w = 0; w < R; ++w) {
+        a += red[w];
+        c += fsm[w];
+      }
+      store_partial(&partials[2 * (int64_t)bid], a);
+      store_partial(&partials[2 * (int64_t)bid + 1], c);
+    }
+    return;
   }
   if (MODE == MODE_JAC && partials != nullptr) {
     dot = wave_sum(dot);
@@ -1965,7 +2012,7 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
 #define TV_MARCH(RR, WW, PP)                                                                                  \
   hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, RR, WW, PP>), dim3(grid), dim3(RR * kWave), 0, s, g, T, in0, in1, \
                      out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first(), \
-                     march_exp(), it_host)
+                     march_exp(), it_host, PostArgs{})
     const int pf = march_pf();
     if (MODE == MODE_JAC && march_dma() && L.rows == 8) {
       hipLaunchKernelGGL((k_cg_march_dma<FUSEP, 8, 4>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1, out, pout,
@@ -2004,7 +2051,94 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
   return false;
 }
 
+// Facet terms of the face-workgroup faces (normal to storage axis 0 and to the
+// row axis) for the POST march: z <- z - omega dinv (facet terms) at those
+// nodes, and the changes of z.z and z.r as records rec0 + block (the march
+// tiles wrote records 0 .. rec0 - 1); the last block reduces all of them and
+// runs the KSPCG logic.  Nodes on both face families are visited once (the
+// row-axis faces skip i = 0 and i = n0 - 1; face_at sums every face of a node).
+__global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis, const double* __restrict__ r,
+                                                         const double* __restrict__ dinv, double omega,
+                                                         double* __restrict__ z, double* __restrict__ partials,
+                                                         int rec0, RedTail rt, const PcgState* __restrict__ st) {
+  if (st->done) return;  // uniform: a converged solve's queued launch
+  const int n0 = fa.n0, n1 = fa.n1, n2 = fa.n2;
+  const int64_t nA = 2 * (int64_t)n1 * n2;
+  const int nO = (raxis == 2) ? n1 : n2;  // the free axis of the row-axis faces besides x
+  const int64_t nB = 2 * (int64_t)(n0 - 2) * nO;
+  double a0 = 0.0, a1 = 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nA + nB; t += (int64_t)gridDim.x * kBlock) {
+    int i, j, k;
+    if (t < nA) {
+      const int64_t pl = (int64_t)n1 * n2;
+      const int side = (int)(t / pl);
+      const int64_t e = t - side * pl;
+      i = side ? n0 - 1 : 0;
+      j = (int)(e % n1);
+      k = (int)(e / n1);
+    } else {
+      const int64_t u = t - nA, pl = (int64_t)(n0 - 2) * nO;
+      const int side = (int)(u / pl);
+      const int64_t e = u - side * pl;
+      i = 1 + (int)(e % (n0 - 2));
+      const int o = (int)(e / (n0 - 2));
+      if (raxis == 2) {
+        j = o;
+        k = side ? n2 - 1 : 0;
+      } else {
+        k = o;
+        j = side ? n1 - 1 : 0;
+      }
+    }
+    const double add = face_at(fa, i, j, k);
+    const int64_t q = i + (int64_t)n0 * (j + (int64_t)n1 * k);
+    const double zo = z[q];
+    const double zn = zo - omega * dinv[q] * add;
+    z[q] = zn;
+    a0 += zn * zn - zo * zo;
+    a1 += (zn - zo) * r[q];
+  }
+  __shared__ double red[2][kBlock / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  if (lane == 0) {
+    red[0][wave] = a0;
+    red[1][wave] = a1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int w = threadIdx.x;
+    store_partial(&partials[2 * ((int64_t)rec0 + blockIdx.x) + w], (red[w][0] + red[w][1]) + (red[w][2] + red[w][3]));
+  }
+  fused_reduce_tail<2>(rt, rec0 + (int)gridDim.x);
+}
+
 }  // namespace
+
+int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
+                          double omega, double* z, const PcgState* st, double* partials, const RedTail* tail,
+                          hipStream_t s) {
+  const Launch L = plan(g, false);
+  // the production march configuration only (experiment switches fall back)
+  if (!L.march || L.rows != 8 || g.n0 < 3 || march_pf() != 2 || march_wpe() != 1 || march_dma() || march_exp() ||
+      g.k_begin != 0 || g.k_end != g.n2)
+    return -1;
+  const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
+  const int grid = L.blocks + fo.off[6];
+  const PostArgs pa{r, dinv, omega};
+  hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, 1, 2, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T, x,
+                     nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks, fo,
+                     face_first(), 0, 0, pa);
+  const FaceAdd fa = cg_face_add(g, 0);
+  const int nO = (L.raxis == 2) ? g.n1 : g.n2;
+  const int64_t nodes = 2 * (int64_t)g.n1 * g.n2 + 2 * (int64_t)(g.n0 - 2) * nO;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, 1024));
+  const RedTail rt = tail ? *tail : RedTail{};
+  hipLaunchKernelGGL(k_mg_post_faces, dim3(nb), dim3(kBlock), 0, s, fa, L.raxis, r, dinv, omega, z, partials,
+                     L.blocks, rt, st);
+  return L.blocks + nb;
+}
 
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }
 

@@ -31,6 +31,14 @@ enum { C_MLO = 0, C_MDI, C_MUP, C_KLO, C_KDI, C_KUP, C_HLO, C_HHI, C_NCOEF };
 // 0 is physical x (fastest), storage axis 2 is the partition axis (slowest);
 // local node index = i + n0*(j + n1*k).  Along axis 2 the local array holds the
 // owned planes plus one ghost plane towards each neighbouring partition.
+// Operands of the multigrid post-smoothing fused into the Jacobian march
+// (k_cg_march POST): z = x + omega dinv (r - J x)
+struct PostArgs {
+  const double* r;
+  const double* dinv;
+  double omega;
+};
+
 struct CgGrid {
   int n0, n1, n2;             // local node counts per storage axis (n2 incl. ghosts)
   int k_begin, k_end;         // owned planes along axis 2, local indexing
@@ -335,6 +343,14 @@ void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x,
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
                       int it_host, int init, hipStream_t s);
+// the same post-smoothing fused into the level-0 J x march (k_cg_march POST)
+// plus a pass over the side-face nodes for the face-workgroup facet terms
+// (k_mg_post_faces, which runs the reduction tail); z <- x + omega dinv (r - J x),
+// w untouched.  Returns the record count, or -1 where the march path does not
+// apply (the caller then runs J x + launch_mg_post)
+int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
+                          double omega, double* z, const PcgState* st, double* partials, const RedTail* tail,
+                          hipStream_t s);
 // z <- x0 + omega dinv (r - (w + facet terms)) (post-smoothing), (z.z, z.r) records + reduction tail;
 // returns the record count
 int launch_mg_post(int64_t n, const PcgState* st, const double* x0, const double* r, const double* w,
