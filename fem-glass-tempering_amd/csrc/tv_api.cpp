@@ -894,6 +894,17 @@ static int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out)
 
 static double mg_omega(double b) { return 2.0 / (1.1 * b); }
 
+// Coarse levels up to this many nodes run the x-row stencil kernel (facet terms
+// inline: one launch per J x instead of march + k_cg_addfaces, no FaceAdd in
+// the consumers); TVFEM_MG_ROWK=<nodes> overrides it (experiments, 0 = march)
+static int64_t mg_rows_kernel_nodes() {
+  static const int64_t v = [] {
+    const char* e = experiment_env("TVFEM_MG_ROWK");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  return v;
+}
+
 // the hierarchy below the fine grid (single partition, 3D CG1 marching path)
 // the CG1 level of the box given by X (single partition), its vectors and weight
 static int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da) {
@@ -906,6 +917,7 @@ static int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da)
   L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
   L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
   L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+  L.g.rows_kernel = L.n <= mg_rows_kernel_nodes() ? 1 : 0;
   for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
     void* p = nullptr;
     HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
@@ -1012,6 +1024,7 @@ static int mg_setup(Ctx* c) {
     L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
     L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
     L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+    L.g.rows_kernel = L.n <= mg_rows_kernel_nodes() ? 1 : 0;
     for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
       void* p = nullptr;
       HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_rows(CgGrid g, const double* __re
   constexpr bool D1 = (DIM <= 2);  // storage axis 1 degenerate
   constexpr bool D2 = (DIM == 1);  // storage axis 2 degenerate
   __shared__ double red[kBlock / kWave];
-  if (FUSEP && st->done) return;  // uniform over the grid
+  if (st != nullptr && st->done) return;  // uniform over the grid (a converged solve's queued launches)
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x >> 6;
   int seg, j, kp;
@@ -1948,7 +1948,7 @@ bool use_march(const CgGrid& g) {
   }
   // the marching kernel addresses the fields with 32-bit buffer offsets
   const int64_t bytes = (int64_t)g.n0 * g.n1 * g.n2 * 8;
-  return dim_of(g) == 3 && !g_force_rows && bytes < (int64_t)kBadOff;
+  return dim_of(g) == 3 && !g_force_rows && !g.rows_kernel && bytes < (int64_t)kBadOff;
 }
 
 int bnd_blocks(const CgGrid& g) {

@@ -63,6 +63,9 @@ struct CgGrid {
   double* ffbuf[2];
   int64_t ffoff[6];
   int64_t ffsize;
+  // 1: the x-row stencil kernel (k_cg_rows, facet terms inline) instead of the
+  // march on this 3D grid -- the multigrid's coarse levels (tv_api.cpp mg_setup)
+  int rows_kernel;
 };
 
 // Grid of the DG1 temperature space: cells per storage axis; dof layout is
