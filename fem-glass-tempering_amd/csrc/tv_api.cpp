@@ -69,6 +69,7 @@ struct MgLevel {
   int64_t* bnodes = nullptr;
   double* ffbuf[2] = {nullptr, nullptr};
   std::vector<void*> bufs;   // T, b, x, w, dinv and the transfer maps
+  bool dinv_interior = false;  // dinv holds the T-independent interior diagonal
 };
 
 struct Ctx {
@@ -88,6 +89,7 @@ struct Ctx {
   int Ncell_glob[3] = {0, 0, 0};
   int plane_begin = 0, plane_end = 0;  // owned global planes (CG) / cell layers (DG) along storage axis 2
   CgGrid cg{};
+  bool dinv_interior = false;  // dinv holds the T-independent interior diagonal (CG march path)
   DgGrid dg{};
   int64_t nT = 0, nS = 0;          // local dofs incl. ghosts
   int64_t ownT_off = 0, ownT_n = 0;
@@ -1098,7 +1100,8 @@ static void mg_prepare(Ctx* c, const double* T) {
       if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
     }
     else launch_mg_inject(L.xf, Tf, L.T, c->stream);
-    launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream);
+    launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream, L.dinv_interior);
+    L.dinv_interior = true;
     Tf = L.T;
   }
 }
@@ -1470,7 +1473,15 @@ static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
   double r0 = 0.0, rn = 0.0;
   op_residual(c, T, Tp, c->r);  // F(u)
   while (!conv && its < c->O.newton_max_it) {
-    if (!c->dggface) op_diag(c, T, c->dinv, 1);  // J(u) (matrix-free) + Jacobi PC setup (DG GMG: cell blocks)
+    if (!c->dggface) {  // J(u) (matrix-free) + Jacobi PC setup (DG GMG: cell blocks)
+      if (!c->um && c->fam_T == TV_CG) {
+        // the T-independent interior of dinv is written once; then the boundary nodes only
+        launch_cg_diag(c->cg, T, c->dinv, 1, c->stream, c->dinv_interior);
+        c->dinv_interior = true;
+      } else {
+        op_diag(c, T, c->dinv, 1);
+      }
+    }
     const bool dir = c->dir_on && c->fam_T == TV_CG;
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;

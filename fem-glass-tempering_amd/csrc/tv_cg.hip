@@ -2206,7 +2206,7 @@ int cg_cgs_records(const CgGrid& g) {
 
 bool cg_cgs_supported(const CgGrid& g) { return use_march(g); }
 
-void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s) {
+void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s, bool bnd_only) {
   const int64_t nown = (int64_t)g.n0 * g.n1 * (g.k_end - g.k_begin);
   int blocks = (int)std::min<int64_t>((nown + kBlock - 1) / kBlock, 4096);
   if (blocks <= 0) return;
@@ -2215,7 +2215,9 @@ void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, 
     case 2: hipLaunchKernelGGL((k_cg_diag<2, true>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert); break;
     default:
       if (use_march(g) && g.bnodes && g.n_bnodes > 0) {  // the boundary-node list of the marching path
-        hipLaunchKernelGGL((k_cg_diag<3, false>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
+        // off the boundary diag J = diag(M + dt alpha K) does not depend on T:
+        // bnd_only (the interior of dinv is already in place) rewrites the boundary nodes only
+        if (!bnd_only) hipLaunchKernelGGL((k_cg_diag<3, false>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);
         hipLaunchKernelGGL(k_cg_diag_bnd, dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, T, dinv, invert);
       } else {
         hipLaunchKernelGGL((k_cg_diag<3, true>), dim3(blocks), dim3(kBlock), 0, s, g, T, dinv, invert);

@@ -239,7 +239,9 @@ bool launch_cg_cgs(const CgGrid& g, bool init, const CgsBuffers& v, PcgState* st
                    hipStream_t s, const RedTail* tail, int it_host, const double* lag_sums);
 int cg_cgs_records(const CgGrid& g);
 bool cg_cgs_supported(const CgGrid& g);
-void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s);
+// bnd_only: only the physical-boundary nodes (3D marching path; the interior of
+// dinv, T-independent, is already in place from an earlier call with the same invert)
+void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s, bool bnd_only = false);
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes);
 
 void launch_dg_residual(const DgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
