@@ -2130,6 +2130,43 @@ int tv_jacobian_diag(void* ctx, double* d_dev) {
   return TV_OK;
 }
 
+int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !r_dev || !z_dev) return TV_ERR_ARG;
+  if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "tv_precond_apply: one partition only");
+  hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
+  const double* T = c->f[TV_F_T].ptr;
+  const int64_t n = c->nT;
+  hipStream_t s = c->stream;
+  // the PC setup of the Newton iteration at this T
+  if (!c->dggface) {
+    if (!c->um && c->fam_T == TV_CG) {
+      launch_cg_diag(c->cg, T, c->dinv, 1, s, c->dinv_interior);
+      c->dinv_interior = true;
+    } else {
+      op_diag(c, T, c->dinv, 1);
+    }
+  }
+  if (!c->mg_on) {
+    launch_mg_jacobi(n, nullptr, r_dev, nullptr, nullptr, c->dinv, 1.0, z_dev, 0, s);  // z = dinv .* r
+  } else {
+    PcgState h{};  // running state: the V-cycle's kernels skip work once a solve is done
+    HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, s));
+    mg_prepare(c, T);
+    HIPC(hipMemcpyAsync(c->r, r_dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    if (c->dggface)  // x0 = omega0 B^-1 r (cell blocks)
+      launch_dg_bsmooth(c->dg, c->st, c->r, nullptr, c->dggface, c->mg_omega0, c->mgx, 0, s);
+    else
+      launch_mg_jacobi(n, c->st, c->r, nullptr, nullptr, c->dinv, c->mg_omega0, c->mgx, 0, s);
+    mg_apply0(c, T, nullptr);
+    HIPC(hipMemcpyAsync(z_dev, c->z, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(s));
+  return TV_OK;
+}
+
 int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c) return TV_ERR_ARG;

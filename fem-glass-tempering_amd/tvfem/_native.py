@@ -32,7 +32,7 @@ EXPORTS = [
     "tv_abi_version", "tv_last_error", "tv_default_options", "tv_default_params", "tv_create", "tv_create_unstructured", "tv_partition_rcb", "tv_destroy",
     "tv_num_dofs", "tv_field_block_size", "tv_dof_coordinates", "tv_set_field", "tv_get_field",
     "tv_field_device_ptr", "tv_set_initial_condition", "tv_sync", "tv_residual", "tv_jacobian_apply",
-    "tv_jacobian_diag", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
+    "tv_jacobian_diag", "tv_precond_apply", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
     "tv_comm_get_unique_id", "tv_comm_init", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes", "tv_kernel_timing", "tv_kernel_stats",
     "tv_last_stats", "tv_comm_init_host", "tv_partition_layout", "tv_pcg_variant",
     "tv_set_dirichlet", "tv_output_open", "tv_output_write", "tv_output_close", "tv_xdmf_open",
@@ -126,6 +126,7 @@ def load_library():
         "tv_residual": (C.c_int, [vp, vp, vp]),
         "tv_jacobian_apply": (C.c_int, [vp, vp, vp]),
         "tv_jacobian_diag": (C.c_int, [vp, vp]),
+        "tv_precond_apply": (C.c_int, [vp, vp, vp]),
         "tv_solve_T": (C.c_int, [vp, ip, ip, ip]),
         "tv_visco_update": (C.c_int, [vp]),
         "tv_step": (C.c_int, [vp, C.c_int, ip, ip]),

@@ -27,6 +27,8 @@
  *                        by dolfinx assemble_matrix [3P] and applied by PETSc
  *                        MatMult inside KSPSolve — here matrix-free.
  *   tv_jacobian_diag     PETSc MatGetDiagonal (PC setup) [3P].
+ *   tv_precond_apply     PCApply of the KSP's preconditioner (PCGAMG, :343-346)
+ *                        [3P]: Jacobi, or one geometric-multigrid V-cycle.
  *   tv_solve_T           _solve_T (:384-391): dolfinx NewtonSolver.solve
  *                        (incremental criterion, rtol 1e-12, :334-337) with
  *                        KSP cg (:343) — Jacobi-PCG instead of GAMG (:344).
@@ -256,6 +258,11 @@ int tv_sync(void* ctx);
 int tv_residual(void* ctx, const double* T_dev, double* F_dev);     /* F(T; T_prev) */
 int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev); /* J(T)·x      */
 int tv_jacobian_diag(void* ctx, double* d_dev);                       /* diag J(T)   */
+/* z = B r with the context's preconditioner at the current T (tv_options.
+ * preconditioner): Jacobi z = r / diag J(T), or one V-cycle of the geometric
+ * multigrid -- exactly the operator the Krylov solve applies (the PC setup of
+ * the current T included).  Single partition; uses the solver's work vectors. */
+int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev);
 
 /* ---- solvers -------------------------------------------------------------- */
 int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged);
