@@ -374,7 +374,9 @@ void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const d
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
                          int check_done, hipStream_t s);
 void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s);
-void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s);
+// T <- T - dx, ||dx||^2 partials; with `tail` the last workgroup reduces them into tail->out
+void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s,
+                          const RedTail* tail = nullptr);
 int pcg_vec_blocks(int64_t n);
 void launch_fill(double* x, int64_t n, double v, hipStream_t s);
 

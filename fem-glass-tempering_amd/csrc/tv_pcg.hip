@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_dx_tail(int64_t n, const PcgState* _
 
 __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __restrict__ T,
                                                           const double* __restrict__ dx,
-                                                          double* __restrict__ partials) {
+                                                          double* __restrict__ partials, RedTail rt) {
   double acc[1] = {0.0};
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     const double d = dx[t];
@@ -234,6 +234,7 @@ __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __r
     acc[0] += d * d;
   }
   block_partials<1>(acc, partials);
+  fused_reduce_tail<1>(rt, gridDim.x);  // ||dx||^2 into rt.out (one partition: no separate reduce launch)
 }
 
 // One-block deterministic reduction of `n` partial records of width W, then
@@ -373,8 +374,10 @@ void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const d
   hipLaunchKernelGGL(k_dx_tail, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, (its - 1) & 1 ? pB : pA, dx);
 }
 
-void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s) {
-  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials);
+void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s,
+                          const RedTail* tail) {
+  const RedTail rt = tail ? *tail : RedTail{};
+  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials, rt);
 }
 
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
