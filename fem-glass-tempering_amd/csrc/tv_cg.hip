@@ -1876,6 +1876,8 @@ static int march_minblk() {  // workgroups the march grid is chunked up to (TVFE
   return v;
 }
 
+constexpr int kMarchSmallTiles = 256;  // one marching tile per CU
+
 static int march_minq() {  // fewest planes per marching chunk when splitting for occupancy (TVFEM_MARCH_MINQ)
   static int v = 0;
   if (!v) {
@@ -1973,6 +1975,10 @@ Launch plan(const CgGrid& g, bool ghosts) {
     int nchunks = 1;
     const int minblk = march_minblk();
     while ((int64_t)L.nseg * nrb * nchunks < minblk && nQ / (nchunks * 2) >= march_minq()) nchunks *= 2;
+    // tiny grids (fewer tiles than CUs): the march is a chain of plane steps, so
+    // shorter chunks down to 2 planes (C2 100x100x10: 26 -> 104 tiles, fused
+    // matvec 15.7 -> 10.1 us, step 1.29 -> 1.08 ms; measured)
+    while ((int64_t)L.nseg * nrb * nchunks < kMarchSmallTiles && nQ / (nchunks * 2) >= 2) nchunks *= 2;
     while ((nQ + nchunks - 1) / nchunks > kFaceChunk) ++nchunks;  // LDS coefficient stage bound
     L.qchunk = (nQ + nchunks - 1) / nchunks;
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
