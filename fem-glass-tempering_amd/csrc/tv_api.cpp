@@ -1112,18 +1112,35 @@ static void mg_prepare(Ctx* c, const double* T) {
 // a per-node facet term inside the 27-point gather measured slower); the one
 // before the post-smoothing leaves the facet terms of the faces along the
 // march to that pointwise consumer (FaceAdd).
+// The prolongation from coarse level index ci (c->mg[ci]) into its finer level:
+// where that level has a post-smoothing step (not the coarsest) and the
+// 2 x 2 block prolongation runs, the step is applied on the fly (CoarsePost)
+// and mg_level skipped its k_mg_jacobi launch.
+static void mg_prolong_from(Ctx* c, size_t ci, double* xf, const double* mask) {
+  MgLevel& C = c->mg[ci];
+  const bool smoothed = ci + 1 < c->mg.size() && mg_prolong_smooths(C.xf);
+  if (smoothed) {
+    const CoarsePost cp{C.b, C.w, C.dinv, C.omega, cg_face_add(C.g, 0)};
+    launch_mg_prolong(C.xf, c->st, xf, C.x, mask, c->stream, &cp);
+  } else {
+    launch_mg_prolong(C.xf, c->st, xf, C.x, mask, c->stream);
+  }
+}
+
 static void mg_level(Ctx* c, size_t l) {
   MgLevel& L = c->mg[l - 1];
   hipStream_t s = c->stream;
   if (l < c->mg.size()) {
-    MgLevel& C = c->mg[l];
+    const MgLevel& C = c->mg[l];
     const FaceAdd fa = cg_face_add(L.g, 0);
     launch_cg_japply(L.g, L.T, L.x, L.w, nullptr, nullptr, s, c->st);
     launch_mg_restrict(C.xf, c->st, L.b, L.w, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
     mg_level(c, l + 1);
-    launch_mg_prolong(C.xf, c->st, L.x, C.x, nullptr, s);
+    mg_prolong_from(c, l, L.x, nullptr);
     launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
-    launch_mg_jacobi(L.n, c->st, L.b, L.w, &fa, L.dinv, L.omega, L.x, 1, s);  // post-smoothing
+    // post-smoothing, unless the prolongation out of this level applies it (mg_prolong_from)
+    if (!mg_prolong_smooths(L.xf))
+      launch_mg_jacobi(L.n, c->st, L.b, L.w, &fa, L.dinv, L.omega, L.x, 1, s);
   }
 }
 
@@ -1161,7 +1178,7 @@ static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
     launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
     launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
     mg_level(c, 1);
-    launch_mg_prolong(C.xf, c->st, c->mgx, C.x, mask, s);
+    mg_prolong_from(c, 0, c->mgx, mask);
   }
   // J x, post-smoothing and (z.z, z.r) in the march epilogue (+ the side-face pass)
   if (!mg_post_split()) {

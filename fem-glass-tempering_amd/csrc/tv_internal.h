@@ -319,9 +319,20 @@ struct MgXfer {
 void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, const double* wf, const FaceAdd* fa,
                         const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
                         hipStream_t s);
-// xf <- xf + P xc on the fine owned nodes (mask as above: x stays 0 on excluded nodes)
+// The coarse level's post-smoothing operands: the prolongation applies
+// xc + omega dinv (b - (w + facet terms fa)) instead of xc
+struct CoarsePost {
+  const double* b;
+  const double* w;
+  const double* dinv;
+  double omega;
+  FaceAdd fa;
+};
+// xf <- xf + P xc on the fine owned nodes (mask as above: x stays 0 on excluded nodes);
+// cp != nullptr: the smoothed xc (only where mg_prolong_smooths(x))
 void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
-                       hipStream_t s);
+                       hipStream_t s, const CoarsePost* cp = nullptr);
+bool mg_prolong_smooths(const MgXfer& x);
 // mode 0: x <- omega dinv b ; mode 1: x <- x + omega dinv (b - (w + facet terms fa))    (damped Jacobi)
 void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
                       const double* dinv, double omega, double* x, int mode, hipStream_t s);

@@ -432,9 +432,15 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_pairs(MgXfer x, const PcgS
 // rows (jb, jb + 1) x (kb, kb + 1) (the odd tail too), so a wave loads those
 // four coarse x-runs once for four fine rows -- 4 coarse loads per 4 x 128 fine
 // nodes instead of 16, and four 1 KB fine runs in flight per wave.
+// SMOOTH: the coarse level's post-smoothing step, xc + omega dinv (b - (w +
+// facet terms)), is formed on the fly from its operands (CoarsePost) instead
+// of by a k_mg_jacobi launch that would write xc back (the prolongation is the
+// smoothed xc's only reader)
+template <bool SMOOTH>
 __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgState* __restrict__ st,
                                                           double* __restrict__ xf, const double* __restrict__ xc,
-                                                          const double* __restrict__ mask, int nseg, int nbj) {
+                                                          const double* __restrict__ mask, int nseg, int nbj,
+                                                          CoarsePost cp) {
   if (st != nullptr && st->done) return;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int blk = bid / nseg;
@@ -455,7 +461,12 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgSta
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
-    v[q] = xc[cc + (int64_t)cn * jcq + cpl * kcq];
+    const int64_t o = cc + (int64_t)cn * jcq + cpl * kcq;
+    v[q] = xc[o];
+    if (SMOOTH) {
+      const double wt = cp.w[o] + face_at(cp.fa, cc, jcq, kcq);
+      v[q] += cp.omega * cp.dinv[o] * (cp.b[o] - wt);
+    }
   }
   // per fine row of the block: its weights on coarse rows jb / jb + 1 (kb / kb + 1)
   double wy[2][2], wz[2][2];
@@ -649,6 +660,16 @@ bool mg_rows_experiment() {
   return on;
 }
 
+// TVFEM_MG_POSTSEP=1: coarse post-smoothing by its own k_mg_jacobi launch
+// instead of on the fly in the 2 x 2 block prolongation
+bool mg_postsep_experiment() {
+  static const bool on = [] {
+    const char* v = experiment_env("TVFEM_MG_POSTSEP");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
+}
+
 // TVFEM_MG_PAIRS=1: the one-row-per-wave pair prolongation instead of the 2 x 2 row blocks
 bool mg_pairs_experiment() {
   static const bool on = [] {
@@ -702,16 +723,27 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
                        dinv_c, omega_c, xc);
 }
 
+bool mg_prolong_blocks(const MgXfer& x) {
+  return x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0 && !mg_rows_experiment() &&
+         !mg_pairs_experiment();
+}
+
+bool mg_prolong_smooths(const MgXfer& x) { return mg_prolong_blocks(x) && !mg_postsep_experiment(); }
+
 void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
-                       hipStream_t s) {
+                       hipStream_t s, const CoarsePost* cp) {
   const int64_t n = (int64_t)x.fn[0] * x.fn[1] * (x.f_ke - x.f_kb);
   if (n <= 0) return;
-  if (x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0 && !mg_rows_experiment() &&
-      !mg_pairs_experiment()) {  // 2 x 2 blocks of fine rows, 16-byte fine pairs
+  if (cp != nullptr && !mg_prolong_smooths(x)) return;  // caller bug guard: never reached (mg_level checks first)
+  if (mg_prolong_blocks(x)) {  // 2 x 2 blocks of fine rows, 16-byte fine pairs
     const int nseg = ((x.fn[0] + 1) / 2 + kPairSeg - 1) / kPairSeg;
     const int nbj = (x.fn[1] + 1) / 2, nbk = (x.f_ke + 1) / 2;
-    hipLaunchKernelGGL(k_mg_prolong_blk, dim3((unsigned)((int64_t)nbj * nbk * nseg)), dim3(kWave), 0, s, x, st, xf, xc,
-                       mask, nseg, nbj);
+    if (cp != nullptr)
+      hipLaunchKernelGGL(k_mg_prolong_blk<true>, dim3((unsigned)((int64_t)nbj * nbk * nseg)), dim3(kWave), 0, s, x, st,
+                         xf, xc, mask, nseg, nbj, *cp);
+    else
+      hipLaunchKernelGGL(k_mg_prolong_blk<false>, dim3((unsigned)((int64_t)nbj * nbk * nseg)), dim3(kWave), 0, s, x, st,
+                         xf, xc, mask, nseg, nbj, CoarsePost{});
     return;
   }
   if (x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment()) {  // by rows, 16-byte fine pairs
