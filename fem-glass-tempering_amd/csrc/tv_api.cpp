@@ -1488,17 +1488,26 @@ static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
   int its = 0, kits = 0;
   bool conv = false;
   double r0 = 0.0, rn = 0.0;
-  op_residual(c, T, Tp, c->r);  // F(u)
+  // F(u); on the CG march path the residual's boundary pass also rewrites the
+  // boundary rows of dinv for the same u once the interior is in place
+  auto residual = [&]() -> bool {
+    if (!c->um && c->fam_T == TV_CG && c->dinv_interior)
+      if (launch_cg_residual_diag(c->cg, T, Tp, c->r, c->dinv, c->stream)) return true;
+    op_residual(c, T, Tp, c->r);
+    return false;
+  };
+  bool dinv_fresh = residual();
   while (!conv && its < c->O.newton_max_it) {
     if (!c->dggface) {  // J(u) (matrix-free) + Jacobi PC setup (DG GMG: cell blocks)
       if (!c->um && c->fam_T == TV_CG) {
         // the T-independent interior of dinv is written once; then the boundary nodes only
-        launch_cg_diag(c->cg, T, c->dinv, 1, c->stream, c->dinv_interior);
+        if (!dinv_fresh) launch_cg_diag(c->cg, T, c->dinv, 1, c->stream, c->dinv_interior);
         c->dinv_interior = true;
       } else {
         op_diag(c, T, c->dinv, 1);
       }
     }
+    dinv_fresh = false;
     const bool dir = c->dir_on && c->fam_T == TV_CG;
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;
@@ -1530,7 +1539,7 @@ static int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     }
     // dolfinx assembles F after every update; in the incremental criterion that
     // last F is never read, so it is assembled only when another iteration follows.
-    if (!conv && its < c->O.newton_max_it) op_residual(c, T, Tp, c->r);
+    if (!conv && its < c->O.newton_max_it) dinv_fresh = residual();
   }
   HIPC(hipGetLastError());
   c->last_newton = its;

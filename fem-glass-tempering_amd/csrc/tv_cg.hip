@@ -1854,11 +1854,14 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
 // and the matching p.w correction for the PCG dot product.  For the fused PCG
 // matvec the input is the freshly written p (buffer selected from st->it).
 template <int MODE, bool FUSEP>
+// dinv != nullptr (residual of the Newton loop): also the inverse Jacobian
+// diagonal at the boundary nodes for the same T (k_cg_diag_bnd's work, one
+// launch fewer per Newton iteration)
 __global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t* __restrict__ bnodes, int64_t nb,
                                                         const double* __restrict__ T, const double* in0,
                                                         const double* pB, double* __restrict__ out,
                                                         const PcgState* __restrict__ st,
-                                                        double* __restrict__ partials) {
+                                                        double* __restrict__ partials, double* __restrict__ dinv) {
   __shared__ double red[kBlock / kWave];
   if (FUSEP && st->done) return;
   const double* x = in0;
@@ -1878,6 +1881,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t*
     }
     out[n] += acc;
     if (MODE == MODE_JAC) dot += x[n] * acc;
+    if (MODE == MODE_RES && dinv != nullptr) dinv[n] = 1.0 / diag_value<3, true>(g, T, n);
   }
   if (MODE == MODE_JAC && partials != nullptr) {
     dot = wave_sum(dot);
@@ -2036,7 +2040,7 @@ Launch plan(const CgGrid& g, bool ghosts) {
 template <int MODE, bool FUSEP>
 bool launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
                  double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s,
-                 const RedTail* tail = nullptr, int it_host = 0, bool addfaces = true) {
+                 const RedTail* tail = nullptr, int it_host = 0, bool addfaces = true, double* dinv_bnd = nullptr) {
   const Launch L = plan(g, ghosts);
   if (L.blocks <= 0) return false;
   if (L.march) {
@@ -2071,7 +2075,7 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     if (g.n_bnodes > 0) {
       hipLaunchKernelGGL((k_cg_boundary<MODE, FUSEP>), dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, g.bnodes,
                          g.n_bnodes, T, FUSEP ? in1 : in0, pout, out, st,
-                         partials ? partials + L.blocks : nullptr);
+                         partials ? partials + L.blocks : nullptr, dinv_bnd);
     }
     return false;
   }
@@ -2199,6 +2203,13 @@ FaceAdd cg_face_add(const CgGrid& g, int64_t t_off) {
 
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
   launch_rows<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, false, s);
+}
+
+bool launch_cg_residual_diag(const CgGrid& g, const double* T, const double* Tp, double* F, double* dinv,
+                             hipStream_t s) {
+  if (!use_march(g) || !g.bnodes || g.n_bnodes <= 0) return false;
+  launch_rows<MODE_RES, false>(g, T, T, Tp, F, nullptr, nullptr, nullptr, false, s, nullptr, 0, true, dinv);
+  return true;
 }
 
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,

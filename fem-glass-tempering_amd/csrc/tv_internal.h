@@ -203,6 +203,11 @@ int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, do
 
 // ---- kernel launchers (tv_cg.hip, tv_dg.hip, tv_visco.hip, tv_pcg.hip) ----
 void launch_cg_residual(const CgGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
+// the residual plus the boundary rows of dinv = 1 / diag J(T) in its boundary
+// pass (3D marching path; the T-independent interior of dinv must already be
+// in place).  Returns false (nothing launched) where that path does not apply.
+bool launch_cg_residual_diag(const CgGrid& g, const double* T, const double* Tp, double* F, double* dinv,
+                             hipStream_t s);
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s, const PcgState* st = nullptr);
 // returns true when the launch ends with the in-kernel reduction tail (the
