@@ -360,7 +360,8 @@ void launch_mg_scale(int64_t n, const double* y, double a, double* x, hipStream_
 void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
                               hipStream_t s);
 // level 0 of the PCG (tv_pcg.hip): r <- r - a (w + facet terms), dx <- dx + a p,
-// x0 <- omega dinv r (the V-cycle's pre-smoothing from 0); init: dx <- 0, x0 <- omega dinv r
+// x0 <- omega dinv r (the V-cycle's pre-smoothing from 0); init: x0 <- omega dinv r (dx is
+// assigned by iteration 1 / launch_mg_dx_finish)
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
                       int it_host, int init, hipStream_t s);
@@ -385,6 +386,10 @@ void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* 
 // iteration (the step the pairwise dx update has not applied yet)
 void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, int its,
                         hipStream_t s);
+// end of a multigrid solve (k_mg_update leaves dx unset until iteration 1
+// assigns it): its 0 -> dx = 0, its 1 -> dx = a p, else launch_pcg_dx_tail
+void launch_mg_dx_finish(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, int its,
+                         hipStream_t s);
 // one-block deterministic reduce of n records of width W (<= 2) into out[W];
 // kind: 0 none, 1 PCG init logic, 2 PCG p.w logic, 3 PCG update logic
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,

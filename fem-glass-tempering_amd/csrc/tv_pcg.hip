@@ -140,7 +140,10 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
 // so the dx stream moves every second iteration only: 40 B per node on even
 // iterations, 72 on odd ones (56 mean, was 64); a solve of odd length ends
 // with k_dx_tail.  U nodes per thread and round, every load issued first.
-template <bool FACES, bool INIT, bool DXU>
+// FIRST (iteration 1, the first DXU one): dx is assigned, not accumulated, so
+// the init pass does not have to zero it (mg_dx_finish covers solves of 0 / 1
+// iterations)
+template <bool FACES, bool INIT, bool DXU, bool FIRST = false>
 __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState* __restrict__ st,
                                                       const double* __restrict__ pA, const double* __restrict__ pB,
                                                       const double* __restrict__ w, FaceAdd fa,
@@ -158,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
     v[2] = ldc<true>(&dinv[q]);
     if (!INIT) v[1] = ldc<true>(&w[q]);
     if (DXU) {
-      v[3] = ldc<true>(&dx[q]);
+      v[3] = FIRST ? 0.0 : ldc<true>(&dx[q]);
       v[4] = ldc<true>(&pp[q]);
       v[5] = ldc<true>(&p[q]);
     }
@@ -166,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
   auto node = [&](int64_t q, const double (&v)[6]) {
     double rr = v[0];
     if (INIT) {
-      dx[q] = 0.0;
+      // dx is left alone: iteration 1 assigns it (FIRST)
     } else {
       double wt = v[1];
       if (FACES) wt += face_terms(fa, q);
@@ -313,15 +316,18 @@ void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const dou
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
   const dim3 g(vec_blocks(n)), b(kBlock);
   const bool odd = (it_host & 1) != 0;
-#define TV_MGU(F, I, D) \
-  hipLaunchKernelGGL((k_mg_update<F, I, D>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host)
-  if (init) TV_MGU(false, true, false);
+  const bool first = it_host == 1;
+#define TV_MGU(F, I, D, FI) \
+  hipLaunchKernelGGL((k_mg_update<F, I, D, FI>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host)
+  if (init) TV_MGU(false, true, false, false);
   else if (f.on) {
-    if (odd) TV_MGU(true, false, true);
-    else TV_MGU(true, false, false);
+    if (first) TV_MGU(true, false, true, true);
+    else if (odd) TV_MGU(true, false, true, false);
+    else TV_MGU(true, false, false, false);
   } else {
-    if (odd) TV_MGU(false, false, true);
-    else TV_MGU(false, false, false);
+    if (first) TV_MGU(false, false, true, true);
+    else if (odd) TV_MGU(false, false, true, false);
+    else TV_MGU(false, false, false, false);
   }
 #undef TV_MGU
 }
@@ -366,6 +372,23 @@ void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* 
     default: TV_UPD(true, 7, true);
   }
 #undef TV_UPD
+}
+
+__global__ __launch_bounds__(kBlock) void k_dx_set(int64_t n, const PcgState* __restrict__ st,
+                                                  const double* __restrict__ p, double* __restrict__ dx) {
+  const double a = p != nullptr ? st->a : 0.0;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
+    dx[t] = p != nullptr ? a * p[t] : 0.0;
+}
+
+void launch_mg_dx_finish(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, int its,
+                         hipStream_t s) {
+  if (its == 0)  // converged at the init: dx = 0
+    hipLaunchKernelGGL(k_dx_set, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, nullptr, dx);
+  else if (its == 1)  // iteration 0 only: dx was never assigned
+    hipLaunchKernelGGL(k_dx_set, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, dx);
+  else
+    launch_pcg_dx_tail(n, st, pA, pB, dx, its, s);
 }
 
 void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, int its,
