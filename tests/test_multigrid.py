@@ -333,3 +333,34 @@ def test_gmg_vcycle_operator_matches_numpy_restatement(case):
     assert sym < 1e-12, sym
     assert r @ z_r > 0.0
     p.close()
+
+
+@pytest.mark.gpu
+def test_gmg_zero_residual_step():
+    """T_0 = T_ambient = 0 and f = 0: F(T_0) = 0 exactly, so every Krylov solve
+    converges at its init (0 iterations) and dx must be exactly 0
+    (launch_mg_dx_finish: the init pass leaves dx to iteration 1); T stays 0 and
+    the Newton counts equal the oracle's (2 per step)."""
+    _torch()
+    axes = CASES["plate"]
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    mp["T_0"] = 0.0
+    mp["T_ambient"] = 0.0
+    mp["f"] = 0.0
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    cfg = {"T": CG, "sigma": CG}
+    dev = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, mp, verbose=False, part_axis=2,
+                             preconditioner="gmg")
+    ref = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), 0.1, cfg, mp, linear="pcg")
+    dev.setup()
+    ref.setup()
+    for _ in range(2):
+        dev.solve_timestep()
+        ref.solve_timestep()
+        assert dev.last_krylov_iterations == 0
+        assert dev.last_newton_iterations == ref.newton_history[-1][0]
+        assert ref.newton_history[-1][1] == 0
+        T = dev.functions_current["T"].x.array
+        assert np.array_equal(T, np.zeros_like(T)), np.abs(T).max()
+    dev.close()
