@@ -2134,13 +2134,14 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
         j = side ? n1 - 1 : 0;
       }
     }
-    const double add = face_at(fa, i, j, k);
     const int64_t q = i + (int64_t)n0 * (j + (int64_t)n1 * k);
-    const double zo = z[q];
-    const double zn = zo - omega * dinv[q] * add;
+    // the node's three loads first, independent of the face lookups (one round trip)
+    const double zo = z[q], dq = dinv[q], rq = r[q];
+    const double add = face_at(fa, i, j, k);
+    const double zn = zo - omega * dq * add;
     z[q] = zn;
     a0 += zn * zn - zo * zo;
-    a1 += (zn - zo) * r[q];
+    a1 += (zn - zo) * rq;
   }
   __shared__ double red[2][kBlock / kWave];
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
