@@ -1133,8 +1133,13 @@ static void mg_level(Ctx* c, size_t l) {
   if (l < c->mg.size()) {
     const MgLevel& C = c->mg[l];
     const FaceAdd fa = cg_face_add(L.g, 0);
-    launch_cg_japply(L.g, L.T, L.x, L.w, nullptr, nullptr, s, c->st);
-    launch_mg_restrict(C.xf, c->st, L.b, L.w, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
+    if (fa.on && mg_restrict_folds_faces(C.xf)) {  // the restriction adds the facet terms (no k_cg_addfaces)
+      launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
+      launch_mg_restrict(C.xf, c->st, L.b, L.w, &fa, nullptr, C.b, C.dinv, C.omega, C.x, s);
+    } else {
+      launch_cg_japply(L.g, L.T, L.x, L.w, nullptr, nullptr, s, c->st);
+      launch_mg_restrict(C.xf, c->st, L.b, L.w, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
+    }
     mg_level(c, l + 1);
     mg_prolong_from(c, l, L.x, nullptr);
     launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
@@ -1142,6 +1147,16 @@ static void mg_level(Ctx* c, size_t l) {
     if (!mg_prolong_smooths(L.xf))
       launch_mg_jacobi(L.n, c->st, L.b, L.w, &fa, L.dinv, L.omega, L.x, 1, s);
   }
+}
+
+// TVFEM_MG_FOLD0=1 (with TVFEM_EXPERIMENTS=1): level 0's facet terms added by the
+// restriction too, as on the coarse levels (instead of k_cg_addfaces)
+static bool mg_fold0() {
+  static const bool on = [] {
+    const char* v = experiment_env("TVFEM_MG_FOLD0");
+    return v != nullptr && v[0] == '1';
+  }();
+  return on;
 }
 
 // TVFEM_MG_POST=split (with TVFEM_EXPERIMENTS=1): level 0's last J x and the
@@ -1175,8 +1190,13 @@ static int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
   const FaceAdd fa = cg_face_add(c->cg, 0);
   if (!c->mg.empty()) {
     MgLevel& C = c->mg[0];
-    launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
-    launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
+    if (mg_fold0() && fa.on && mg_restrict_folds_faces(C.xf)) {
+      launch_cg_japply_partial(c->cg, T, c->mgx, c->w, c->st, s);
+      launch_mg_restrict(C.xf, c->st, c->r, c->w, &fa, mask, C.b, C.dinv, C.omega, C.x, s);
+    } else {
+      launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+      launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
+    }
     mg_level(c, 1);
     mg_prolong_from(c, 0, c->mgx, mask);
   }

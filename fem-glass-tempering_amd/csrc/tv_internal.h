@@ -338,6 +338,9 @@ struct CoarsePost {
 void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
                        hipStream_t s, const CoarsePost* cp = nullptr);
 bool mg_prolong_smooths(const MgXfer& x);
+// launch_mg_restrict adds the facet terms of a FaceAdd itself (else the caller
+// must hand it a complete J x)
+bool mg_restrict_folds_faces(const MgXfer& x);
 // mode 0: x <- omega dinv b ; mode 1: x <- x + omega dinv (b - (w + facet terms fa))    (damped Jacobi)
 void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
                       const double* dinv, double omega, double* x, int mode, hipStream_t s);

@@ -318,13 +318,17 @@ __device__ __forceinline__ d2a8 ld_pair(const double* p) { return *reinterpret_c
 // node I = 63 seg - 1 + l (lane 0 = the halo lane whose right fine node is
 // lane 1's left neighbour).  A lane whose fine centre is the row's last node
 // (even cell count, or the odd tail) loads that node alone; its right weight is 0.
-template <bool MASK>
+// FACES: wf is a partial J x (k_cg_march without k_cg_addfaces); the facet
+// terms of the face-workgroup faces (fa) are added here, on the boundary rows
+// (wave-uniform test) and the two x-boundary lanes only -- one launch fewer per
+// coarse level (bitwise the same r - (w + faces) as with k_cg_addfaces)
+template <bool MASK, bool FACES = false>
 __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const PcgState* __restrict__ st,
                                                              const double* __restrict__ bf,
                                                              const double* __restrict__ wf,
                                                              const double* __restrict__ mask, double* __restrict__ bc,
                                                              const double* __restrict__ dinv_c, double omega_c,
-                                                             double* __restrict__ xc, int nseg) {
+                                                             double* __restrict__ xc, int nseg, FaceAdd fa) {
   if (st != nullptr && st->done) return;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int row = bid / nseg;
@@ -344,9 +348,17 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
   for (int q = 0; q < 9; ++q) {
     const int c = q / 3, b = q % 3;
     wq[q] = x.rw[2][3 * K + c] * x.rw[1][3 * J + b];
-    const int64_t f = (int64_t)x.ri[1][3 * J + b] * nf + fpl * x.ri[2][3 * K + c] + f1;
+    const int fj = x.ri[1][3 * J + b], fk = x.ri[2][3 * K + c];
+    const int64_t f = (int64_t)fj * nf + fpl * fk + f1;
     if (pair) {
-      const d2a8 r = ld_pair(bf + f), w = ld_pair(wf + f);
+      const d2a8 r = ld_pair(bf + f);
+      d2a8 w = ld_pair(wf + f);
+      if (FACES) {
+        const bool rowface = (fa.ff[2] && fj == 0) || (fa.ff[3] && fj == fa.n1 - 1) || (fa.ff[4] && fk == 0) ||
+                             (fa.ff[5] && fk == fa.n2 - 1);  // wave-uniform
+        if (rowface || f1 == 0) w.x += face_at(fa, f1, fj, fk);
+        if (rowface || f1 + 1 == nf - 1) w.y += face_at(fa, f1 + 1, fj, fk);
+      }
       dc[q] = r.x - w.x;
       dr[q] = r.y - w.y;
       if (MASK) {
@@ -355,7 +367,9 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
         if (m.y == 0.0) dr[q] = 0.0;
       }
     } else {
-      double d = bf[f] - wf[f];
+      double wt = wf[f];
+      if (FACES) wt += face_at(fa, f1, fj, fk);  // the row's last node: an x-face node
+      double d = bf[f] - wt;
       if (MASK && mask[f] == 0.0) d = 0.0;
       dc[q] = dr[q] = d;
     }
@@ -690,18 +704,26 @@ int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kBlock - 1) /
 void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, const double* wf, const FaceAdd* fa,
                         const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
                         hipStream_t s) {
-  (void)fa;  // the restriction consumes a complete J x (k_cg_addfaces): see mg_level in tv_api.cpp
+  // fa (on): wf lacks the face-workgroup facet terms, added here (only where
+  // mg_restrict_folds_faces(x): the caller checks, see mg_level in tv_api.cpp)
+  const bool faces = fa != nullptr && fa->on;
   const int64_t n = (int64_t)x.cn[0] * x.cn[1] * (x.c_ke - x.c_kb);
   if (n <= 0) return;
-  if (x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment()) {  // by rows, 16-byte fine pairs
+  if (mg_restrict_folds_faces(x)) {  // by rows, 16-byte fine pairs
     const int nseg = (x.cn[0] + kPairSeg - 1) / kPairSeg;
     const dim3 g((unsigned)((int64_t)x.cn[1] * (x.c_ke - x.c_kb) * nseg));
-    if (mask != nullptr)
-      hipLaunchKernelGGL(k_mg_restrict_pairs<true>, g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c,
-                         xc, nseg);
-    else
-      hipLaunchKernelGGL(k_mg_restrict_pairs<false>, g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c,
-                         xc, nseg);
+    const FaceAdd f = faces ? *fa : FaceAdd{};
+#define TV_RP(M, F) \
+  hipLaunchKernelGGL((k_mg_restrict_pairs<M, F>), g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c, xc, \
+                     nseg, f)
+    if (mask != nullptr) {
+      if (faces) TV_RP(true, true);
+      else TV_RP(true, false);
+    } else {
+      if (faces) TV_RP(false, true);
+      else TV_RP(false, false);
+    }
+#undef TV_RP
     return;
   }
   if (x.coarse[0] && x.fn[0] >= 3) {  // by rows, lane-shared x gathers
@@ -722,6 +744,8 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
     hipLaunchKernelGGL(k_mg_restrict<false>, dim3(xfer_blocks(n)), dim3(kBlock), 0, s, x, st, bf, wf, mask, bc,
                        dinv_c, omega_c, xc);
 }
+
+bool mg_restrict_folds_faces(const MgXfer& x) { return x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment(); }
 
 bool mg_prolong_blocks(const MgXfer& x) {
   return x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0 && !mg_rows_experiment() &&
