@@ -1091,7 +1091,38 @@ static int mg_setup(Ctx* c) {
 
 // per Newton iteration: T injected down the hierarchy (DG: the vertex mean of
 // the cell-local values onto the CG level), coarse Jacobi diagonals
+static bool mg_prep_split();
+
 static void mg_prepare(Ctx* c, const double* T) {
+  // after the first call (dinv interiors in place): the CG levels below the
+  // base in two launches (launch_mg_prepare)
+  const size_t base = c->mg_dg ? 1 : 0;  // DG: level 1 is the vertex mean of the DG field
+  const size_t ncg = c->mg.size() - std::min(c->mg.size(), base);
+  bool ready = ncg > 0 && ncg <= (size_t)kMgPrepMax && !mg_prep_split();
+  for (size_t l = base; l < c->mg.size() && ready; ++l)
+    ready = c->mg[l].dinv_interior && cg_uses_march(c->mg[l].g) && c->mg[l].g.bnodes != nullptr;
+  if (ready) {
+    if (base == 1) {
+      MgLevel& L = c->mg[0];
+      launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+      if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
+      launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream, true);
+    }
+    MgPrep p{};
+    p.nlev = (int)ncg;
+    p.Tbase = base == 1 ? c->mg[0].T : T;
+    for (size_t i = 0; i < ncg; ++i) {
+      MgLevel& L = c->mg[base + i];
+      p.xf[i] = L.xf;
+      p.T[i] = L.T;
+      p.dinv[i] = L.dinv;
+      p.g[i] = L.g;
+      p.off_n[i + 1] = p.off_n[i] + (L.n + 63) / 64 * 64;
+      p.off_b[i + 1] = p.off_b[i] + (L.g.n_bnodes + 63) / 64 * 64;
+    }
+    launch_mg_prepare(p, c->stream);
+    return;
+  }
   const double* Tf = T;
   for (size_t l = 0; l < c->mg.size(); ++l) {
     MgLevel& L = c->mg[l];
@@ -1147,6 +1178,16 @@ static void mg_level(Ctx* c, size_t l) {
     if (!mg_prolong_smooths(L.xf))
       launch_mg_jacobi(L.n, c->st, L.b, L.w, &fa, L.dinv, L.omega, L.x, 1, s);
   }
+}
+
+// TVFEM_MG_PREP=split (with TVFEM_EXPERIMENTS=1): the per-level injection and
+// boundary-diagonal launches instead of the two merged ones
+static bool mg_prep_split() {
+  static const bool on = [] {
+    const char* v = experiment_env("TVFEM_MG_PREP");
+    return v != nullptr && v[0] == 's';
+  }();
+  return on;
 }
 
 // TVFEM_MG_FOLD0=1 (with TVFEM_EXPERIMENTS=1): level 0's facet terms added by the

@@ -2159,6 +2159,43 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
   fused_reduce_tail<2>(rt, rec0 + (int)gridDim.x);
 }
 
+// Injection of every coarse level straight from the base level (nested grids:
+// coarse node I of a level is fine node ri[3 I + 1] of the level above).  The
+// level of a thread is wave-uniform (64-padded ranges).
+__global__ __launch_bounds__(kBlock) void k_mg_prep_inject(MgPrep p) {
+  const int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  int l = 0;
+  while (l + 1 < p.nlev && t >= p.off_n[l + 1]) ++l;
+  l = __builtin_amdgcn_readfirstlane(l);
+  const MgXfer& x = p.xf[l];
+  const int64_t e = t - p.off_n[l];
+  const int64_t nc = (int64_t)x.cn[0] * x.cn[1] * x.cn[2];
+  if (e >= nc) return;
+  int c0 = (int)(e % x.cn[0]);
+  int c1 = (int)((e / x.cn[0]) % x.cn[1]);
+  int c2 = (int)(e / ((int64_t)x.cn[0] * x.cn[1]));
+  for (int m = l; m >= 0; --m) {  // down to the base level
+    const MgXfer& y = p.xf[m];
+    c0 = y.ri[0][3 * c0 + 1];
+    c1 = y.ri[1][3 * c1 + 1];
+    c2 = y.ri[2][3 * c2 + 1];
+  }
+  const MgXfer& b = p.xf[0];
+  p.T[l][e] = p.Tbase[c0 + (int64_t)b.fn[0] * (c1 + (int64_t)b.fn[1] * c2)];
+}
+
+__global__ __launch_bounds__(kBlock) void k_mg_prep_diag(MgPrep p) {
+  const int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  int l = 0;
+  while (l + 1 < p.nlev && t >= p.off_b[l + 1]) ++l;
+  l = __builtin_amdgcn_readfirstlane(l);
+  const CgGrid& g = p.g[l];
+  const int64_t e = t - p.off_b[l];
+  if (e >= g.n_bnodes) return;
+  const int64_t n = g.bnodes[e];
+  p.dinv[l][n] = 1.0 / diag_value<3, true>(g, p.T[l], n);
+}
+
 }  // namespace
 
 int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
@@ -2183,6 +2220,14 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
   hipLaunchKernelGGL(k_mg_post_faces, dim3(nb), dim3(kBlock), 0, s, fa, L.raxis, r, dinv, omega, z, partials,
                      L.blocks, rt, st);
   return L.blocks + nb;
+}
+
+bool cg_uses_march(const CgGrid& g) { return use_march(g); }
+
+void launch_mg_prepare(const MgPrep& p, hipStream_t s) {
+  const int64_t nn = p.off_n[p.nlev], nb = p.off_b[p.nlev];
+  if (nn > 0) hipLaunchKernelGGL(k_mg_prep_inject, dim3((unsigned)((nn + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p);
+  if (nb > 0) hipLaunchKernelGGL(k_mg_prep_diag, dim3((unsigned)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p);
 }
 
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }

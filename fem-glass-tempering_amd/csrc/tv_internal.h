@@ -345,6 +345,24 @@ bool mg_restrict_folds_faces(const MgXfer& x);
 void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
                       const double* dinv, double omega, double* x, int mode, hipStream_t s);
 void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t s);  // coarse T <- fine T
+// Per-Newton preparation of up to kMgPrepMax coarse CG levels in two launches
+// (instead of an injection and a boundary-diagonal launch per level): T of
+// every level injected straight from the base level's T through the composed
+// index maps, then the boundary rows of every level's dinv (the
+// T-independent interiors must already be in place)
+constexpr int kMgPrepMax = 4;  // keeps the kernel argument block near 2 KB
+struct MgPrep {
+  int nlev;
+  const double* Tbase;            // T of the level the first transfer starts from
+  MgXfer xf[kMgPrepMax];          // level i's transfer from level i - 1 (i = 0: from the base)
+  double* T[kMgPrepMax];
+  double* dinv[kMgPrepMax];
+  CgGrid g[kMgPrepMax];
+  int64_t off_n[kMgPrepMax + 1];  // 64-padded offsets of the levels' nodes / boundary nodes
+  int64_t off_b[kMgPrepMax + 1];
+};
+void launch_mg_prepare(const MgPrep& p, hipStream_t s);
+bool cg_uses_march(const CgGrid& g);  // the 3D marching kernels (not the x-row kernel) serve this grid
 // DG1 level 0 -> CG1 level 1 of the same box (3D; cells c0 x c1 x c2, DG dof
 // (l, cell) at l * ncell + cell, l = a + 2b + 4c over the storage axes):
 // restriction = sum of the cell-local copies at each vertex (P = injection of
