@@ -1315,9 +1315,9 @@ static int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   }
   *its = c->h_st[0].it;
   *reason = c->h_st[0].reason;
-  // CG level 0 updates dx in pairs of iterations (k_mg_update DXU): the last
-  // step of an odd-length solve (the DG block update applies every step)
-  if (!c->dggface) launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
+  // level 0 updates dx in pairs of iterations from iteration 1 on (k_mg_update /
+  // k_dg_bupdate DXU): solves of 0 / 1 iterations and the last step of an odd-length one
+  launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
   c->pcg_hint = std::max(1, c->h_st[0].it);
   if (c->ktime) {
     for (int it = 0; it < *its; it += c->kstride)

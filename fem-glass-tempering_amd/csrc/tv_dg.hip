@@ -823,7 +823,10 @@ __global__ __launch_bounds__(kBlock) void k_dg_bsmooth(DgGrid g, const PcgState*
 
 // KSPCG update with the explicit residual for the DG multigrid: r <- r - a w,
 // dx <- dx + a p, x0 <- omega B^-1 r (INIT: dx <- 0, x0 <- omega B^-1 r)
-template <bool INIT>
+// dx moves in pairs of iterations as in k_mg_update: DXU (odd iterations)
+// dx <- (dx + a_prev p_prev) + a p, FIRST (iteration 1) assigns it, so the
+// init pass leaves dx alone (launch_mg_dx_finish ends the solve)
+template <bool INIT, bool DXU = false, bool FIRST = false>
 __global__ __launch_bounds__(kBlock) void k_dg_bupdate(DgGrid g, const PcgState* __restrict__ st,
                                                        const double* __restrict__ pA, const double* __restrict__ pB,
                                                        const double* __restrict__ w, const double* __restrict__ gface,
@@ -832,19 +835,23 @@ __global__ __launch_bounds__(kBlock) void k_dg_bupdate(DgGrid g, const PcgState*
   const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
   if (st->done) return;
   const double a = INIT ? 0.0 : st->a;
+  const double ap = DXU ? st->a_prev : 0.0;
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
+  const double* __restrict__ pp = (it_host & 1) ? pA : pB;
   for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
     double v[8], y[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       const int64_t o = l * ncell + c;
       double rr = r[o];
-      if (INIT) {
-        dx[o] = 0.0;
-      } else {
+      if (!INIT) {
         rr -= a * __builtin_nontemporal_load(&w[o]);
         r[o] = rr;
-        __builtin_nontemporal_store(__builtin_nontemporal_load(&dx[o]) + a * __builtin_nontemporal_load(&p[o]), &dx[o]);
+        if (DXU) {
+          const double d0 = FIRST ? 0.0 : __builtin_nontemporal_load(&dx[o]);
+          __builtin_nontemporal_store((d0 + ap * __builtin_nontemporal_load(&pp[o])) + a * __builtin_nontemporal_load(&p[o]),
+                                      &dx[o]);
+        }
       }
       v[l] = rr;
     }
@@ -1005,12 +1012,14 @@ void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, co
                        const double* gface, double omega, double* r, double* dx, double* x0, int it_host, int init,
                        hipStream_t s) {
   const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
-  if (init)
-    hipLaunchKernelGGL(k_dg_bupdate<true>, dim3(nb), dim3(kBlock), 0, s, g, st, pA, pB, w, gface, omega, r, dx, x0,
-                       it_host);
-  else
-    hipLaunchKernelGGL(k_dg_bupdate<false>, dim3(nb), dim3(kBlock), 0, s, g, st, pA, pB, w, gface, omega, r, dx, x0,
-                       it_host);
+#define TV_DGU(I, D, F) \
+  hipLaunchKernelGGL((k_dg_bupdate<I, D, F>), dim3(nb), dim3(kBlock), 0, s, g, st, pA, pB, w, gface, omega, r, dx, x0, \
+                     it_host)
+  if (init) TV_DGU(true, false, false);
+  else if (it_host == 1) TV_DGU(false, true, true);
+  else if (it_host & 1) TV_DGU(false, true, false);
+  else TV_DGU(false, false, false);
+#undef TV_DGU
 }
 
 int launch_dg_bpost(const DgGrid& g, const PcgState* st, const double* x0, const double* r, const double* w,

@@ -267,7 +267,8 @@ void launch_dg_gface(const DgGrid& g, const double* T, double* gface, hipStream_
 // mode 0: x <- omega B^-1 b ; mode 1: x <- x + omega B^-1 (b - w)
 void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* gface,
                        double omega, double* x, int mode, hipStream_t s);
-// r <- r - a w, dx <- dx + a p, x0 <- omega B^-1 r (init: dx <- 0, x0 <- omega B^-1 r)
+// r <- r - a w, x0 <- omega B^-1 r, dx moved every second iteration from iteration 1 on
+// (init: x0 <- omega B^-1 r only; launch_mg_dx_finish ends the solve)
 void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* gface, double omega, double* r, double* dx, double* x0, int it_host, int init,
                        hipStream_t s);
