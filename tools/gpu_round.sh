@@ -33,6 +33,8 @@ timeout -k 10 600 python3 bench.py --mesh distorted --steps 5 --warmup 1 > $OUT/
 step "bench C4 under rocprofv3 --kernel-trace --stats"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_bench -o run --output-format csv -- python3 bench.py > $OUT/bench_prof.json 2> $OUT/bench_prof.err || { tail -5 $OUT/bench_prof.err; exit 1; }
 python3 tools/profile_summary.py $OUT/prof_bench $OUT/bench_prof.json $OUT/profile_summary.json > $OUT/profile_summary.log 2>&1
+step "bench C5 under rocprofv3 --kernel-trace"
+timeout -k 10 600 rocprofv3 --kernel-trace -d $OUT/prof_c5 -o run --output-format csv -- python3 bench.py --family DG --cells 200,200,25 --steps 5 --warmup 1 --kernel-reps 3 --no-cpu-baseline > $OUT/bench_c5_prof.json 2> $OUT/bench_c5_prof.err || { tail -5 $OUT/bench_c5_prof.err; exit 1; }
 step "bench C4 plain"
 timeout -k 10 600 python3 bench.py > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail -5 $OUT/bench_c4.err; exit 1; }
 cat $OUT/bench_c4.json
