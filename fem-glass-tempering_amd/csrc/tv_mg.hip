@@ -758,7 +758,13 @@ void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const do
                        hipStream_t s, const CoarsePost* cp) {
   const int64_t n = (int64_t)x.fn[0] * x.fn[1] * (x.f_ke - x.f_kb);
   if (n <= 0) return;
-  if (cp != nullptr && !mg_prolong_smooths(x)) return;  // caller bug guard: never reached (mg_level checks first)
+  if (cp != nullptr && !mg_prolong_smooths(x)) {
+    // not reached (mg_prolong_from asks mg_prolong_smooths first); kept correct
+    // anyway: the coarse post-smoothing step in place, then the plain prolongation
+    const int64_t nc = (int64_t)x.cn[0] * x.cn[1] * x.cn[2];
+    launch_mg_jacobi(nc, st, cp->b, cp->w, &cp->fa, cp->dinv, cp->omega, const_cast<double*>(xc), 1, s);
+    cp = nullptr;
+  }
   if (mg_prolong_blocks(x)) {  // 2 x 2 blocks of fine rows, 16-byte fine pairs
     const int nseg = ((x.fn[0] + 1) / 2 + kPairSeg - 1) / kPairSeg;
     const int nbj = (x.fn[1] + 1) / 2, nbk = (x.f_ke + 1) / 2;
