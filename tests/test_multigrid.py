@@ -364,3 +364,29 @@ def test_gmg_zero_residual_step():
         T = dev.functions_current["T"].x.array
         assert np.array_equal(T, np.zeros_like(T)), np.abs(T).max()
     dev.close()
+
+
+@pytest.mark.gpu
+def test_precond_apply_jacobi_matches_oracle_diagonal():
+    """tv_precond_apply with the Jacobi preconditioner: z = r / diag J(T), the
+    diagonal of the oracle's assembled Jacobian at a non-uniform T (1e-13)."""
+    torch = _torch()
+    from tvfem import RectilinearMesh
+    from tvfem.problem import ThermoViscoProblem
+    axes = CASES["graded"]
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    p = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, {"T": CG, "sigma": CG}, mp, verbose=False,
+                           part_axis=2, preconditioner="jacobi")
+    p.setup()
+    n = p.get_field("T").size
+    rng = np.random.default_rng(5)
+    T = 700.0 + rng.uniform(0.0, 150.0, n)
+    p.set_field("T", T)
+    p._flush()
+    r = rng.standard_normal(n)
+    rd = torch.tensor(r, dtype=torch.float64, device="cuda")
+    zd = torch.empty_like(rd)
+    assert p._lib.tv_precond_apply(p._ctx, rd.data_ptr(), zd.data_ptr()) == 0
+    J = O.HeatForm(O.Space(O.rectilinear_mesh(axes), "CG", 1), 0.1, O.ThermalParams.from_dict(mp)).jacobian(T)
+    assert relerr(zd.cpu().numpy(), r / J.diagonal()) < 1e-13
+    p.close()
