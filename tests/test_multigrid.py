@@ -282,6 +282,10 @@ VCYCLE_CASES = {
     # four explicit levels down to a 3-node axis (generic transfer kernels there)
     "odd_graded_4": ([np.concatenate([np.linspace(0.0, 0.6, 7), np.linspace(0.6, 3.0, 21)[1:]]),
                       np.linspace(0.0, 2.2, 12), np.linspace(0.0, 0.9, 10)], 4),
+    # a thin x axis (4 -> 3 -> 2 nodes): the generic transfer kernels, the separate
+    # coarse post-smoothing and k_cg_addfaces on the levels where the x-pair kernels
+    # do not apply
+    "thin_x_4": ([np.linspace(0.0, 0.3, 4), np.linspace(0.0, 2.0, 17), np.linspace(0.0, 1.0, 9)], 4),
 }
 
 
