@@ -2400,12 +2400,17 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
     case 8:
       *bytes = 48.0 * n;
       break;
-    case 11: {  // one multigrid V-cycle (level 0: 2 J x, restriction, prolongation, post-smoothing)
+    case 11: {  // one multigrid V-cycle, per node of each level (streams counted once)
       if (!c->mg_on) return c->fail(TV_ERR_ARG, "kernel 11: preconditioner GMG not enabled");
-      double b = (16.0 * 2 + 16 + 16 + 40) * n;
+      // level 0: J x0 (16), restriction reads r, w (16), prolongation x0 -> x (16),
+      // then CG: J x with the post-smoothing in its epilogue (x, r, dinv in, z out: 32),
+      // DG: J x (16) + the cell-block post-smoothing (x0, r, w in, z out: 32)
+      double b = (c->mg_dg ? 16.0 + 16 + 16 + 16 + 32 : 16.0 + 16 + 16 + 32) * n;
       for (size_t l = 0; l < c->mg.size(); ++l) {
         const double nl = (double)c->mg[l].n;
-        b += (l + 1 < c->mg.size()) ? (24.0 + 16 * 2 + 16 + 16 + 40) * nl + 8.0 * nl : 24.0 * nl + 8.0 * nl;
+        b += 24.0 * nl;  // the restriction's outputs b, x (pre-smoothing) and the dinv it reads
+        if (l + 1 < c->mg.size())  // J x (16), restriction reads (16), partial J x (16), prolongation in (16),
+          b += (16.0 + 16 + 16 + 16 + 24) * nl;  // post-smoothing operands b, w, dinv (24)
       }
       *bytes = b;
       break;
