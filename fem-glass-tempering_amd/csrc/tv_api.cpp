@@ -478,6 +478,8 @@ static int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   return TV_OK;
 }
 
+constexpr int64_t kCgsAutoMaxNodes = 3000000;  // AUTO Krylov form: single reduction up to this slab size
+
 static int setup_fields(Ctx* c) {
   const int d = c->dim, dd = d * d;
   const bool all = c->O.materialize != 0;
@@ -549,12 +551,16 @@ static int setup_fields(Ctx* c) {
   const bool can = c->fam_T == TV_CG && !c->um && cg_cgs_supported(c->cg);
   if (var == TV_PCG_SINGLE_REDUCTION && !can)
     return c->fail(TV_ERR_ARG, "pcg_variant SINGLE_REDUCTION needs a 3D CG1 temperature space");
-  // AUTO: the single-reduction form where the mesh is partitioned (one RCCL
-  // group per iteration instead of two all-reduces + a halo + two logic
-  // launches); on one partition KSPCG's two lighter launches are faster
-  // (measured, DESIGN.md §5: 32 vs 37 us per iteration at 1M nodes, 130 vs
-  // 217 us at C4)
-  c->cgs = can && (var == TV_PCG_SINGLE_REDUCTION || (var == TV_PCG_AUTO && c->n_parts > 1));
+  // AUTO: the single-reduction form where the mesh is partitioned into slabs
+  // of at most kCgsAutoMaxNodes owned nodes (one RCCL group per iteration
+  // instead of two all-reduces + a halo + two logic launches); on one
+  // partition, and on larger slabs where its heavier launch is bandwidth-bound,
+  // KSPCG's two lighter launches are faster (measured on the C4 per-rank
+  // shares, DESIGN.md §5: 4.1M nodes 13.2 vs 18.3 ms/step, against ~2.7 ms of
+  // communication the single reduction saves; 2M nodes 7.6 vs 8.6 ms; 1M
+  // nodes 6.5 vs 6.7 ms)
+  c->cgs = can && (var == TV_PCG_SINGLE_REDUCTION ||
+                   (var == TV_PCG_AUTO && c->n_parts > 1 && c->ownT_n <= kCgsAutoMaxNodes));
   if (c->cgs) {
     for (double** q : {&c->cr[0], &c->cr[1], &c->cs[0], &c->cs[1], &c->cw1}) {
       HIPC(hipMalloc(q, nb));

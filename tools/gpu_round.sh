@@ -39,8 +39,8 @@ step "bench C4 plain"
 timeout -k 10 600 python3 bench.py > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail -5 $OUT/bench_c4.err; exit 1; }
 cat $OUT/bench_c4.json
 # n8 / n4 / n2: one rank's share of the C4 slab partition, with the partitioned
-# path's solver (Jacobi, single-reduction CG); C4j / C5j: the Jacobi-PCG lines
-for spec in "C2 100,100,10 --thermal-only" "C3 200,200,25" "C5 200,200,25 --family DG" "C5j 200,200,25 --family DG --pc jacobi --no-cpu-baseline" "C4j 400,400,50 --pc jacobi --no-cpu-baseline" "n8 400,50,50 --pc jacobi --pcg single --no-cpu-baseline" "n4 400,100,50 --pc jacobi --pcg single --no-cpu-baseline" "n2 400,200,50 --pc jacobi --pcg single --no-cpu-baseline"; do
+# path's solver (Jacobi; single-reduction CG up to 3M owned nodes, KSPCG above); C4j / C5j: the Jacobi-PCG lines
+for spec in "C2 100,100,10 --thermal-only" "C3 200,200,25" "C5 200,200,25 --family DG" "C5j 200,200,25 --family DG --pc jacobi --no-cpu-baseline" "C4j 400,400,50 --pc jacobi --no-cpu-baseline" "n8 400,50,50 --pc jacobi --pcg single --no-cpu-baseline" "n4 400,100,50 --pc jacobi --pcg single --no-cpu-baseline" "n2 400,200,50 --pc jacobi --pcg kspcg --no-cpu-baseline"; do
   set -- $spec; tag=$1; cells=$2; shift 2
   step "bench $tag"
   timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 --cells $cells "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err || { tail -5 $OUT/bench_$tag.err; exit 1; }
