@@ -53,9 +53,6 @@ __device__ __forceinline__ buf_t mk_rsrc(const void* p, uint32_t bytes) {
 __device__ __forceinline__ double bload(buf_t r, uint32_t off) {
   return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0));
 }
-__device__ __forceinline__ double bload_nt(buf_t r, uint32_t off) {  // non-temporal (streaming) policy
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 2));
-}
 __device__ __forceinline__ void bstore(buf_t r, uint32_t off, double v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(b64v, v), r, (int)off, 0, 0);
 }
@@ -708,8 +705,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
                                                         const PcgState* __restrict__ st,
                                                         double* __restrict__ partials, int nseg, int raxis,
                                                         int qchunk, RedTail rt, int nrec, int nmarch,
-                                                        FaceOff fo, int ffirst, int exp, int it_host,
-                                                        PostArgs pa) {
+                                                        FaceOff fo, int it_host, PostArgs pa) {
   static_assert(!POST || (MODE == MODE_JAC && !FUSEP), "POST: plain Jacobian march only");
   stamp_start(rt);
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
@@ -720,30 +716,13 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   constexpr int kFaceLds = (MODE == MODE_JAC) ? (8 * R + 8) * kWave : 1;
   __shared__ double fsm[kFaceLds];
   // Jacobian mode: workgroups past the marching tiles evaluate the Robin facet
-  // terms of the boundary faces (k_face_block) -- independent work that fills
+  // terms of the boundary faces (face_block) -- independent work that fills
   // the tail of the march; the terms go to g.fface and are added to w by the
   // consumer (PCG update / k_cg_addfaces), their p.w share joins the partials
-  // face workgroups first (dispatched early, alongside the first marching
-  // round) or last (ffirst = 0)
-  // face workgroup placement: after the marching tiles (ffirst 0), before them
-  // (1), or interleaved one in every `fs` workgroups (2)
-  const int nface = (int)gridDim.x - nmarch;
-  int bid = (int)blockIdx.x, fidx = -1;
-  if (MODE == MODE_JAC && nface > 0) {
-    if (ffirst == 2) {
-      const int fs = (int)gridDim.x / nface;
-      const int b0 = (int)blockIdx.x;
-      if (b0 % fs == fs - 1 && b0 / fs < nface) fidx = b0 / fs;
-      else bid = b0 - min(nface, (b0 + 1) / fs);
-    } else if (ffirst == 1) {
-      if ((int)blockIdx.x < nface) fidx = (int)blockIdx.x;
-      else bid = (int)blockIdx.x - nface;
-    } else if ((int)blockIdx.x >= nmarch) {
-      fidx = (int)blockIdx.x - nmarch;
-    }
-  }
+  // (placed before the tiles or interleaved with them: measured no better)
+  const int bid = (int)blockIdx.x;
+  const int fidx = (MODE == MODE_JAC && bid >= nmarch) ? bid - nmarch : -1;
   if (fidx >= 0) {
-    if (exp & 16) return;  // timing experiment only (TVFEM_MARCH_EXP): no face work
     if (st != nullptr && st->done) return;
     face_block<FUSEP, R>(g, T, in0, in1, pout, st, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx, fo,
                          fsm, red, it_host);
@@ -792,8 +771,8 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   // the tile's prologue -- T and p of the face plane's R + 2 rows staged in
   // LDS, one facet row per wave (wave 0 also the row below the tile), corner
   // exchange through LDS -- and added to that plane's output in the march.
-  const bool fq0 = (MODE == MODE_JAC) && q0 == 0 && g.bnd[qaxis][0] && !(exp & 32);
-  const bool fq1 = (MODE == MODE_JAC) && q1 == nQ && g.bnd[qaxis][1] && !(exp & 32);
+  const bool fq0 = (MODE == MODE_JAC) && q0 == 0 && g.bnd[qaxis][0];
+  const bool fq1 = (MODE == MODE_JAC) && q1 == nQ && g.bnd[qaxis][1];
   double (*sFq)[2][R + 2][kWave] = reinterpret_cast<double (*)[2][R + 2][kWave]>(fsm);  // [face][T, p]
   double (*sCD)[2][R][kWave] = reinterpret_cast<double (*)[2][R][kWave]>(fsm + 4 * (R + 2) * kWave);
   double yq0 = 0.0, yq1 = 0.0;
@@ -815,12 +794,10 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const double* second = (MODE == MODE_RES) ? in1 : pold;
   constexpr bool TWO = (MODE == MODE_RES) || FUSEP;
   const uint32_t nbytes = (uint32_t)g.n0 * (uint32_t)g.n1 * (uint32_t)g.n2 * 8u;
-  // exp (TVFEM_MARCH_EXP, timing experiments only, wrong results): a zero-sized
-  // descriptor drops one stream's loads / stores while the instruction stream stays
-  const buf_t rs0 = mk_rsrc(in0, (exp & 8) ? 0u : nbytes);
-  const buf_t rs1 = mk_rsrc(TWO ? second : in0, ((FUSEP && first) || (exp & 4)) ? 0u : nbytes);  // p_old unused at it 0
-  const buf_t rso = mk_rsrc(out, (exp & 1) ? 0u : nbytes);
-  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, (FUSEP && !(exp & 1)) ? nbytes : 0u);
+  const buf_t rs0 = mk_rsrc(in0, nbytes);
+  const buf_t rs1 = mk_rsrc(TWO ? second : in0, (FUSEP && first) ? 0u : nbytes);  // p_old unused at it 0
+  const buf_t rso = mk_rsrc(out, nbytes);
+  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, FUSEP ? nbytes : 0u);
   const buf_t rsT = mk_rsrc(T, (fq0 || fq1) ? nbytes : 0u);
   const buf_t rsZ = mk_rsrc(in0, (fq0 || fq1) ? nbytes : 0u);
   const buf_t rsO = mk_rsrc(TWO ? second : in0, ((fq0 || fq1) && FUSEP && !first) ? nbytes : 0u);
@@ -834,7 +811,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   };
   // the halo row offset of the other waves is out of range: their halo loads
   // return 0 without a memory request, the instruction stream stays uniform
-  const uint32_t vo_own = lane_off(r), vo_halo = (halo && !(exp & 2)) ? lane_off(hrow) : kBadOff;
+  const uint32_t vo_own = lane_off(r), vo_halo = halo ? lane_off(hrow) : kBadOff;
   const uint32_t vo_wr = writer ? vo_own : kBadOff;  // stores of the own row
   auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? (uint32_t)(sQ * L) * 8u : kBadOff; };
   // (a streaming policy for these loads, bload_nt, measured no gain; a runtime
@@ -1073,291 +1050,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       store_partial(&partials[blockIdx.x], s);
     }
     fused_reduce_tail<1>(rt, nrec);  // p.w over all tiles (+ KSPCG logic)
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Jacobian march with an LDS-DMA plane ring (the production PCG matvec).
-//
-// Same decomposition and arithmetic as k_cg_march, but the plane loads go
-// straight from HBM into a ring of NB LDS plane slabs (buffer_load ... lds,
-// range-checked: out-of-domain lanes write 0): no VGPRs hold in-flight data,
-// so NB - 1 planes per wave stay in flight at full occupancy (in k_cg_march the
-// register ring caps the bytes in flight per CU, and with them the bandwidth
-// once the inputs come from HBM rather than the Infinity Cache).  Every wave
-// issues the same number of DMA and store instructions per step (halo rows:
-// waves 0 and R-1; the others DMA an out-of-range dummy row; masked stores use
-// out-of-range offsets), so one counted s_waitcnt vmcnt + a raw s_barrier per
-// plane retire exactly the plane about to be read.  All LDS lives in ONE
-// __shared__ array (hipcc drains the DMA queue before LDS reads when there are
-// several).  The faces normal to the march axis are integrated in the
-// epilogue (the output of that plane is held in registers until then).
-// ---------------------------------------------------------------------------
-// buffer_load_dword ... lds: lane l moves 4 bytes to LDS[lds + 4 l].  hipcc
-// tracks these writes and waits for them before any LDS read it cannot prove
-// disjoint -- so every DMA of the march targets a compile-time LDS address
-// (unrolled slab index, constant slot per wave-uniform branch) and the plane
-// coefficients come through the scalar cache, not LDS
-__device__ __forceinline__ void dma4(buf_t r, double* lds, uint32_t voff, uint32_t soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 4, voff, soff, 0, 0);
-}
-// s_waitcnt vmcnt(n) with expcnt / lgkmcnt left alone (gfx9 encoding)
-#define TV_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | 0x70 | 0xF00)
-
-template <bool FUSEP, int R, int NB>
-__global__ __launch_bounds__(R * kWave) void k_cg_march_dma(CgGrid g, const double* __restrict__ T,
-                                                            const double* __restrict__ in0, const double* in1,
-                                                            double* __restrict__ out, double* pout,
-                                                            const PcgState* __restrict__ st,
-                                                            double* __restrict__ partials, int nseg, int raxis,
-                                                            int qchunk, RedTail rt, int nrec, int nmarch, FaceOff fo,
-                                                            int exp, int it_host) {
-  stamp_start(rt);
-  constexpr int NA = FUSEP ? 2 : 1;                 // arrays per row: z (x) [, p_old]
-  // plane slab: rows r0 - 1 .. r0 + R (slots 0 .. R + 1) and slot R + 2, the
-  // target of the non-halo waves' halo DMAs (all of a step's DMAs stay inside
-  // one compile-time slab, which is what lets hipcc see them miss the slab read)
-  constexpr int SLAB = (R + 3) * NA * kWave;
-  constexpr int RING = (NB * SLAB > (8 * R + 8) * kWave) ? NB * SLAB : (8 * R + 8) * kWave;  // + face LDS alias
-  constexpr int OFF_CX = (NB - 1) * SLAB;           // x coefficients, 8 per column: staged in the last slab
-  static_assert(kWave * C_NCOEF <= SLAB, "x coefficient stage fits one slab");
-  constexpr int OFF_RED = RING;
-  constexpr int TOTAL = OFF_RED + R;
-  __shared__ double sm[TOTAL];
-  double* red = sm + OFF_RED;
-  const int nface = (int)gridDim.x - nmarch;
-  (void)nface;
-  if ((int)blockIdx.x >= nmarch) {  // face workgroups after the marching tiles
-    if (exp & 16) return;
-    if (FUSEP && st->done) return;
-    face_block<FUSEP, R>(g, T, in0, in1, pout, st, partials, rt, nrec, (int)blockIdx.x - nmarch, fo, sm, red,
-                         it_host);
-    return;
-  }
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n0 = g.n0;
-  const int nR = (raxis == 1) ? g.n1 : g.n2;
-  const int nQ = (raxis == 1) ? g.n2 : g.n1;
-  const uint32_t sR = (raxis == 1) ? (uint32_t)n0 : (uint32_t)n0 * g.n1;
-  const uint32_t sQ = (raxis == 1) ? (uint32_t)n0 * g.n1 : (uint32_t)n0;
-  const int qaxis = 3 - raxis;
-  const int nch = (nQ + qchunk - 1) / qchunk;
-  const int b = xcd_remap((int)blockIdx.x, nmarch);
-  const int chunk = b % nch;
-  const int t = b / nch;
-  const int seg = t % nseg;
-  const int rb = t / nseg;
-  const int r0 = rb * R;
-  const int r = r0 + wave;
-  const bool row_ok = r < nR;
-  const int q0 = chunk * qchunk;
-  const int q1 = min(q0 + qchunk, nQ);
-  const int i0 = seg * kSeg - 1;  // first column of the segment (lane 0)
-  const int i = i0 + lane;
-  const bool col_ok = (i >= 0) && (i < n0);
-  const bool writer = col_ok && lane >= 1 && lane <= kSeg;
-  const bool first = FUSEP ? (it_host == 0) : false;
-  const double* pold = in1;
-  if (FUSEP && !(it_host & 1)) {
-    pold = pout;
-    pout = const_cast<double*>(in1);
-  }
-  const int kb = g.k_begin, ke = g.k_end;
-  const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
-  const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
-  const double My0 = uniform(cr[C_MLO]), My1 = uniform(cr[C_MDI]), My2 = uniform(cr[C_MUP]);
-  const double Ky0 = uniform(cr[C_KLO]), Ky1 = uniform(cr[C_KDI]), Ky2 = uniform(cr[C_KUP]);
-  const double da = g.dt_alpha;
-
-  const uint32_t nbytes = (uint32_t)g.n0 * (uint32_t)g.n1 * (uint32_t)g.n2 * 8u;
-  const buf_t rs0 = mk_rsrc(in0, (exp & 8) ? 0u : nbytes);
-  const buf_t rs1 = mk_rsrc(FUSEP ? pold : in0, (FUSEP && !first && !(exp & 4)) ? nbytes : 0u);
-  const buf_t rso = mk_rsrc(out, (exp & 1) ? 0u : nbytes);
-  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, (FUSEP && !(exp & 1)) ? nbytes : 0u);
-  // DMA lane offsets: one row (64 doubles = 128 dwords) = 2 instructions of 64
-  // dwords; lane l moves dword l (resp. 64 + l) of the row, i.e. half of
-  // column i0 + l / 2 (resp. i0 + 32 + l / 2)
-  const bool halo = (wave == 0) || (wave == R - 1);
-  const int hrow = (wave == 0) ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
-  const int hslot = (wave == 0) ? 0 : R + 1;
-  const int dslot = (wave == 0) ? 0 : (wave == R - 1 ? R + 1 : R + 2);  // halo DMA slot (R + 2: dummy)
-  auto dma_off = [&](int rr, int h) -> uint32_t {
-    const int ic = i0 + 32 * h + (lane >> 1);
-    const bool ok = rr >= 0 && rr < nR && ic >= 0 && ic < n0;
-    return ok ? (uint32_t)(i0 + sR * (uint32_t)rr) * 8u + 256u * h + 4u * lane : kBadOff;
-  };
-  const uint32_t d_own0 = dma_off(r, 0), d_own1 = dma_off(r, 1);
-  const uint32_t d_hal0 = (halo && !(exp & 2)) ? dma_off(hrow, 0) : kBadOff;
-  const uint32_t d_hal1 = (halo && !(exp & 2)) ? dma_off(hrow, 1) : kBadOff;
-  auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? sQ * (uint32_t)L * 8u : kBadOff; };
-  // plane L lives in slab (L - q0 + 1) % NB: the unrolled march below reads and
-  // fills compile-time slab indices, so hipcc can see that a step's DMAs never
-  // alias the slab it reads (with runtime indices it drains the DMA queue)
-  auto slab_row = [&](int sb, int slot, int a) -> double* { return sm + sb * SLAB + (slot * NA + a) * kWave; };
-  // one plane: own row (+ halo row, or a dummy) of every array; D = 4 NA DMAs per wave
-  auto dma_plane = [&](int L, int sb) {
-    const uint32_t po = plane_off(L);
-#pragma unroll
-    for (int a = 0; a < NA; ++a) {
-      const buf_t rs = a == 0 ? rs0 : rs1;
-      double* own = slab_row(sb, wave + 1, a);
-      dma4(rs, own, d_own0, po);
-      dma4(rs, own + 32, d_own1, po);
-      double* hd = slab_row(sb, dslot, a);
-      dma4(rs, hd, d_hal0, po);
-      dma4(rs, hd + 32, d_hal1, po);
-    }
-  };
-  // prologue: the x coefficients of the 64 columns (8 per column) into the
-  // last slab (free until the first step's DMAs), then the first NB - 1 planes
-  {
-    const buf_t rcx = mk_rsrc(g.coef[0], (uint32_t)n0 * C_NCOEF * 8u);
-#pragma unroll
-    for (int k = 0; k < (kWave * C_NCOEF * 8) / 256 / R; ++k) {
-      const int piece = k * R + wave;                 // 256-byte piece of the 64-column block
-      const uint32_t off = 256u * piece + 4u * lane;  // byte of the block
-      const int ic = i0 + (int)(off / (C_NCOEF * 8u));
-      dma4(rcx, sm + OFF_CX + 32 * piece, (ic >= 0 && ic < n0) ? (uint32_t)i0 * C_NCOEF * 8u + off : kBadOff, 0);
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < NB - 1; ++s) dma_plane(q0 - 1 + s, s);
-  double bcoef = 0.0;
-  TV_WAIT_VM(0);  // prologue DMAs landed (also before an early exit: LDS stays owned until then)
-  if (FUSEP) {
-    if (st->done) return;  // converged: every launch of the batch exits here
-    bcoef = first ? 0.0 : st->beta / st->betaold;
-  }
-  __syncthreads();
-  // x coefficients of the own column in registers for the whole march
-  const double* cx = sm + OFF_CX + lane * C_NCOEF;
-  const double xMlo = cx[C_MLO], xMdi = cx[C_MDI], xMup = cx[C_MUP];
-  const double xKlo = cx[C_KLO], xKdi = cx[C_KDI], xKup = cx[C_KUP], xH = cx[C_HHI];
-
-  const bool fq0 = q0 == 0 && g.bnd[qaxis][0] && !(exp & 32);
-  const bool fq1 = q1 == nQ && g.bnd[qaxis][1] && !(exp & 32);
-  double yk0 = 0.0, xk0 = 0.0, yk1 = 0.0, xk1 = 0.0;  // face-plane outputs held for the epilogue
-
-  double us_m = 0.0, us_c = 0.0, t_m = 0.0, t_c = 0.0, xc = 0.0, dot = 0.0;
-  const uint32_t vo_wr = (writer && row_ok) ? (uint32_t)(i + sR * (uint32_t)r) * 8u : kBadOff;
-  // VMEM instructions a wave issues after a plane's DMA group before that
-  // plane is consumed: the stores of that step + (NB - 2) whole later steps
-  constexpr int D = 4 * NA, S = FUSEP ? 2 : 1;
-  constexpr int NWAIT = S + (NB - 2) * (D + S);
-  auto step = [&](int L, const int sb) {
-    TV_WAIT_VM(NWAIT);
-    __builtin_amdgcn_s_barrier();              // plane L is in LDS; every wave is done with slab sb - 1
-    dma_plane(L + NB - 1, (sb + NB - 1) % NB);  // into the slab of plane L - 1
-    const double* z0 = slab_row(sb, wave, 0);
-    double x0 = z0[lane], x1 = z0[NA * kWave + lane], x2 = z0[2 * NA * kWave + lane];
-    if (FUSEP) {
-      const double* o0 = slab_row(sb, wave, 1);
-      x0 += bcoef * o0[lane];
-      x1 += bcoef * o0[NA * kWave + lane];
-      x2 += bcoef * o0[2 * NA * kWave + lane];
-    }
-    const bool qin = (L >= q0 && L < q1);
-    if (FUSEP) bstore(rsp, vo_wr + (qin ? plane_off(L) : kBadOff), x1);
-    const double us_p = My0 * x0 + My1 * x1 + My2 * x2;
-    const double vs_p = Ky0 * x0 + Ky1 * x1 + Ky2 * x2;
-    const double t_p = us_p + da * vs_p;
-    const int q = L - 1;
-    const bool qout = (L >= q0 + 1 && L <= q1);
-    const __attribute__((address_space(4))) double* cq =
-        (const __attribute__((address_space(4))) double*)g.coef[qaxis] + (int64_t)(qout ? q : 0) * C_NCOEF;
-    const double Mz0 = cq[C_MLO], Mz1 = cq[C_MDI], Mz2 = cq[C_MUP];
-    const double Kz0 = cq[C_KLO], Kz1 = cq[C_KDI], Kz2 = cq[C_KUP];
-    const double S1 = Mz0 * t_m + Mz1 * t_c + Mz2 * t_p + da * (Kz0 * us_m + Kz1 * us_c + Kz2 * us_p);
-    const double S2 = da * (Mz0 * us_m + Mz1 * us_c + Mz2 * us_p);
-    const double Lt = xMup * S1 + xKup * S2;
-    const double Rt = xMlo * S1 + xKlo * S2;
-    const double y = (xMdi * S1 + xKdi * S2) + (shr1(Lt) + shl1(Rt));
-    const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
-    const bool own = qout && row_ok && row_owned && q_owned;
-    const bool hold = (fq0 && q == 0) || (fq1 && q == nQ - 1);  // face plane: stored in the epilogue
-    bstore(rso, vo_wr + ((own && !hold) ? plane_off(q) : kBadOff), y);
-    if (fq0 && q == 0) { yk0 = y; xk0 = xc; }
-    if (fq1 && q == nQ - 1) { yk1 = y; xk1 = xc; }
-    dot += (own && writer && !hold) ? xc * y : 0.0;
-    xc = x1;
-    us_m = us_c; us_c = us_p;
-    t_m = t_c; t_c = t_p;
-  };
-  // steps past q1 only touch LDS (their DMAs and stores are out of range)
-  for (int L0 = q0 - 1; L0 <= q1; L0 += NB) {
-#pragma unroll
-    for (int sb = 0; sb < NB; ++sb) step(L0 + sb, sb);
-  }
-  TV_WAIT_VM(0);
-  __syncthreads();  // ring free: the face planes reuse it
-  if (fq0 || fq1) {
-    // T and p of the face plane's R + 2 rows, then one facet row per wave
-    // (wave 0 also row r0 - 1), corner exchange through LDS
-    double (*sFq)[2][R + 2][kWave] = reinterpret_cast<double (*)[2][R + 2][kWave]>(sm);
-    double (*sCD)[2][R][kWave] = reinterpret_cast<double (*)[2][R][kWave]>(sm + 4 * (R + 2) * kWave);
-    const uint32_t vo_own = (col_ok && row_ok) ? (uint32_t)(i + sR * (uint32_t)r) * 8u : kBadOff;
-    const uint32_t vo_hal = (halo && col_ok && hrow >= 0 && hrow < nR) ? (uint32_t)(i + sR * (uint32_t)hrow) * 8u : kBadOff;
-    const buf_t rsT = mk_rsrc(T, nbytes);
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      if (!(f == 0 ? fq0 : fq1)) continue;
-      const uint32_t po = plane_off(f == 0 ? 0 : nQ - 1);
-      const double tO = bload(rsT, vo_own + po), tH = bload(rsT, vo_hal + po);
-      const double zO = bload(rs0, vo_own + po), zH = bload(rs0, vo_hal + po);
-      const double oO = FUSEP ? bload(rs1, vo_own + po) : 0.0, oH = FUSEP ? bload(rs1, vo_hal + po) : 0.0;
-      sFq[f][0][wave + 1][lane] = tO;
-      sFq[f][1][wave + 1][lane] = FUSEP ? zO + bcoef * oO : zO;
-      if (halo) {
-        sFq[f][0][hslot][lane] = tH;
-        sFq[f][1][hslot][lane] = FUSEP ? zH + bcoef * oH : zH;
-      }
-    }
-    __syncthreads();
-    const bool cok = i >= 0 && i < n0 - 1;
-    const double hq_own = uniform(g.coef[raxis][(int64_t)(row_ok ? r : 0) * C_NCOEF + C_HHI]);
-    const double hq_low = uniform(g.coef[raxis][(int64_t)(r0 >= 1 ? r0 - 1 : 0) * C_NCOEF + C_HHI]);
-    double yq[2] = {0.0, 0.0};
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      if (!(f == 0 ? fq0 : fq1)) continue;
-      double ya, yb, yc, yd;
-      facet_corners(g, cok && r < nR - 1, xH, hq_own, sFq[f][0][wave + 1][lane], sFq[f][0][wave + 2][lane],
-                    sFq[f][1][wave + 1][lane], sFq[f][1][wave + 2][lane], ya, yb, yc, yd);
-      yq[f] = ya + shr1(yb);
-      sCD[f][0][wave][lane] = yc;
-      sCD[f][1][wave][lane] = yd;
-      if (wave == 0) {
-        facet_corners(g, cok && r0 >= 1 && r0 - 1 < nR - 1, xH, hq_low, sFq[f][0][0][lane], sFq[f][0][1][lane],
-                      sFq[f][1][0][lane], sFq[f][1][1][lane], ya, yb, yc, yd);
-        yq[f] += yc + shr1(yd);
-      }
-    }
-    __syncthreads();
-    const int lm = lane >= 1 ? lane - 1 : 0;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      if (!(f == 0 ? fq0 : fq1)) continue;
-      if (wave >= 1) yq[f] += sCD[f][0][wave - 1][lane] + sCD[f][1][wave - 1][lm];
-      const int qf = f == 0 ? 0 : nQ - 1;
-      const bool q_owned = (raxis == 2) ? true : (qf >= kb && qf < ke);
-      const bool own = row_ok && row_owned && q_owned;
-      const double yv = (f == 0 ? yk0 : yk1) + yq[f];
-      bstore(rso, vo_wr + (own ? plane_off(qf) : kBadOff), yv);
-      dot += (own && writer) ? (f == 0 ? xk0 : xk1) * yv : 0.0;
-    }
-  }
-  if (partials != nullptr) {
-    dot = wave_sum(dot);
-    if (lane == 0) red[wave] = dot;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double s2 = 0.0;
-#pragma unroll
-      for (int w = 0; w < R; ++w) s2 += red[w];
-      store_partial(&partials[blockIdx.x], s2);
-    }
-    fused_reduce_tail<1>(rt, nrec);
   }
 }
 
@@ -1895,81 +1587,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_boundary(CgGrid g, const int64_t*
 
 int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 
-static int march_rows() {
-  static int rows = 0;
-  if (!rows) {
-    const char* e = experiment_env("TVFEM_MARCH_ROWS");
-    rows = (e && atoi(e) == 16) ? 16 : kRows;
-  }
-  return rows;
-}
-
-static int march_minblk() {  // workgroups the march grid is chunked up to (TVFEM_MARCH_MINBLK)
-  static int v = 0;
-  if (!v) {
-    const char* e = experiment_env("TVFEM_MARCH_MINBLK");
-    v = (e && atoi(e) > 0) ? atoi(e) : 1024;
-  }
-  return v;
-}
-
+// march chunking: split the march axis until the grid has kMarchMinBlocks
+// tiles (256 CUs x 4), down to kMarchMinQ planes per chunk; tiny grids further
+constexpr int kMarchMinBlocks = 1024;
+constexpr int kMarchMinQ = 6;
 constexpr int kMarchSmallTiles = 256;  // one marching tile per CU
-
-static int march_minq() {  // fewest planes per marching chunk when splitting for occupancy (TVFEM_MARCH_MINQ)
-  static int v = 0;
-  if (!v) {
-    const char* e = experiment_env("TVFEM_MARCH_MINQ");
-    v = (e && atoi(e) >= 2) ? atoi(e) : 6;
-  }
-  return v;
-}
-
-static int march_wpe() {  // TVFEM_MARCH_WPE=8: register budget for 8 waves / SIMD
-  static int v = -1;
-  if (v < 0) {
-    const char* e = experiment_env("TVFEM_MARCH_WPE");
-    v = (e && atoi(e) == 8) ? 8 : 1;
-  }
-  return v;
-}
-
-static int march_pf() {  // prefetch depth of the march (TVFEM_MARCH_PF = 2 | 3 | 4)
-  static int v = 0;
-  if (!v) {
-    const char* e = experiment_env("TVFEM_MARCH_PF");
-    v = e ? atoi(e) : 2;  // 2 measured best: deeper rings cost occupancy (66 -> 89 VGPRs)
-    if (v < 2 || v > 4) v = 2;
-  }
-  return v;
-}
-
-static int march_dma() {  // Jacobian march with the LDS-DMA plane ring (TVFEM_MARCH_DMA=0 selects k_cg_march)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = experiment_env("TVFEM_MARCH_DMA");
-    v = e ? (atoi(e) != 0) : 0;  // off: measured 80 vs 70 us in the PCG iteration (register ring + cache policy)
-  }
-  return v;
-}
-
-static int march_exp() {  // TVFEM_MARCH_EXP: timing-experiment bits (see k_cg_march); 0 in production
-  static int v = -1;
-  if (v < 0) {
-    const char* e = experiment_env("TVFEM_MARCH_EXP");
-    v = e ? atoi(e) : 0;
-  }
-  return v;
-}
-
-static int face_first() {  // face workgroups ahead of the marching tiles (TVFEM_FACE_FIRST=0|1)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = experiment_env("TVFEM_FACE_FIRST");
-    v = e ? atoi(e) : 0;
-    if (v < 0 || v > 2) v = 0;
-  }
-  return v;
-}
 
 struct Launch {
   int blocks, nseg, kfirst, nplanes, wmode, rows;
@@ -1978,16 +1600,10 @@ struct Launch {
   int raxis, qchunk;
 };
 
-static int g_force_rows = -1;  // TVFEM_CG_KERNEL=rows selects the row kernel (testing)
-
 bool use_march(const CgGrid& g) {
-  if (g_force_rows < 0) {
-    const char* e = experiment_env("TVFEM_CG_KERNEL");
-    g_force_rows = (e && e[0] == 'r') ? 1 : 0;
-  }
   // the marching kernel addresses the fields with 32-bit buffer offsets
   const int64_t bytes = (int64_t)g.n0 * g.n1 * g.n2 * 8;
-  return dim_of(g) == 3 && !g_force_rows && !g.rows_kernel && bytes < (int64_t)kBadOff;
+  return dim_of(g) == 3 && bytes < (int64_t)kBadOff;
 }
 
 int bnd_blocks(const CgGrid& g) {
@@ -2004,14 +1620,13 @@ Launch plan(const CgGrid& g, bool ghosts) {
     // the kernel covers every local node (ghost planes included) so the fused
     // PCG matvec refreshes p everywhere; outputs go to owned nodes only.
     L.raxis = (g.n2 >= g.n1) ? 2 : 1;
-    L.rows = march_rows();
+    L.rows = kRows;
     const int nR = (L.raxis == 1) ? g.n1 : g.n2;
     const int nQ = (L.raxis == 1) ? g.n2 : g.n1;
     const int nrb = (nR + L.rows - 1) / L.rows;
     // enough workgroups to fill 256 CUs x ~4: split the march into chunks
     int nchunks = 1;
-    const int minblk = march_minblk();
-    while ((int64_t)L.nseg * nrb * nchunks < minblk && nQ / (nchunks * 2) >= march_minq()) nchunks *= 2;
+    while ((int64_t)L.nseg * nrb * nchunks < kMarchMinBlocks && nQ / (nchunks * 2) >= kMarchMinQ) nchunks *= 2;
     // tiny grids (fewer tiles than CUs): the march is a chain of plane steps, so
     // shorter chunks down to 2 planes (C2 100x100x10: 26 -> 104 tiles, fused
     // matvec 15.7 -> 10.1 us, step 1.29 -> 1.08 ms; measured)
@@ -2052,20 +1667,11 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     if (folded && tail && partials) rt = *tail;
     const FaceOff fo = folded ? face_offsets(g, L.rows, 3 - L.raxis) : FaceOff{};
     const int grid = L.blocks + fo.off[6];
-#define TV_MARCH(RR, WW, PP)                                                                                  \
-  hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, RR, WW, PP>), dim3(grid), dim3(RR * kWave), 0, s, g, T, in0, in1, \
-                     out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, face_first(), \
-                     march_exp(), it_host, PostArgs{})
-    const int pf = march_pf();
-    if (MODE == MODE_JAC && march_dma() && L.rows == 8) {
-      hipLaunchKernelGGL((k_cg_march_dma<FUSEP, 8, 4>), dim3(grid), dim3(8 * kWave), 0, s, g, T, in0, in1, out, pout,
-                         st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, march_exp(), it_host);
-    } else if (L.rows == 16) TV_MARCH(16, 1, 4);
-    else if (march_wpe() == 8) TV_MARCH(8, 8, 2);
-    else if (pf == 2) TV_MARCH(8, 1, 2);
-    else if (pf == 3) TV_MARCH(8, 1, 3);
-    else TV_MARCH(8, 1, 4);
-#undef TV_MARCH
+    // R = 8 rows, prefetch depth 2 (measured best, round 1-2: R = 16, PF 3 / 4,
+    // 8 waves per SIMD and an LDS-DMA plane ring were all slower)
+    hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, kRows, 1, 2>), dim3(grid), dim3(kRows * kWave), 0, s, g, T, in0, in1,
+                       out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, it_host,
+                       PostArgs{});
     if (folded && !FUSEP && addfaces && fo.off[6] > 0) {  // complete J x (else the consumer adds them)
       const int64_t nodes = 2 * ((int64_t)g.n1 * (g.k_end - g.k_begin) + (int64_t)g.n0 * std::max(g.n1, g.n2));
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, 1024));
@@ -2203,24 +1809,19 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
                           hipStream_t s) {
   const Launch L = plan(g, false);
   // the production march configuration only (experiment switches fall back)
-  if (!L.march || L.rows != 8 || g.n0 < 3 || march_pf() != 2 || march_wpe() != 1 || march_dma() || march_exp() ||
-      g.k_begin != 0 || g.k_end != g.n2)
-    return -1;
+  if (!L.march || g.n0 < 3 || g.k_begin != 0 || g.k_end != g.n2) return -1;
   const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
   const int grid = L.blocks + fo.off[6];
   const PostArgs pa{r, dinv, omega};
   hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, 1, 2, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T, x,
                      nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks, fo,
-                     face_first(), 0, 0, pa);
+                     0, pa);
   const FaceAdd fa = cg_face_add(g, 0);
   const int nO = (L.raxis == 2) ? g.n1 : g.n2;
   const int64_t nodes = 2 * (int64_t)g.n1 * g.n2 + 2 * (int64_t)(g.n0 - 2) * nO;
   // 240 workgroups (some threads take two nodes): 11.6 -> 11.0 us at C4 against
-  // one node per thread (319); TVFEM_POSTF_BLOCKS overrides the cap (experiments)
-  static const int cap = [] {
-    const char* e = experiment_env("TVFEM_POSTF_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 240;
-  }();
+  // one node per thread (319)
+  constexpr int cap = 240;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, cap));
   const RedTail rt = tail ? *tail : RedTail{};
   hipLaunchKernelGGL(k_mg_post_faces, dim3(nb), dim3(kBlock), 0, s, fa, L.raxis, r, dinv, omega, z, partials,

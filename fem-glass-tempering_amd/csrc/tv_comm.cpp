@@ -1,0 +1,213 @@
+// Communication of the partitioned (multi-GPU) path: ghost-plane exchanges
+// and reductions over RCCL (production, one process per GPU over xGMI) or the
+// host-staged callbacks (several partitions on one GPU, tests).  Replaces the
+// reference's MPI layer: dolfinx Scatterer::scatter_forward
+// (ThermoViscoProblem.py:351) and PETSc's MPI_Allreduce in VecNorm / VecDot [3P].
+#include "tv_ctx.h"
+
+namespace tv {
+// --------------------------------------------------------------------------------------
+// communication
+// --------------------------------------------------------------------------------------
+bool multi_rank(const Ctx* c) { return c->nranks > 1 && (c->comm || c->host_sendrecv); }
+
+int halo_host(Ctx* c, double* v) {
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  double* s_lo = c->h_halo;
+  double* s_hi = c->h_halo + plane;
+  double* r_lo = c->h_halo + 2 * plane;
+  double* r_hi = c->h_halo + 3 * plane;
+  if (g.g_lo) HIPC(hipMemcpyAsync(s_lo, v + plane * g.k_begin, plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (g.g_hi) HIPC(hipMemcpyAsync(s_hi, v + plane * (g.k_end - 1), plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  if (g.g_lo && c->host_sendrecv(s_lo, (size_t)plane, c->rank - 1, r_lo, (size_t)plane, c->rank - 1, c->host_user))
+    return c->fail(TV_ERR_COMM, "host sendrecv failed");
+  if (g.g_hi && c->host_sendrecv(s_hi, (size_t)plane, c->rank + 1, r_hi, (size_t)plane, c->rank + 1, c->host_user))
+    return c->fail(TV_ERR_COMM, "host sendrecv failed");
+  if (g.g_lo) HIPC(hipMemcpyAsync(v, r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (g.g_hi) HIPC(hipMemcpyAsync(v + plane * g.k_end, r_hi, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+int halo(Ctx* c, double* v) {
+  if (!multi_rank(c) || c->fam_T != TV_CG) return TV_OK;
+  if (c->host_sendrecv) return halo_host(c, v);
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  NCCLC(ncclGroupStart());
+  if (g.g_lo) {  // neighbour rank-1: send first owned plane, receive ghost plane 0
+    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclRecv(v, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+  }
+  if (g.g_hi) {
+    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
+int allreduce(Ctx* c, double* v, int n) {
+  if (!multi_rank(c)) return TV_OK;
+  if (c->host_allreduce) {
+    HIPC(hipMemcpyAsync(c->h_sums + 4, v, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (c->host_allreduce(c->h_sums + 4, n, c->host_user)) return c->fail(TV_ERR_COMM, "host allreduce failed");
+    HIPC(hipMemcpyAsync(v, c->h_sums + 4, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return TV_OK;
+  }
+  NCCLC(ncclAllReduce(v, v, n, ncclDouble, ncclSum, c->comm, c->stream));
+  return TV_OK;
+}
+
+// reduce partial records -> (allreduce) -> scalar logic
+int reduce_logic(Ctx* c, int n, int W, int kind, int check_done) {
+  if (!multi_rank(c)) {
+    launch_reduce_logic(c->partials, n, W, c->sums, c->st, kind, check_done, c->stream);
+  } else {
+    launch_reduce_logic(c->partials, n, W, c->sums, c->st, 0, 0, c->stream);
+    if (int e = allreduce(c, c->sums, W)) return e;
+    if (kind) launch_logic(c->st, c->sums, kind, c->stream);
+  }
+  return TV_OK;
+}
+
+// ---- single-reduction PCG (Chronopoulos-Gear form, k_cgs_march) -------------
+// w of the owned boundary planes + the face-workgroup facet terms (the value a
+// neighbour's ghost plane must hold), packed for the halo
+__global__ __launch_bounds__(kBlock) void k_cgs_pack(CgGrid g, const double* __restrict__ w,
+                                                     const double* __restrict__ ff, int raxis,
+                                                     double* __restrict__ out) {
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < 2 * plane; t += (int64_t)gridDim.x * kBlock) {
+    const int side = (int)(t / plane);
+    const int64_t e = t - side * plane;
+    const int k = side ? g.k_end - 1 : g.k_begin;
+    const int i = (int)(e % g.n0), j = (int)(e / g.n0);
+    // facet terms in the order of k_cgs_march: x face, then the row-axis face
+    double fx = 0.0, fr = 0.0;
+    const int fxi = (i == 0) ? 0 : (i == g.n0 - 1 ? 1 : -1);
+    if (fxi >= 0 && g.ffoff[fxi] >= 0) fx = ff[g.ffoff[fxi] + j + (int64_t)g.n1 * k];
+    const int c = (raxis == 1) ? j : k, n = (raxis == 1) ? g.n1 : g.n2;
+    const int sd = (c == 0) ? 0 : (c == n - 1 ? 1 : -1);
+    if (sd >= 0 && g.ffoff[2 * raxis + sd] >= 0) fr = ff[g.ffoff[2 * raxis + sd] + i + (int64_t)g.n0 * ((raxis == 1) ? k : j)];
+    out[t] = w[e + plane * k] + (fx + fr);
+  }
+}
+
+int cgs_raxis(const Ctx* c) { return (c->cg.n2 >= c->cg.n1) ? 2 : 1; }  // = plan(g).raxis
+
+// ghost planes of w_i: neighbours' packed boundary planes (RCCL group with
+// the all-reduce of the iteration's sums, or the host-staged transport)
+int cgs_exchange(Ctx* c, double* wout, const double* fout) {
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  const int blocks = (int)std::min<int64_t>(1024, (2 * plane + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_cgs_pack, dim3(blocks), dim3(kBlock), 0, c->stream, g, wout, fout, cgs_raxis(c), c->wsend);
+  if (c->host_sendrecv) {
+    if (int e = allreduce(c, c->sums, 3)) return e;
+    double* s_lo = c->h_halo;
+    double* s_hi = c->h_halo + plane;
+    double* r_lo = c->h_halo + 2 * plane;
+    double* r_hi = c->h_halo + 3 * plane;
+    HIPC(hipMemcpyAsync(s_lo, c->wsend, 2 * plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (g.g_lo && c->host_sendrecv(s_lo, (size_t)plane, c->rank - 1, r_lo, (size_t)plane, c->rank - 1, c->host_user))
+      return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (g.g_hi && c->host_sendrecv(s_hi, (size_t)plane, c->rank + 1, r_hi, (size_t)plane, c->rank + 1, c->host_user))
+      return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (g.g_lo) HIPC(hipMemcpyAsync(wout, r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (g.g_hi) HIPC(hipMemcpyAsync(wout + plane * g.k_end, r_hi, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    return TV_OK;
+  }
+  // one group: the 3-scalar all-reduce and the ghost planes of w (<= 2 peers)
+  NCCLC(ncclGroupStart());
+  NCCLC(ncclAllReduce(c->sums, c->sums, 3, ncclDouble, ncclSum, c->comm, c->stream));
+  if (g.g_lo) {
+    NCCLC(ncclSend(c->wsend, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclRecv(wout, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+  }
+  if (g.g_hi) {
+    NCCLC(ncclSend(c->wsend + plane, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclRecv(wout + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
+}  // namespace tv
+
+using namespace tv;
+
+extern "C" {
+
+int tv_comm_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+
+int tv_comm_get_unique_id(char* id_out) {
+  if (!id_out) return TV_ERR_ARG;
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    set_global_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    return TV_ERR_COMM;
+  }
+  std::memcpy(id_out, &id, sizeof(id));
+  return TV_OK;
+}
+
+
+int tv_comm_init(void* ctx, const char* id, int n_ranks, int rank) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !id) return TV_ERR_ARG;
+  if (n_ranks != c->n_parts || rank != c->part)
+    return c->fail(TV_ERR_ARG, "communicator size/rank must match the mesh partition (n_parts/part)");
+  hipSetDevice(c->device);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCLC(ncclCommInitRank(&c->comm, n_ranks, uid, rank));
+  c->nranks = n_ranks;
+  c->rank = rank;
+  // bring ghost planes of the state up to date
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
+                      tv_host_sendrecv_fn sendrecv_fn, void* user) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !allreduce_fn || !sendrecv_fn) return TV_ERR_ARG;
+  if (n_ranks != c->n_parts || rank != c->part)
+    return c->fail(TV_ERR_ARG, "communicator size/rank must match the mesh partition (n_parts/part)");
+  hipSetDevice(c->device);
+  c->nranks = n_ranks;
+  c->rank = rank;
+  c->host_allreduce = allreduce_fn;
+  c->host_sendrecv = sendrecv_fn;
+  c->host_user = user;
+  if (c->fam_T == TV_CG) {
+    const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
+    HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)plane));
+  }
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_halo_exchange(void* ctx, int field) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || field < 0 || field >= TV_NUM_FIELDS || !c->f[field].ptr) return TV_ERR_ARG;
+  if (c->f[field].space != 0 || c->f[field].bs != 1) return c->fail(TV_ERR_ARG, "halo exchange: scalar T-space fields only");
+  if (int e = halo(c, c->f[field].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,217 @@
+// Host runtime of libtvfem.so: the per-context state (struct Ctx) shared by
+// the runtime's translation units, and the functions they call across files.
+// Not part of the C-ABI (include/tvfem.h).
+//
+//   tv_context.cpp  context creation / destruction, mesh partition, device
+//                   state, field transfer, output and Dirichlet settings
+//   tv_comm.cpp     halo exchanges and reductions (RCCL or host-staged)
+//   tv_solver.cpp   Newton + Krylov drivers (KSPCG, single-reduction), the
+//                   Dirichlet lifting, the viscoelastic step, the operators
+//   tv_mgsolve.cpp  geometric-multigrid hierarchy and the preconditioned solve
+//   tv_measure.cpp  in-solve kernel timing, algorithmic bytes, timed launches
+//
+// Reference mapping (file:line under /root/reference):
+//   Ctx construction      ThermoViscoProblem.__init__ (ThermoViscoProblem.py:24-58)
+//   initial condition     _set_initial_condition (:187-233)
+//   tv_solve_T            _solve_T (:384-391) -> dolfinx NewtonSolver [3P]
+//                         configured at _setup_solver (:330-346)
+//   tv_visco_update       _solve_Tf .. _solve_stress (:393-595)
+//   tv_step               solve_timestep (:367-381) without _write_output
+#pragma once
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "tv_internal.h"
+
+namespace tv {
+
+struct FieldInfo {
+  double* ptr = nullptr;
+  int bs = 1;       // components
+  int space = 0;    // 0 T space, 1 sigma space
+  bool alloc = false;
+};
+
+// One coarse level of the geometric-multigrid hierarchy (tv_mg.hip): a
+// single-partition CG grid of the box coarsened by two along the axes with an
+// even cell count, its transfer from the next finer level and its vectors.
+struct MgLevel {
+  CgGrid g{};
+  std::vector<double> X[3];  // storage-axis node coordinates
+  int64_t n = 0;
+  double omega = 0.0;        // damped-Jacobi weight 2 / (1.1 b), b >= lambda_max(D^-1 J)
+  double *T = nullptr, *b = nullptr, *x = nullptr, *w = nullptr, *dinv = nullptr;
+  MgXfer xf{};               // finer level -> this level
+  double* coef[3] = {nullptr, nullptr, nullptr};
+  int64_t* bnodes = nullptr;
+  double* ffbuf[2] = {nullptr, nullptr};
+  std::vector<void*> bufs;   // T, b, x, w, dinv and the transfer maps
+  bool dinv_interior = false;  // dinv holds the T-independent interior diagonal
+};
+
+struct Ctx {
+  std::string err;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t evp[2] = {nullptr, nullptr};  // PCG convergence polls (double-buffered)
+  tv_params P{};
+  tv_options O{};
+  int dim = 1;
+  int fam_T = TV_CG, fam_S = TV_CG;
+  int perm[3] = {0, -1, -1};  // storage axis -> physical axis (-1 degenerate)
+  int n_parts = 1, part = 0;
+  // global / local sizes
+  int Nnode_glob[3] = {1, 1, 1};  // per storage axis
+  int Ncell_glob[3] = {0, 0, 0};
+  int plane_begin = 0, plane_end = 0;  // owned global planes (CG) / cell layers (DG) along storage axis 2
+  CgGrid cg{};
+  bool dinv_interior = false;  // dinv holds the T-independent interior diagonal (CG march path)
+  DgGrid dg{};
+  int64_t nT = 0, nS = 0;          // local dofs incl. ghosts
+  int64_t ownT_off = 0, ownT_n = 0;
+  int64_t ownS_off = 0, ownS_n = 0;
+  int64_t globT_off = 0, globS_off = 0;
+  std::vector<std::vector<double>> coords;  // physical axes
+  FieldInfo f[TV_NUM_FIELDS];
+  double* coef[3] = {nullptr, nullptr, nullptr};
+  double* dgh[3] = {nullptr, nullptr, nullptr};
+  int* map = nullptr;
+  int64_t* bnodes = nullptr;
+  double* ffbuf[2] = {nullptr, nullptr};  // Robin facet-term face arrays (CgGrid::ffbuf)
+  // PCG work (T space, local size)
+  double *r = nullptr, *z = nullptr, *pA = nullptr, *pB = nullptr, *w = nullptr, *dinv = nullptr;
+  // single-reduction PCG (k_cgs_march): r, s, w in two parities (w[0] = w);
+  // p = pA, x = the dx field; wsend: the two packed boundary planes of w + facet
+  // terms sent to the neighbours (multi-rank)
+  bool cgs = false;
+  // Dirichlet mode (tv_set_dirichlet): dB = T - value on the boundary nodes, tmp = J dB
+  bool dir_on = false;
+  double dir_value = 0.0;
+  double *dB = nullptr, *dtmp = nullptr;
+  double* Tfo = nullptr;  // paper mode, mixed families: previous Tf per T dof
+  Output* out = nullptr;  // time-series output (tv_output_*)
+  // geometric multigrid (options.preconditioner = TV_PC_GMG): levels 1.. (level 0 = cg)
+  bool mg_on = false;
+  bool mg_dg = false;       // DG1 level 0 over the CG1 hierarchy of the same box
+  std::vector<MgLevel> mg;
+  double mg_omega0 = 0.0;
+  double* mgx = nullptr;    // level-0 V-cycle iterate
+  double* dggface = nullptr; // DG level 0: facet means of dg(T) for the cell-block Jacobi smoother
+  // unstructured mesh (tv_create_unstructured, tv_um.hip)
+  bool um = false;
+  UmGrid umg{};
+  std::vector<double> um_xyz;        // host copy: 3 per vertex
+  std::vector<int64_t> um_cells;     // host copy: 2^dim per cell (input order)
+  UmDevice* umd = nullptr;            // assembled operators, facet data (tv_um.hip)
+  unsigned char* um_bmask = nullptr;  // boundary vertices (Dirichlet mode)
+  std::vector<int> out_fields;
+  double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
+  double* wsend = nullptr;
+  double* partials = nullptr;
+  int n_partials_cap = 0;
+  double* sums = nullptr;
+  unsigned* counters = nullptr;  // arrival counters of the in-kernel reduction tails
+  PcgState* st = nullptr;
+  PcgState* h_st = nullptr;  // pinned, 3 slots: 0 / 1 the PCG polls, 2 the state uploaded at a solve's start
+  double* h_sums = nullptr;  // pinned
+  int* tflag = nullptr;       // device: s_tilde / sigma_tilde all +0.0 (0) or general (1), see ViscoFields
+  double* scratch = nullptr;  // transfer scratch
+  size_t scratch_bytes = 0;
+  // comm: RCCL (production) or host-staged callbacks (testing several ranks on one GPU)
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  tv_host_allreduce_fn host_allreduce = nullptr;
+  tv_host_sendrecv_fn host_sendrecv = nullptr;
+  void* host_user = nullptr;
+  double* h_halo = nullptr;  // pinned staging: 2 send + 2 recv planes
+  size_t h_halo_n = 0;
+  // in-solve kernel timing (tv_kernel_timing): the fused matvec and the PCG
+  // update stamp the device REALTIME clock at their start (workgroup 0) and at
+  // the end of their reduction tail into d_ts (4 stamps per PCG iteration, one
+  // slot per iteration, read back in bulk); HIP events around the visco update
+  bool ktime = false;
+  int kstride = 1;                   // every kstride-th PCG iteration is timed
+  uint64_t* d_ts = nullptr;          // kTsCap slots x {matvec start, end, update start, end}
+  int ts_next = 0;                   // first free slot
+  std::vector<int> ts_pending;       // slots of productive iterations not yet read back
+  double ts_khz = 0.0;               // REALTIME clock (hipDeviceAttributeWallClockRate)
+  hipEvent_t vev[2] = {nullptr, nullptr};
+  double ksum[3] = {0.0, 0.0, 0.0};  // ms: fused matvec, PCG update, visco update
+  int64_t kcnt[3] = {0, 0, 0};
+  // stats
+  int last_newton = 0, last_krylov = 0;
+  double last_dx = 0.0;
+  int pcg_hint = 0;
+
+  int fail(int code, const std::string& m) {
+    err = m;
+    return code;
+  }
+};
+
+#define HIPC(expr)                                                                              \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return c->fail(TV_ERR_HIP, std::string("HIP error ") + hipGetErrorString(e_) + " at " +  \
+                                     __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr); \
+  } while (0)
+
+#define NCCLC(expr)                                                                             \
+  do {                                                                                          \
+    ncclResult_t r_ = (expr);                                                                   \
+    if (r_ != ncclSuccess)                                                                      \
+      return c->fail(TV_ERR_COMM, std::string("RCCL error ") + ncclGetErrorString(r_) + " at " + \
+                                      std::to_string(__LINE__) + ": " #expr);                   \
+  } while (0)
+
+constexpr int64_t kCgsAutoMaxNodes = 3000000;  // AUTO Krylov form: single reduction up to this slab size
+constexpr int kTsCap = 1 << 15;                // timestamp slots of the in-solve kernel timing
+
+// ---- tv_context.cpp ----
+void set_global_error(const std::string& m);
+void axis_coefs(const std::vector<double>& X, int first, int count, std::vector<double>& out);
+const std::vector<double>& storage_coords(Ctx* c, int s, std::vector<double>& tmp);
+bool storage_perm(const tv_mesh_desc* m, int perm[3]);
+void part_planes(int N2, int P, int p, int* b0, int* b1);  // owned planes [b0, b1) of partition p of P
+int build_cg_grid(Ctx* c, int d, const std::vector<double> (&X)[3], int first2, int n2, int g_lo, int g_hi,
+                  bool bnd2lo, bool bnd2hi, CgGrid& g, double** coef, int64_t** bnodes, double** ffbuf);
+int transfer(Ctx* c, int field, double* host, size_t n, int dir);
+
+// ---- tv_comm.cpp ----
+bool multi_rank(const Ctx* c);
+int halo(Ctx* c, double* v);  // ghost planes of a T-space vector of the fine grid
+int allreduce(Ctx* c, double* v, int n);
+int reduce_logic(Ctx* c, int n, int W, int kind, int check_done);  // records -> (all-reduce) -> scalar logic
+int cgs_raxis(const Ctx* c);
+int cgs_exchange(Ctx* c, double* wout, const double* fout);
+
+// ---- tv_solver.cpp ----
+void op_residual(Ctx* c, const double* T, const double* Tp, double* F);
+void op_diag(Ctx* c, const double* T, double* d, int invert);
+void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np);
+bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr, int it = 0);
+int ts_flush(Ctx* c);
+CgsBuffers cgs_buffers(Ctx* c, const double* T, int it);
+int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv);
+int visco(Ctx* c, bool copy_Tprev);
+void launch_bc_mask(Ctx* c, double* dinv);  // dinv = 0 on the Dirichlet-constrained rows
+
+// ---- tv_mgsolve.cpp ----
+int mg_setup(Ctx* c);
+void mg_prepare(Ctx* c, const double* T);
+int mg_dg_weight(Ctx* c, const double* T);
+int mg_apply0(Ctx* c, const double* T, const RedTail* tail);
+int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason);
+
+}  // namespace tv

@@ -725,7 +725,7 @@ DgTile dg_tile_plan(const DgGrid& g) {
   p.nseg = (g.c0 + kSeg - 1) / kSeg;
   p.ra = (g.c2 >= g.c1) ? 2 : 1;  // rows along the longer of axes 1 / 2, march along the other
   const int nr = (p.ra == 2) ? g.c2 : g.c1, npl = (p.ra == 2) ? g.c1 : g.c2;
-  const int rows = dg_rows(g.tile == 2);
+  const int rows = dg_rows(true);
   const int nrb = (nr + rows - 1) / rows;
   p.nch = (npl + qmax - 1) / qmax;
   p.qchunk = (npl + p.nch - 1) / p.nch;
@@ -968,13 +968,10 @@ static bool launch_tile(const DgGrid& g, const double* T, const double* in0, con
 #define TV_DG_TILE(HLV, RAV)                                                                                  \
   hipLaunchKernelGGL((k_dg_tile<FUSEP, HLV, RAV>), dim3(p.blocks), dim3(512), 0, s, g, T, in0, in1, out, pout, st, \
                      partials, p.nseg, p.qchunk, p.nch, rt)
-  if (g.tile == 2) {
-    if (p.ra == 2) TV_DG_TILE(true, 2);
-    else TV_DG_TILE(true, 1);
-  } else {
-    if (p.ra == 2) TV_DG_TILE(false, 2);
-    else TV_DG_TILE(false, 1);
-  }
+  // HL: 8 computing waves whose edge waves load the halo rows (the round-1
+  // layout of 6 computing + 2 halo waves measured slower: J x 82 vs 64 us)
+  if (p.ra == 2) TV_DG_TILE(true, 2);
+  else TV_DG_TILE(true, 1);
 #undef TV_DG_TILE
   return rt.counter != nullptr;
 }

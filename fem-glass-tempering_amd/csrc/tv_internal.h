@@ -10,13 +10,6 @@
 
 namespace tv {
 
-// Experiment switches (TVFEM_MARCH_*, TVFEM_NT, TVFEM_DG_TILE, ...) select
-// kernel variants for measurements only.  They take effect only when
-// TVFEM_EXPERIMENTS=1 is set as well, and the library reports every switch it
-// honours on stderr once; a stray variable alone never changes the solver path.
-// Returns the variable's value, or nullptr when unset or not enabled.
-const char* experiment_env(const char* name);
-
 constexpr int kWave = 64;         // CDNA wavefront
 constexpr int kSeg = kWave - 2;   // outputs per wave of the x-row stencil kernels
 constexpr int kBlock = 256;       // 4 waves
@@ -63,9 +56,6 @@ struct CgGrid {
   double* ffbuf[2];
   int64_t ffoff[6];
   int64_t ffsize;
-  // 1: the x-row stencil kernel (k_cg_rows, facet terms inline) instead of the
-  // march on this 3D grid -- the multigrid's coarse levels (tv_api.cpp mg_setup)
-  int rows_kernel;
 };
 
 // Grid of the DG1 temperature space: cells per storage axis; dof layout is
@@ -82,10 +72,10 @@ struct DgGrid {
   double a_rad, a_conv;
   double T_amb, T_amb4;
   double penalty;             // SIPG penalty (ThermoViscoProblem.py:313)
-  // 3D Jacobian kernel: 2 = marching tiles (k_dg_tile) of 8 computing waves whose
-  // edge waves load the halo rows (default), 1 = 6 computing + 2 halo waves,
-  // both of `tile_chunk` planes; 0 = one thread per cell (k_dg_cells); from
-  // TVFEM_DG_TILE / TVFEM_DG_CHUNK when the context is created
+  // 3D Jacobian kernel: 1 = marching tiles (k_dg_tile) of 8 computing waves whose
+  // edge waves load the halo rows, `tile_chunk` planes per workgroup (default);
+  // 0 = one thread per cell (k_dg_cells, the reference the tile kernel is
+  // tested against); tv_options.dg_kernel / dg_tile_chunk
   int tile, tile_chunk;
 };
 
@@ -433,6 +423,7 @@ bool output_add_field(Output* o, const std::string& name, int ncomp, bool dg, si
 bool output_start(Output* o, int device, std::string& err);
 double* output_acquire(Output* o, int* set);
 size_t output_offset(const Output* o, size_t k);
+void output_release(Output* o, int set);  // an acquired set whose write is abandoned
 bool output_submit(Output* o, int set, double t, hipStream_t compute, std::string& err);
 std::string output_destroy(Output* o);
 void launch_copy(double* dst, const double* src, int64_t n, hipStream_t s);

@@ -188,118 +188,6 @@ __global__ __launch_bounds__(kBlock) void k_mg_prolong(MgXfer x, const PcgState*
   }
 }
 
-// Prolongation by rows, x coarsened: one wave per (fine row, 64-node x
-// segment), lanes = consecutive fine x nodes (segments start at even i).  Every
-// lane loads ONE coarse x value per coarse row, (i + 1) / 2 -- its own node
-// (even i) or its right coarse neighbour (odd i) -- and an odd lane takes its
-// left neighbour from lane - 1 through a DPP wave shift: 4 gathers per fine
-// node instead of 8.  The y / z (index, weight) pairs are uniform per block.
-__global__ __launch_bounds__(kWave) void k_mg_prolong_rows(MgXfer x, const PcgState* __restrict__ st,
-                                                           double* __restrict__ xf, const double* __restrict__ xc,
-                                                           const double* __restrict__ mask, int nseg) {
-  if (st != nullptr && st->done) return;
-  // consecutive rows on one XCD (xcd_remap): neighbouring fine rows read the
-  // same coarse rows from one L2
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int row = bid / nseg;
-  const int seg = bid - row * nseg;
-  const int j = row % x.fn[1], k = row / x.fn[1] + x.f_kb;
-  const int nf = x.fn[0];
-  const int i = seg * kWave + (int)threadIdx.x;
-  const bool ok = i < nf;
-  const int ii = ok ? i : nf - 1;
-  const int cx = (ii + 1) >> 1;
-  const bool odd = (ii & 1) != 0;
-  const bool tail = odd && ii == nf - 1;  // odd cell count: the last fine node is a coarse node
-  const double wl = x.pw[0][2 * ii], wr = x.pw[0][2 * ii + 1];
-  const int64_t cpl = (int64_t)x.cn[0] * x.cn[1];
-  const int64_t f = (int64_t)ii + (int64_t)nf * (j + (int64_t)x.fn[1] * k);
-  // the four coarse rows' loads and the fine value first, all in flight at
-  // once (a load per row followed by its DPP would serialise four round
-  // trips); zero-weight rows read a valid row and contribute 0
-  double v[4], w[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = q >> 1, b = q & 1;
-    w[q] = x.pw[2][2 * k + c] * x.pw[1][2 * j + b];
-    v[q] = xc[cx + (int64_t)x.cn[0] * x.pi[1][2 * j + b] + cpl * x.pi[2][2 * k + c]];
-  }
-  const double xo = xf[f];
-  double acc = 0.0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const double vl = shr1(v[q]);  // lane - 1's value: coarse (i - 1) / 2 for odd i
-    acc += w[q] * ((odd && !tail) ? wl * vl + wr * v[q] : v[q]);
-  }
-  if (!ok) return;
-  const bool off = mask != nullptr && mask[f] == 0.0;
-  xf[f] = off ? 0.0 : xo + acc;
-}
-
-// Restriction by rows, x coarsened: one wave per (coarse row, 64-node x
-// segment), lanes = consecutive coarse x nodes.  A lane loads its fine centre
-// and right neighbour (2I, 2I + 1) of the nine fine rows, all 36 loads in
-// flight at once; its left neighbour 2I - 1 is lane - 1's right one (DPP wave
-// shift), lane 0 loads it itself.
-template <bool MASK>
-__global__ __launch_bounds__(kWave) void k_mg_restrict_rows(MgXfer x, const PcgState* __restrict__ st,
-                                                            const double* __restrict__ bf,
-                                                            const double* __restrict__ wf,
-                                                            const double* __restrict__ mask, double* __restrict__ bc,
-                                                            const double* __restrict__ dinv_c, double omega_c,
-                                                            double* __restrict__ xc, int nseg) {
-  if (st != nullptr && st->done) return;
-  // consecutive coarse rows on one XCD (xcd_remap): the fine rows they share
-  // (2J + 1, 2K + 1) are read once from HBM into that XCD's L2
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const int row = bid / nseg;
-  const int seg = bid - row * nseg;
-  const int J = row % x.cn[1], K = row / x.cn[1] + x.c_kb;
-  const int lane = (int)threadIdx.x;
-  const int I = seg * kWave + lane;
-  const bool ok = I < x.cn[0];
-  const int II = ok ? I : x.cn[0] - 1;
-  const int nf = x.fn[0];
-  const int f1 = (II == x.cn[0] - 1 && ((nf - 1) & 1)) ? nf - 1 : 2 * II;
-  const int fr = (f1 + 1 < nf) ? f1 + 1 : f1;
-  const int fl = (f1 >= 1) ? f1 - 1 : f1;
-  const double wl = x.rw[0][3 * II], wr = x.rw[0][3 * II + 2];
-  const int64_t fpl = (int64_t)nf * x.fn[1];
-  auto d = [&](int64_t f) -> double {
-    const double r = bf[f] - wf[f];
-    return (MASK && mask[f] == 0.0) ? 0.0 : r;
-  };
-  double dc[9], dr[9], dl0[9], wq[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    const int c = q / 3, b = q % 3;
-    wq[q] = x.rw[2][3 * K + c] * x.rw[1][3 * J + b];
-    const int64_t base = (int64_t)x.ri[1][3 * J + b] * nf + fpl * x.ri[2][3 * K + c];
-    dc[q] = d(base + f1);
-    dr[q] = d(base + fr);
-    dl0[q] = 0.0;
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < 9; ++q) {
-      const int c = q / 3, b = q % 3;
-      const int64_t base = (int64_t)x.ri[1][3 * J + b] * nf + fpl * x.ri[2][3 * K + c];
-      dl0[q] = d(base + fl);
-    }
-  }
-  double acc = 0.0;
-#pragma unroll
-  for (int q = 0; q < 9; ++q) {
-    double dl = shr1(dr[q]);  // lane - 1's right neighbour = fine 2I - 1
-    if (lane == 0) dl = dl0[q];
-    acc += wq[q] * ((wl * dl + dc[q]) + wr * dr[q]);
-  }
-  if (!ok) return;
-  const int64_t o = (int64_t)I + (int64_t)x.cn[0] * (J + (int64_t)x.cn[1] * K);
-  bc[o] = acc;
-  if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;  // the coarse pre-smoothing step from 0
-}
-
 // ---- x-pair transfers --------------------------------------------------------
 // A lane owns the fine pair (2I, 2I + 1) of coarse x node I and moves it with
 // ONE 16-byte load / store (rows of an odd node count start 8-byte aligned:
@@ -664,35 +552,6 @@ __global__ __launch_bounds__(kBlock) void k_mg_scale(int64_t n, const double* __
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = a * y[t];
 }
 
-// TVFEM_MG_ROWS=1 (with TVFEM_EXPERIMENTS=1): the row-per-wave transfers of
-// one fine node per lane instead of the x-pair kernels (measurements only)
-bool mg_rows_experiment() {
-  static const bool on = [] {
-    const char* v = experiment_env("TVFEM_MG_ROWS");
-    return v != nullptr && v[0] == '1';
-  }();
-  return on;
-}
-
-// TVFEM_MG_POSTSEP=1: coarse post-smoothing by its own k_mg_jacobi launch
-// instead of on the fly in the 2 x 2 block prolongation
-bool mg_postsep_experiment() {
-  static const bool on = [] {
-    const char* v = experiment_env("TVFEM_MG_POSTSEP");
-    return v != nullptr && v[0] == '1';
-  }();
-  return on;
-}
-
-// TVFEM_MG_PAIRS=1: the one-row-per-wave pair prolongation instead of the 2 x 2 row blocks
-bool mg_pairs_experiment() {
-  static const bool on = [] {
-    const char* v = experiment_env("TVFEM_MG_PAIRS");
-    return v != nullptr && v[0] == '1';
-  }();
-  return on;
-}
-
 int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, 8192)); }
 // restriction: one coarse node per thread (27-point gathers: the coarse
 // levels' few hundred blocks must not serialise rounds -- 4 nodes per thread
@@ -726,17 +585,6 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
 #undef TV_RP
     return;
   }
-  if (x.coarse[0] && x.fn[0] >= 3) {  // by rows, lane-shared x gathers
-    const int nseg = (x.cn[0] + kWave - 1) / kWave;
-    const dim3 g((unsigned)((int64_t)x.cn[1] * (x.c_ke - x.c_kb) * nseg));
-    if (mask != nullptr)
-      hipLaunchKernelGGL(k_mg_restrict_rows<true>, g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c, xc,
-                         nseg);
-    else
-      hipLaunchKernelGGL(k_mg_restrict_rows<false>, g, dim3(kWave), 0, s, x, st, bf, wf, mask, bc, dinv_c, omega_c, xc,
-                         nseg);
-    return;
-  }
   if (mask != nullptr)
     hipLaunchKernelGGL(k_mg_restrict<true>, dim3(xfer_blocks(n)), dim3(kBlock), 0, s, x, st, bf, wf, mask, bc, dinv_c,
                        omega_c, xc);
@@ -745,14 +593,13 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
                        dinv_c, omega_c, xc);
 }
 
-bool mg_restrict_folds_faces(const MgXfer& x) { return x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment(); }
+bool mg_restrict_folds_faces(const MgXfer& x) { return x.coarse[0] && x.fn[0] >= 3; }
 
 bool mg_prolong_blocks(const MgXfer& x) {
-  return x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0 && !mg_rows_experiment() &&
-         !mg_pairs_experiment();
+  return x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0;
 }
 
-bool mg_prolong_smooths(const MgXfer& x) { return mg_prolong_blocks(x) && !mg_postsep_experiment(); }
+bool mg_prolong_smooths(const MgXfer& x) { return mg_prolong_blocks(x); }
 
 void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const double* xc, const double* mask,
                        hipStream_t s, const CoarsePost* cp) {
@@ -776,16 +623,10 @@ void launch_mg_prolong(const MgXfer& x, const PcgState* st, double* xf, const do
                          xf, xc, mask, nseg, nbj, CoarsePost{});
     return;
   }
-  if (x.coarse[0] && x.fn[0] >= 3 && !mg_rows_experiment()) {  // by rows, 16-byte fine pairs
+  if (x.coarse[0] && x.fn[0] >= 3) {  // by rows, 16-byte fine pairs
     const int nseg = ((x.fn[0] + 1) / 2 + kPairSeg - 1) / kPairSeg;
     const int64_t rows = (int64_t)x.fn[1] * (x.f_ke - x.f_kb);
     hipLaunchKernelGGL(k_mg_prolong_pairs, dim3((unsigned)(rows * nseg)), dim3(kWave), 0, s, x, st, xf, xc, mask, nseg);
-    return;
-  }
-  if (x.coarse[0] && x.fn[0] >= 3) {  // by rows, lane-shared x gathers
-    const int nseg = (x.fn[0] + kWave - 1) / kWave;
-    const int64_t rows = (int64_t)x.fn[1] * (x.f_ke - x.f_kb);
-    hipLaunchKernelGGL(k_mg_prolong_rows, dim3((unsigned)(rows * nseg)), dim3(kWave), 0, s, x, st, xf, xc, mask, nseg);
     return;
   }
   hipLaunchKernelGGL(k_mg_prolong, dim3((unsigned)((n + kPU * kBlock - 1) / (kPU * kBlock))), dim3(kBlock), 0, s, x, st, xf, xc, mask);

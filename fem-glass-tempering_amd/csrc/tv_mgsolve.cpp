@@ -1,0 +1,501 @@
+// Geometric multigrid on the box hierarchy: setup, per-Newton preparation and
+// the multigrid-preconditioned KSPCG (the reference's PCGAMG,
+// ThermoViscoProblem.py:343-346, replaced for rectilinear 3D meshes).
+#include "tv_ctx.h"
+
+namespace tv {
+// ---- geometric-multigrid preconditioned CG (options.preconditioner = GMG) ----
+// Gershgorin bound of D^-1 J on a rectilinear level: max over nodes of the
+// exact absolute row sum of the 27-point cell operator M + dt alpha K over its
+// diagonal (the tensor-product entries from the per-axis 1D rows), over the
+// distinct (row_x, row_y, row_z) combinations only.  The Robin facet rows are
+// facet masses (row sum / diagonal <= 2.25 for Q1 facets): floor 2.25, then 5 %.
+double mg_gershgorin(const std::vector<double> (&X)[3], double dt_alpha) {
+  using Row = std::array<double, 6>;  // M lo / di / up, K lo / di / up
+  std::vector<Row> rows[3];
+  for (int s = 0; s < 3; ++s) {
+    std::vector<double> cf;
+    axis_coefs(X[s], 0, (int)X[s].size(), cf);
+    for (size_t i = 0; i < X[s].size(); ++i) {
+      const double* c = &cf[i * C_NCOEF];
+      rows[s].push_back({c[C_MLO], c[C_MDI], c[C_MUP], c[C_KLO], c[C_KDI], c[C_KUP]});
+    }
+    std::sort(rows[s].begin(), rows[s].end());
+    rows[s].erase(std::unique(rows[s].begin(), rows[s].end()), rows[s].end());
+  }
+  double b = 0.0;
+  for (const Row& r0 : rows[0])
+    for (const Row& r1 : rows[1])
+      for (const Row& r2 : rows[2]) {
+        double sum = 0.0, diag = 0.0;
+        for (int a = 0; a < 3; ++a)
+          for (int bb = 0; bb < 3; ++bb)
+            for (int cc = 0; cc < 3; ++cc) {
+              const double v = r0[a] * r1[bb] * r2[cc] +
+                               dt_alpha * (r0[3 + a] * r1[bb] * r2[cc] + r0[a] * r1[3 + bb] * r2[cc] +
+                                           r0[a] * r1[bb] * r2[3 + cc]);
+              sum += std::fabs(v);
+              if (a == 1 && bb == 1 && cc == 1) diag = v;
+            }
+        b = std::max(b, sum / diag);
+      }
+  return std::max(b, 2.25) * 1.05;
+}
+
+template <class T>
+int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
+  void* p = nullptr;
+  HIPC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, h.size())));
+  L.bufs.push_back(p);
+  HIPC(hipMemcpy(p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  *out = static_cast<const T*>(p);
+  return TV_OK;
+}
+
+double mg_omega(double b) { return 2.0 / (1.1 * b); }
+
+// the hierarchy below the fine grid (single partition, 3D CG1 marching path)
+// the CG1 level of the box given by X (single partition), its vectors and weight
+int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da) {
+  c->mg.emplace_back();
+  MgLevel& L = c->mg.back();
+  for (int s = 0; s < 3; ++s) L.X[s] = X[s];
+  if (int e = build_cg_grid(c, 3, L.X, 0, (int)L.X[2].size(), 0, 0, true, true, L.g, L.coef, &L.bnodes, L.ffbuf))
+    return e;
+  const CgGrid& f = c->cg;  // thermal constants (set by setup_fields for both families)
+  L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
+  L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
+  L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+  for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
+    void* p = nullptr;
+    HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
+    HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)L.n, c->stream));
+    L.bufs.push_back(p);
+    *q = static_cast<double*>(p);
+  }
+  L.omega = mg_omega(mg_gershgorin(L.X, da));
+  return TV_OK;
+}
+
+// lambda_max(B^-1 J) of the DG1 operator by power iteration, B the cell blocks;
+// SIPG rows have no closed-form
+// Gershgorin bound here.  The smoother takes it with a 21 % margin
+int mg_dg_lambda(Ctx* c, const double* T, double* lam) {
+  const int64_t n = c->nT;
+  std::vector<double> h((size_t)n);
+  uint64_t st = 0x9E3779B97F4A7C15ull;
+  double nrm = 0.0;
+  for (int64_t t = 0; t < n; ++t) {  // fixed-seed xorshift start vector in (0.5, 1.5)
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    h[(size_t)t] = 0.5 + (double)(st >> 11) * (1.0 / 9007199254740992.0);
+    nrm += h[(size_t)t] * h[(size_t)t];
+  }
+  for (double& v : h) v /= std::sqrt(nrm);
+  HIPC(hipMemcpyAsync(c->mgx, h.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
+  else launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
+  std::vector<double> part(1024);
+  double l = 0.0;
+  for (int it = 0; it < 30; ++it) {
+    op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
+    if (c->dggface) launch_dg_bsmooth(c->dg, nullptr, c->w, nullptr, c->dggface, 1.0, c->w, 0, c->stream);  // in place, per cell
+    const int nb = launch_mg_pow(n, c->dggface ? nullptr : c->dinv, c->w, c->partials, c->stream);
+    HIPC(hipMemcpyAsync(part.data(), c->partials, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    double s2 = 0.0;
+    for (int b = 0; b < nb; ++b) s2 += part[(size_t)b];
+    l = std::sqrt(s2);  // ||D^-1 J x|| with ||x|| = 1
+    if (!(l > 0.0) || !std::isfinite(l)) return c->fail(TV_ERR_HIP, "GMG: DG eigenvalue estimate failed");
+    launch_mg_scale(n, c->w, 1.0 / l, c->mgx, c->stream);
+  }
+  *lam = l;
+  return TV_OK;
+}
+
+// The DG level-0 smoother weight omega0 = 2 / (1.21 lambda_max) is estimated
+// lazily, at the first multigrid solve (or V-cycle application), from the
+// temperature it will precondition -- the Robin term 4 a_rad T^3 of the cell
+// blocks vanishes at the T = 0 a freshly created context holds
+int mg_dg_weight(Ctx* c, const double* T) {
+  if (!c->mg_dg || c->mg_omega0 > 0.0) return TV_OK;
+  double lam = 0.0;
+  if (int e = mg_dg_lambda(c, T, &lam)) return e;
+  c->mg_omega0 = 2.0 / (1.1 * 1.1 * lam);
+  return TV_OK;
+}
+
+int mg_setup(Ctx* c) {
+  const bool dg = c->fam_T == TV_DG;
+  if (c->dim != 3 || c->um || (!dg && !cg_cgs_supported(c->cg)) || (dg && (c->dg.deg1 || c->dg.deg2)))
+    return c->fail(TV_ERR_ARG, "preconditioner GMG: 3D CG1 or DG1 temperature space on a rectilinear mesh only");
+  if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "preconditioner GMG: one partition (use TV_PC_JACOBI when partitioned)");
+  if (c->cgs) return c->fail(TV_ERR_ARG, "preconditioner GMG runs in the KSPCG form (pcg_variant KSPCG or AUTO)");
+  std::vector<double> tmp, Xf[3];
+  for (int s = 0; s < 3; ++s) Xf[s] = storage_coords(c, s, tmp);
+  const double da = c->P.dt * c->P.alpha;
+  HIPC(hipMalloc(&c->mgx, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
+  HIPC(hipMemsetAsync(c->mgx, 0, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT), c->stream));
+  if (dg) {
+    // level 1: the CG1 space of the same box (two-level DG -> CG, then the CG hierarchy)
+    c->mg_dg = true;
+    HIPC(hipMalloc(&c->dggface, sizeof(double) * (size_t)dg_gface_size(c->dg)));
+    c->mg_omega0 = 0.0;  // estimated at the first solve, at its T (mg_dg_weight)
+    if (int e = mg_add_cg_level(c, Xf, da)) return e;
+  } else {
+    c->mg_omega0 = mg_omega(mg_gershgorin(Xf, da));
+  }
+  const int max_levels = c->O.mg_levels > 0 ? c->O.mg_levels : 8;
+  const bool automatic = c->O.mg_levels <= 0;
+  std::vector<double> Xp[3] = {Xf[0], Xf[1], Xf[2]};
+  for (int lev = 1 + (dg ? 1 : 0); lev < max_levels; ++lev) {
+    double h = 1e300;  // smallest mean cell length over the axes
+    bool coarsen[3], any = false;
+    for (int s = 0; s < 3; ++s) {
+      const int cells = (int)Xp[s].size() - 1;
+      coarsen[s] = cells >= 2;
+      any = any || coarsen[s];
+      if (cells >= 1) h = std::min(h, (Xp[s].back() - Xp[s].front()) / cells);
+    }
+    // stop where the operator is mass-dominated: a Jacobi step is then a good solve
+    if (!any || (automatic && da / (h * h) <= 0.5)) break;
+    c->mg.emplace_back();
+    MgLevel& L = c->mg.back();
+    std::vector<char> is_c[3];  // fine node kept on this level
+    for (int s = 0; s < 3; ++s) {
+      const int nf = (int)Xp[s].size();
+      is_c[s].assign(nf, 1);
+      if (!coarsen[s]) {
+        L.X[s] = Xp[s];
+        continue;
+      }
+      // every other node, and the last one (an odd cell count keeps one fine cell at the end)
+      for (int i = 0; i < nf; ++i) is_c[s][i] = (i % 2 == 0 || i == nf - 1) ? 1 : 0;
+      for (int i = 0; i < nf; ++i)
+        if (is_c[s][i]) L.X[s].push_back(Xp[s][i]);
+    }
+    if (int e = build_cg_grid(c, 3, L.X, 0, (int)L.X[2].size(), 0, 0, true, true, L.g, L.coef, &L.bnodes, L.ffbuf))
+      return e;
+    const CgGrid& f = c->cg;
+    L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
+    L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
+    L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+      for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
+      void* p = nullptr;
+      HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
+      HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)L.n, c->stream));
+      L.bufs.push_back(p);
+      *q = static_cast<double*>(p);
+    }
+    L.omega = mg_omega(mg_gershgorin(L.X, da));
+    // transfer maps (finer level Xp -> this level)
+    MgXfer& x = L.xf;
+    for (int s = 0; s < 3; ++s) {
+      const int nf = (int)Xp[s].size(), nc = (int)L.X[s].size();
+      std::vector<int> pi(2 * (size_t)nf), ri(3 * (size_t)nc), cpos(nf, -1), fpos;
+      std::vector<double> pw(2 * (size_t)nf, 0.0), rw(3 * (size_t)nc, 0.0);
+      for (int i = 0; i < nf; ++i)
+        if (is_c[s][i]) {
+          cpos[i] = (int)fpos.size();
+          fpos.push_back(i);
+        }
+      for (int i = 0; i < nf; ++i) {
+        if (is_c[s][i]) {
+          pi[2 * i] = pi[2 * i + 1] = cpos[i];
+          pw[2 * i] = 1.0;
+        } else {  // linear interpolation between the coarse neighbours i - 1 and i + 1
+          const double wl = (Xp[s][i + 1] - Xp[s][i]) / (Xp[s][i + 1] - Xp[s][i - 1]);
+          pi[2 * i] = cpos[i - 1];
+          pi[2 * i + 1] = cpos[i + 1];
+          pw[2 * i] = wl;
+          pw[2 * i + 1] = 1.0 - wl;
+        }
+      }
+      for (int I = 0; I < nc; ++I) {  // R = P^T: the fine nodes that interpolate from I
+        const int fc = fpos[I];
+        for (int q = 0; q < 3; ++q) ri[3 * I + q] = fc;
+        rw[3 * I + 1] = 1.0;
+        if (fc - 1 >= 0 && !is_c[s][fc - 1]) {
+          ri[3 * I] = fc - 1;
+          rw[3 * I] = pw[2 * (fc - 1) + 1];  // fine fc - 1: its right coarse neighbour is I
+        }
+        if (fc + 1 < nf && !is_c[s][fc + 1]) {
+          ri[3 * I + 2] = fc + 1;
+          rw[3 * I + 2] = pw[2 * (fc + 1)];  // fine fc + 1: its left coarse neighbour is I
+        }
+      }
+      if (int e = mg_upload(c, L, pi, &x.pi[s])) return e;
+      if (int e = mg_upload(c, L, pw, &x.pw[s])) return e;
+      if (int e = mg_upload(c, L, ri, &x.ri[s])) return e;
+      if (int e = mg_upload(c, L, rw, &x.rw[s])) return e;
+      x.fn[s] = nf;
+      x.cn[s] = nc;
+      x.coarse[s] = coarsen[s] ? 1 : 0;
+    }
+    x.f_kb = 0;
+    x.f_ke = x.fn[2];
+    x.c_kb = 0;
+    x.c_ke = x.cn[2];
+    for (int s = 0; s < 3; ++s) Xp[s] = L.X[s];
+  }
+  c->mg_on = true;
+  return TV_OK;
+}
+
+// per Newton iteration: T injected down the hierarchy (DG: the vertex mean of
+// the cell-local values onto the CG level), coarse Jacobi diagonals
+
+void mg_prepare(Ctx* c, const double* T) {
+  // after the first call (dinv interiors in place): the CG levels below the
+  // base in two launches (launch_mg_prepare)
+  const size_t base = c->mg_dg ? 1 : 0;  // DG: level 1 is the vertex mean of the DG field
+  const size_t ncg = c->mg.size() - std::min(c->mg.size(), base);
+  bool ready = ncg > 0 && ncg <= (size_t)kMgPrepMax;
+  for (size_t l = base; l < c->mg.size() && ready; ++l)
+    ready = c->mg[l].dinv_interior && cg_uses_march(c->mg[l].g) && c->mg[l].g.bnodes != nullptr;
+  if (ready) {
+    if (base == 1) {
+      MgLevel& L = c->mg[0];
+      launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+      if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
+      launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream, true);
+    }
+    MgPrep p{};
+    p.nlev = (int)ncg;
+    p.Tbase = base == 1 ? c->mg[0].T : T;
+    for (size_t i = 0; i < ncg; ++i) {
+      MgLevel& L = c->mg[base + i];
+      p.xf[i] = L.xf;
+      p.T[i] = L.T;
+      p.dinv[i] = L.dinv;
+      p.g[i] = L.g;
+      p.off_n[i + 1] = p.off_n[i] + (L.n + 63) / 64 * 64;
+      p.off_b[i + 1] = p.off_b[i] + (L.g.n_bnodes + 63) / 64 * 64;
+    }
+    launch_mg_prepare(p, c->stream);
+    return;
+  }
+  const double* Tf = T;
+  for (size_t l = 0; l < c->mg.size(); ++l) {
+    MgLevel& L = c->mg[l];
+    if (l == 0 && c->mg_dg) {
+      launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+      if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
+    }
+    else launch_mg_inject(L.xf, Tf, L.T, c->stream);
+    launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream, L.dinv_interior);
+    L.dinv_interior = true;
+    Tf = L.T;
+  }
+}
+
+// V-cycle on coarse level l >= 1 (index l - 1 in c->mg): rhs b -> x; the
+// pre-smoothing step from 0 (x = omega D^-1 b) was formed by the restriction
+// that produced b.  The J x before the restriction is complete (k_cg_addfaces:
+// a per-node facet term inside the 27-point gather measured slower); the one
+// before the post-smoothing leaves the facet terms of the faces along the
+// march to that pointwise consumer (FaceAdd).
+// The prolongation from coarse level index ci (c->mg[ci]) into its finer level:
+// where that level has a post-smoothing step (not the coarsest) and the
+// 2 x 2 block prolongation runs, the step is applied on the fly (CoarsePost)
+// and mg_level skipped its k_mg_jacobi launch.
+void mg_prolong_from(Ctx* c, size_t ci, double* xf, const double* mask) {
+  MgLevel& C = c->mg[ci];
+  const bool smoothed = ci + 1 < c->mg.size() && mg_prolong_smooths(C.xf);
+  if (smoothed) {
+    const CoarsePost cp{C.b, C.w, C.dinv, C.omega, cg_face_add(C.g, 0)};
+    launch_mg_prolong(C.xf, c->st, xf, C.x, mask, c->stream, &cp);
+  } else {
+    launch_mg_prolong(C.xf, c->st, xf, C.x, mask, c->stream);
+  }
+}
+
+void mg_level(Ctx* c, size_t l) {
+  MgLevel& L = c->mg[l - 1];
+  hipStream_t s = c->stream;
+  if (l < c->mg.size()) {
+    const MgLevel& C = c->mg[l];
+    const FaceAdd fa = cg_face_add(L.g, 0);
+    if (fa.on && mg_restrict_folds_faces(C.xf)) {  // the restriction adds the facet terms (no k_cg_addfaces)
+      launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
+      launch_mg_restrict(C.xf, c->st, L.b, L.w, &fa, nullptr, C.b, C.dinv, C.omega, C.x, s);
+    } else {
+      launch_cg_japply(L.g, L.T, L.x, L.w, nullptr, nullptr, s, c->st);
+      launch_mg_restrict(C.xf, c->st, L.b, L.w, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
+    }
+    mg_level(c, l + 1);
+    mg_prolong_from(c, l, L.x, nullptr);
+    launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
+    // post-smoothing, unless the prolongation out of this level applies it (mg_prolong_from)
+    if (!mg_prolong_smooths(L.xf))
+      launch_mg_jacobi(L.n, c->st, L.b, L.w, &fa, L.dinv, L.omega, L.x, 1, s);
+  }
+}
+
+// level 0: x0 = omega dinv r is in c->mgx (k_mg_update); coarse correction,
+// post-smoothing into z with the (z.z, z.r) reduction tail
+int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
+  const int64_t n = c->nT;
+  hipStream_t s = c->stream;
+  const double* mask = c->dir_on ? c->dinv : nullptr;  // Dirichlet: the free subspace
+  if (c->mg_dg) {  // DG1 level 0: complete DG J x (Robin facets inline), vertex sums / injection to CG1
+    const DgGrid& d = c->dg;
+    MgLevel& C = c->mg[0];
+    launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+    launch_mg_dg_restrict(d.c0, d.c1, d.c2, c->st, c->r, c->w, mask, C.b, C.dinv, C.omega, C.x, s);
+    mg_level(c, 1);
+    launch_mg_dg_prolong(d.c0, d.c1, d.c2, c->st, c->mgx, C.x, mask, s);
+    launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+    if (c->dggface)
+      return launch_dg_bpost(d, c->st, c->mgx, c->r, c->w, c->dggface, c->mg_omega0, c->z, c->partials, tail, s);
+    return launch_mg_post(n, c->st, c->mgx, c->r, c->w, nullptr, c->dinv, c->mg_omega0, c->z, c->partials, tail, s);
+  }
+  const FaceAdd fa = cg_face_add(c->cg, 0);
+  if (!c->mg.empty()) {
+    MgLevel& C = c->mg[0];
+    // a complete J x (k_cg_addfaces) here: folding the facet terms into the
+    // restriction as on the coarse levels measured no gain on level 0
+    launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+    launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
+    mg_level(c, 1);
+    mg_prolong_from(c, 0, c->mgx, mask);
+  }
+  // J x, post-smoothing and (z.z, z.r) in the march epilogue (+ the side-face pass)
+  {
+    const int nrec = launch_cg_japply_post(c->cg, T, c->mgx, c->r, c->dinv, c->mg_omega0, c->z, c->st, c->partials,
+                                           tail, s);
+    if (nrec >= 0) return nrec;
+  }
+  launch_cg_japply_partial(c->cg, T, c->mgx, c->w, c->st, s);
+  return launch_mg_post(n, c->st, c->mgx, c->r, c->w, &fa, c->dinv, c->mg_omega0, c->z, c->partials, tail, s);
+}
+
+int mg_iteration(Ctx* c, const double* T, int it) {
+  const int64_t n = c->nT;
+  const int slot = c->ts_next + it;
+  uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
+  RedTail t1{c->counters, c->partials, c->sums, c->st, 2, ts};
+  int np = 0;
+  if (!op_japply_fused(c, T, &np, &t1, it))  // p <- z + b p ; w <- J p ; p.w ; alpha
+    if (int e = reduce_logic(c, np, 1, 2, 1)) return e;
+  const FaceAdd fa = c->mg_dg ? FaceAdd{} : cg_face_add(c->cg, 0);  // DG: w is complete
+  if (c->dggface)
+    launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
+                      c->stream);
+  else
+    launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
+                     c->stream);
+  RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 3, nullptr};
+  mg_apply0(c, T, &t2);  // z <- V(r); z.z, z.r; beta, convergence
+  return TV_OK;
+}
+
+int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
+  const int64_t n = c->nT;
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  // from pinned memory (an asynchronous upload; a pageable source is staged by
+  // the runtime -- no step-time change measured at C2 / C3 / C4)
+  c->h_st[2] = h;
+  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  mg_prepare(c, T);
+  if (int e = mg_dg_weight(c, T)) return e;
+  if (c->dggface)
+    launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
+                      c->stream);  // dx <- 0, x0 <- omega B^-1 r
+  else
+    launch_mg_update(n, c->st, c->pA, c->pB, c->w, nullptr, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
+                     c->stream);  // dx <- 0, x0 <- omega dinv r
+  RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 1, nullptr};
+  mg_apply0(c, T, &t0);  // z <- V(r); dp, beta (KSPCG init)
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
+  // an MG iteration is ~25 launches: the previous solve's count (hint) is queued
+  // right behind the init, with no host wait in between (the GPU would idle
+  // while the host enqueues ~100 launches; an init that already converged
+  // makes every queued launch exit at once), then one iteration at a time
+  // behind a poll.  The Newton solves of a step take near-constant counts, so
+  // the hint usually ends the solve at the first poll.
+  int launched = 0;
+  auto enqueue = [&](int nb) -> int {
+    for (int b = 0; b < nb; ++b)
+      if (int e = mg_iteration(c, T, launched + b)) return e;
+    launched += nb;
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[0], c->stream));
+    return TV_OK;
+  };
+  if (int e = enqueue(std::max(1, c->pcg_hint))) return e;
+  for (;;) {
+    HIPC(hipEventSynchronize(c->evp[0]));
+    if (c->h_st[0].done) break;
+    if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    if (int e = enqueue(1)) return e;
+  }
+  *its = c->h_st[0].it;
+  *reason = c->h_st[0].reason;
+  // level 0 updates dx in pairs of iterations from iteration 1 on (k_mg_update /
+  // k_dg_bupdate DXU): solves of 0 / 1 iterations and the last step of an odd-length one
+  launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
+  c->pcg_hint = std::max(1, c->h_st[0].it);
+  if (c->ktime) {
+    for (int it = 0; it < *its; it += c->kstride)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
+  }
+  return TV_OK;
+}
+
+}  // namespace tv
+
+using namespace tv;
+
+extern "C" {
+
+int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !r_dev || !z_dev) return TV_ERR_ARG;
+  if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "tv_precond_apply: one partition only");
+  hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
+  const double* T = c->f[TV_F_T].ptr;
+  const int64_t n = c->nT;
+  hipStream_t s = c->stream;
+  // the PC setup of the Newton iteration at this T
+  if (!c->dggface) {
+    if (!c->um && c->fam_T == TV_CG) {
+      launch_cg_diag(c->cg, T, c->dinv, 1, s, c->dinv_interior);
+      c->dinv_interior = true;
+    } else {
+      op_diag(c, T, c->dinv, 1);
+    }
+  }
+  // Dirichlet mode: the solve's preconditioner acts on the free subspace only
+  // (dinv = 0 on the constrained rows, as k_bc_lift sets it before every solve;
+  // the V-cycle masks its transfers with the same dinv)
+  if (c->dir_on && c->fam_T == TV_CG) launch_bc_mask(c, c->dinv);
+  if (c->mg_dg)
+    if (int e = mg_dg_weight(c, T)) return e;
+  if (!c->mg_on) {
+    launch_mg_jacobi(n, nullptr, r_dev, nullptr, nullptr, c->dinv, 1.0, z_dev, 0, s);  // z = dinv .* r
+  } else {
+    PcgState h{};  // running state: the V-cycle's kernels skip work once a solve is done
+    HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, s));
+    mg_prepare(c, T);
+    HIPC(hipMemcpyAsync(c->r, r_dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    if (c->dggface)  // x0 = omega0 B^-1 r (cell blocks)
+      launch_dg_bsmooth(c->dg, c->st, c->r, nullptr, c->dggface, c->mg_omega0, c->mgx, 0, s);
+    else
+      launch_mg_jacobi(n, c->st, c->r, nullptr, nullptr, c->dinv, c->mg_omega0, c->mgx, 0, s);
+    mg_apply0(c, T, nullptr);
+    HIPC(hipMemcpyAsync(z_dev, c->z, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(s));
+  return TV_OK;
+}
+
+}  // extern "C"

@@ -306,15 +306,21 @@ struct Output {
         j = q.front();
         q.pop_front();
       }
-      hipEventSynchronize(copied[j.set]);
-      // one thread per field: the page-cache copy of one fwrite is single-threaded
-      std::vector<std::thread> ws;
+      // a failed copy (device fault) must not append stale pinned data: the
+      // error is recorded and this step's write skipped
+      const hipError_t ce = hipEventSynchronize(copied[j.set]);
       std::vector<std::string> errs(field_n.size());
-      for (size_t k = 0; k < field_n.size(); ++k)
-        ws.emplace_back([&, k] {
-          if (!series.append_field(k, j.t, hstage[j.set] + field_off[k], field_n[k], errs[k])) return;
-        });
-      for (auto& w : ws) w.join();
+      if (ce != hipSuccess) {
+        errs[0] = std::string("output: device-to-host copy failed: ") + hipGetErrorString(ce);
+      } else {
+        // one thread per field: the page-cache copy of one fwrite is single-threaded
+        std::vector<std::thread> ws;
+        for (size_t k = 0; k < field_n.size(); ++k)
+          ws.emplace_back([&, k] {
+            if (!series.append_field(k, j.t, hstage[j.set] + field_off[k], field_n[k], errs[k])) return;
+          });
+        for (auto& w : ws) w.join();
+      }
       for (const auto& e : errs)
         if (!e.empty()) {
           std::lock_guard<std::mutex> lk(mu);
@@ -415,6 +421,16 @@ double* output_acquire(Output* o, int* set) {
 }
 size_t output_offset(const Output* o, size_t k) { return o->field_off[k]; }
 
+// gives an acquired set back without a write (its submission failed), so a
+// later output_acquire does not wait for it forever
+void output_release(Output* o, int set) {
+  {
+    std::lock_guard<std::mutex> lk(o->mu);
+    o->busy[set] = false;
+  }
+  o->cv.notify_all();
+}
+
 // the gathers into set `set` are queued on `compute`: copy after them on the
 // copy stream, then hand the set to the writer thread
 bool output_submit(Output* o, int set, double t, hipStream_t compute, std::string& err) {
@@ -423,6 +439,7 @@ bool output_submit(Output* o, int set, double t, hipStream_t compute, std::strin
           hipSuccess ||
       hipEventRecord(o->copied[set], o->copy) != hipSuccess) {
     err = "output: copy submission failed";
+    output_release(o, set);
     return false;
   }
   {

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kBlock) void k_pcg_init(int64_t n, const double* __
   block_partials<2>(acc, partials);
 }
 
-// Cache policy of the update's streams (TVFEM_NT bits, default 7): 1 = w, dx,
+// Cache policy of the update's streams (template bits, 7 in production): 1 = w, dx,
 // p_prev loads non-temporal, 2 = dx stores non-temporal, 4 = dinv load
 // non-temporal.  Only p (the next matvec's p_old) and z (its input) are written
 // or read with the default policy, so they are what the Infinity Cache keeps
@@ -281,11 +281,6 @@ __global__ __launch_bounds__(kBlock) void k_copy(double* __restrict__ d, const d
 }
 
 int vec_blocks(int64_t n) {
-  static int cap = -1;  // TVFEM_VEC_BLOCKS (experiment): fixed grid cap of the vector kernels
-  if (cap < 0) {
-    const char* e = experiment_env("TVFEM_VEC_BLOCKS");
-    cap = e ? std::min(kVecBlocksMax, std::max(64, atoi(e))) : 0;
-  }
   int64_t b = (n + kBlock - 1) / kBlock;
   // default: at least kVecNodesPerThread nodes per thread (four 4-node rounds of
   // the PCG update), between kVecBlocksMin and kVecBlocks workgroups.  Fewer
@@ -294,9 +289,8 @@ int vec_blocks(int64_t n) {
   // on 8 GPUs; 256 workgroups measured at or below 512 on every box, 128 worse);
   // at C4 on one GPU the cap of 1024 still holds.  (8 nodes per thread and load
   // round instead of 4: no gain at 1M nodes or at C4.)
-  const int64_t lim = cap ? cap
-                          : std::min<int64_t>(kVecBlocks, std::max<int64_t>(kVecBlocksMin,
-                                (n + (int64_t)kBlock * kVecNodesPerThread - 1) / ((int64_t)kBlock * kVecNodesPerThread)));
+  const int64_t lim = std::min<int64_t>(kVecBlocks, std::max<int64_t>(kVecBlocksMin,
+      (n + (int64_t)kBlock * kVecNodesPerThread - 1) / ((int64_t)kBlock * kVecNodesPerThread)));
   if (b > lim) b = lim;
   return b < 1 ? 1 : (int)b;
 }
@@ -350,26 +344,19 @@ void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* 
                        const RedTail* tail, const FaceAdd* fa, int it_host) {
   RedTail rt{};
   if (tail) rt = *tail;
-  static int nt = -1;  // TVFEM_NT: 7 (default) or 0 (every stream with the default policy)
-  if (nt < 0) {
-    const char* e = experiment_env("TVFEM_NT");
-    nt = (e && atoi(e) == 0) ? 0 : 7;
-  }
+  // non-temporal policy (7) on w, dinv, dx, p_prev: the Infinity Cache keeps z
+  // and p for the next matvec (measured against the default policy, round 1)
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
-  const int v = (fa && fa->on ? 4 : 0) | (nt ? 2 : 0) | (it_host & 1);
-#define TV_UPD(F, N, D)                                                                                       \
-  hipLaunchKernelGGL((k_pcg_update<F, N, D>), dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, \
+  const int v = (fa && fa->on ? 2 : 0) | (it_host & 1);
+#define TV_UPD(F, D)                                                                                          \
+  hipLaunchKernelGGL((k_pcg_update<F, 7, D>), dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, w, dinv, \
                      dx, z, partials, rt, f, it_host);                                                          \
   break
   switch (v) {
-    case 0: TV_UPD(false, 0, false);
-    case 1: TV_UPD(false, 0, true);
-    case 2: TV_UPD(false, 7, false);
-    case 3: TV_UPD(false, 7, true);
-    case 4: TV_UPD(true, 0, false);
-    case 5: TV_UPD(true, 0, true);
-    case 6: TV_UPD(true, 7, false);
-    default: TV_UPD(true, 7, true);
+    case 0: TV_UPD(false, false);
+    case 1: TV_UPD(false, true);
+    case 2: TV_UPD(true, false);
+    default: TV_UPD(true, true);
   }
 #undef TV_UPD
 }

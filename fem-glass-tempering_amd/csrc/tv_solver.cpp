@@ -1,0 +1,536 @@
+// The Newton + Krylov drivers of the heat solve and the viscoelastic step.
+//   newton               dolfinx NewtonSolver::solve, incremental criterion,
+//                        configured at ThermoViscoProblem.py:330-346 [3P]
+//   pcg_solve            PETSc KSPSolve_CG + PCJACOBI restated on the device
+//   pcg_solve_cgs        the single-reduction (Chronopoulos-Gear) form
+//   visco                _solve_Tf .. _solve_stress (ThermoViscoProblem.py:393-595)
+#include "tv_ctx.h"
+
+namespace tv {
+// --------------------------------------------------------------------------------------
+// operators
+// --------------------------------------------------------------------------------------
+void op_residual(Ctx* c, const double* T, const double* Tp, double* F) {
+  if (c->um) launch_um_residual(c->umg, T, Tp, F, c->stream);
+  else if (c->fam_T == TV_CG) launch_cg_residual(c->cg, T, Tp, F, c->stream);
+  else launch_dg_residual(c->dg, T, Tp, F, c->stream);
+}
+void op_diag(Ctx* c, const double* T, double* d, int invert) {
+  // Jacobian "assembly": the diagonal for the Jacobi PC (J(T) itself is matrix-free)
+  if (c->um) launch_um_diag(c->umg, T, d, invert, c->stream);
+  else if (c->fam_T == TV_CG) launch_cg_diag(c->cg, T, d, invert, c->stream);
+  else launch_dg_diag(c->dg, T, d, invert, c->stream);
+}
+void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
+  if (c->um) launch_um_japply(c->umg, T, x, y, c->stream);
+  else if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
+  else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
+}
+bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail, int it) {
+  if (c->um) {  // p <- z + b p, w <- J p, p.w and the reduction tail in one launch
+    *np = launch_um_japply_fused(c->umg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, it, tail, c->stream);
+    return tail && tail->counter;
+  }
+  if (c->fam_T == TV_CG)
+    return launch_cg_japply_fused(c->cg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail, it);
+  return launch_dg_japply_fused(c->dg, T, c->z, c->pA, c->pB, c->w, c->st, c->partials, np, c->stream, tail);
+}
+
+// --------------------------------------------------------------------------------------
+// Jacobi-PCG for J(T) dx = r  (PETSc KSPCG restated; see tv_pcg.hip)
+// --------------------------------------------------------------------------------------
+// it: index of this iteration within the solve (the device counter st->it
+// equals it until convergence, after which every kernel exits at once)
+
+// reads the pending timestamp slots back and adds them to the stats
+int ts_flush(Ctx* c) {
+  if (!c->d_ts) return TV_OK;
+  if (!c->ts_pending.empty()) {
+    std::vector<uint64_t> h((size_t)4 * c->ts_next);
+    HIPC(hipMemcpyAsync(h.data(), c->d_ts, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (int sl : c->ts_pending) {
+      const uint64_t* t = &h[(size_t)4 * sl];
+      for (int k = 0; k < 2; ++k) {
+        if (t[2 * k] == 0 || t[2 * k + 1] < t[2 * k]) continue;  // launch without a timed tail
+        c->ksum[k] += (double)(t[2 * k + 1] - t[2 * k]) / c->ts_khz;
+        c->kcnt[k] += 1;
+      }
+    }
+    c->ts_pending.clear();
+  }
+  c->ts_next = 0;
+  HIPC(hipMemsetAsync(c->d_ts, 0, (size_t)4 * kTsCap * sizeof(uint64_t), c->stream));
+  return TV_OK;
+}
+
+int pcg_iteration(Ctx* c, const double* T, int it) {
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  // timestamp slot of this iteration (see ts_flush); the matvec launchers
+  // without a reduction tail (DG, 1D/2D CG) leave theirs at 0
+  const int slot = c->ts_next + it;
+  uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
+  const bool multi = multi_rank(c);
+  // single GPU: the last-arriving workgroup of each launch reduces the partial
+  // records and runs the KSPCG scalar logic in-kernel (no separate reduce
+  // launch); multi-GPU: it only reduces, RCCL all-reduces, then the logic runs.
+  RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2, ts};
+  int np = 0;
+  const bool fused1 = op_japply_fused(c, T, &np, &t1, it);  // p <- z + b p ; w <- J p ; p.w
+  if (!fused1) {
+    if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
+  } else if (multi) {
+    if (int e = allreduce(c, c->sums, 1)) return e;
+    launch_logic(c->st, c->sums, 2, c->stream);
+  }
+  RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
+  const FaceAdd fa = (c->fam_T == TV_CG && !c->um) ? cg_face_add(c->cg, off) : FaceAdd{};
+  launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
+                    c->z + off, c->partials, c->stream, &t2, &fa, it);
+  if (multi) {  // dp, beta, convergence
+    if (int e = allreduce(c, c->sums, 2)) return e;
+    launch_logic(c->st, c->sums, 3, c->stream);
+  }
+  if (int e = halo(c, c->z)) return e;
+  return TV_OK;
+}
+
+int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  // state init
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  // from pinned memory (an asynchronous upload; a pageable source is staged by
+  // the runtime -- no step-time change measured at C2 / C3 / C4)
+  c->h_st[2] = h;
+  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  launch_pcg_init(n, c->r + off, c->dinv + off, c->z + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
+  if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 1, 0)) return e;
+  if (int e = halo(c, c->z)) return e;
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 4 * c->O.pcg_batch + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
+  // Batches of iterations are queued one ahead of the convergence poll: while
+  // the host waits for the state copied at the end of batch k, batch k + 1 is
+  // already in the stream, so the GPU never idles on the host's turnaround.
+  // After convergence the queued launches exit at their first instruction.
+  int launched = 0, slot = 0;
+  auto enqueue = [&](int nb, int k) -> int {
+    for (int b = 0; b < nb; ++b)
+      if (int e = pcg_iteration(c, T, launched + b)) return e;
+    launched += nb;
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[k], c->stream));
+    return TV_OK;
+  };
+  // batches queued behind the first: pcg_batch / 8 iterations (1 by default);
+  // the host's turnaround (~30 us) is well inside one iteration (~130 us at C4),
+  // and every iteration queued past convergence costs two early-exit launches
+  const int small = std::max(1, c->O.pcg_batch / 8);
+  if (int e = enqueue(std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
+  for (;;) {
+    if (int e = enqueue(small, slot ^ 1)) return e;
+    HIPC(hipEventSynchronize(c->evp[slot]));
+    if (c->h_st[slot].done) break;
+    if (launched > c->O.ksp_max_it + 2 * small + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    slot ^= 1;
+  }
+  // (the batch queued behind the converged one exits early; stream order covers it)
+  *its = c->h_st[slot].it;
+  *reason = c->h_st[slot].reason;
+  launch_pcg_dx_tail(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
+  c->pcg_hint = c->h_st[slot].it;
+  if (c->ktime) {  // productive iterations only (launches queued behind convergence exit at once)
+    for (int it = 0; it < *its; it += c->kstride)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
+  }
+  return TV_OK;
+}
+
+CgsBuffers cgs_buffers(Ctx* c, const double* T, int it) {
+  // iteration it reads parity (it - 1) & 1 and writes it & 1; r_0 is the Newton
+  // residual (c->r), read by iterations 0 and 1
+  CgsBuffers v{};
+  const int o = (it + 1) & 1, w = it & 1;
+  double* W[2] = {c->w, c->cw1};
+  v.T = T;
+  v.rin = (it <= 1) ? c->r : c->cr[o];
+  v.rout = c->cr[w];
+  v.sin = c->cs[o];
+  v.sout = c->cs[w];
+  v.win = W[o];
+  v.wout = W[w];
+  v.fin = c->cg.ffbuf[o];
+  v.fout = c->cg.ffbuf[w];
+  v.p = c->pA;
+  v.x = c->f[TV_F_DX].ptr;
+  v.dinv = c->dinv;
+  return v;
+}
+
+int cgs_iteration(Ctx* c, const double* T, int it) {
+  const bool multi = multi_rank(c);
+  const int slot = c->ts_next + it;
+  uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
+  const int kind = multi ? 0 : (it == 0 ? 4 : 5);
+  RedTail rt{c->counters, c->partials, c->sums, c->st, kind, ts};
+  const CgsBuffers v = cgs_buffers(c, T, it);
+  launch_cg_cgs(c->cg, it == 0, v, c->st, c->partials, c->stream, &rt, it, (multi && it > 0) ? c->sums : nullptr);
+  if (multi)
+    if (int e = cgs_exchange(c, v.wout, v.fout)) return e;
+  return TV_OK;
+}
+
+int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  // from pinned memory (an asynchronous upload; a pageable source is staged by
+  // the runtime -- no step-time change measured at C2 / C3 / C4)
+  c->h_st[2] = h;
+  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  // ghost planes of r_0 and diag^-1 (the halo rows recompute z there)
+  if (int e = halo(c, c->r)) return e;
+  if (int e = halo(c, c->dinv)) return e;
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 4 * c->O.pcg_batch + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
+  int launched = 0, slot = 0;
+  auto enqueue = [&](int nb, int k) -> int {
+    for (int b = 0; b < nb; ++b)
+      if (int e = cgs_iteration(c, T, launched + b)) return e;
+    launched += nb;
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[k], c->stream));
+    return TV_OK;
+  };
+  // iteration 0 and the first batch, then one more iteration queued behind
+  // every poll (see pcg_solve); multi-rank the state lags one launch
+  const int lag = multi_rank(c) ? 1 : 0;
+  const int small = 1 + lag;
+  if (int e = enqueue(1 + std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
+  for (;;) {
+    if (int e = enqueue(small, slot ^ 1)) return e;
+    HIPC(hipEventSynchronize(c->evp[slot]));
+    if (c->h_st[slot].done) break;
+    if (launched > c->O.ksp_max_it + 2 * small + 4) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    slot ^= 1;
+  }
+  *its = c->h_st[slot].it;
+  *reason = c->h_st[slot].reason;
+  c->pcg_hint = *its;
+  if (c->ktime) {
+    for (int it = 1; it <= *its; it += c->kstride)  // productive iterations (iteration 0 is the init launch)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
+  }
+  return TV_OK;
+}
+
+const char* reason_str(int r) {
+  switch (r) {
+    case R_DIV_ITS: return "DIVERGED_ITS";
+    case R_DIV_DTOL: return "DIVERGED_DTOL";
+    case R_DIV_INDEF_PC: return "DIVERGED_INDEFINITE_PC";
+    case R_DIV_NANINF: return "DIVERGED_NANORINF";
+    case R_DIV_INDEF_MAT: return "DIVERGED_INDEFINITE_MAT";
+    default: return "UNKNOWN";
+  }
+}
+
+// ---- Dirichlet mode ----------------------------------------------------------
+struct BndTest {
+  CgGrid g;
+  const unsigned char* mask;  // unstructured: boundary vertices (else nullptr)
+};
+__device__ __forceinline__ bool cg_on_boundary(const CgGrid& g, int64_t n);
+__device__ __forceinline__ bool on_boundary(const BndTest& b, int64_t n) {
+  return b.mask ? b.mask[n] != 0 : cg_on_boundary(b.g, n);
+}
+__device__ __forceinline__ bool cg_on_boundary(const CgGrid& g, int64_t n) {
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  const int k = (int)(n / plane);
+  const int64_t rem = n - (int64_t)k * plane;
+  const int j = (int)(rem / g.n0), i = (int)(rem - (int64_t)j * g.n0);
+  return (i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1]) || (j == 0 && g.bnd[1][0]) ||
+         (j == g.n1 - 1 && g.bnd[1][1]) || (k == 0 && g.bnd[2][0]) || (k == g.n2 - 1 && g.bnd[2][1]);
+}
+// dB = T - value on constrained nodes, 0 elsewhere (every local node)
+__global__ __launch_bounds__(kBlock) void k_bc_dvec(BndTest b, const double* __restrict__ T, double value,
+                                                    double* __restrict__ dB, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
+    dB[t] = on_boundary(b, t) ? T[t] - value : 0.0;
+}
+// F -= J dB (lifting; the constrained rows are never read: diag^-1 = 0 there)
+// and diag^-1 = 0 on constrained nodes, so z = B r and every Krylov vector
+// stay in the free subspace: PCG on P J P with the Jacobi preconditioner P B P
+__global__ __launch_bounds__(kBlock) void k_bc_lift(BndTest b, double* __restrict__ F, const double* __restrict__ JdB,
+                                                    double* __restrict__ dinv, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    F[t] -= JdB[t];
+    if (on_boundary(b, t)) dinv[t] = 0.0;
+  }
+}
+// dinv = 0 on the constrained rows only (tv_precond_apply: the solve's preconditioner)
+__global__ __launch_bounds__(kBlock) void k_bc_mask(BndTest b, double* __restrict__ dinv, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
+    if (on_boundary(b, t)) dinv[t] = 0.0;
+}
+// dx += dB (the constrained part of the Newton step: x - dx lands on the value)
+__global__ __launch_bounds__(kBlock) void k_bc_step(double* __restrict__ dx, const double* __restrict__ dB, int64_t n) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) dx[t] += dB[t];
+}
+
+void launch_bc_mask(Ctx* c, double* dinv) {
+  const int64_t n = c->nT;
+  const BndTest bt{c->cg, c->um ? c->um_bmask : nullptr};
+  hipLaunchKernelGGL(k_bc_mask, dim3((int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     c->stream, bt, dinv, n);
+}
+
+int dirichlet_pre(Ctx* c, const double* T) {
+  const int64_t n = c->nT;
+  const int blocks = (int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock);
+  const BndTest bt{c->cg, c->um ? c->um_bmask : nullptr};
+  hipLaunchKernelGGL(k_bc_dvec, dim3(blocks), dim3(kBlock), 0, c->stream, bt, T, c->dir_value, c->dB, n);
+  op_japply(c, T, c->dB, c->dtmp, nullptr, nullptr);
+  hipLaunchKernelGGL(k_bc_lift, dim3(blocks), dim3(kBlock), 0, c->stream, bt, c->r, c->dtmp, c->dinv, n);
+  HIPC(hipGetLastError());
+  return TV_OK;
+}
+
+// dolfinx NewtonSolver::solve, convergence_criterion = "incremental"
+int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
+  double* T = c->f[TV_F_T].ptr;
+  const double* Tp = c->f[TV_F_T_PREV].ptr;
+  // NonlinearProblem.form: ghost update of the state before the first F
+  // (ThermoViscoProblem.py:351 scatter_forward); every rank enters it, every step
+  if (int e = halo(c, T)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  int its = 0, kits = 0;
+  bool conv = false;
+  double r0 = 0.0, rn = 0.0;
+  // F(u); on the CG march path the residual's boundary pass also rewrites the
+  // boundary rows of dinv for the same u once the interior is in place
+  auto residual = [&]() -> bool {
+    if (!c->um && c->fam_T == TV_CG && c->dinv_interior)
+      if (launch_cg_residual_diag(c->cg, T, Tp, c->r, c->dinv, c->stream)) return true;
+    op_residual(c, T, Tp, c->r);
+    return false;
+  };
+  bool dinv_fresh = residual();
+  while (!conv && its < c->O.newton_max_it) {
+    if (!c->dggface) {  // J(u) (matrix-free) + Jacobi PC setup (DG GMG: cell blocks)
+      if (!c->um && c->fam_T == TV_CG) {
+        // the T-independent interior of dinv is written once; then the boundary nodes only
+        if (!dinv_fresh) launch_cg_diag(c->cg, T, c->dinv, 1, c->stream, c->dinv_interior);
+        c->dinv_interior = true;
+      } else {
+        op_diag(c, T, c->dinv, 1);
+      }
+    }
+    dinv_fresh = false;
+    const bool dir = c->dir_on && c->fam_T == TV_CG;
+    if (dir)
+      if (int e = dirichlet_pre(c, T)) return e;
+    int k = 0, reason = 0;
+    if (int e = (c->mg_on ? pcg_solve_mg(c, T, &k, &reason)
+                          : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
+      return e;
+    kits += k;
+    if (reason < 0)
+      return c->fail(TV_ERR_KSP, std::string("Krylov solver did not converge (") + reason_str(reason) + ")");
+    if (dir)
+      hipLaunchKernelGGL(k_bc_step, dim3((int)std::min<int64_t>(4096, (c->nT + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                         c->stream, c->f[TV_F_DX].ptr, c->dB, c->nT);
+    // u <- u - dx; ||dx||^2 by a separate one-block reduce (a reduction tail on
+    // the update's 1024 workgroups measured 7 us slower: 1024 serialised arrivals)
+    launch_newton_update(n, T + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
+    if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
+    HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (int e = halo(c, T)) return e;
+    HIPC(hipStreamSynchronize(c->stream));
+    rn = std::sqrt(c->h_sums[0]);
+    ++its;
+    if (its == 1) {
+      r0 = rn;  // residual0 = ||dx_1||; no test at the first iteration
+      conv = false;
+    } else {
+      const double rel = rn / r0;
+      conv = (rel < c->O.newton_rtol) || (rn < c->O.newton_atol);
+    }
+    // dolfinx assembles F after every update; in the incremental criterion that
+    // last F is never read, so it is assembled only when another iteration follows.
+    if (!conv && its < c->O.newton_max_it) dinv_fresh = residual();
+  }
+  HIPC(hipGetLastError());
+  c->last_newton = its;
+  c->last_krylov = kits;
+  c->last_dx = rn;
+  if (out_its) *out_its = its;
+  if (out_kits) *out_kits = kits;
+  if (out_conv) *out_conv = conv ? 1 : 0;
+  if (!conv && c->O.error_on_nonconvergence)
+    return c->fail(TV_ERR_NOT_CONVERGED, "Newton solver did not converge because maximum number of iterations reached");
+  return TV_OK;
+}
+
+// --------------------------------------------------------------------------------------
+// viscoelastic update
+// --------------------------------------------------------------------------------------
+void visco_setup(Ctx* c, ViscoConst& k, ViscoFields& v) {
+  const tv_params& P = c->P;
+  k.H_over_Rg = P.H / P.Rg;
+  k.inv_Tb = 1.0 / P.Tb;
+  k.dt = P.dt;
+  k.half_dt = P.dt / 2;
+  k.alpha_s = P.alpha_solid;
+  k.dalpha = P.alpha_liquid - P.alpha_solid;
+  k.inv_dim = 1.0 / c->dim;
+  k.chi = 0.5;  // ViscoelasticModel.py:15
+  k.paper = (c->O.model_mode == TV_MODEL_PAPER) ? 1 : 0;
+  for (int i = 0; i < 6; ++i) {
+    k.lambda_m[i] = P.lambda_m[i]; k.m_n[i] = P.m_n[i];
+    k.lambda_g[i] = P.lambda_g[i]; k.g_n[i] = P.g_n[i];
+    k.lambda_k[i] = P.lambda_k[i]; k.k_n[i] = P.k_n[i];
+  }
+  std::memset(&v, 0, sizeof(v));
+  v.sT = c->nT;
+  v.sS = c->nS;
+  v.T = c->f[TV_F_T].ptr; v.Tp = c->f[TV_F_T_PREV].ptr; v.Tn = c->f[TV_F_T_NEXT].ptr;
+  v.phi = c->f[TV_F_PHI].ptr; v.phin = c->f[TV_F_PHI_NEXT].ptr; v.xi = c->f[TV_F_XI].ptr;
+  v.Tf = c->f[TV_F_TF].ptr; v.Tfp = c->f[TV_F_TF_PARTIAL].ptr;
+  v.th = c->f[TV_F_THERMAL_STRAIN].ptr; v.tot = c->f[TV_F_TOTAL_STRAIN].ptr; v.dev = c->f[TV_F_DEVIATORIC_STRAIN].ptr;
+  v.ds = c->f[TV_F_DS_PARTIAL].ptr; v.dsig = c->f[TV_F_DSIGMA_PARTIAL].ptr;
+  v.st = c->f[TV_F_S_TILDE].ptr; v.sgt = c->f[TV_F_SIGMA_TILDE].ptr;
+  v.sp = c->f[TV_F_S_PARTIAL].ptr; v.sgp = c->f[TV_F_SIGMA_PARTIAL].ptr;
+  v.sigma = c->f[TV_F_SIGMA].ptr;
+  v.tflag = c->tflag;
+  v.Tfo = c->Tfo;
+}
+
+int visco(Ctx* c, bool copy_Tprev) {
+  ViscoConst k;
+  ViscoFields v;
+  visco_setup(c, k, v);
+  const int all = c->O.materialize ? 1 : 0;
+  if (c->fam_T == c->fam_S) {
+    v.n = c->ownT_n;
+    v.off_T = c->ownT_off;
+    v.off_S = c->ownS_off;
+    v.copy_Tprev = copy_Tprev ? 1 : 0;
+    launch_visco(c->dim, all, k, v, c->stream);
+    if (copy_Tprev && c->ownT_off > 0) {  // ghost planes of T_prev
+      launch_copy(v.Tp, v.T, c->ownT_off, c->stream);
+    }
+    if (copy_Tprev && c->nT > c->ownT_off + c->ownT_n) {
+      const int64_t o = c->ownT_off + c->ownT_n;
+      launch_copy(v.Tp + o, v.T + o, c->nT - o, c->stream);
+    }
+  } else {
+    v.n = c->ownT_n;
+    v.off_T = c->ownT_off;
+    launch_visco_Tpass(c->dim, all, k, v, c->stream);
+    v.n = c->ownS_n;
+    v.off_S = c->ownS_off;
+    v.map = c->map;
+    launch_visco_Spass(c->dim, all, k, v, c->stream);
+    if (copy_Tprev) launch_copy(v.Tp, v.T, c->nT, c->stream);
+  }
+  HIPC(hipGetLastError());
+  return TV_OK;
+}
+
+}  // namespace tv
+
+using namespace tv;
+
+extern "C" {
+
+int tv_residual(void* ctx, const double* T_dev, double* F_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !T_dev || !F_dev) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
+  op_residual(c, T_dev, c->f[TV_F_T_PREV].ptr, F_dev);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_jacobian_apply(void* ctx, const double* x_dev, double* y_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !x_dev || !y_dev) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
+  op_japply(c, c->f[TV_F_T].ptr, x_dev, y_dev, nullptr, nullptr);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_jacobian_diag(void* ctx, double* d_dev) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !d_dev) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
+  op_diag(c, c->f[TV_F_T].ptr, d_dev, 0);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  return newton(c, newton_its, krylov_its, converged);
+}
+
+
+int tv_visco_update(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  if (int e = visco(c, false)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  hipSetDevice(c->device);
+  int conv = 0;
+  if (int e = newton(c, newton_its, krylov_its, &conv)) return e;
+  if (!thermal_only) {
+    if (c->ktime) HIPC(hipEventRecord(c->vev[0], c->stream));
+    if (int e = visco(c, true)) return e;  // includes T_prev <- T (ThermoViscoProblem.py:378-379)
+    if (c->ktime) {
+      HIPC(hipEventRecord(c->vev[1], c->stream));
+      HIPC(hipEventSynchronize(c->vev[1]));
+      float a = 0.f;
+      HIPC(hipEventElapsedTime(&a, c->vev[0], c->vev[1]));
+      c->ksum[2] += a;
+      c->kcnt[2] += 1;
+    }
+  } else {
+    launch_copy(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, c->stream);
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+}  // extern "C"

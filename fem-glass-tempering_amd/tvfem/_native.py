@@ -17,6 +17,8 @@ TV_CG, TV_DG = 0, 1
 TV_PCG_AUTO, TV_PCG_KSPCG, TV_PCG_SINGLE_REDUCTION = 0, 1, 2
 TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
 TV_PC_JACOBI, TV_PC_GMG = 0, 1
+TV_DG_KERNEL_AUTO, TV_DG_KERNEL_TILE, TV_DG_KERNEL_CELLS = 0, 1, 2
+ABI_VERSION = 3
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -80,7 +82,8 @@ class Options(C.Structure):
                 ("error_on_nonconvergence", C.c_int), ("ksp_rtol", C.c_double), ("ksp_atol", C.c_double),
                 ("ksp_dtol", C.c_double), ("ksp_max_it", C.c_int), ("materialize", C.c_int),
                 ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
-                ("model_mode", C.c_int), ("preconditioner", C.c_int), ("mg_levels", C.c_int)]
+                ("model_mode", C.c_int), ("preconditioner", C.c_int), ("mg_levels", C.c_int),
+                ("dg_kernel", C.c_int), ("dg_tile_chunk", C.c_int)]
 
 
 _lib = None
@@ -155,7 +158,7 @@ def load_library():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.tv_abi_version() != 2:
+    if lib.tv_abi_version() != ABI_VERSION:
         raise NativeError(TV_ERR_ARG, "libtvfem ABI version mismatch")
     _lib = lib
     return lib

@@ -146,10 +146,33 @@ def interval_mesh(length, n_cells):
 
 # gmsh element types and the gmsh -> tensor (l = a + 2b + 4c) vertex order
 _GMSH_TYPES = {1: (1, 2, [0, 1]), 3: (2, 4, [0, 1, 3, 2]), 5: (3, 8, [0, 1, 3, 2, 4, 5, 7, 6])}
+# topological dimension of the gmsh element types this reader does NOT support
+# (triangles, tetrahedra, prisms, pyramids, higher-order lines / quads / hexes)
+_GMSH_UNSUPPORTED = {2: 2, 4: 3, 6: 3, 7: 3, 8: 1, 9: 2, 10: 2, 11: 3, 12: 3, 13: 3, 14: 3, 16: 2, 17: 3, 18: 3,
+                     19: 3, 20: 2, 21: 2, 22: 2, 23: 2, 24: 2, 25: 2, 26: 1, 27: 1, 28: 1, 29: 3, 30: 3, 31: 3,
+                     36: 2, 37: 2, 38: 2, 92: 3, 93: 3}
+_GMSH_NAMES = {2: "3-node triangle", 4: "4-node tetrahedron", 6: "6-node prism", 7: "5-node pyramid",
+               8: "3-node line", 9: "6-node triangle", 10: "9-node quadrilateral", 11: "10-node tetrahedron",
+               12: "27-node hexahedron", 16: "8-node quadrilateral", 17: "20-node hexahedron"}
+
+
+def _elem_dim(etype):
+    """Topological dimension of a gmsh element type (0 for points), None if unknown."""
+    if etype == 15:
+        return 0
+    if etype in _GMSH_TYPES:
+        return _GMSH_TYPES[etype][0]
+    return _GMSH_UNSUPPORTED.get(etype)
 
 
 def _read_msh_raw(path):
-    """nodes {tag: (x, y, z)} and elements {dim: [node tags in gmsh order]}."""
+    """nodes {tag: (x, y, z)} and elements {dim: [node tags in gmsh order]}.
+
+    Every element type in the file is recorded: a top-dimension element that is
+    not a 2-node line, 4-node quadrilateral or 8-node hexahedron (a triangle,
+    tetrahedron, prism, pyramid or a second-order cell) raises ValueError rather
+    than being skipped, which would leave a hole in the domain with spurious
+    Robin boundaries (or read a triangle mesh as its boundary lines)."""
     with open(path, "r") as fh:
         lines = [ln.strip() for ln in fh]
     try:
@@ -163,6 +186,7 @@ def _read_msh_raw(path):
     ei = lines.index("$Elements")
     nodes = {}
     elems = {1: [], 2: [], 3: []}
+    seen = set()  # every element type in the file
     if version < 3:
         n = int(lines[ni + 1])
         for k in range(n):
@@ -171,6 +195,7 @@ def _read_msh_raw(path):
         m = int(lines[ei + 1])
         for k in range(m):
             t = [int(v) for v in lines[ei + 2 + k].split()]
+            seen.add(t[1])
             if t[1] in _GMSH_TYPES:
                 d, nn, _ = _GMSH_TYPES[t[1]]
                 ntags = t[2]
@@ -190,12 +215,26 @@ def _read_msh_raw(path):
         pos = ei + 2
         for _ in range(nblocks):
             _, _, etype, nb = (int(v) for v in lines[pos].split()[:4])
+            if nb > 0:
+                seen.add(etype)
             for q in range(nb):
                 t = [int(v) for v in lines[pos + 1 + q].split()]
                 if etype in _GMSH_TYPES:
                     d, nn, _ = _GMSH_TYPES[etype]
                     elems[d].append(t[1:1 + nn])
             pos += 1 + nb
+    dims = {}
+    for et in seen:
+        d = _elem_dim(et)
+        if d is None:
+            raise ValueError(f"{path}: unsupported gmsh element type {et}")
+        dims.setdefault(d, set()).add(et)
+    top = max(dims, default=0)
+    bad = sorted(et for et in dims.get(top, ()) if et not in _GMSH_TYPES)
+    if bad:
+        names = ", ".join(_GMSH_NAMES.get(et, f"type {et}") for et in bad)
+        raise ValueError(f"{path}: {top}D cells of unsupported element types ({names}); "
+                         "libtvfem reads 2-node lines, 4-node quadrilaterals and 8-node hexahedra")
     return nodes, elems
 
 

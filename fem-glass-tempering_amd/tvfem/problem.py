@@ -103,7 +103,7 @@ class ThermoViscoProblem:
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
                  write_output: bool = False, output_dir: str = "output", preconditioner: str = "jacobi",
-                 mg_levels: int = 0) -> None:
+                 mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -135,6 +135,12 @@ class ThermoViscoProblem:
                              "(geometric multigrid on the box hierarchy)")
         self.preconditioner = preconditioner
         self._mg_levels = int(mg_levels)
+        if dg_kernel not in ("auto", "tile", "cells"):
+            raise ValueError("dg_kernel must be 'auto' (= 'tile', the marching tile kernel) or 'cells' "
+                             "(one thread per cell, the reference evaluation)")
+        self._dg_kernel = {"auto": N.TV_DG_KERNEL_AUTO, "tile": N.TV_DG_KERNEL_TILE,
+                           "cells": N.TV_DG_KERNEL_CELLS}[dg_kernel]
+        self._dg_tile_chunk = int(dg_tile_chunk)
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -208,6 +214,8 @@ class ThermoViscoProblem:
         opts.model_mode = N.TV_MODEL_PAPER if self.model_mode == "paper" else N.TV_MODEL_REFERENCE
         opts.preconditioner = N.TV_PC_GMG if self.preconditioner == "gmg" else N.TV_PC_JACOBI
         opts.mg_levels = self._mg_levels
+        opts.dg_kernel = self._dg_kernel
+        opts.dg_tile_chunk = self._dg_tile_chunk
         ctx = C.c_void_p()
         create = lib.tv_create_unstructured if um else lib.tv_create
         N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))

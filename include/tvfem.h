@@ -51,7 +51,8 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 2  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels */
+#define TV_ABI_VERSION 3  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+                            3: dg_kernel, dg_tile_chunk */
 
 /* status codes */
 #define TV_OK 0
@@ -132,7 +133,16 @@ typedef struct {
   int model_mode;         /* TV_MODEL_REFERENCE (default) / TV_MODEL_PAPER       */
   int preconditioner;     /* TV_PC_JACOBI (default) / TV_PC_GMG                  */
   int mg_levels;          /* GMG: levels incl. the fine one (0: automatic)       */
+  int dg_kernel;          /* 3D DG1 Jacobian: TV_DG_KERNEL_AUTO / _TILE / _CELLS */
+  int dg_tile_chunk;      /* planes per marching DG tile (0: automatic = 5)      */
 } tv_options;
+
+/* 3D DG1 Jacobian kernel: AUTO = TILE, the marching tile kernel (production);
+ * CELLS = one thread per cell, the straightforward SIPG evaluation the tile
+ * kernel is checked against (tests/test_gpu_parity.py). */
+#define TV_DG_KERNEL_AUTO 0
+#define TV_DG_KERNEL_TILE 1
+#define TV_DG_KERNEL_CELLS 2
 
 /* Preconditioner of the Krylov solve (the reference configures PCGAMG,
  * ThermoViscoProblem.py:343-346; PETSc's GAMG is not reproducible here):

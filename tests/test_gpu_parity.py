@@ -324,15 +324,15 @@ def test_in_solve_kernel_timing():
         assert 0.0 < st[kid][0] < 50.0, st
 
 
-def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
-    """The marching DG1 Jacobian (k_dg_tile; TVFEM_DG_TILE 1: 6 computing + 2
-    halo waves, 2 (default): 8 computing waves whose edge waves load the halo
-    rows) against the one-thread-per-cell kernel (k_dg_cells, itself pinned to
+def test_dg_tile_kernel_matches_cell_kernel():
+    """The marching DG1 Jacobian (k_dg_tile: 8 computing waves whose edge waves
+    load the halo rows; tv_options.dg_kernel TILE, the default) against the
+    one-thread-per-cell kernel (k_dg_cells, dg_kernel CELLS, itself pinned to
     the oracle above) on a grid large enough for two x segments, several row
-    tiles (13 rows, 6 or 8 per tile) and several march chunks (7 planes in
-    chunks of 2 and 5): J x at a random T (1e-12) and one coupled time step
-    through the fused PCG matvec (T 1e-10).  The oracle itself is too slow to
-    assemble DG1 at this size."""
+    tiles (13 rows, 8 per tile) and several march chunks (7 planes in chunks of
+    2, 3 and 5): J x at a random T (1e-12) and one coupled time step through the
+    fused PCG matvec (T 1e-10).  The oracle itself is too slow to assemble DG1 at
+    this size."""
     torch = _torch()
     from tvfem import RectilinearMesh
     from tvfem.problem import ThermoViscoProblem
@@ -341,12 +341,9 @@ def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
     cfg = {"T": DG, "sigma": DG}
     rng = np.random.default_rng(3)
     out = {}
-    monkeypatch.setenv("TVFEM_EXPERIMENTS", "1")  # the kernel-variant switches below are gated by it
-    for tile, chunk in ((0, 5), (1, 2), (1, 5), (2, 2), (2, 5)):
-        monkeypatch.setenv("TVFEM_DG_TILE", str(tile))
-        monkeypatch.setenv("TVFEM_DG_CHUNK", str(chunk))
+    for kern, chunk in (("cells", 0), ("tile", 2), ("tile", 3), ("auto", 0)):
         p = ThermoViscoProblem(RectilinearMesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
-                               part_axis=2, materialize=False, verbose=False)
+                               part_axis=2, materialize=False, verbose=False, dg_kernel=kern, dg_tile_chunk=chunk)
         p.setup()
         p.solve_timestep()
         T1 = p.get_field("T")
@@ -359,10 +356,10 @@ def test_dg_tile_kernel_matches_cell_kernel(monkeypatch):
         xd = torch.tensor(device_layout(p, x, "DG"), dtype=torch.float64, device="cuda")
         yd = torch.zeros_like(xd)
         assert p._lib.tv_jacobian_apply(p._ctx, xd.data_ptr(), yd.data_ptr()) == 0
-        out[(tile, chunk)] = (T1, host_layout(p, yd.cpu().numpy(), "DG"))
+        out[(kern, chunk)] = (T1, host_layout(p, yd.cpu().numpy(), "DG"))
         p.close()
-    T_ref, y_ref = out[(0, 5)]
-    for key in ((1, 2), (1, 5), (2, 2), (2, 5)):
+    T_ref, y_ref = out[("cells", 0)]
+    for key in (("tile", 2), ("tile", 3), ("auto", 0)):
         T1, y = out[key]
         assert relerr(y, y_ref) < 1e-12, key
         assert relerr(T1, T_ref) < 1e-10, key

@@ -64,6 +64,52 @@ def test_graded_bar_geometry(tmp_path):
     assert h[0] < 0.2 and h[len(h) // 2] > 2.0  # fine at the surface, coarse in the core
 
 
+_MIXED_22 = """$MeshFormat
+2.2 0 8
+$EndMeshFormat
+$Nodes
+5
+1 0 0 0
+2 1 0 0
+3 1 1 0
+4 0 1 0
+5 2 0.5 0
+$EndNodes
+$Elements
+{n}
+{elems}$EndElements
+"""
+
+
+@pytest.mark.parametrize("extra,ok", [("", True), ("6 2 2 0 1 2 5 3\n", False), ("6 15 2 0 1 5\n", True),
+                                      ("6 1 2 0 1 2 5\n", True)])
+def test_msh_element_types_checked(tmp_path, extra, ok):
+    """Every element type is recorded: a quadrilateral mesh with a triangle among
+    its 2D cells is rejected instead of read with a hole (boundary lines and
+    points alongside the quads are fine)."""
+    from tvfem.mesh import read_msh
+    base = "1 3 2 0 1 1 2 3 4\n2 1 2 0 1 1 2\n3 1 2 0 1 2 3\n4 1 2 0 1 3 4\n5 1 2 0 1 4 1\n"
+    body = base + extra
+    p = tmp_path / "mixed.msh"
+    p.write_text(_MIXED_22.format(n=body.count("\n"), elems=body))
+    if ok:
+        m = read_msh(str(p))
+        assert m.dim == 2 and m.num_cells == 1
+    else:
+        with pytest.raises(ValueError, match="3-node triangle"):
+            read_msh(str(p))
+
+
+def test_msh_triangle_only_mesh_rejected(tmp_path):
+    """A triangle-only 2D mesh must not fall back to its boundary lines (a 1D bar)."""
+    from tvfem.mesh import read_msh
+    body = "1 2 2 0 1 1 2 3\n2 2 2 0 1 1 3 4\n3 1 2 0 1 1 2\n4 1 2 0 1 2 3\n"
+    p = tmp_path / "tri.msh"
+    p.write_text(_MIXED_22.format(n=4, elems=body))
+    with pytest.raises(ValueError, match="unsupported element types"):
+        read_msh(str(p))
+
+
 def test_bad_mesh_rejected(tmp_path):
     from tvfem.mesh import RectilinearMesh, read_msh
     with pytest.raises(ValueError):

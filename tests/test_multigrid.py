@@ -224,7 +224,7 @@ def _omega(axes, da):
 
 
 def _vcycle_reference(axes, T, mp, dt, levels):
-    """The box hierarchy of tv_api.cpp mg_setup restated with the oracle's
+    """The box hierarchy of tv_mgsolve.cpp mg_setup restated with the oracle's
     assembled Jacobians: every other node plus the last one along each axis with
     >= 2 cells, P = linear interpolation (kron of the per-axis maps), R = P^T,
     coarse J(T) re-assembled with T injected, damped Jacobi before and after the

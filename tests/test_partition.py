@@ -139,6 +139,32 @@ def test_partitioned_run_matches_single_partition(world, pcg):
 
 
 @pytest.mark.gpu
+def test_auto_krylov_form_agrees_across_ranks():
+    """pcg_variant AUTO must pick the same Krylov form on every rank (the two
+    forms issue different collectives).  A 400 x 292 x 50 plate on 2 ranks gives
+    slabs of 146 and 147 planes of 401 x 51 nodes, 2.986M and 3.006M owned nodes,
+    on both sides of the 3M single-reduction bound: the choice follows the
+    largest slab, so both ranks take KSPCG."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tvfem import box_mesh
+    from tvfem.problem import ThermoViscoProblem
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from partition_check import CFG, MP
+    mesh = box_mesh([50.0, 36.5, 5.0], [400, 292, 50])
+    forms, owned = [], []
+    for part in range(2):
+        p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, n_parts=2, part=part, part_axis=1, verbose=False,
+                               materialize=False, pcg_variant="auto")
+        forms.append(p.pcg_variant)
+        owned.append(p.num_dofs(0)[0])
+        p.close()
+    assert owned[0] < 3_000_000 < owned[1], owned
+    assert forms == ["kspcg", "kspcg"], forms
+
+
+@pytest.mark.gpu
 def test_partitioned_host_edit_on_one_rank():
     """A host-side in-place edit of T made by one rank only (a local hot spot
     after setup()) must neither hang the other rank nor leave stale ghost
