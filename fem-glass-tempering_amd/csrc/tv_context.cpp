@@ -885,6 +885,11 @@ int tv_set_initial_condition(void* ctx, double T0) {
 
 // ---- time-series output (ThermoViscoProblem.py:246-276, 357-364, 614-620) ----
 int tv_output_open(void* ctx, const char* dir, const int* field_ids, int n_fields) {
+  return tv_output_open_named(ctx, dir, field_ids, nullptr, n_fields);
+}
+
+int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const char* const* series_names,
+                         int n_fields) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !dir || !field_ids || n_fields < 1) return TV_ERR_ARG;
   if (c->out) return c->fail(TV_ERR_STATE, "output already open");
@@ -917,7 +922,13 @@ int tv_output_open(void* ctx, const char* dir, const int* field_ids, int n_field
     const FieldInfo& fi = c->f[id];
     const bool dg = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
     const int64_t n = (fi.space == 0) ? c->ownT_n : c->ownS_n;
-    if (!output_add_field(o, names[id], fi.bs, dg, (size_t)n * fi.bs, err)) {
+    const char* nm = (series_names && series_names[k] && series_names[k][0]) ? series_names[k] : names[id];
+    for (const char* q = nm; *q; ++q)
+      if (*q == '/' || *q == '\\') {
+        output_destroy(o);
+        return c->fail(TV_ERR_ARG, "output: a series name must not contain a path separator");
+      }
+    if (!output_add_field(o, nm, fi.bs, dg, (size_t)n * fi.bs, err)) {
       output_destroy(o);
       return c->fail(TV_ERR_STATE, "output: " + err);
     }

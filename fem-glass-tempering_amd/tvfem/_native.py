@@ -37,7 +37,7 @@ EXPORTS = [
     "tv_jacobian_diag", "tv_precond_apply", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
     "tv_comm_get_unique_id", "tv_comm_init", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes", "tv_kernel_timing", "tv_kernel_stats",
     "tv_last_stats", "tv_comm_init_host", "tv_partition_layout", "tv_pcg_variant",
-    "tv_set_dirichlet", "tv_output_open", "tv_output_write", "tv_output_close", "tv_xdmf_open",
+    "tv_set_dirichlet", "tv_output_open", "tv_output_open_named", "tv_output_write", "tv_output_close", "tv_xdmf_open",
     "tv_xdmf_add_field", "tv_xdmf_append", "tv_xdmf_close",
 ]
 
@@ -147,6 +147,7 @@ def load_library():
         "tv_pcg_variant": (C.c_int, [vp, ip]),
         "tv_set_dirichlet": (C.c_int, [vp, C.c_int, C.c_double]),
         "tv_output_open": (C.c_int, [vp, C.c_char_p, ip, C.c_int]),
+        "tv_output_open_named": (C.c_int, [vp, C.c_char_p, ip, C.POINTER(C.c_char_p), C.c_int]),
         "tv_output_write": (C.c_int, [vp, C.c_double]),
         "tv_output_close": (C.c_int, [vp]),
         "tv_xdmf_open": (vp, [C.c_char_p, C.c_int, ip, C.POINTER(dp)]),

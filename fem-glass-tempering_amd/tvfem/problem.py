@@ -15,8 +15,10 @@ Differences that are part of the contract:
   * the linear solver is matrix-free Jacobi-PCG (reference: CG + GAMG); T and
     sigma agree with the CPU restatement within the tolerances stated in
     tests/;
-  * file output (:246-276, VTX / XDMF there) is XDMF over raw binary here
-    and written only with ``write_output=True`` (into ``output_dir``).
+  * file output (:246-276, VTX / XDMF there) is XDMF over raw binary here,
+    written by default as the reference does (T, phi, Tf, xi and sigma every
+    step into ``output_dir`` = "output"); ``write_output=False`` opts out
+    (the benchmark, tests).
 """
 from __future__ import annotations
 
@@ -98,11 +100,16 @@ class Function:
 
 
 class ThermoViscoProblem:
+    # setup() opens the output writers unless write_output=False is passed: the
+    # reference always writes (ThermoViscoProblem.py:182, 246-276, 374).
+    # tests/conftest.py turns the default off for the test session.
+    WRITE_OUTPUT_DEFAULT = True
+
     def __init__(self, mesh_path, time: tuple, dt: float, config: dict, model_parameters: dict,
                  jit_options: dict | None = None, *, device: int = 0, materialize: bool = True,
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
-                 write_output: bool = False, output_dir: str = "output", preconditioner: str = "jacobi",
+                 write_output: bool | None = None, output_dir: str = "output", preconditioner: str = "jacobi",
                  mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
@@ -127,7 +134,7 @@ class ThermoViscoProblem:
         if model_mode not in ("reference", "paper"):
             raise ValueError("model_mode must be 'reference' (the reference as it runs) or 'paper'")
         self.model_mode = model_mode
-        self.write_output = write_output
+        self.write_output = self.WRITE_OUTPUT_DEFAULT if write_output is None else bool(write_output)
         self.output_dir = output_dir
         self._output_open = False
         if preconditioner not in ("jacobi", "gmg"):
@@ -322,12 +329,24 @@ class ThermoViscoProblem:
             # solve as dolfinx NonlinearProblem(bcs=[bc]) applies it
             N.check(self._lib.tv_set_dirichlet(self._ctx, 1, float(self.physical_model.T_ambient)), self._ctx)
         self.dirichlet_bc = bool(dirichlet_bc)
+        self._outfile_names = (outfile_name, outfile_name1)
         if self.write_output:
             self._write_initial_output(t=self.t)
 
     # the reference's five series (ThermoViscoProblem.py:246-276): T, phi, Tf,
     # xi and sigma, as XDMF over raw binary (tvfem.xdmf reads them back)
     OUTPUT_FIELDS = ("T", "phi", "Tf", "xi", "sigma")
+
+    def series_names(self, outfile_name: str = "visco", outfile_name1: str = "stresses"):
+        """File stems of the five series.  With setup()'s defaults they are the
+        reference's own file names (output/T, phi, Tf, xi and sigma,
+        ThermoViscoProblem.py:249-268, which never reads the two arguments);
+        a non-default ``outfile_name`` prefixes the four scalar series
+        (``<outfile_name>_T`` ...) and a non-default ``outfile_name1`` names the
+        stress series."""
+        pre = "" if outfile_name == "visco" else f"{outfile_name}_"
+        sig = "sigma" if outfile_name1 == "stresses" else outfile_name1
+        return [f"{pre}{f}" for f in self.OUTPUT_FIELDS[:4]] + [sig]
 
     def _write_initial_output(self, t: float = 0.0) -> None:
         import os
@@ -337,7 +356,10 @@ class ThermoViscoProblem:
             d = os.path.join(d, f"part{self._part}")
         os.makedirs(d, exist_ok=True)
         ids = (C.c_int * len(self.OUTPUT_FIELDS))(*[N.FIELD_ID[f] for f in self.OUTPUT_FIELDS])
-        N.check(self._lib.tv_output_open(self._ctx, d.encode(), ids, len(self.OUTPUT_FIELDS)), self._ctx)
+        names = (C.c_char_p * len(self.OUTPUT_FIELDS))(*[n.encode() for n in self.series_names(
+            *getattr(self, "_outfile_names", ("visco", "stresses")))])
+        N.check(self._lib.tv_output_open_named(self._ctx, d.encode(), ids, names, len(self.OUTPUT_FIELDS)),
+                self._ctx)
         self._output_open = True
         self._write_output(t)
 

@@ -289,6 +289,11 @@ int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its);
  * the files while the next steps run; it blocks only when two writes are still
  * in flight.  tv_output_close drains.  A partition writes its owned nodes. */
 int tv_output_open(void* ctx, const char* dir, const int* field_ids, int n_fields);
+/* as tv_output_open, with the file stem of each series (<dir>/<name>.xdmf);
+ * a NULL array or entry keeps the field's own name (setup()'s outfile_name /
+ * outfile_name1, ThermoViscoProblem.py:176-178) */
+int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const char* const* series_names,
+                         int n_fields);
 int tv_output_write(void* ctx, double t);
 int tv_output_close(void* ctx);
 /* The file format without a GPU (tests, tools): a rectilinear mesh as

@@ -12,6 +12,11 @@ for p in (PKG, ROOT):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X GPU and the built libtvfem.so")
+    # the reference writes its five output series every step, and so does
+    # ThermoViscoProblem by default; the test session turns that off (tests that
+    # check the writers pass write_output=True, and python main.py keeps it on)
+    from tvfem.problem import ThermoViscoProblem
+    ThermoViscoProblem.WRITE_OUTPUT_DEFAULT = False
 
 
 @pytest.fixture(scope="session")

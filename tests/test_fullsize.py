@@ -1,8 +1,14 @@
-"""Parity at BASELINE.json's full sizes through size-independent properties
-(the oracle cannot assemble 8M dofs in a test's time).
+"""Parity at BASELINE.json's full sizes.
 
-C4 (400 x 400 x 50 CG1 hex, 8.2M dofs) and C5 (200 x 200 x 25 DG1, 8M dofs) on
-the 50 x 50 x 5 plate of bench.py:
+C3 (200 x 200 x 25 CG1 hex, 1.05M dofs, coupled): pinned to the oracle at full
+size -- its own residual (HeatForm.residual, one vectorised assembly) at the
+device's converged T, and its own visco_update (OracleProblem.visco_update)
+applied to the device's T / T_prev / Tf / Tf_partial, against every state field
+the device wrote (test_c3_fullsize_steps_pinned_to_oracle).
+
+C3, C4 (400 x 400 x 50 CG1 hex, 8.2M dofs) and C5 (200 x 200 x 25 DG1, 8M dofs)
+on the 50 x 50 x 5 plate of bench.py, through size-independent properties (the
+oracle cannot run a Newton solve at these sizes in a test's time):
   * J(T) is symmetric: y.(J x) = x.(J y) for random x, y (SIPG and the Robin
     facet terms included);
   * J(T0) 1 sums to |Omega| + dt dg(T0) |dOmega| at a uniform T0: the stiffness
@@ -20,7 +26,7 @@ import pytest
 from oracle import tv_oracle as O
 
 L = (50.0, 50.0, 5.0)
-SIZES = {"C4": ("CG", (400, 400, 50)), "C5": ("DG", (200, 200, 25))}
+SIZES = {"C3": ("CG", (200, 200, 25)), "C4": ("CG", (400, 400, 50)), "C5": ("DG", (200, 200, 25))}
 
 
 def _torch():
@@ -30,12 +36,12 @@ def _torch():
     return torch
 
 
-def _problem(fam, nc, pc):
+def _problem(fam, nc, pc, part_axis=1):
     from tvfem import box_mesh
     from tvfem.problem import ThermoViscoProblem
     cfg = {"T": {"element": fam, "degree": 1}, "sigma": {"element": fam, "degree": 1}}
     return ThermoViscoProblem(box_mesh(L, nc), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False,
-                              materialize=False, part_axis=1, preconditioner=pc)
+                              materialize=False, part_axis=part_axis, preconditioner=pc)
 
 
 @pytest.mark.gpu
@@ -111,3 +117,56 @@ def test_fullsize_gmg_step_matches_jacobi_step(case):
     assert ng == nj
     assert kg * 3 <= kj
     assert rg < 1e-6 and rj < 1e-6, (rg, rj)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc", ["jacobi", "gmg"])
+def test_c3_fullsize_steps_pinned_to_oracle(pc):
+    """C3 at full size (200 x 200 x 25 CG1/CG1, 1,050,426 T-dofs, coupled, 6-term
+    Prony), three steps with the default (Jacobi) and the multigrid
+    preconditioner.  After every step:
+      * the oracle's residual F(T_dev; T_prev) (ThermoViscoProblem.py:293-306,
+        oracle HeatForm.residual) is <= 1e-10 relative to F(T_prev; T_prev), the
+        residual the step started from;
+      * the oracle's viscoelastic pipeline (OracleProblem.visco_update,
+        ViscoelasticModel.py:100-228 in the order of ThermoViscoProblem.py:393-595)
+        run on the device's T, T_prev and pre-step Tf / Tf_partial reproduces
+        the device's phi, Tf, Tf_partial (1e-12), xi and sigma (check_field:
+        rel. 1e-6 on the dofs with |T - T_prev| > 1e-6 K, >= 90 % of them, the
+        rest bounded in absolute terms).
+    part_axis=2 keeps the device's storage order equal to the oracle's dof order."""
+    _torch()
+    from parity_util import check_field, cond_mask, relerr
+    fam, nc = SIZES["C3"]
+    dev = _problem(fam, nc, pc, part_axis=2)
+    dev.setup()
+    mesh = O.box_mesh(L, nc)
+    cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+    ref = O.OracleProblem(mesh, (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS))
+    ref.setup()
+    hf = ref.form
+    assert hf.congruent and ref.VT.n == dev.num_dofs(0)[0] == 1_050_426
+    for step in range(3):
+        Tp = dev.get_field("T")  # T_prev of this step (T_prev <- T ended the last one)
+        Tf0, Tfp0 = dev.get_field("Tf"), dev.get_field("Tf_partial")
+        dev.solve_timestep()
+        T1 = dev.get_field("T")
+        F0 = np.linalg.norm(hf.residual(Tp, Tp))
+        F1 = np.linalg.norm(hf.residual(T1, Tp))
+        print(f"[c3 {pc}] step {step}: Newton {dev.last_newton_iterations}, Krylov {dev.last_krylov_iterations}, "
+              f"|F(T1)| / |F(T0)| = {F1 / F0:.2e}, |T1 - T0| max {np.abs(T1 - Tp).max():.3e} K")
+        assert F1 <= 1e-10 * F0, (step, F1, F0)
+        # the oracle's visco pipeline on the device's inputs
+        ref.functions_current["T"][:] = T1
+        ref.functions_previous["T"][:] = Tp
+        for fd in (ref.functions_current, ref.functions_previous):
+            fd["Tf"][:] = Tf0
+            fd["Tf_partial"][:] = Tfp0
+        ref.visco_update()
+        mT, _ = cond_mask(T1, Tp)
+        assert relerr(dev.get_field("phi"), ref.functions["phi"]) < 1e-12
+        assert relerr(dev.get_field("Tf"), ref.functions_current["Tf"]) < 1e-12
+        assert relerr(dev.get_field("Tf_partial"), ref.functions_current["Tf_partial"]) < 1e-12
+        check_field("xi", dev.get_field("xi"), ref.functions["xi"], mT, min_frac=0.9)
+        check_field("sigma", dev.get_field("sigma"), ref.functions_next["sigma"], mT, bs=9, min_frac=0.9)
+    dev.close()

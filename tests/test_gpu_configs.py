@@ -99,6 +99,13 @@ def test_c1_main_py_script_runs(tmp_path):
     assert sum(ln.startswith("t=") for ln in lines) == 500
     assert lines[-1].startswith("Solve finished in ")
     assert (tmp_path / "mesh1d.msh").exists()
+    # the five output series every step, as the reference writes them
+    # (ThermoViscoProblem.py:182, 246-276, 374): the initial state + 500 steps
+    from tvfem.xdmf import read_series
+    for f in ("T", "phi", "Tf", "xi", "sigma"):
+        s = read_series(str(tmp_path / "output" / f"{f}.xdmf"))
+        assert len(s["times"]) == 501, f
+        assert abs(s["times"][-1] - 50.0) < 1e-9
 
 
 def test_c1_main_py_surface_matches_oracle(tmp_path):

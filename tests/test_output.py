@@ -106,3 +106,82 @@ def test_async_output_matches_device_fields(tmp_path):
         X = s["geometry"]
     # geometry in physical coordinates for the (x, z, y) storage order of part_axis=1
     assert np.isclose(X[:, 0].max(), 2.0) and np.isclose(X[:, 1].max(), 2.0) and np.isclose(X[:, 2].max(), 1.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fam", ["CG", "DG"])
+def test_output_series_match_oracle(tmp_path, fam):
+    """The five written series (T, phi, Tf, xi, sigma: ThermoViscoProblem.py:246-276
+    at setup, :357-364 after every step) against the ORACLE's fields of the same
+    steps (oracle/tv_oracle.py OracleProblem, run alongside): T and Tf rel. L2
+    <= 1e-10, phi <= 1e-9, xi and sigma by check_field (rel. 1e-6 on the dofs
+    whose T changed by more than 1e-6 K in that step, the rest bounded), at the
+    initial output and after each of four steps.  part_axis=2 keeps the written
+    node order equal to the oracle's dof order.  Also checks setup()'s default
+    series names (the reference's T, phi, Tf, xi, sigma)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tvfem import box_mesh
+    from tvfem.problem import ThermoViscoProblem
+    from tvfem.xdmf import read_series
+    from oracle import tv_oracle as O
+    from parity_util import check_field, cond_mask, relerr
+    cfg = {"T": {"element": fam, "degree": 1}, "sigma": {"element": fam, "degree": 1}}
+    L, nc = [2.0, 2.0, 1.0], [10, 8, 5]
+    dev = ThermoViscoProblem(box_mesh(L, nc), (0.0, 0.4), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), part_axis=2,
+                             verbose=False, write_output=True, output_dir=str(tmp_path))
+    ref = O.OracleProblem(O.box_mesh(L, nc), (0.0, 0.4), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), linear="pcg")
+    dev.setup()
+    ref.setup()
+    snaps = [{"T": ref.functions_current["T"].copy(), "phi": ref.functions["phi"].copy(),
+              "Tf": ref.functions_current["Tf"].copy(), "xi": ref.functions["xi"].copy(),
+              "sigma": ref.functions_next["sigma"].copy(), "T_before": ref.functions_current["T"].copy()}]
+    with np.errstate(all="ignore"):
+        for _ in range(4):
+            T_before = ref.functions_current["T"].copy()
+            dev.t += dev.dt
+            dev.solve_timestep()
+            ref.solve_timestep()
+            snaps.append({"T": ref.functions_current["T"].copy(), "phi": ref.functions["phi"].copy(),
+                          "Tf": ref.functions_current["Tf"].copy(), "xi": ref.functions["xi"].copy(),
+                          "sigma": ref.functions_next["sigma"].copy(), "T_before": T_before})
+    dev.close()  # drains the writer
+    series = {f: read_series(str(tmp_path / f"{f}.xdmf")) for f in ("T", "phi", "Tf", "xi", "sigma")}
+    for f, s in series.items():
+        assert s["times"] == pytest.approx([0.0, 0.1, 0.2, 0.3, 0.4]), f
+    for k, sn in enumerate(snaps):
+        got = {f: series[f]["values"][k].ravel() for f in series}
+        assert relerr(got["T"], sn["T"]) <= 1e-10, k
+        assert relerr(got["Tf"], sn["Tf"]) <= 1e-10, k
+        assert relerr(got["phi"], sn["phi"]) <= 1e-9, k
+        if k == 0:  # the initial output: xi and sigma are the zero-initialised functions
+            assert not got["xi"].any() and not got["sigma"].any()
+            continue
+        mT, _ = cond_mask(sn["T"], sn["T_before"])
+        check_field(f"xi step {k}", got["xi"], sn["xi"], mT)
+        check_field(f"sigma step {k}", got["sigma"], sn["sigma"], mT, bs=9)
+
+
+@pytest.mark.gpu
+def test_output_series_names_follow_setup_arguments(tmp_path):
+    """setup(outfile_name=..., outfile_name1=...) (ThermoViscoProblem.py:176-178):
+    the defaults give the reference's file names; other values prefix the four
+    scalar series and name the stress series."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tvfem import box_mesh
+    from tvfem.problem import ThermoViscoProblem
+    from tvfem.xdmf import read_series
+    from oracle import tv_oracle as O
+    cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+    p = ThermoViscoProblem(box_mesh([1.0, 1.0, 1.0], [4, 4, 4]), (0.0, 0.2), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                           verbose=False, write_output=True, output_dir=str(tmp_path))
+    assert p.series_names() == ["T", "phi", "Tf", "xi", "sigma"]
+    p.setup(outfile_name="run1", outfile_name1="stress_run1")
+    p.solve()
+    for stem in ("run1_T", "run1_phi", "run1_Tf", "run1_xi", "stress_run1"):
+        s = read_series(str(tmp_path / f"{stem}.xdmf"))
+        assert len(s["times"]) == 3, stem
+    p.close()

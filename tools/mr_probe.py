@@ -12,7 +12,7 @@ mp = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
       "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0, "Rg": 8.314, "alpha_solid": 9.1e-6, "alpha_liquid": 25.1e-6}
 cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 mesh = box_mesh([2.0, 4.0, 1.0], [8, 16, 4])
-prob = ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, mp, device=0, n_parts=world, part=rank, part_axis=1, verbose=False)
+prob = ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, mp, device=0, n_parts=world, part=rank, part_axis=1, verbose=False, write_output=False)
 lib, ctx = prob._lib, prob._ctx
 buf = C.create_string_buffer(lib.tv_comm_unique_id_size())
 if rank == 0:

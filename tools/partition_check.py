@@ -32,7 +32,7 @@ CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree":
 
 def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False):
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
-                           verbose=False, pcg_variant=pcg)
+                           verbose=False, pcg_variant=pcg, write_output=False)
     if comm is not None:
         comm(p)
     p.setup()

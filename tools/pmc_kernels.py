@@ -36,7 +36,7 @@ nc = [int(v) for v in a.cells.split(",")]
 cfg = {"T": {"element": a.family, "degree": 1}, "sigma": {"element": a.family, "degree": 1}}
 um = a.mesh == "distorted"
 mesh = (distorted_box_mesh if um else box_mesh)([50.0, 50.0, 5.0], nc)
-prob = ThermoViscoProblem(mesh, (0.0, 1.0), 0.1, cfg, dict(MP), materialize=False,
+prob = ThermoViscoProblem(mesh, (0.0, 1.0), 0.1, cfg, dict(MP), materialize=False, write_output=False,
                           verbose=False, **({} if um else {"part_axis": 1}))
 prob.setup()
 prob.solve_timestep()
