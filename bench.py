@@ -56,8 +56,9 @@ def parse():
                     help="box: the rectilinear plate (tensor-product kernels); distorted: the same plate as a "
                          "general hexahedral mesh (jittered, sheared, warped; element-local kernels, one GPU)")
     ap.add_argument("--pc", choices=["auto", "jacobi", "gmg"], default="auto",
-                    help="preconditioner: gmg (geometric multigrid on the box hierarchy; 3D box, one "
-                         "partition), jacobi, or auto (gmg where it applies and the mesh has >= 4M T-dofs)")
+                    help="preconditioner: gmg (geometric multigrid on the box hierarchy, 3D box; distributed "
+                         "over the ranks when partitioned), jacobi, or auto (gmg where it applies and the mesh "
+                         "has >= 4M T-dofs, at every rank count)")
     ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto",
                     help="Krylov form: single-reduction (Chronopoulos-Gear, 3D CG) or PETSc KSPCG as written")
@@ -107,7 +108,9 @@ def main():
         # C3 4.06 vs 3.19 ms; C4 13.4 vs 19.8 ms, C5 16.5 vs 32.5 ms)
         cells = nc[0] * nc[1] * nc[2]
         big = cells * (8 if a.family == "DG" else 1) >= 4_000_000
-        pc = "gmg" if (not um and world == 1 and a.pcg != "single" and big) else "jacobi"
+        # the same solver at every rank count: partitioned boxes run the distributed
+        # V-cycle (tv_mgdist.cpp), so N = 1 and N > 1 lines compare like with like
+        pc = "gmg" if (not um and a.pcg != "single" and big) else "jacobi"
     kw = {} if um else {"n_parts": world, "part": rank, "part_axis": 1}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
                               verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,

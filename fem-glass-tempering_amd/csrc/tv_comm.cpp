@@ -11,8 +11,10 @@ namespace tv {
 // --------------------------------------------------------------------------------------
 bool multi_rank(const Ctx* c) { return c->nranks > 1 && (c->comm || c->host_sendrecv); }
 
-int halo_host(Ctx* c, double* v) {
-  const CgGrid& g = c->cg;
+// ghost planes of v on grid g (the fine grid or a distributed multigrid level:
+// one plane per interface, storage axis 2): send the first / last owned plane,
+// receive into ghost plane 0 / n2 - 1
+int halo_host(Ctx* c, const CgGrid& g, double* v) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
   double* s_lo = c->h_halo;
   double* s_hi = c->h_halo + plane;
@@ -31,10 +33,9 @@ int halo_host(Ctx* c, double* v) {
   return TV_OK;
 }
 
-int halo(Ctx* c, double* v) {
-  if (!multi_rank(c) || c->fam_T != TV_CG) return TV_OK;
-  if (c->host_sendrecv) return halo_host(c, v);
-  const CgGrid& g = c->cg;
+int halo_grid(Ctx* c, const CgGrid& g, double* v) {
+  if (!multi_rank(c)) return TV_OK;
+  if (c->host_sendrecv) return halo_host(c, g, v);
   const int64_t plane = (int64_t)g.n0 * g.n1;
   NCCLC(ncclGroupStart());
   if (g.g_lo) {  // neighbour rank-1: send first owned plane, receive ghost plane 0
@@ -46,6 +47,34 @@ int halo(Ctx* c, double* v) {
     NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
   }
   NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
+int halo(Ctx* c, double* v) {
+  if (!multi_rank(c) || c->fam_T != TV_CG) return TV_OK;
+  return halo_grid(c, c->cg, v);
+}
+
+// sum of a device vector over the ranks, in place (the agglomerated coarse
+// levels of the partitioned multigrid: each rank contributes the coarse nodes
+// its owned fine nodes restrict to, zeros elsewhere)
+int allreduce_vec(Ctx* c, double* v, int64_t n) {
+  if (!multi_rank(c) || n <= 0) return TV_OK;
+  if (c->host_allreduce) {
+    if (c->h_big_n < (size_t)n) {
+      if (c->h_big) HIPC(hipHostFree(c->h_big));
+      c->h_big = nullptr;
+      HIPC(hipHostMalloc(&c->h_big, sizeof(double) * (size_t)n));
+      c->h_big_n = (size_t)n;
+    }
+    HIPC(hipMemcpyAsync(c->h_big, v, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (c->host_allreduce(c->h_big, (int)n, c->host_user)) return c->fail(TV_ERR_COMM, "host allreduce failed");
+    HIPC(hipMemcpyAsync(v, c->h_big, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));  // h_big is reused by the next call
+    return TV_OK;
+  }
+  NCCLC(ncclAllReduce(v, v, (size_t)n, ncclDouble, ncclSum, c->comm, c->stream));
   return TV_OK;
 }
 

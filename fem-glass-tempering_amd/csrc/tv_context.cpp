@@ -399,7 +399,8 @@ int setup_fields(Ctx* c) {
     }
   }
   c->cgs = can && (var == TV_PCG_SINGLE_REDUCTION ||
-                   (var == TV_PCG_AUTO && c->n_parts > 1 && max_slab <= kCgsAutoMaxNodes));
+                   (var == TV_PCG_AUTO && c->n_parts > 1 && max_slab <= kCgsAutoMaxNodes &&
+                    c->O.preconditioner != TV_PC_GMG));  // the multigrid solve runs in the KSPCG form
   if (c->cgs) {
     for (double** q : {&c->cr[0], &c->cr[1], &c->cs[0], &c->cs[1], &c->cw1}) {
       HIPC(hipMalloc(q, nb));
@@ -510,6 +511,8 @@ void tv_default_options(tv_options* o) {
   o->mg_levels = 0;
   o->dg_kernel = TV_DG_KERNEL_AUTO;
   o->dg_tile_chunk = 0;
+  o->mg_replicate_nodes = 0;
+  o->ksp_fixed_its = 0;
 }
 
 
@@ -737,6 +740,7 @@ int tv_destroy(void* ctx) {
     if (L.bnodes) hipFree(L.bnodes);
     for (int q = 0; q < 2; ++q)
       if (L.ffbuf[q]) hipFree(L.ffbuf[q]);
+    if (L.mask) hipFree(L.mask);
   }
   if (c->mgx) hipFree(c->mgx);
   if (c->dggface) hipFree(c->dggface);
@@ -756,6 +760,8 @@ int tv_destroy(void* ctx) {
   if (c->h_st) hipHostFree(c->h_st);
   if (c->h_sums) hipHostFree(c->h_sums);
   if (c->h_halo) hipHostFree(c->h_halo);
+  if (c->h_big) hipHostFree(c->h_big);
+  if (c->mg_mask0) hipFree(c->mg_mask0);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);

@@ -56,6 +56,15 @@ struct MgLevel {
   double* ffbuf[2] = {nullptr, nullptr};
   std::vector<void*> bufs;   // T, b, x, w, dinv and the transfer maps
   bool dinv_interior = false;  // dinv holds the T-independent interior diagonal
+  // partitioned contexts (tv_mgdist.cpp): a distributed level is this rank's
+  // slab of the global level with one ghost plane per interface (dist); a
+  // replicated level is the whole global level on every rank.  first2 = global
+  // plane of local plane 0 along storage axis 2; [inj0, inj1) = the local
+  // planes whose T this rank injects (its coarse planes)
+  bool dist = false;
+  int first2 = 0;
+  int inj0 = 0, inj1 = 0;
+  double* mask = nullptr;    // the level above the replicated ones: 1 owned / 0 ghost
 };
 
 struct Ctx {
@@ -107,6 +116,12 @@ struct Ctx {
   double mg_omega0 = 0.0;
   double* mgx = nullptr;    // level-0 V-cycle iterate
   double* dggface = nullptr; // DG level 0: facet means of dg(T) for the cell-block Jacobi smoother
+  // partitioned GMG (tv_mgdist.cpp): levels 0 .. mg_A - 1 are distributed over
+  // the partitions, mg_A .. the coarsest are replicated on every rank
+  int mg_A = 0;
+  double* mg_mask0 = nullptr;  // level 0 restriction mask when mg_A == 1 (1 owned / 0 ghost)
+  double* h_big = nullptr;     // pinned staging of vector all-reduces (host-staged transport)
+  size_t h_big_n = 0;
   // unstructured mesh (tv_create_unstructured, tv_um.hip)
   bool um = false;
   UmGrid umg{};
@@ -191,6 +206,8 @@ int transfer(Ctx* c, int field, double* host, size_t n, int dir);
 // ---- tv_comm.cpp ----
 bool multi_rank(const Ctx* c);
 int halo(Ctx* c, double* v);  // ghost planes of a T-space vector of the fine grid
+int halo_grid(Ctx* c, const CgGrid& g, double* v);  // ghost planes of a vector of grid g (a GMG level)
+int allreduce_vec(Ctx* c, double* v, int64_t n);  // sum over the ranks of a device vector, in place
 int allreduce(Ctx* c, double* v, int n);
 int reduce_logic(Ctx* c, int n, int W, int kind, int check_done);  // records -> (all-reduce) -> scalar logic
 int cgs_raxis(const Ctx* c);
@@ -201,6 +218,7 @@ void op_residual(Ctx* c, const double* T, const double* Tp, double* F);
 void op_diag(Ctx* c, const double* T, double* d, int invert);
 void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np);
 bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nullptr, int it = 0);
+PcgState pcg_state_init(const Ctx* c);
 int ts_flush(Ctx* c);
 CgsBuffers cgs_buffers(Ctx* c, const double* T, int it);
 int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv);
@@ -213,5 +231,28 @@ void mg_prepare(Ctx* c, const double* T);
 int mg_dg_weight(Ctx* c, const double* T);
 int mg_apply0(Ctx* c, const double* T, const RedTail* tail);
 int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason);
+bool mg_next_level(const std::vector<double> (&Xp)[3], double da, bool automatic, std::vector<double> (&Xc)[3],
+                   std::vector<char> (&is_c)[3], int coarse[3]);
+void mg_axis_tables(const std::vector<double>& Xf, const std::vector<char>& is_c, std::vector<int>& pi,
+                    std::vector<double>& pw, std::vector<int>& ri, std::vector<double>& rw);
+int mg_level_vectors(Ctx* c, MgLevel& L);
+double mg_gershgorin(const std::vector<double> (&X)[3], double dt_alpha);
+double mg_omega(double b);
+void mg_level(Ctx* c, size_t l);
+template <class T>
+int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
+  void* p = nullptr;
+  HIPC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, h.size())));
+  L.bufs.push_back(p);
+  HIPC(hipMemcpy(p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  *out = static_cast<const T*>(p);
+  return TV_OK;
+}
+
+// ---- tv_mgdist.cpp (GMG on a slab-partitioned box) ----
+int mg_setup_dist(Ctx* c);
+int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason);
+int mg_prepare_dist(Ctx* c, const double* T);
+int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail);
 
 }  // namespace tv

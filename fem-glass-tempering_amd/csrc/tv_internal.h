@@ -308,6 +308,10 @@ struct MgXfer {
   const double* pw[3];
   const int* ri[3];           // [3 cn[a]]
   const double* rw[3];
+  // 1: fine local plane 2K + b interpolates from coarse local planes K, K + 1
+  // along axis 2 (both levels whole boxes: the 2 x 2 block prolongation
+  // applies); 0 on a partitioned level, whose local planes start anywhere
+  int aligned;
 };
 // bc <- P^T (bf - (wf + facet terms fa)) on the coarse owned nodes (mask:
 // level-0 dinv, 0 = excluded node); xc != nullptr: also the coarse level's
@@ -336,6 +340,14 @@ bool mg_restrict_folds_faces(const MgXfer& x);
 void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const double* w, const FaceAdd* fa,
                       const double* dinv, double omega, double* x, int mode, hipStream_t s);
 void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t s);  // coarse T <- fine T
+// the same on the coarse local planes [k0, k1) only
+void launch_mg_inject_range(const MgXfer& x, const double* Tf, double* Tc, int k0, int k1, hipStream_t s);
+// w <- b - (w + facet terms fa) on n nodes (0 where mask == 0): the residual a
+// partitioned level exchanges and restricts
+void launch_mg_resid(int64_t n, const PcgState* st, const double* b, double* w, const FaceAdd* fa, const double* mask,
+                     hipStream_t s);
+// mask <- 1 on the local nodes [own0, own1) where dinv != 0 (dinv may be null), else 0
+void launch_mg_ownmask(int64_t n, int64_t own0, int64_t own1, const double* dinv, double* mask, hipStream_t s);
 // Per-Newton preparation of up to kMgPrepMax coarse CG levels in two launches
 // (instead of an injection and a boundary-diagonal launch per level): T of
 // every level injected straight from the base level's T through the composed

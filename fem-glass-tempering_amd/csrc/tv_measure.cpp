@@ -97,13 +97,20 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     PcgState h{};
     h.max_it = 1 << 30;
     HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
-    mg_prepare(c, c->f[TV_F_T].ptr);
+    if (c->n_parts > 1) {
+      if (int e = mg_prepare_dist(c, c->f[TV_F_T].ptr)) return e;
+    } else {
+      mg_prepare(c, c->f[TV_F_T].ptr);
+    }
     if (int e = mg_dg_weight(c, c->f[TV_F_T].ptr)) return e;
   }
   auto one = [&]() -> int {
     int np = 0;
     switch (kernel) {
-      case 11: mg_apply0(c, c->f[TV_F_T].ptr, nullptr); return TV_OK;
+      case 11:  // partitioned: the distributed V-cycle, its exchanges included (every rank calls this)
+        if (c->n_parts > 1) return mg_apply0_dist(c, c->f[TV_F_T].ptr, nullptr);
+        mg_apply0(c, c->f[TV_F_T].ptr, nullptr);
+        return TV_OK;
       case 0: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); return TV_OK;
       case 1: return visco(c, false);
       case 2: op_residual(c, c->f[TV_F_T].ptr, c->f[TV_F_T_PREV].ptr, c->r); return TV_OK;

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
     const int64_t f = (int64_t)fj * nf + fpl * fk + f1;
     if (pair) {
       const d2a8 r = ld_pair(bf + f);
-      d2a8 w = ld_pair(wf + f);
+      d2a8 w = (wf != nullptr) ? ld_pair(wf + f) : d2a8{0.0, 0.0};  // wf null: bf is the residual itself
       if (FACES) {
         const bool rowface = (fa.ff[2] && fj == 0) || (fa.ff[3] && fj == fa.n1 - 1) || (fa.ff[4] && fk == 0) ||
                              (fa.ff[5] && fk == fa.n2 - 1);  // wave-uniform
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
         if (m.y == 0.0) dr[q] = 0.0;
       }
     } else {
-      double wt = wf[f];
+      double wt = (wf != nullptr) ? wf[f] : 0.0;
       if (FACES) wt += face_at(fa, f1, fj, fk);  // the row's last node: an x-face node
       double d = bf[f] - wt;
       if (MASK && mask[f] == 0.0) d = 0.0;
@@ -457,14 +457,40 @@ __global__ __launch_bounds__(kBlock) void k_mg_jacobi(int64_t n, const PcgState*
 }
 
 __global__ __launch_bounds__(kBlock) void k_mg_inject(MgXfer x, const double* __restrict__ Tf,
-                                                      double* __restrict__ Tc, int nxb) {
+                                                      double* __restrict__ Tc, int nxb, int k0) {
   const int row = (int)blockIdx.x / nxb;
   const int i = ((int)blockIdx.x - row * nxb) * kBlock + (int)threadIdx.x;
-  const int j = row % x.cn[1], k = row / x.cn[1];
+  const int j = row % x.cn[1], k = k0 + row / x.cn[1];
   if (i >= x.cn[0]) return;
   // the fine node that coincides with coarse node (i, j, k): restriction entry 1 (weight 1)
   const int64_t f = x.ri[0][3 * i + 1] + (int64_t)x.fn[0] * (x.ri[1][3 * j + 1] + (int64_t)x.fn[1] * x.ri[2][3 * k + 1]);
   Tc[(int64_t)i + (int64_t)x.cn[0] * (j + (int64_t)x.cn[1] * k)] = Tf[f];
+}
+
+// the residual of a level in place of its J x, on the owned nodes of a
+// partitioned level (pointers offset to the first owned node): w <- b - (w +
+// facet terms); 0 where mask == 0 (Dirichlet-constrained rows).  The
+// distributed V-cycle exchanges it and restricts it (tv_mgdist.cpp).
+template <bool FACES>
+__global__ __launch_bounds__(kBlock) void k_mg_resid(int64_t n, const PcgState* __restrict__ st,
+                                                     const double* __restrict__ b, double* __restrict__ w, FaceAdd fa,
+                                                     const double* __restrict__ mask) {
+  if (st != nullptr && st->done) return;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    double wt = w[t];
+    if (FACES) wt += face_terms(fa, t);
+    const double d = b[t] - wt;
+    w[t] = (mask != nullptr && mask[t] == 0.0) ? 0.0 : d;
+  }
+}
+
+// restriction mask of a partitioned level: 1 on the owned nodes [own0, own1),
+// 0 on the ghost planes (the ranks' partial restrictions then add up exactly)
+// and on Dirichlet-constrained rows (dinv == 0, when dinv is given)
+__global__ __launch_bounds__(kBlock) void k_mg_ownmask(int64_t n, int64_t own0, int64_t own1,
+                                                       const double* __restrict__ dinv, double* __restrict__ mask) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
+    mask[t] = (t >= own0 && t < own1 && (dinv == nullptr || dinv[t] != 0.0)) ? 1.0 : 0.0;
 }
 
 // ---- DG1 level 0 <-> CG1 level 1 ------------------------------------------------------
@@ -596,7 +622,7 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
 bool mg_restrict_folds_faces(const MgXfer& x) { return x.coarse[0] && x.fn[0] >= 3; }
 
 bool mg_prolong_blocks(const MgXfer& x) {
-  return x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0;
+  return x.aligned && x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0;
 }
 
 bool mg_prolong_smooths(const MgXfer& x) { return mg_prolong_blocks(x); }
@@ -643,9 +669,26 @@ void launch_mg_jacobi(int64_t n, const PcgState* st, const double* b, const doub
 }
 
 void launch_mg_inject(const MgXfer& x, const double* Tf, double* Tc, hipStream_t s) {
+  launch_mg_inject_range(x, Tf, Tc, 0, x.cn[2], s);
+}
+
+void launch_mg_inject_range(const MgXfer& x, const double* Tf, double* Tc, int k0, int k1, hipStream_t s) {
   const int nxb = (x.cn[0] + kBlock - 1) / kBlock;
-  const int64_t rows = (int64_t)x.cn[1] * x.cn[2];
-  if (rows > 0) hipLaunchKernelGGL(k_mg_inject, dim3((unsigned)(rows * nxb)), dim3(kBlock), 0, s, x, Tf, Tc, nxb);
+  const int64_t rows = (int64_t)x.cn[1] * (k1 - k0);
+  if (rows > 0) hipLaunchKernelGGL(k_mg_inject, dim3((unsigned)(rows * nxb)), dim3(kBlock), 0, s, x, Tf, Tc, nxb, k0);
+}
+
+void launch_mg_resid(int64_t n, const PcgState* st, const double* b, double* w, const FaceAdd* fa, const double* mask,
+                     hipStream_t s) {
+  if (n <= 0) return;
+  const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
+  if (f.on) hipLaunchKernelGGL((k_mg_resid<true>), dim3(blocks_for(n)), dim3(kBlock), 0, s, n, st, b, w, f, mask);
+  else hipLaunchKernelGGL((k_mg_resid<false>), dim3(blocks_for(n)), dim3(kBlock), 0, s, n, st, b, w, f, mask);
+}
+
+void launch_mg_ownmask(int64_t n, int64_t own0, int64_t own1, const double* dinv, double* mask, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_mg_ownmask, dim3(blocks_for(n)), dim3(kBlock), 0, s, n, own0, own1, dinv, mask);
 }
 
 void launch_mg_dg_restrict(int c0, int c1, int c2, const PcgState* st, const double* bf, const double* wf,

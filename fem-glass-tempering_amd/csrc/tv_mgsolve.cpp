@@ -42,16 +42,6 @@ double mg_gershgorin(const std::vector<double> (&X)[3], double dt_alpha) {
   return std::max(b, 2.25) * 1.05;
 }
 
-template <class T>
-int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
-  void* p = nullptr;
-  HIPC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, h.size())));
-  L.bufs.push_back(p);
-  HIPC(hipMemcpy(p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
-  *out = static_cast<const T*>(p);
-  return TV_OK;
-}
-
 double mg_omega(double b) { return 2.0 / (1.1 * b); }
 
 // the hierarchy below the fine grid (single partition, 3D CG1 marching path)
@@ -62,17 +52,7 @@ int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da) {
   for (int s = 0; s < 3; ++s) L.X[s] = X[s];
   if (int e = build_cg_grid(c, 3, L.X, 0, (int)L.X[2].size(), 0, 0, true, true, L.g, L.coef, &L.bnodes, L.ffbuf))
     return e;
-  const CgGrid& f = c->cg;  // thermal constants (set by setup_fields for both families)
-  L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
-  L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
-  L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
-  for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
-    void* p = nullptr;
-    HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
-    HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)L.n, c->stream));
-    L.bufs.push_back(p);
-    *q = static_cast<double*>(p);
-  }
+  if (int e = mg_level_vectors(c, L)) return e;
   L.omega = mg_omega(mg_gershgorin(L.X, da));
   return TV_OK;
 }
@@ -124,12 +104,104 @@ int mg_dg_weight(Ctx* c, const double* T) {
   return TV_OK;
 }
 
+// Coarsening rule of the box hierarchy (identical for a whole box and for its
+// partitions, which plan it over the global grid): every other node kept
+// along each axis with at least two cells, plus the last node when the cell
+// count is odd (coarse nodes are a subset of the fine ones); stop where the
+// operator is mass-dominated (dt alpha / h^2 <= 0.5 with h the smallest mean
+// cell length: a Jacobi step is then a good solve) or nothing coarsens.
+bool mg_next_level(const std::vector<double> (&Xp)[3], double da, bool automatic, std::vector<double> (&Xc)[3],
+                   std::vector<char> (&is_c)[3], int coarse[3]) {
+  double h = 1e300;
+  bool any = false;
+  for (int s = 0; s < 3; ++s) {
+    const int cells = (int)Xp[s].size() - 1;
+    coarse[s] = cells >= 2;
+    any = any || coarse[s];
+    if (cells >= 1) h = std::min(h, (Xp[s].back() - Xp[s].front()) / cells);
+  }
+  if (!any || (automatic && da / (h * h) <= 0.5)) return false;
+  for (int s = 0; s < 3; ++s) {
+    const int nf = (int)Xp[s].size();
+    Xc[s].clear();
+    is_c[s].assign(nf, 1);
+    if (!coarse[s]) {
+      Xc[s] = Xp[s];
+      continue;
+    }
+    for (int i = 0; i < nf; ++i) is_c[s][i] = (i % 2 == 0 || i == nf - 1) ? 1 : 0;
+    for (int i = 0; i < nf; ++i)
+      if (is_c[s][i]) Xc[s].push_back(Xp[s][i]);
+  }
+  return true;
+}
+
+// Transfer tables of one axis over the whole (global) axis: prolongation = two
+// (coarse index, weight) pairs per fine node (exact linear interpolation),
+// restriction R = P^T = three (fine index, weight) pairs per coarse node
+void mg_axis_tables(const std::vector<double>& Xf, const std::vector<char>& is_c, std::vector<int>& pi,
+                    std::vector<double>& pw, std::vector<int>& ri, std::vector<double>& rw) {
+  const int nf = (int)Xf.size();
+  std::vector<int> cpos(nf, -1), fpos;
+  for (int i = 0; i < nf; ++i)
+    if (is_c[i]) {
+      cpos[i] = (int)fpos.size();
+      fpos.push_back(i);
+    }
+  const int nc = (int)fpos.size();
+  pi.assign(2 * (size_t)nf, 0);
+  pw.assign(2 * (size_t)nf, 0.0);
+  ri.assign(3 * (size_t)nc, 0);
+  rw.assign(3 * (size_t)nc, 0.0);
+  for (int i = 0; i < nf; ++i) {
+    if (is_c[i]) {
+      pi[2 * i] = pi[2 * i + 1] = cpos[i];
+      pw[2 * i] = 1.0;
+    } else {  // linear interpolation between the coarse neighbours i - 1 and i + 1
+      const double wl = (Xf[i + 1] - Xf[i]) / (Xf[i + 1] - Xf[i - 1]);
+      pi[2 * i] = cpos[i - 1];
+      pi[2 * i + 1] = cpos[i + 1];
+      pw[2 * i] = wl;
+      pw[2 * i + 1] = 1.0 - wl;
+    }
+  }
+  for (int I = 0; I < nc; ++I) {  // R = P^T: the fine nodes that interpolate from I
+    const int fc = fpos[I];
+    for (int q = 0; q < 3; ++q) ri[3 * I + q] = fc;
+    rw[3 * I + 1] = 1.0;
+    if (fc - 1 >= 0 && !is_c[fc - 1]) {
+      ri[3 * I] = fc - 1;
+      rw[3 * I] = pw[2 * (fc - 1) + 1];  // fine fc - 1: its right coarse neighbour is I
+    }
+    if (fc + 1 < nf && !is_c[fc + 1]) {
+      ri[3 * I + 2] = fc + 1;
+      rw[3 * I + 2] = pw[2 * (fc + 1)];  // fine fc + 1: its left coarse neighbour is I
+    }
+  }
+}
+
+// T, b, x, w, dinv of a level (local size L.n), zeroed
+int mg_level_vectors(Ctx* c, MgLevel& L) {
+  const CgGrid& f = c->cg;  // thermal constants (set by setup_mesh for both families)
+  L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
+  L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
+  L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+  for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
+    void* p = nullptr;
+    HIPC(hipMalloc(&p, sizeof(double) * (size_t)std::max<int64_t>(1, L.n)));
+    HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)std::max<int64_t>(1, L.n), c->stream));
+    L.bufs.push_back(p);
+    *q = static_cast<double*>(p);
+  }
+  return TV_OK;
+}
+
 int mg_setup(Ctx* c) {
   const bool dg = c->fam_T == TV_DG;
   if (c->dim != 3 || c->um || (!dg && !cg_cgs_supported(c->cg)) || (dg && (c->dg.deg1 || c->dg.deg2)))
     return c->fail(TV_ERR_ARG, "preconditioner GMG: 3D CG1 or DG1 temperature space on a rectilinear mesh only");
-  if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "preconditioner GMG: one partition (use TV_PC_JACOBI when partitioned)");
   if (c->cgs) return c->fail(TV_ERR_ARG, "preconditioner GMG runs in the KSPCG form (pcg_variant KSPCG or AUTO)");
+  if (c->n_parts > 1) return mg_setup_dist(c);  // slab-partitioned box (tv_mgdist.cpp)
   std::vector<double> tmp, Xf[3];
   for (int s = 0; s < 3; ++s) Xf[s] = storage_coords(c, s, tmp);
   const double da = c->P.dt * c->P.alpha;
@@ -148,93 +220,36 @@ int mg_setup(Ctx* c) {
   const bool automatic = c->O.mg_levels <= 0;
   std::vector<double> Xp[3] = {Xf[0], Xf[1], Xf[2]};
   for (int lev = 1 + (dg ? 1 : 0); lev < max_levels; ++lev) {
-    double h = 1e300;  // smallest mean cell length over the axes
-    bool coarsen[3], any = false;
-    for (int s = 0; s < 3; ++s) {
-      const int cells = (int)Xp[s].size() - 1;
-      coarsen[s] = cells >= 2;
-      any = any || coarsen[s];
-      if (cells >= 1) h = std::min(h, (Xp[s].back() - Xp[s].front()) / cells);
-    }
-    // stop where the operator is mass-dominated: a Jacobi step is then a good solve
-    if (!any || (automatic && da / (h * h) <= 0.5)) break;
+    std::vector<double> Xc[3];
+    std::vector<char> is_c[3];  // fine node kept on this level
+    int coarse[3];
+    if (!mg_next_level(Xp, da, automatic, Xc, is_c, coarse)) break;
     c->mg.emplace_back();
     MgLevel& L = c->mg.back();
-    std::vector<char> is_c[3];  // fine node kept on this level
-    for (int s = 0; s < 3; ++s) {
-      const int nf = (int)Xp[s].size();
-      is_c[s].assign(nf, 1);
-      if (!coarsen[s]) {
-        L.X[s] = Xp[s];
-        continue;
-      }
-      // every other node, and the last one (an odd cell count keeps one fine cell at the end)
-      for (int i = 0; i < nf; ++i) is_c[s][i] = (i % 2 == 0 || i == nf - 1) ? 1 : 0;
-      for (int i = 0; i < nf; ++i)
-        if (is_c[s][i]) L.X[s].push_back(Xp[s][i]);
-    }
+    for (int s = 0; s < 3; ++s) L.X[s] = Xc[s];
     if (int e = build_cg_grid(c, 3, L.X, 0, (int)L.X[2].size(), 0, 0, true, true, L.g, L.coef, &L.bnodes, L.ffbuf))
       return e;
-    const CgGrid& f = c->cg;
-    L.g.dt = f.dt; L.g.dt_alpha = f.dt_alpha; L.g.dt_f = f.dt_f;
-    L.g.a_rad = f.a_rad; L.g.a_conv = f.a_conv; L.g.T_amb = f.T_amb; L.g.T_amb4 = f.T_amb4;
-    L.n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
-      for (double** q : {&L.T, &L.b, &L.x, &L.w, &L.dinv}) {
-      void* p = nullptr;
-      HIPC(hipMalloc(&p, sizeof(double) * (size_t)L.n));
-      HIPC(hipMemsetAsync(p, 0, sizeof(double) * (size_t)L.n, c->stream));
-      L.bufs.push_back(p);
-      *q = static_cast<double*>(p);
-    }
+    if (int e = mg_level_vectors(c, L)) return e;
     L.omega = mg_omega(mg_gershgorin(L.X, da));
     // transfer maps (finer level Xp -> this level)
     MgXfer& x = L.xf;
     for (int s = 0; s < 3; ++s) {
-      const int nf = (int)Xp[s].size(), nc = (int)L.X[s].size();
-      std::vector<int> pi(2 * (size_t)nf), ri(3 * (size_t)nc), cpos(nf, -1), fpos;
-      std::vector<double> pw(2 * (size_t)nf, 0.0), rw(3 * (size_t)nc, 0.0);
-      for (int i = 0; i < nf; ++i)
-        if (is_c[s][i]) {
-          cpos[i] = (int)fpos.size();
-          fpos.push_back(i);
-        }
-      for (int i = 0; i < nf; ++i) {
-        if (is_c[s][i]) {
-          pi[2 * i] = pi[2 * i + 1] = cpos[i];
-          pw[2 * i] = 1.0;
-        } else {  // linear interpolation between the coarse neighbours i - 1 and i + 1
-          const double wl = (Xp[s][i + 1] - Xp[s][i]) / (Xp[s][i + 1] - Xp[s][i - 1]);
-          pi[2 * i] = cpos[i - 1];
-          pi[2 * i + 1] = cpos[i + 1];
-          pw[2 * i] = wl;
-          pw[2 * i + 1] = 1.0 - wl;
-        }
-      }
-      for (int I = 0; I < nc; ++I) {  // R = P^T: the fine nodes that interpolate from I
-        const int fc = fpos[I];
-        for (int q = 0; q < 3; ++q) ri[3 * I + q] = fc;
-        rw[3 * I + 1] = 1.0;
-        if (fc - 1 >= 0 && !is_c[s][fc - 1]) {
-          ri[3 * I] = fc - 1;
-          rw[3 * I] = pw[2 * (fc - 1) + 1];  // fine fc - 1: its right coarse neighbour is I
-        }
-        if (fc + 1 < nf && !is_c[s][fc + 1]) {
-          ri[3 * I + 2] = fc + 1;
-          rw[3 * I + 2] = pw[2 * (fc + 1)];  // fine fc + 1: its left coarse neighbour is I
-        }
-      }
+      std::vector<int> pi, ri;
+      std::vector<double> pw, rw;
+      mg_axis_tables(Xp[s], is_c[s], pi, pw, ri, rw);
       if (int e = mg_upload(c, L, pi, &x.pi[s])) return e;
       if (int e = mg_upload(c, L, pw, &x.pw[s])) return e;
       if (int e = mg_upload(c, L, ri, &x.ri[s])) return e;
       if (int e = mg_upload(c, L, rw, &x.rw[s])) return e;
-      x.fn[s] = nf;
-      x.cn[s] = nc;
-      x.coarse[s] = coarsen[s] ? 1 : 0;
+      x.fn[s] = (int)Xp[s].size();
+      x.cn[s] = (int)L.X[s].size();
+      x.coarse[s] = coarse[s];
     }
     x.f_kb = 0;
     x.f_ke = x.fn[2];
     x.c_kb = 0;
     x.c_ke = x.cn[2];
+    x.aligned = 1;
     for (int s = 0; s < 3; ++s) Xp[s] = L.X[s];
   }
   c->mg_on = true;
@@ -391,11 +406,7 @@ int mg_iteration(Ctx* c, const double* T, int it) {
 
 int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   const int64_t n = c->nT;
-  PcgState h{};
-  h.rtol = c->O.ksp_rtol;
-  h.atol = c->O.ksp_atol;
-  h.dtol = c->O.ksp_dtol;
-  h.max_it = c->O.ksp_max_it;
+  const PcgState h = pcg_state_init(c);
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;

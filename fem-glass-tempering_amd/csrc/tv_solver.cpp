@@ -43,6 +43,24 @@ bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail, int 
 // equals it until convergence, after which every kernel exits at once)
 
 // reads the pending timestamp slots back and adds them to the stats
+// the scalars of a Krylov solve at its start (PETSc KSPSetTolerances); with
+// ksp_fixed_its the solve runs exactly that many iterations (no convergence
+// test: KSP_NORM_NONE), which newton() accepts
+PcgState pcg_state_init(const Ctx* c) {
+  PcgState h{};
+  h.rtol = c->O.ksp_rtol;
+  h.atol = c->O.ksp_atol;
+  h.dtol = c->O.ksp_dtol;
+  h.max_it = c->O.ksp_max_it;
+  if (c->O.ksp_fixed_its > 0) {
+    h.rtol = 0.0;
+    h.atol = 0.0;
+    h.dtol = 1e300;
+    h.max_it = c->O.ksp_fixed_its;
+  }
+  return h;
+}
+
 int ts_flush(Ctx* c) {
   if (!c->d_ts) return TV_OK;
   if (!c->ts_pending.empty()) {
@@ -98,11 +116,7 @@ int pcg_iteration(Ctx* c, const double* T, int it) {
 int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
   // state init
-  PcgState h{};
-  h.rtol = c->O.ksp_rtol;
-  h.atol = c->O.ksp_atol;
-  h.dtol = c->O.ksp_dtol;
-  h.max_it = c->O.ksp_max_it;
+  const PcgState h = pcg_state_init(c);
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
@@ -186,11 +200,7 @@ int cgs_iteration(Ctx* c, const double* T, int it) {
 }
 
 int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
-  PcgState h{};
-  h.rtol = c->O.ksp_rtol;
-  h.atol = c->O.ksp_atol;
-  h.dtol = c->O.ksp_dtol;
-  h.max_it = c->O.ksp_max_it;
+  const PcgState h = pcg_state_init(c);
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
@@ -341,11 +351,11 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;
     int k = 0, reason = 0;
-    if (int e = (c->mg_on ? pcg_solve_mg(c, T, &k, &reason)
+    if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason) : pcg_solve_mg(c, T, &k, &reason))
                           : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
       return e;
     kits += k;
-    if (reason < 0)
+    if (reason < 0 && !(reason == R_DIV_ITS && c->O.ksp_fixed_its > 0))
       return c->fail(TV_ERR_KSP, std::string("Krylov solver did not converge (") + reason_str(reason) + ")");
     if (dir)
       hipLaunchKernelGGL(k_bc_step, dim3((int)std::min<int64_t>(4096, (c->nT + kBlock - 1) / kBlock)), dim3(kBlock), 0,

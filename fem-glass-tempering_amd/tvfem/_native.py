@@ -83,7 +83,8 @@ class Options(C.Structure):
                 ("ksp_dtol", C.c_double), ("ksp_max_it", C.c_int), ("materialize", C.c_int),
                 ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
                 ("model_mode", C.c_int), ("preconditioner", C.c_int), ("mg_levels", C.c_int),
-                ("dg_kernel", C.c_int), ("dg_tile_chunk", C.c_int)]
+                ("dg_kernel", C.c_int), ("dg_tile_chunk", C.c_int), ("mg_replicate_nodes", C.c_int),
+                ("ksp_fixed_its", C.c_int)]
 
 
 _lib = None

@@ -110,7 +110,8 @@ class ThermoViscoProblem:
                  ksp_rtol: float = 1e-5, n_parts: int = 1, part: int = 0, part_axis: int = -1,
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
                  write_output: bool | None = None, output_dir: str = "output", preconditioner: str = "jacobi",
-                 mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0) -> None:
+                 mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0,
+                 mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -148,6 +149,8 @@ class ThermoViscoProblem:
         self._dg_kernel = {"auto": N.TV_DG_KERNEL_AUTO, "tile": N.TV_DG_KERNEL_TILE,
                            "cells": N.TV_DG_KERNEL_CELLS}[dg_kernel]
         self._dg_tile_chunk = int(dg_tile_chunk)
+        self._mg_replicate_nodes = int(mg_replicate_nodes)
+        self._ksp_fixed_its = int(ksp_fixed_its)
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -223,6 +226,8 @@ class ThermoViscoProblem:
         opts.mg_levels = self._mg_levels
         opts.dg_kernel = self._dg_kernel
         opts.dg_tile_chunk = self._dg_tile_chunk
+        opts.mg_replicate_nodes = self._mg_replicate_nodes
+        opts.ksp_fixed_its = self._ksp_fixed_its
         ctx = C.c_void_p()
         create = lib.tv_create_unstructured if um else lib.tv_create
         N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))

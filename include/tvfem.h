@@ -52,7 +52,7 @@ extern "C" {
 #endif
 
 #define TV_ABI_VERSION 3  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
-                            3: dg_kernel, dg_tile_chunk */
+                            3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its */
 
 /* status codes */
 #define TV_OK 0
@@ -135,6 +135,12 @@ typedef struct {
   int mg_levels;          /* GMG: levels incl. the fine one (0: automatic)       */
   int dg_kernel;          /* 3D DG1 Jacobian: TV_DG_KERNEL_AUTO / _TILE / _CELLS */
   int dg_tile_chunk;      /* planes per marching DG tile (0: automatic = 5)      */
+  int mg_replicate_nodes; /* partitioned GMG: coarse levels of at most this many
+                             nodes are replicated on every rank (0: 300000)     */
+  int ksp_fixed_its;      /* > 0: every Krylov solve runs exactly this many
+                             iterations, with no convergence test (PETSc
+                             KSP_NORM_NONE + max_it; timing of partition shares
+                             with the communication stubbed)                    */
 } tv_options;
 
 /* 3D DG1 Jacobian kernel: AUTO = TILE, the marching tile kernel (production);

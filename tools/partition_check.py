@@ -30,9 +30,10 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
 
-def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False):
+def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0):
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
-                           verbose=False, pcg_variant=pcg, write_output=False)
+                           verbose=False, pcg_variant=pcg, write_output=False, preconditioner=pc,
+                           mg_replicate_nodes=mg_rep)
     if comm is not None:
         comm(p)
     p.setup()
@@ -59,6 +60,9 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
     ap.add_argument("--edit", action="store_true", help="host edit of T on the owning rank only, after setup()")
+    ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi")
+    ap.add_argument("--mg-replicate", type=int, default=0,
+                    help="GMG: coarse levels of at most this many nodes replicated (0: the library default)")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
@@ -71,15 +75,15 @@ def main():
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
-                       pcg=a.pcg, edit=a.edit)
+                       pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate)
     else:
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
-                       edit=a.edit)
+                       edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
-        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit)
-        res = {"comm": a.comm, "pcg": a.pcg, "its_parts": its, "its_single": its_ref}
+        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc)
+        res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             full = np.concatenate([np.asarray(g[k]) for g in gathered])
             e = np.linalg.norm(full - ref[k]) / np.linalg.norm(ref[k])
