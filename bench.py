@@ -239,7 +239,7 @@ def main():
             cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
                    "sample": "no unstructured path in oracle/tv_cpu.c (the numpy oracle covers its parity only)"}
         else:
-            cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only, a.family)
+            cpu = cpu_baseline(nc, L, mp, a.cpu_seconds, a.thermal_only, a.family, pc)
 
     prob.close()
     if rank == 0:
@@ -280,7 +280,7 @@ def main():
         print(json.dumps(out))
 
 
-def cpu_baseline(nc, L, mp, seconds, thermal_only, family="CG"):
+def cpu_baseline(nc, L, mp, seconds, thermal_only, family="CG", pc="jacobi"):
     """Time the oracle's C/OpenMP restatement (oracle/tv_cpu.c, a port of the same
     algorithm) on a bounded sample of the same workload: the same mesh and
     physics, as many full time steps as fit ~`seconds` (at least one)."""
@@ -288,7 +288,7 @@ def cpu_baseline(nc, L, mp, seconds, thermal_only, family="CG"):
         from oracle import tv_cpu
     except Exception as e:  # the baseline is reported, never required
         return {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
-    return tv_cpu.time_baseline(nc, L, mp, seconds, thermal_only, family)
+    return tv_cpu.time_baseline(nc, L, mp, seconds, thermal_only, family, pc)
 
 
 if __name__ == "__main__":

@@ -31,6 +31,9 @@ def load():
         lib.tvcpu_num_dofs.argtypes = [C.c_void_p]
         lib.tvcpu_get.argtypes = [C.c_void_p, C.c_int, dp]
         lib.tvcpu_destroy.argtypes = [C.c_void_p]
+        lib.tvcpu_set_gmg.argtypes = [C.c_void_p]
+        lib.tvcpu_set_gmg.restype = C.c_int
+        lib.tvcpu_precond_apply.argtypes = [C.c_void_p, dp, dp]
         _lib = lib
     return _lib
 
@@ -39,7 +42,7 @@ class CpuProblem:
     """Structured 3D plate on the CPU (axes: node coordinates per axis), CG1/CG1
     or (family "DG") DG1/DG1 with cell-local dofs at l * ncell + cell."""
 
-    def __init__(self, axes, mp, dt, family="CG"):
+    def __init__(self, axes, mp, dt, family="CG", pc="jacobi"):
         lib = load()
         self.axes = [np.ascontiguousarray(a, dtype=np.float64) for a in axes]
         nc = (C.c_int * 3)(*[len(a) - 1 for a in self.axes])
@@ -52,6 +55,19 @@ class CpuProblem:
         self.h = create(nc, dp(self.axes[0]), dp(self.axes[1]), dp(self.axes[2]), dp(params), dp(tabs))
         self.n = lib.tvcpu_num_dofs(self.h)
         self.lib = lib
+        self.levels = 1
+        if pc == "gmg":  # the GPU line's geometric multigrid (tv_cpu.c tvcpu_set_gmg)
+            self.levels = lib.tvcpu_set_gmg(self.h)
+            if self.levels < 1:
+                raise ValueError("GMG: CG1 plates only in the CPU port")
+
+    def precond_apply(self, r):
+        """z = B r at the current T (Jacobi or one V-cycle)."""
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        z = np.empty_like(r)
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+        self.lib.tvcpu_precond_apply(self.h, dp(r), dp(z))
+        return z
 
     def step(self, thermal_only=False):
         a, b = C.c_int(), C.c_int()
@@ -80,12 +96,14 @@ def cores():
         return os.cpu_count() or 1
 
 
-def time_baseline(nc, L, mp, seconds=15.0, thermal_only=False, family="CG"):
+def time_baseline(nc, L, mp, seconds=15.0, thermal_only=False, family="CG", pc="jacobi"):
     """Bounded sample of the bench workload: the full mesh, as many whole time
-    steps as fit about `seconds` (at least one, at most 10).  Returns the
+    steps as fit about `seconds` (at least one, at most 10), with the GPU
+    line's preconditioner where the port has it (GMG: CG1).  Returns the
     cpu_baseline record of bench.py."""
     axes = [np.linspace(0.0, l, n + 1) for l, n in zip(L, nc)]
-    P = CpuProblem(axes, mp, 0.1, family)
+    pc = pc if family == "CG" else "jacobi"
+    P = CpuProblem(axes, mp, 0.1, family, pc=pc)
     t0 = time.perf_counter()
     steps = 0
     while True:
@@ -95,9 +113,12 @@ def time_baseline(nc, L, mp, seconds=15.0, thermal_only=False, family="CG"):
         if el >= seconds or steps >= 10 or el / steps * (steps + 1) > 2 * seconds:
             break
     n = P.n
+    P_levels = P.levels
     P.close()
     return {"value": n * steps / el, "unit": "DOF-updates/s", "cores": int(os.environ.get("OMP_NUM_THREADS", cores())),
             "kind": "port",
             "sample": f"{steps} full time step(s) of the same {nc[0]}x{nc[1]}x{nc[2]} hex mesh "
                       f"({n} dofs, {'thermal-only' if thermal_only else 'coupled'}) in {el:.1f} s, "
-                      f"oracle/tv_cpu.c (C/OpenMP port, {family}1: matrix-free Jacobi-PCG Newton + visco update)"}
+                      f"oracle/tv_cpu.c (C/OpenMP port, {family}1: matrix-free "
+                      + (f"GMG-preconditioned ({P_levels} levels) " if pc == "gmg" else "Jacobi-") + "PCG Newton "
+                      "+ visco update)", "algorithm": "gmg" if pc == "gmg" else "jacobi"}

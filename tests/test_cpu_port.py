@@ -58,3 +58,38 @@ def test_cpu_port_matches_oracle(fam):
                     min_frac=0.9)
     finally:
         cpu.close()
+
+
+def test_cpu_port_gmg_matches_jacobi_and_vcycle_restatement():
+    """The port's geometric multigrid (tv_cpu.c tvcpu_set_gmg, the GPU line's
+    preconditioner restated for the CPU baseline): three coupled steps give the
+    same T as the Jacobi port (Newton to 1e-12 either way) with the same Newton
+    counts and far fewer Krylov iterations, and one V-cycle equals the numpy
+    V-cycle of tests/test_multigrid.py on the oracle's assembled Jacobians."""
+    tv_cpu = _port()
+    import test_multigrid as TM
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    axes = [np.linspace(0.0, 2.0, 17), np.linspace(0.0, 2.0, 13), np.linspace(0.0, 1.0, 9)]
+    jac = tv_cpu.CpuProblem(axes, mp, 0.1, "CG")
+    gmg = tv_cpu.CpuProblem(axes, mp, 0.1, "CG", pc="gmg")
+    try:
+        assert gmg.levels >= 2
+        kj = kg = 0
+        for s in range(3):
+            nj, a = jac.step()
+            ng, b = gmg.step()
+            kj += a
+            kg += b
+            assert nj == ng, (s, nj, ng)
+            assert relerr(gmg.get("T"), jac.get("T")) < 1e-10, s
+        print(f"[cpu port gmg] {gmg.levels} levels, Krylov {kg} vs Jacobi {kj}")
+        assert 2 * kg < kj
+        # the V-cycle operator at the current T against the numpy restatement
+        T = gmg.get("T")
+        r = np.random.default_rng(5).standard_normal(gmg.n)
+        z = gmg.precond_apply(r)
+        zr = TM._vcycle_reference(axes, T, mp, 0.1, gmg.levels)(r)
+        assert relerr(z, zr) < 1e-12, relerr(z, zr)
+    finally:
+        jac.close()
+        gmg.close()
