@@ -60,6 +60,12 @@ def parse():
                          "over the ranks when partitioned), jacobi, or auto (gmg where it applies and the mesh "
                          "has >= 4M T-dofs, at every rank count)")
     ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
+    ap.add_argument("--share", type=int, default=0, metavar="N",
+                    help="time ONE rank's share of an N-way partition of the mesh on this GPU with the "
+                         "communication stubbed (halos and all-reduces are no-ops) and the iteration counts "
+                         "fixed (--share-its): the per-rank compute floor of an N-GPU run")
+    ap.add_argument("--share-its", type=str, default="4,5", metavar="NEWTON,KRYLOV",
+                    help="--share: Newton iterations per step, Krylov iterations per Newton solve")
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto",
                     help="Krylov form: single-reduction (Chronopoulos-Gear, 3D CG) or PETSc KSPCG as written")
     return ap.parse_args()
@@ -112,6 +118,12 @@ def main():
         # V-cycle (tv_mgdist.cpp), so N = 1 and N > 1 lines compare like with like
         pc = "gmg" if (not um and a.pcg != "single" and big) else "jacobi"
     kw = {} if um else {"n_parts": world, "part": rank, "part_axis": 1}
+    if a.share > 1:  # a middle rank's slab (ghost planes both sides), no communicator
+        if world > 1 or um:
+            raise SystemExit("--share: one process, box mesh")
+        nn, kk = (int(v) for v in a.share_its.split(","))
+        kw = {"n_parts": a.share, "part": a.share // 2, "part_axis": 1, "newton_fixed_its": nn,
+              "ksp_fixed_its": kk}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
                               verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,
                               write_output=a.output is not None, output_dir=a.output or "output", **kw)
@@ -234,7 +246,7 @@ def main():
                 "hbm_flushed": flushed}
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.share <= 1:
         if um:
             cpu = {"value": None, "unit": "DOF-updates/s", "cores": 0, "kind": "port",
                    "sample": "no unstructured path in oracle/tv_cpu.c (the numpy oracle covers its parity only)"}
@@ -262,7 +274,12 @@ def main():
                                    + f"{cname} 3D plate {a.family}1/{a.family}1 {nc[0]}x{nc[1]}x{nc[2]} hex "
                                    f"({n_global} T-dofs), dt 0.1, "
                                    + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
-                       "parallelism": ("single GPU, one partition (no communication)" if world == 1 else
+                       "parallelism": (f"ONE rank's share (partition {a.share // 2} of {a.share}, its slab of "
+                                       f"{n_owned} owned T-dofs) on one GPU, communication stubbed, iterations "
+                                       f"fixed at {a.share_its} (Newton per step, Krylov per solve): the per-rank "
+                                       "compute floor, not a multi-GPU measurement"
+                                       if a.share > 1 else
+                                       "single GPU, one partition (no communication)" if world == 1 else
                                        f"mesh partition along y x{world} ("
                                        + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")"),
                        "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,

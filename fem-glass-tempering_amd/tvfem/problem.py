@@ -111,7 +111,7 @@ class ThermoViscoProblem:
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
                  write_output: bool | None = None, output_dir: str = "output", preconditioner: str = "jacobi",
                  mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0,
-                 mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0) -> None:
+                 mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0, newton_fixed_its: int = 0) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -151,6 +151,7 @@ class ThermoViscoProblem:
         self._dg_tile_chunk = int(dg_tile_chunk)
         self._mg_replicate_nodes = int(mg_replicate_nodes)
         self._ksp_fixed_its = int(ksp_fixed_its)
+        self._newton_fixed_its = int(newton_fixed_its)
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -228,6 +229,11 @@ class ThermoViscoProblem:
         opts.dg_tile_chunk = self._dg_tile_chunk
         opts.mg_replicate_nodes = self._mg_replicate_nodes
         opts.ksp_fixed_its = self._ksp_fixed_its
+        if self._newton_fixed_its > 0:  # timing runs only: exactly this many Newton iterations per step
+            opts.newton_rtol = 0.0
+            opts.newton_atol = 0.0
+            opts.newton_max_it = self._newton_fixed_its
+            opts.error_on_nonconvergence = 0
         ctx = C.c_void_p()
         create = lib.tv_create_unstructured if um else lib.tv_create
         N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
