@@ -174,9 +174,10 @@ def test_gmg_rejects_unsupported_meshes():
     with pytest.raises(NativeError):
         ThermoViscoProblem(RectilinearMesh(axes2), (0, 1), 0.1, cfg, mp, verbose=False, preconditioner="gmg")
     axes3 = CASES["plate"]
-    with pytest.raises(NativeError):
+    # (partitioned boxes are supported: the distributed V-cycle, tests/test_partition.py)
+    with pytest.raises(NativeError):  # the single-reduction form with GMG
         ThermoViscoProblem(RectilinearMesh(axes3), (0, 1), 0.1, cfg, mp, verbose=False, preconditioner="gmg",
-                           n_parts=2, part=0, part_axis=2)
+                           pcg_variant="single")
     with pytest.raises(NativeError):
         ThermoViscoProblem(UnstructuredMesh.from_rectilinear(RectilinearMesh(axes3)), (0, 1), 0.1, cfg, mp,
                            verbose=False, preconditioner="gmg")
