@@ -229,10 +229,13 @@ def main():
     # the timed run); traffic_source names the file
     traffic, traffic_src = None, None
     dname = names[0] if um else names[3]
-    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{dname}_{a.family}_{nc[0]}x{nc[1]}x{nc[2]}_n{world}.json")
+    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{dname}_{a.family}_{nc[0]}x{nc[1]}x{nc[2]}_n{world}"
+                            + ("_gmg" if pc == "gmg" else "") + ".json")
+    pmc = None
     if os.path.exists(pmc_file):
         with open(pmc_file) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch")
+            pmc = json.load(fh)
+        traffic = pmc.get("hbm_bytes_per_launch")
         traffic_src = "committed rocprofv3 --pmc record " + os.path.relpath(pmc_file, ROOT)
     roofline = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -244,6 +247,13 @@ def main():
                 "timing": ("effective (in-solve, Infinity-Cache assisted)" if dom["launches_timed"]
                            else "isolated"),
                 "hbm_flushed": flushed}
+    if "mg_vcycle" in kern:  # the multigrid V-cycle as a whole (every launch of one application, all levels)
+        v = kern["mg_vcycle"]
+        vt = (pmc or {}).get("kernels", {}).get("mg_vcycle", {}).get("hbm_bytes_per_launch")
+        roofline["vcycle"] = {"achieved": v["GBps"], "frac": v["GBps"] / HBM_PEAK_GBS, "unit": "GB/s",
+                              "bytes_per_cycle": v["bytes"], "ms_per_cycle": v["ms"], "traffic": vt,
+                              "traffic_source": traffic_src if vt else None,
+                              "timing": "isolated: back-to-back V-cycles on the current state (tv_time_kernel 11)"}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.share <= 1:

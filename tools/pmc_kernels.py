@@ -31,16 +31,28 @@ ap.add_argument("--cells", default="400,400,50")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--family", choices=["CG", "DG"], default="CG")
 ap.add_argument("--mesh", choices=["box", "distorted"], default="box")
+ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi",
+                help="gmg: the bench line's solver -- whole coupled steps under the counters (the fused "
+                     "matvec and every V-cycle kernel in the cache state of the multigrid solve)")
+ap.add_argument("--steps", type=int, default=2)
 a = ap.parse_args()
 nc = [int(v) for v in a.cells.split(",")]
 cfg = {"T": {"element": a.family, "degree": 1}, "sigma": {"element": a.family, "degree": 1}}
 um = a.mesh == "distorted"
 mesh = (distorted_box_mesh if um else box_mesh)([50.0, 50.0, 5.0], nc)
 prob = ThermoViscoProblem(mesh, (0.0, 1.0), 0.1, cfg, dict(MP), materialize=False, write_output=False,
-                          verbose=False, **({} if um else {"part_axis": 1}))
+                          verbose=False, preconditioner=a.pc, **({} if um else {"part_axis": 1}))
 prob.setup()
 prob.solve_timestep()
 lib, ctx = prob._lib, prob._ctx
+if a.pc == "gmg":  # whole steps of the bench's solve, then the flushed J x
+    for _ in range(a.steps):
+        prob.solve_timestep()
+        print("step", prob.last_newton_iterations, prob.last_krylov_iterations, flush=True)
+    ms = C.c_double()
+    N.check(lib.tv_time_kernel(ctx, 10, a.reps, C.byref(ms)), ctx)
+    prob.close()
+    sys.exit(0)
 for kid in ((0, 1) if um else (5, 1, 10) if a.family == "CG" else (3, 1, 10)):
     ms = C.c_double()
     N.check(lib.tv_time_kernel(ctx, kid, a.reps, C.byref(ms)), ctx)

@@ -24,7 +24,15 @@ GROUPS = {
     "dg_matvec_fused": ("k_dg_tile<true",),
     "pcg_iteration_single_reduction": ("k_cgs_march<false",),
     "jacobian_apply_unstructured": ("k_um_rows<3, 1>",),  # SELL-64 J x of tv_um.hip
+    # multigrid kernels (pmc_kernels.py --pc gmg)
+    "mg_update": ("k_mg_update",),
+    "mg_post_march": ("k_cg_march<1, false, 8, 1, 2, true",),
+    "mg_restrict": ("k_mg_restrict_pairs",),
+    "mg_prolong": ("k_mg_prolong_blk",),
 }
+# one V-cycle (tv_mgsolve.cpp mg_apply0): every launch of these, all levels, per
+# k_mg_post_faces dispatch (one per V-cycle)
+VCYCLE = ("k_cg_march<1, false", "k_cg_addfaces", "k_mg_restrict", "k_mg_prolong", "k_mg_jacobi", "k_mg_post_faces")
 
 
 def per_kernel(d, counter):
@@ -69,6 +77,13 @@ def main():
         wr = wb * 1024.0
         res["kernels"][name] = {"fetch_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
                                 "dispatches": ff}
+    ncyc = sum(len(v) for k, v in fetch.items() if "k_mg_post_faces" in k)
+    if ncyc:
+        fsum = sum(sum(v) for k, v in fetch.items() if any(p in k for p in VCYCLE))
+        wsum = sum(sum(v) for k, v in write.items() if any(p in k for p in VCYCLE))
+        res["kernels"]["mg_vcycle"] = {"fetch_bytes": 2.0 * fsum * 1024.0 / ncyc, "write_bytes": wsum * 1024.0 / ncyc,
+                                       "hbm_bytes_per_launch": (2.0 * fsum + wsum) * 1024.0 / ncyc,
+                                       "dispatches": [("V-cycles (k_mg_post_faces dispatches)", ncyc)]}
     dom = sys.argv[4] if len(sys.argv) > 4 else "pcg_matvec_fused"
     if dom in res["kernels"]:
         res["dominant"] = dom
