@@ -232,7 +232,7 @@ def main():
     pmc_file = os.path.join(ROOT, "profiles", f"pmc_{dname}_{a.family}_{nc[0]}x{nc[1]}x{nc[2]}_n{world}"
                             + ("_gmg" if pc == "gmg" else "") + ".json")
     pmc = None
-    if os.path.exists(pmc_file):
+    if os.path.exists(pmc_file) and a.share <= 1:  # a share's slab is not the recorded command
         with open(pmc_file) as fh:
             pmc = json.load(fh)
         traffic = pmc.get("hbm_bytes_per_launch")
