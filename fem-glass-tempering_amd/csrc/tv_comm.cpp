@@ -50,8 +50,41 @@ int halo_grid(Ctx* c, const CgGrid& g, double* v) {
   return TV_OK;
 }
 
+// ghosts of a partitioned unstructured mesh: pack the owned values each
+// neighbour holds, then one exchange per neighbour straight into the ghost
+// block that neighbour owns (ascending ranks: the host-staged pairwise
+// exchanges cannot deadlock)
+int halo_um(Ctx* c, double* v) {
+  const int64_t nown = c->ownT_n;
+  const int64_t stot = c->um_soff.empty() ? 0 : c->um_soff.back() + c->um_scnt.back();
+  const int64_t rtot = c->nT - nown;
+  launch_um_pack(c->um_sidx, stot, v, c->um_sbuf, c->stream);
+  if (c->host_sendrecv) {
+    double* hs = c->h_halo;
+    double* hr = c->h_halo + stot;
+    if (stot) HIPC(hipMemcpyAsync(hs, c->um_sbuf, stot * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (size_t k = 0; k < c->um_peer.size(); ++k)
+      if (c->host_sendrecv(hs + c->um_soff[k], (size_t)c->um_scnt[k], c->um_peer[k], hr + c->um_roff[k],
+                           (size_t)c->um_rcnt[k], c->um_peer[k], c->host_user))
+        return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (rtot) HIPC(hipMemcpyAsync(v + nown, hr, rtot * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return TV_OK;
+  }
+  NCCLC(ncclGroupStart());
+  for (size_t k = 0; k < c->um_peer.size(); ++k) {
+    if (c->um_scnt[k]) NCCLC(ncclSend(c->um_sbuf + c->um_soff[k], c->um_scnt[k], ncclDouble, c->um_peer[k], c->comm, c->stream));
+    if (c->um_rcnt[k])
+      NCCLC(ncclRecv(v + nown + c->um_roff[k], c->um_rcnt[k], ncclDouble, c->um_peer[k], c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
 int halo(Ctx* c, double* v) {
   if (!multi_rank(c) || c->fam_T != TV_CG) return TV_OK;
+  if (c->um) return halo_um(c, v);
   return halo_grid(c, c->cg, v);
 }
 
@@ -219,7 +252,10 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
   c->host_allreduce = allreduce_fn;
   c->host_sendrecv = sendrecv_fn;
   c->host_user = user;
-  if (c->fam_T == TV_CG) {
+  if (c->um) {  // the packed sends, then the ghosts
+    const int64_t stot = c->um_soff.empty() ? 0 : c->um_soff.back() + c->um_scnt.back();
+    HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * (size_t)std::max<int64_t>(1, stot + c->nT - c->ownT_n)));
+  } else if (c->fam_T == TV_CG) {
     const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
     HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)plane));
   }

@@ -593,7 +593,7 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
 }
 
 
-static int setup_umesh(Ctx* c, const tv_umesh_desc* m) {
+static int setup_umesh(Ctx* c, const tv_umesh_desc* m, const tv_upart_desc* pd) {
   const int d = m->dim;
   if (d != 2 && d != 3) return c->fail(TV_ERR_ARG, "unstructured meshes: dim 2 (quadrilaterals) or 3 (hexahedra)");
   if (c->fam_T != TV_CG || c->fam_S != TV_CG)
@@ -603,6 +603,44 @@ static int setup_umesh(Ctx* c, const tv_umesh_desc* m) {
   const int nl = 1 << d;
   for (int64_t k = 0; k < m->n_cells * nl; ++k)
     if (m->cells[k] < 0 || m->cells[k] >= m->n_vertices) return c->fail(TV_ERR_ARG, "cell vertex index out of range");
+  int64_t nown = m->n_vertices;
+  if (pd) {  // the partition's communication plan (tv_upart_desc)
+    if (pd->n_parts < 1 || pd->part < 0 || pd->part >= pd->n_parts || pd->n_owned < 1 ||
+        pd->n_owned > m->n_vertices || pd->n_owned_cells < 1 || pd->n_owned_cells > m->n_cells ||
+        pd->global_offset < 0 || pd->n_neighbors < 0 || pd->n_neighbors >= pd->n_parts ||
+        (pd->n_neighbors > 0 && (!pd->neighbors || !pd->recv_count || !pd->send_count)))
+      return c->fail(TV_ERR_ARG, "tv_upart_desc: inconsistent partition description");
+    nown = pd->n_owned;
+    int64_t rt = 0, stot = 0;
+    for (int k = 0; k < pd->n_neighbors; ++k) {
+      const int q = pd->neighbors[k];
+      if (q < 0 || q >= pd->n_parts || q == pd->part || (k > 0 && q <= pd->neighbors[k - 1]) ||
+          pd->recv_count[k] < 0 || pd->send_count[k] < 0)
+        return c->fail(TV_ERR_ARG, "tv_upart_desc: neighbours must be distinct ascending ranks other than part");
+      c->um_peer.push_back(q);
+      c->um_rcnt.push_back(pd->recv_count[k]);
+      c->um_roff.push_back(rt);
+      c->um_scnt.push_back(pd->send_count[k]);
+      c->um_soff.push_back(stot);
+      rt += pd->recv_count[k];
+      stot += pd->send_count[k];
+    }
+    if (nown + rt != m->n_vertices) return c->fail(TV_ERR_ARG, "tv_upart_desc: n_owned + received ghosts != vertices");
+    if (stot > 0 && !pd->send_idx) return c->fail(TV_ERR_ARG, "tv_upart_desc: send_idx missing");
+    for (int64_t k = 0; k < stot; ++k)
+      if (pd->send_idx[k] < 0 || pd->send_idx[k] >= nown)
+        return c->fail(TV_ERR_ARG, "tv_upart_desc: send_idx must name owned vertices");
+    if (stot > 0) {
+      HIPC(hipMalloc(&c->um_sidx, sizeof(int64_t) * (size_t)stot));
+      HIPC(hipMemcpy(c->um_sidx, pd->send_idx, sizeof(int64_t) * (size_t)stot, hipMemcpyHostToDevice));
+      HIPC(hipMalloc(&c->um_sbuf, sizeof(double) * (size_t)stot));
+    }
+    c->n_parts = pd->n_parts;
+    c->part = pd->part;
+    c->um_own_cells = pd->n_owned_cells;
+  } else {
+    c->um_own_cells = m->n_cells;
+  }
   c->um = true;
   c->dim = d;
   c->um_xyz.assign(m->coords, m->coords + 3 * m->n_vertices);
@@ -613,7 +651,7 @@ static int setup_umesh(Ctx* c, const tv_umesh_desc* m) {
   g.a_rad = 0.001 * (P.sigma * P.epsilon); g.a_conv = 0.001 * P.htc;
   g.T_amb = P.T_ambient; g.T_amb4 = P.T_ambient * P.T_ambient * P.T_ambient * P.T_ambient;
   std::string err;
-  if (um_setup(d, m->n_vertices, m->coords, m->n_cells, m->cells, g, c->umd, c->stream, err) != 0)
+  if (um_setup(d, m->n_vertices, nown, m->coords, m->n_cells, m->cells, g, c->umd, c->stream, err) != 0)
     return c->fail(err.rfind("HIP", 0) == 0 ? TV_ERR_HIP : TV_ERR_ARG, err);
   std::vector<unsigned char> bm;
   um_boundary_vertices(c->umd, bm);
@@ -621,14 +659,14 @@ static int setup_umesh(Ctx* c, const tv_umesh_desc* m) {
   HIPC(hipMemcpy(c->um_bmask, bm.data(), bm.size(), hipMemcpyHostToDevice));
   c->nT = c->nS = g.nv;
   c->ownT_off = c->ownS_off = 0;
-  c->ownT_n = c->ownS_n = g.nv;
-  c->globT_off = c->globS_off = 0;
+  c->ownT_n = c->ownS_n = nown;
+  c->globT_off = c->globS_off = pd ? pd->global_offset : 0;
   return TV_OK;
 }
 
 
-int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
-                           const tv_options* opts, int device, void** ctx_out) {
+static int create_unstructured(const tv_umesh_desc* mesh, const tv_upart_desc* part, const tv_fe_config* fe,
+                               const tv_params* params, const tv_options* opts, int device, void** ctx_out) {
   if (!mesh || !fe || !params || !ctx_out) {
     set_global_error("tv_create_unstructured: null argument");
     return TV_ERR_ARG;
@@ -667,7 +705,7 @@ int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, co
     set_global_error("unstructured meshes: preconditioner TV_PC_JACOBI only");
     return TV_ERR_ARG;
   }
-  int rc = setup_umesh(c.get(), mesh);
+  int rc = setup_umesh(c.get(), mesh, part);
   if (rc == TV_OK) rc = setup_fields(c.get());
   if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
   if (rc != TV_OK) {
@@ -677,6 +715,22 @@ int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, co
   }
   *ctx_out = c.release();
   return TV_OK;
+}
+
+
+int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
+                           const tv_options* opts, int device, void** ctx_out) {
+  return create_unstructured(mesh, nullptr, fe, params, opts, device, ctx_out);
+}
+
+
+int tv_create_unstructured_part(const tv_umesh_desc* local_mesh, const tv_upart_desc* part, const tv_fe_config* fe,
+                                const tv_params* params, const tv_options* opts, int device, void** ctx_out) {
+  if (!part) {
+    set_global_error("tv_create_unstructured_part: null partition description");
+    return TV_ERR_ARG;
+  }
+  return create_unstructured(local_mesh, part, fe, params, opts, device, ctx_out);
 }
 
 
@@ -733,6 +787,8 @@ int tv_destroy(void* ctx) {
     if (p) hipFree(p);
   um_free(c->umd);
   if (c->um_bmask) hipFree(c->um_bmask);
+  if (c->um_sidx) hipFree(c->um_sidx);
+  if (c->um_sbuf) hipFree(c->um_sbuf);
   for (MgLevel& L : c->mg) {
     for (void* p : L.bufs) hipFree(p);
     for (int s = 0; s < 3; ++s)
@@ -911,7 +967,13 @@ int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const
   if (c->fam_T == TV_CG && c->n_parts > 1 && !c->um)
     Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin, Xs[2].begin() + c->plane_end);
   std::string err;
-  Output* o = c->um ? output_create_unstructured(dir, c->dim, c->um_xyz, c->um_cells, err)
+  // a partitioned unstructured mesh writes its own cells over all its local
+  // vertices (the ghosts' values are kept current: visco runs on every local vertex)
+  const size_t ncl = (size_t)c->um_own_cells << c->dim;
+  Output* o = c->um ? output_create_unstructured(
+                          dir, c->dim, c->um_xyz,
+                          std::vector<int64_t>(c->um_cells.begin(), c->um_cells.begin() + std::min(ncl, c->um_cells.size())),
+                          err)
                     : output_create(dir, c->dim, Xs, phys, err);
   if (!o) return c->fail(TV_ERR_STATE, "output: " + err);
   static const char* names[TV_NUM_FIELDS] = {
@@ -927,7 +989,7 @@ int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const
     }
     const FieldInfo& fi = c->f[id];
     const bool dg = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
-    const int64_t n = (fi.space == 0) ? c->ownT_n : c->ownS_n;
+    const int64_t n = (c->um && c->n_parts > 1) ? c->nT : (fi.space == 0) ? c->ownT_n : c->ownS_n;
     const char* nm = (series_names && series_names[k] && series_names[k][0]) ? series_names[k] : names[id];
     for (const char* q = nm; *q; ++q)
       if (*q == '/' || *q == '\\') {
@@ -961,8 +1023,9 @@ int tv_output_write(void* ctx, double t) {
   double* d = output_acquire(c->out, &set);
   for (size_t k = 0; k < c->out_fields.size(); ++k) {
     const FieldInfo& fi = c->f[c->out_fields[k]];
-    const int64_t ndof = (fi.space == 0) ? c->ownT_n : c->ownS_n;
-    const int64_t off = (fi.space == 0) ? c->ownT_off : c->ownS_off;
+    const bool local_all = c->um && c->n_parts > 1;  // see tv_output_open_named
+    const int64_t ndof = local_all ? c->nT : (fi.space == 0) ? c->ownT_n : c->ownS_n;
+    const int64_t off = local_all ? 0 : (fi.space == 0) ? c->ownT_off : c->ownS_off;
     const int64_t stride = (fi.space == 0) ? c->nT : c->nS;
     const bool dgsp = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
     const int nl = dgsp ? (1 << c->dim) : 0;

@@ -129,6 +129,15 @@ struct Ctx {
   std::vector<int64_t> um_cells;     // host copy: 2^dim per cell (input order)
   UmDevice* umd = nullptr;            // assembled operators, facet data (tv_um.hip)
   unsigned char* um_bmask = nullptr;  // boundary vertices (Dirichlet mode)
+  // partitioned unstructured mesh (tv_create_unstructured_part): owned vertices
+  // first, ghosts grouped by owner; per neighbour k: the ghosts received from
+  // um_peer[k] at [nown + um_roff[k], + um_rcnt[k]), the owned values sent to it
+  // packed at [um_soff[k], + um_scnt[k]) of um_sbuf (indices um_sidx)
+  int64_t um_own_cells = 0;
+  std::vector<int> um_peer;
+  std::vector<int64_t> um_rcnt, um_roff, um_scnt, um_soff;
+  int64_t* um_sidx = nullptr;
+  double* um_sbuf = nullptr;
   std::vector<int> out_fields;
   double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
   double* wsend = nullptr;

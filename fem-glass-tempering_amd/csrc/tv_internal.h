@@ -154,6 +154,7 @@ struct ViscoFields {
 struct UmGrid {
   int dim;
   int64_t nv, nc, nf, nslice;
+  int64_t nrow;          // rows computed: all nv, or a partition's owned vertices (numbered first)
   // assembled cell operators (entry k of row r: soff[r / 64] + 64 k + r % 64)
   const int64_t* soff;   // nslice + 1
   const int* cols;
@@ -174,8 +175,11 @@ struct UmGrid {
 
 struct UmDevice;  // device allocations of one unstructured mesh (tv_um.hip)
 // builds the operators on the device (stream s, synchronised before return)
-int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g, UmDevice*& dev,
-             hipStream_t s, std::string& err);
+int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g,
+             UmDevice*& dev, hipStream_t s, std::string& err);
+// halo of a partitioned unstructured mesh: out[k] = v[idx[k]], k < n (pack of
+// the owned values every neighbour holds as ghosts)
+void launch_um_pack(const int64_t* idx, int64_t n, const double* v, double* out, hipStream_t s);
 void um_free(UmDevice* dev);
 int64_t um_boundary_vertices(const UmDevice* dev, std::vector<unsigned char>& mask);  // host mask, returns count
 int64_t um_nnz(const UmDevice* dev);                       // stored entries incl. SELL padding

@@ -309,6 +309,9 @@ int dirichlet_pre(Ctx* c, const double* T) {
   const int blocks = (int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock);
   const BndTest bt{c->cg, c->um ? c->um_bmask : nullptr};
   hipLaunchKernelGGL(k_bc_dvec, dim3(blocks), dim3(kBlock), 0, c->stream, bt, T, c->dir_value, c->dB, n);
+  // ghosts from their owners (a partitioned unstructured mesh marks only its
+  // owned boundary vertices; the box's ghost planes agree either way)
+  if (int e = halo(c, c->dB)) return e;
   op_japply(c, T, c->dB, c->dtmp, nullptr, nullptr);
   hipLaunchKernelGGL(k_bc_lift, dim3(blocks), dim3(kBlock), 0, c->stream, bt, c->r, c->dtmp, c->dinv, n);
   HIPC(hipGetLastError());
@@ -431,7 +434,16 @@ int visco(Ctx* c, bool copy_Tprev) {
   ViscoFields v;
   visco_setup(c, k, v);
   const int all = c->O.materialize ? 1 : 0;
-  if (c->fam_T == c->fam_S) {
+  if (c->um && c->n_parts > 1) {
+    // partitioned unstructured mesh: every local vertex, ghosts included (their
+    // T is exchanged after each Newton update and the update is pointwise, so
+    // they evolve exactly as on their owners: the output writes the local cells'
+    // vertices without a further exchange)
+    v.n = c->nT;
+    v.off_T = v.off_S = 0;
+    v.copy_Tprev = copy_Tprev ? 1 : 0;
+    launch_visco(c->dim, all, k, v, c->stream);
+  } else if (c->fam_T == c->fam_S) {
     v.n = c->ownT_n;
     v.off_T = c->ownT_off;
     v.off_S = c->ownS_off;

@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
         for (int j = 0; j < U; ++j) acc += a[j] * u[c[j]];
       }
     }
-    if (r < g.nv) {
+    if (r < g.nrow) {
       double val;
       if (MODE == UM_DIAG) val = g.vdiag[r];
       else if (MODE == UM_RES) val = (acc + acc2) - g.dt_f * g.bvec[r];
@@ -450,6 +450,12 @@ __global__ __launch_bounds__(kBlock) void k_um_pvec(int64_t n, const PcgState* _
     p[t] = first ? z[t] : z[t] + b * po[t];
 }
 
+// the owned values the neighbours hold as ghosts, gathered into the send buffer
+__global__ __launch_bounds__(kBlock) void k_um_pack(const int64_t* __restrict__ idx, int64_t n,
+                                                    const double* __restrict__ v, double* __restrict__ out) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) out[t] = v[idx[t]];
+}
+
 int row_blocks(const UmGrid& g) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((g.nslice + 3) / 4, kUmBlocksMax));
 }
@@ -467,6 +473,11 @@ void launch_rows(const UmGrid& g, const double* T, const double* u, const double
 }  // namespace
 
 int um_num_blocks(const UmGrid& g) { return row_blocks(g); }
+void launch_um_pack(const int64_t* idx, int64_t n, const double* v, double* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_um_pack, dim3((unsigned)std::min<int64_t>(1024, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                     idx, n, v, out);
+}
 int64_t um_nnz(const UmDevice* d) { return d ? d->nnz : 0; }
 int64_t um_boundary_vertices(const UmDevice* d, std::vector<unsigned char>& mask) {
   mask = d->bmask;
@@ -594,9 +605,13 @@ void um_free(UmDevice* d) {
   delete d;
 }
 
-int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g, UmDevice*& dev,
-             hipStream_t s, std::string& err) {
+int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g,
+             UmDevice*& dev, hipStream_t s, std::string& err) {
   const int nl = 1 << dim;
+  if (nrow < 1 || nrow > nv) {
+    err = "unstructured setup: owned rows out of range";
+    return 1;
+  }
   dev = new UmDevice();
   UmDevice* d = dev;
   // -- boundary facets
@@ -612,12 +627,14 @@ int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* 
     for (int64_t e = 0; e < nc; ++e)
       for (int l = 0; l < nl; ++l) inc[(size_t)fill[(size_t)cells[e * nl + l]]++] = (e << 3) | l;
   }
-  // -- sparsity pattern: the vertices of the cells around each vertex (sorted)
+  // -- sparsity pattern: the vertices of the cells around each vertex (sorted);
+  // rows [0, nrow) only (a partition: its owned vertices, whose cells are all
+  // local -- the ghost rows are never computed)
   const int nth = n_threads();
-  std::vector<int> rnnz((size_t)nv, 0);
+  std::vector<int> rnnz((size_t)nrow, 0);
   std::vector<std::vector<int>> part((size_t)nth);
   std::vector<int64_t> r0((size_t)nth + 1);
-  for (int t = 0; t <= nth; ++t) r0[t] = nv * t / nth;
+  for (int t = 0; t <= nth; ++t) r0[t] = nrow * t / nth;
   {
     std::vector<std::thread> th;
     for (int t = 0; t < nth; ++t)
@@ -639,11 +656,11 @@ int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* 
     for (auto& x : th) x.join();
   }
   // -- SELL-64 layout
-  const int64_t nslice = (nv + 63) / 64;
+  const int64_t nslice = (nrow + 63) / 64;
   std::vector<int64_t> soff((size_t)nslice + 1, 0);
   for (int64_t sl = 0; sl < nslice; ++sl) {
     int w = 0;
-    for (int64_t r = sl * 64; r < std::min(nv, sl * 64 + 64); ++r) w = std::max(w, rnnz[(size_t)r]);
+    for (int64_t r = sl * 64; r < std::min(nrow, sl * 64 + 64); ++r) w = std::max(w, rnnz[(size_t)r]);
     soff[(size_t)sl + 1] = soff[(size_t)sl] + 64 * (int64_t)w;
   }
   const int64_t nnz = soff[(size_t)nslice];
@@ -664,7 +681,7 @@ int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* 
       });
     for (auto& x : th) x.join();
   }
-  // padding lanes of the last slice (rows >= nv) keep column 0, value 0
+  // padding lanes of the last slice (rows >= nrow) keep column 0, value 0
   std::vector<std::vector<int>>().swap(part);
   d->nnz = nnz;
   // -- boundary facet data (host): incidences of the boundary rows
@@ -692,9 +709,11 @@ int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* 
         if (((l >> (lf >> 1)) & 1) == (lf & 1)) binc[(size_t)fill[(size_t)cells[e * nl + l]]++] = (int)(4 * f + m++);
     }
   }
+  // (a partition's ghost layer has outer facets that are not on the domain
+  // boundary; no owned row touches them, and the mask covers owned rows only)
   d->bmask.assign((size_t)nv, 0);
   d->nb = 0;
-  for (int64_t v = 0; v < nv; ++v)
+  for (int64_t v = 0; v < nrow; ++v)
     if (boff[(size_t)v + 1] > boff[(size_t)v]) {
       d->bmask[(size_t)v] = 1;
       d->nb++;
@@ -734,14 +753,14 @@ int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* 
   UMC(hipMemsetAsync(vdiag, 0, sizeof(double) * (size_t)nv, s));
   const double dt_alpha = g.dt_alpha;
   const dim3 bl(kBlock);
-  const dim3 gr_v((unsigned)((nv + kBlock - 1) / kBlock)), gr_f((unsigned)std::max<int64_t>(1, (nf + kBlock - 1) / kBlock));
+  const dim3 gr_v((unsigned)((nrow + kBlock - 1) / kBlock)), gr_f((unsigned)std::max<int64_t>(1, (nf + kBlock - 1) / kBlock));
   if (dim == 2) {
-    hipLaunchKernelGGL((k_um_assemble<2>), gr_v, bl, 0, s, nv, nc, cell_d, Xd[0], Xd[1], Xd[2], inc_off_d, inc_d,
+    hipLaunchKernelGGL((k_um_assemble<2>), gr_v, bl, 0, s, nrow, nc, cell_d, Xd[0], Xd[1], Xd[2], inc_off_d, inc_d,
                        soff_d, cols_d, rnnz_d, dt_alpha, V, M, K, bvec, vdiag);
     if (nf) hipLaunchKernelGGL((k_um_facet_setup<2>), gr_f, bl, 0, s, nf, nc, fcell_d, flf_d, cell_d, Xd[0], Xd[1],
                                Xd[2], fv_d, fw);
   } else {
-    hipLaunchKernelGGL((k_um_assemble<3>), gr_v, bl, 0, s, nv, nc, cell_d, Xd[0], Xd[1], Xd[2], inc_off_d, inc_d,
+    hipLaunchKernelGGL((k_um_assemble<3>), gr_v, bl, 0, s, nrow, nc, cell_d, Xd[0], Xd[1], Xd[2], inc_off_d, inc_d,
                        soff_d, cols_d, rnnz_d, dt_alpha, V, M, K, bvec, vdiag);
     if (nf) hipLaunchKernelGGL((k_um_facet_setup<3>), gr_f, bl, 0, s, nf, nc, fcell_d, flf_d, cell_d, Xd[0], Xd[1],
                                Xd[2], fv_d, fw);
@@ -754,6 +773,7 @@ int um_setup(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* 
     release(d, p);
   g.dim = dim;
   g.nv = nv;
+  g.nrow = nrow;
   g.nc = nc;
   g.nf = nf;
   g.nslice = nslice;

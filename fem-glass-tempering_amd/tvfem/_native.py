@@ -18,7 +18,7 @@ TV_PCG_AUTO, TV_PCG_KSPCG, TV_PCG_SINGLE_REDUCTION = 0, 1, 2
 TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
 TV_PC_JACOBI, TV_PC_GMG = 0, 1
 TV_DG_KERNEL_AUTO, TV_DG_KERNEL_TILE, TV_DG_KERNEL_CELLS = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -31,7 +31,7 @@ FIELD_ID = {n: i for i, n in enumerate(FIELDS)}
 
 # every C symbol include/tvfem.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "tv_abi_version", "tv_last_error", "tv_default_options", "tv_default_params", "tv_create", "tv_create_unstructured", "tv_partition_rcb", "tv_destroy",
+    "tv_abi_version", "tv_last_error", "tv_default_options", "tv_default_params", "tv_create", "tv_create_unstructured", "tv_create_unstructured_part", "tv_partition_rcb", "tv_destroy",
     "tv_num_dofs", "tv_field_block_size", "tv_dof_coordinates", "tv_set_field", "tv_get_field",
     "tv_field_device_ptr", "tv_set_initial_condition", "tv_sync", "tv_residual", "tv_jacobian_apply",
     "tv_jacobian_diag", "tv_precond_apply", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
@@ -60,6 +60,13 @@ class MeshDesc(C.Structure):
 class UMeshDesc(C.Structure):
     _fields_ = [("dim", C.c_int), ("n_vertices", C.c_int64), ("coords", C.POINTER(C.c_double)),
                 ("n_cells", C.c_int64), ("cells", C.POINTER(C.c_int64))]
+
+
+class UPartDesc(C.Structure):
+    _fields_ = [("n_parts", C.c_int), ("part", C.c_int), ("n_owned", C.c_int64), ("n_owned_cells", C.c_int64),
+                ("global_offset", C.c_int64), ("n_neighbors", C.c_int), ("neighbors", C.POINTER(C.c_int)),
+                ("recv_count", C.POINTER(C.c_int64)), ("send_count", C.POINTER(C.c_int64)),
+                ("send_idx", C.POINTER(C.c_int64))]
 
 
 class FeConfig(C.Structure):
@@ -115,6 +122,9 @@ def load_library():
         "tv_default_params": (None, [C.POINTER(Params)]),
         "tv_create_unstructured": (C.c_int, [C.POINTER(UMeshDesc), C.POINTER(FeConfig), C.POINTER(Params),
                                              C.POINTER(Options), C.c_int, C.POINTER(C.c_void_p)]),
+        "tv_create_unstructured_part": (C.c_int, [C.POINTER(UMeshDesc), C.POINTER(UPartDesc), C.POINTER(FeConfig),
+                                                  C.POINTER(Params), C.POINTER(Options), C.c_int,
+                                                  C.POINTER(C.c_void_p)]),
         "tv_partition_rcb": (C.c_int, [C.POINTER(UMeshDesc), C.c_int, C.POINTER(C.c_int)]),
         "tv_create": (C.c_int, [C.POINTER(MeshDesc), C.POINTER(FeConfig), C.POINTER(Params), C.POINTER(Options),
                                 C.c_int, C.POINTER(vp)]),

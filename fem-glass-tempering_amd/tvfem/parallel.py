@@ -85,6 +85,78 @@ def partition_submesh(mesh, part: np.ndarray, p: int):
     return {"mesh": sub, "l2g": l2g, "n_owned": len(own), "ghost_owner": owner[ghost]}
 
 
+def ghosted_partition(mesh, part: np.ndarray, p: int, n_parts: int | None = None) -> dict:
+    """Partition ``p`` of an unstructured mesh with its ghost layer and halo
+    plan, as tv_create_unstructured_part takes it (include/tvfem.h
+    tv_upart_desc).  ``part``: cell -> part ids (rcb_partition).
+
+    A vertex is owned by the lowest part among the cells around it.  Local
+    cells: the part's own cells, then every other cell that touches one of its
+    owned vertices, so each owned row of F and J is complete on the part (the
+    ghost layer dolfinx keeps for ThermoViscoProblem.py:351's scatter_forward).
+    Local vertices: owned first (ascending global id), then the ghosts grouped
+    by owner (ascending rank), each group ascending -- the order in which the
+    owner packs them.  Neighbours: the parts this one receives from or sends
+    to (the relation is symmetric by construction, so both sides of every pair
+    call the exchange).  Every rank computes the plan from the global mesh."""
+    from .mesh import UnstructuredMesh
+    cells = np.asarray(mesh.cells, dtype=np.int64)
+    part = np.asarray(part, dtype=np.int64)
+    nv, nl = mesh.num_vertices, cells.shape[1]
+    P = int(part.max()) + 1 if n_parts is None else int(n_parts)
+    owner = np.full(nv, np.iinfo(np.int64).max, dtype=np.int64)
+    np.minimum.at(owner, cells.ravel(), np.repeat(part, nl))
+    counts = np.bincount(owner, minlength=P)
+    ocell = owner[cells]                                   # (nc, nl) owners of each cell's vertices
+    own_c = np.flatnonzero(part == p)
+    ghost_c = np.flatnonzero((part != p) & (ocell == p).any(axis=1))
+    lc = np.concatenate([own_c, ghost_c])
+    used = np.unique(cells[lc].ravel())
+    own_v = used[owner[used] == p]
+    gv = used[owner[used] != p]
+    gv = gv[np.lexsort((gv, owner[gv]))]
+    l2g = np.concatenate([own_v, gv])
+    g2l = np.full(nv, -1, dtype=np.int64)
+    g2l[l2g] = np.arange(len(l2g))
+    # sends: owned vertex v goes to every part q != p for which a cell around v
+    # is local: q = the cell's part or an owner of one of its vertices
+    cand = lc[(np.concatenate([part[lc, None], ocell[lc]], axis=1) != p).any(axis=1)]
+    lp = np.concatenate([part[cand, None], ocell[cand]], axis=1)   # (m, nl + 1) parts the cell is local to
+    cv = cells[cand]                                                 # (m, nl)
+    qq = np.repeat(lp[:, :, None], nl, axis=2)                       # (m, nl + 1, nl)
+    vv = np.repeat(cv[:, None, :], lp.shape[1], axis=1)
+    ok = (qq != p) & (owner[vv] == p)
+    pairs = np.unique(np.stack([qq[ok], vv[ok]], axis=1), axis=0) if ok.any() else np.zeros((0, 2), np.int64)
+    recv_from = np.unique(owner[gv])
+    nbrs = np.union1d(recv_from, np.unique(pairs[:, 0])).astype(np.int64)
+    recv_count = np.array([np.count_nonzero(owner[gv] == q) for q in nbrs], dtype=np.int64)
+    send_idx, send_count = [], []
+    for q in nbrs:
+        sv = pairs[pairs[:, 0] == q, 1]                              # ascending global ids (np.unique order)
+        send_idx.append(g2l[sv])
+        send_count.append(len(sv))
+    sub = UnstructuredMesh(mesh.dim, mesh.x[l2g], g2l[cells[lc]])
+    return {"mesh": sub, "l2g": l2g, "n_owned": len(own_v), "n_owned_cells": len(own_c),
+            "global_offset": int(counts[:p].sum()), "neighbors": nbrs.astype(np.int32),
+            "recv_count": recv_count, "send_count": np.array(send_count, dtype=np.int64),
+            "send_idx": (np.concatenate(send_idx) if send_idx else np.zeros(0, np.int64)).astype(np.int64),
+            "n_parts": P, "part": int(p)}
+
+
+def upart_desc(gp: dict):
+    """(tv_upart_desc, buffers to keep alive) of a ghosted_partition record."""
+    d = N.UPartDesc()
+    bufs = [np.ascontiguousarray(gp[k]) for k in ("neighbors", "recv_count", "send_count", "send_idx")]
+    d.n_parts, d.part = gp["n_parts"], gp["part"]
+    d.n_owned, d.n_owned_cells, d.global_offset = gp["n_owned"], gp["n_owned_cells"], gp["global_offset"]
+    d.n_neighbors = len(bufs[0])
+    d.neighbors = bufs[0].ctypes.data_as(C.POINTER(C.c_int))
+    d.recv_count = bufs[1].ctypes.data_as(C.POINTER(C.c_int64))
+    d.send_count = bufs[2].ctypes.data_as(C.POINTER(C.c_int64))
+    d.send_idx = bufs[3].ctypes.data_as(C.POINTER(C.c_int64))
+    return d, bufs
+
+
 def init_rccl(problem, rank: int, world: int, dist=None):
     """Create the RCCL communicator of a partitioned problem (rank 0 makes the id)."""
     if dist is None:

@@ -111,7 +111,8 @@ class ThermoViscoProblem:
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
                  write_output: bool | None = None, output_dir: str = "output", preconditioner: str = "jacobi",
                  mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0,
-                 mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0, newton_fixed_its: int = 0) -> None:
+                 mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0, newton_fixed_its: int = 0,
+                 cell_parts=None) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -152,6 +153,8 @@ class ThermoViscoProblem:
         self._mg_replicate_nodes = int(mg_replicate_nodes)
         self._ksp_fixed_its = int(ksp_fixed_its)
         self._newton_fixed_its = int(newton_fixed_its)
+        # partitioned unstructured mesh: cell -> part ids (default: tv_partition_rcb)
+        self._cell_parts = None if cell_parts is None else np.asarray(cell_parts)
         self.__init_native(model_parameters, device, materialize, ksp_rtol, n_parts, part, part_axis, pcg_variant)
         self.__init_functions()
         self.material_model._init_expressions(functionSpaces=self.functionSpaces, functions=self.functions,
@@ -184,16 +187,23 @@ class ThermoViscoProblem:
         um = isinstance(self.mesh, UnstructuredMesh)
         if um:
             # general quadrilateral / hexahedral cells: element-local kernels
-            # (csrc/tv_um.hip), one partition, CG1 spaces
-            if n_parts != 1:
-                raise NotImplementedError("unstructured meshes run on one partition (see tvfem.parallel.rcb_partition)")
+            # (csrc/tv_um.hip), CG1 spaces; partitioned: recursive coordinate
+            # bisection of the cells + a ghost layer (tvfem.parallel.ghosted_partition,
+            # the mesh distribution of gmshio.read_from_msh at ThermoViscoProblem.py:27-28)
             if self._fam["T"] != "CG" or self._fam["sigma"] != "CG":
                 raise NotImplementedError("unstructured meshes: CG temperature and stress spaces")
+            local = self.mesh
+            self._upart = None
+            if n_parts > 1:
+                from .parallel import ghosted_partition, rcb_partition
+                cp = rcb_partition(self.mesh, n_parts) if self._cell_parts is None else self._cell_parts
+                self._upart = ghosted_partition(self.mesh, cp, part, n_parts)
+                local = self._upart["mesh"]
             desc = N.UMeshDesc()
             desc.dim = self.dim
-            xyz = np.zeros((self.mesh.num_vertices, 3))
-            xyz[:, :self.dim] = self.mesh.x[:, :self.dim]
-            cells = np.ascontiguousarray(self.mesh.cells, dtype=np.int64)
+            xyz = np.zeros((local.num_vertices, 3))
+            xyz[:, :self.dim] = local.x[:, :self.dim]
+            cells = np.ascontiguousarray(local.cells, dtype=np.int64)
             self._coord_bufs = [xyz, cells]
             desc.n_vertices = xyz.shape[0]
             desc.coords = xyz.ctypes.data_as(C.POINTER(C.c_double))
@@ -235,8 +245,15 @@ class ThermoViscoProblem:
             opts.newton_max_it = self._newton_fixed_its
             opts.error_on_nonconvergence = 0
         ctx = C.c_void_p()
-        create = lib.tv_create_unstructured if um else lib.tv_create
-        N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
+        if um and self._upart is not None:
+            from .parallel import upart_desc
+            pdesc, pbufs = upart_desc(self._upart)
+            self._coord_bufs.append(pbufs)
+            N.check(lib.tv_create_unstructured_part(C.byref(desc), C.byref(pdesc), C.byref(fe), C.byref(params),
+                                                    C.byref(opts), device, C.byref(ctx)))
+        else:
+            create = lib.tv_create_unstructured if um else lib.tv_create
+            N.check(create(C.byref(desc), C.byref(fe), C.byref(params), C.byref(opts), device, C.byref(ctx)))
         self._ctx = ctx
         self.materialize = materialize
         self._bs = {}

@@ -51,8 +51,9 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 3  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
-                            3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its */
+#define TV_ABI_VERSION 4  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+                            3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its;
+                            4: tv_upart_desc / tv_create_unstructured_part */
 
 /* status codes */
 #define TV_OK 0
@@ -89,8 +90,8 @@ typedef struct {
  * shape, as gmsh writes them (geometry.py / gmshio.read_from_msh at
  * ThermoViscoProblem.py:27-28).  coords: 3 doubles per vertex; cells: 2^dim
  * vertex ids per cell in the tensor local order l = a + 2b + 4c (basix /
- * dolfinx order).  One partition, CG1 temperature and stress spaces;
- * assembled by the element-local kernels (csrc/tv_um.hip). */
+ * dolfinx order).  CG1 temperature and stress spaces; assembled by the
+ * element-local kernels (csrc/tv_um.hip). */
 typedef struct {
   int dim;
   int64_t n_vertices;
@@ -98,6 +99,33 @@ typedef struct {
   int64_t n_cells;
   const int64_t* cells;
 } tv_umesh_desc;
+
+/* One partition of a distributed unstructured mesh (the dolfinx mesh
+ * distribution of gmshio.read_from_msh(..., MPI.COMM_WORLD, 0) at
+ * ThermoViscoProblem.py:27-28, with the ghost layer dolfinx keeps for the
+ * scatter_forward of :351).  The local tv_umesh_desc passed with it holds
+ *   vertices: the n_owned owned vertices first, then the ghosts grouped by
+ *             owner in the order of `neighbors` (recv_count[k] of them for
+ *             neighbors[k]), each group in the owner's send order;
+ *   cells:    the n_owned_cells cells of this part first, then every other
+ *             cell that touches an owned vertex (so each owned row of F and J
+ *             is complete).
+ * The halo sends send_count[k] owned values, at the local indices listed in
+ * send_idx (concatenated over k), to neighbors[k] and receives that
+ * neighbour's ghosts in place.  global_offset: global index of owned vertex 0
+ * in the partition-major numbering (sum of the lower parts' n_owned). */
+typedef struct {
+  int n_parts;
+  int part;
+  int64_t n_owned;
+  int64_t n_owned_cells;
+  int64_t global_offset;
+  int n_neighbors;
+  const int* neighbors;        /* ascending ranks */
+  const int64_t* recv_count;   /* n_neighbors */
+  const int64_t* send_count;   /* n_neighbors */
+  const int64_t* send_idx;     /* sum(send_count) local owned indices */
+} tv_upart_desc;
 
 typedef struct {
   int T_family;      /* TV_CG / TV_DG  (fe_config["T"]["element"])      */
@@ -228,6 +256,11 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
               const tv_options* opts, int device, void** ctx_out);
 int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, const tv_params* params,
                            const tv_options* opts, int device, void** ctx_out);
+/* partition `part->part` of a distributed unstructured mesh (local mesh as
+ * tv_upart_desc describes); the communicator (tv_comm_init / _host) must be
+ * set before the first step.  Jacobi-PCG (KSPCG form), no Dirichlet mode. */
+int tv_create_unstructured_part(const tv_umesh_desc* local_mesh, const tv_upart_desc* part, const tv_fe_config* fe,
+                                const tv_params* params, const tv_options* opts, int device, void** ctx_out);
 int tv_destroy(void* ctx);
 
 /* Host-only (no GPU needed): layout of partition `part` of a CG1 mesh —

@@ -39,7 +39,7 @@ fi
 step "bench C4 (CPU baseline: the C/OpenMP port with the same GMG)"
 timeout -k 10 600 python3 bench.py > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail -5 $OUT/bench_c4.err; exit 1; }
 cat $OUT/bench_c4.json
-for spec in "C2 100,100,10 --thermal-only" "C3 200,200,25" "C3j 200,200,25 --pc jacobi" "C5 200,200,25 --family DG" "C4j 400,400,50 --pc jacobi" "n2 400,400,50 --share 2" "n4 400,400,50 --share 4" "n8 400,400,50 --share 8"; do
+for spec in "C2 100,100,10 --thermal-only" "C3 200,200,25" "C3g 200,200,25 --pc gmg" "C5 200,200,25 --family DG" "C4j 400,400,50 --pc jacobi" "n2 400,400,50 --share 2" "n4 400,400,50 --share 4" "n8 400,400,50 --share 8"; do
   set -- $spec; tag=$1; cells=$2; shift 2
   step "bench $tag"
   timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --cells $cells "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err || { tail -5 $OUT/bench_$tag.err; exit 1; }

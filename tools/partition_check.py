@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from tvfem import box_mesh  # noqa: E402
+from tvfem import box_mesh, distorted_box_mesh  # noqa: E402
 from tvfem.parallel import init_host_comm, init_rccl  # noqa: E402
 from tvfem.problem import ThermoViscoProblem  # noqa: E402
 
@@ -49,6 +49,9 @@ def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False,
         p.solve_timestep()
         its.append((p.last_newton_iterations, p.last_krylov_iterations))
     out = {k: p.get_field(k) for k in ("T", "phi", "xi", "sigma")}
+    up = getattr(p, "_upart", None)
+    if up is not None:  # unstructured partition: owned vertices -> global ids
+        out["l2g"] = up["l2g"][:up["n_owned"]]
     p.close()
     return out, its
 
@@ -61,6 +64,8 @@ def main():
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
     ap.add_argument("--edit", action="store_true", help="host edit of T on the owning rank only, after setup()")
     ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi")
+    ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
+                    help="distorted: the box as a general hexahedral mesh (tv_um.hip), RCB cell partition + ghost layer")
     ap.add_argument("--mg-replicate", type=int, default=0,
                     help="GMG: coarse levels of at most this many nodes replicated (0: the library default)")
     a = ap.parse_args()
@@ -69,7 +74,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", rank))
     dist.init_process_group("gloo")
     nc = [int(v) for v in a.cells.split(",")]
-    mesh = box_mesh([2.0, 6.0, 1.0], nc)
+    mesh = (distorted_box_mesh if a.mesh == "distorted" else box_mesh)([2.0, 6.0, 1.0], nc)
     steps = a.steps
     if a.comm == "rccl":
         if torch.cuda.device_count() < world:
@@ -83,9 +88,15 @@ def main():
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
         ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc)
-        res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "its_parts": its, "its_single": its_ref}
+        res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "mesh": a.mesh, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
-            full = np.concatenate([np.asarray(g[k]) for g in gathered])
+            if "l2g" in gathered[0]:  # scatter every part's owned vertices to their global ids
+                full = np.zeros_like(ref[k]).reshape(mesh.num_vertices, -1)
+                for g in gathered:
+                    full[np.asarray(g["l2g"], dtype=np.int64)] = np.asarray(g[k]).reshape(len(g["l2g"]), -1)
+                full = full.ravel()
+            else:
+                full = np.concatenate([np.asarray(g[k]) for g in gathered])
             e = np.linalg.norm(full - ref[k]) / np.linalg.norm(ref[k])
             res[k] = float(e)
         print("PARTITION_CHECK " + json.dumps(res), flush=True)
