@@ -55,10 +55,11 @@ def parse():
     ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
                     help="box: the rectilinear plate (tensor-product kernels); distorted: the same plate as a "
                          "general hexahedral mesh (jittered, sheared, warped; element-local kernels, one GPU)")
-    ap.add_argument("--pc", choices=["auto", "jacobi", "gmg"], default="auto",
+    ap.add_argument("--pc", choices=["auto", "jacobi", "gmg", "amg"], default="auto",
                     help="preconditioner: gmg (geometric multigrid on the box hierarchy, 3D box; distributed "
-                         "over the ranks when partitioned), jacobi, or auto (gmg where it applies and the mesh "
-                         "has >= 4M T-dofs, at every rank count)")
+                         "over the ranks when partitioned), amg (smoothed-aggregation AMG, --mesh distorted on "
+                         "one GPU), jacobi, or auto (gmg where it applies and the mesh has >= 4M T-dofs, at "
+                         "every rank count)")
     ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
     ap.add_argument("--share", type=int, default=0, metavar="N",
                     help="time ONE rank's share of an N-way partition of the mesh on this GPU with the "
@@ -94,8 +95,8 @@ def main():
         nc[1] *= world
         L[1] *= world
     um = a.mesh == "distorted"
-    if um and (world > 1 or a.family != "CG"):
-        raise SystemExit("--mesh distorted: one GPU, CG1 (unstructured meshes run on one partition)")
+    if um and a.family != "CG":
+        raise SystemExit("--mesh distorted: CG1 (unstructured meshes)")
     mesh = distorted_box_mesh(L, nc) if um else box_mesh(L, nc)
     mp = {
         "f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0,
@@ -117,7 +118,8 @@ def main():
         # the same solver at every rank count: partitioned boxes run the distributed
         # V-cycle (tv_mgdist.cpp), so N = 1 and N > 1 lines compare like with like
         pc = "gmg" if (not um and a.pcg != "single" and big) else "jacobi"
-    kw = {} if um else {"n_parts": world, "part": rank, "part_axis": 1}
+    # unstructured: RCB cell partition + ghost layer (tvfem.parallel.ghosted_partition)
+    kw = {"n_parts": world, "part": rank} if um else {"n_parts": world, "part": rank, "part_axis": 1}
     if a.share > 1:  # a middle rank's slab (ghost planes both sides), no communicator
         if world > 1 or um:
             raise SystemExit("--share: one process, box mesh")
@@ -193,6 +195,9 @@ def main():
         names = {3: "pcg_matvec_fused", 11: "mg_vcycle", 0: "jacobian_apply", 2: "residual"}
     if um:  # element-local kernels: J x (coloured cell + facet launches) is the roofline kernel
         names = {0: "jacobian_apply_unstructured", 3: "pcg_matvec_unstructured", 4: "pcg_update", 2: "residual"}
+        if pc == "amg":  # the update is k_mg_update (no stamps); the algebraic V-cycle timed as a whole
+            names = {0: "jacobian_apply_unstructured", 3: "pcg_matvec_unstructured", 11: "mg_vcycle",
+                     2: "residual"}
     if not a.thermal_only:
         names[1] = "visco_update"
     for kid, name in names.items():
@@ -290,13 +295,16 @@ def main():
                                        "compute floor, not a multi-GPU measurement"
                                        if a.share > 1 else
                                        "single GPU, one partition (no communication)" if world == 1 else
-                                       f"mesh partition along y x{world} ("
+                                       (f"RCB cell partition x{world} with a ghost-cell layer ("
+                                        if um else f"mesh partition along y x{world} (")
                                        + ("RCCL halo + allreduce" if a.comm == "rccl" else "host-staged gloo") + ")"),
                        "newton_its_per_step": nits / a.steps, "krylov_its_per_step": kits / a.steps,
                        "output": (f"T, phi, Tf, xi, sigma written every step (async XDMF) to {a.output}"
                                   if a.output else "none (reference writes VTX/XDMF every step)"),
                        "krylov_form": ("single-reduction (Chronopoulos-Gear) Jacobi-PCG" if single
                                        else "PETSc KSPCG Jacobi-PCG" if pc == "jacobi"
+                                       else "PETSc KSPCG, smoothed-aggregation AMG preconditioner (additive "
+                                       "level 0)" if pc == "amg"
                                        else "PETSc KSPCG, geometric-multigrid V-cycle preconditioner"),
                        "preconditioner": pc,
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},

@@ -1,0 +1,436 @@
+// Smoothed-aggregation algebraic multigrid (options.preconditioner = TV_PC_AMG)
+// for the unstructured meshes: host setup of the hierarchy and the V-cycle.
+//
+// The reference preconditions its CG with PETSc's PCGAMG (ThermoViscoProblem.py:
+// 343-346), a smoothed-aggregation AMG built from the assembled matrix; the box
+// meshes use the geometric hierarchy of tv_mgsolve.cpp instead.  Here, for
+// general hexahedra / quadrilaterals:
+//   * the hierarchy is built ONCE, from the T-independent cell operator
+//     V = M + dt alpha K (the SELL-64 matrix tv_um.hip assembles at creation);
+//     the Robin term of J(T) enters the fine level only (its diagonal in the
+//     smoother, its product in the Krylov matvec), so B is a fixed SPD
+//     operator per Newton iteration and CG stays CG;
+//   * aggregation: greedy, every off-diagonal nonzero strong (PCGAMG's default
+//     threshold 0): (1) a node whose neighbours are all free seeds an aggregate
+//     of itself and its neighbours, (2) the remaining free nodes join the
+//     aggregate of their first aggregated neighbour, (3) leftovers seed
+//     aggregates of their free neighbours;
+//   * tentative prolongation: piecewise constant (the constant near-null
+//     space of the heat operator); smoothed P = (I - 4/3 / lambda D^-1 A) P0,
+//     lambda = lambda_max(D^-1 A) by power iteration; Galerkin A_c = P^T A P;
+//     until <= kAmgCoarseRows rows (or the options.mg_levels depth);
+//   * cycle: level 0 ADDITIVE -- z = omega0 D^-1 r + P_0 V_1(P_0^T r) -- so the
+//     preconditioner never applies the fine operator (a fine J x streams
+//     ~330 B per row on these meshes; the Krylov matvec is the only one per
+//     iteration); levels >= 1 multiplicative V(1,1) with damped Jacobi
+//     (omega = 2 / (1.1 lambda_max(D^-1 A_l))), one Jacobi step on the
+//     coarsest level.  Measured in a numpy model of the distorted plate
+//     (544K vertices, the Newton right-hand side): Jacobi-PCG 35 iterations,
+//     this cycle 12, a multiplicative V(1,1) 11 (at three fine J x per
+//     iteration instead of one), unsmoothed aggregation 16.
+#include <numeric>
+#include <thread>
+
+#include "tv_ctx.h"
+
+namespace tv {
+namespace {
+
+constexpr int64_t kAmgCoarseRows = 2000;
+
+struct Csr {
+  int64_t n = 0, m = 0;  // rows, columns
+  std::vector<int64_t> ptr;
+  std::vector<int> col;
+  std::vector<double> val;
+};
+
+int n_workers() {
+  const unsigned h = std::thread::hardware_concurrency();
+  return (int)std::max(1u, std::min(16u, h ? h : 1u));
+}
+
+// f(t, r0, r1) on contiguous row ranges, one per worker thread
+template <class F>
+void par_ranges(int64_t n, F f) {
+  const int nt = (int)std::min<int64_t>(n_workers(), std::max<int64_t>(1, n / 4096));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) th.emplace_back([&, t]() { f(t, n * t / nt, n * (t + 1) / nt); });
+  for (auto& x : th) x.join();
+}
+
+void spmv(const Csr& A, const std::vector<double>& x, std::vector<double>& y) {
+  par_ranges(A.n, [&](int, int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      double s = 0.0;
+      for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k) s += A.val[k] * x[A.col[k]];
+      y[r] = s;
+    }
+  });
+}
+
+std::vector<double> diag_inv(const Csr& A) {
+  std::vector<double> d((size_t)A.n, 0.0);
+  for (int64_t r = 0; r < A.n; ++r)
+    for (int64_t k = A.ptr[r]; k < A.ptr[r + 1]; ++k)
+      if (A.col[k] == (int)r) d[r] = 1.0 / A.val[k];
+  return d;
+}
+
+// lambda_max(D^-1 A) by power iteration (fixed-seed start vector: reproducible)
+double lam_max(const Csr& A, const std::vector<double>& dinv, int its) {
+  std::vector<double> v((size_t)A.n), w((size_t)A.n);
+  uint64_t st = 0x2545F4914F6CDD1Dull;
+  for (auto& e : v) {
+    st ^= st << 13; st ^= st >> 7; st ^= st << 17;
+    e = 0.5 + (double)(st >> 11) * (1.0 / 9007199254740992.0);
+  }
+  double l = 1.0;
+  for (int it = 0; it < its; ++it) {
+    double nv = 0.0;
+    for (double e : v) nv += e * e;
+    nv = std::sqrt(nv);
+    for (auto& e : v) e /= nv;
+    spmv(A, v, w);
+    double s = 0.0;
+    for (int64_t r = 0; r < A.n; ++r) {
+      w[r] *= dinv[r];
+      s += w[r] * w[r];
+    }
+    l = std::sqrt(s);
+    v.swap(w);
+  }
+  return l;
+}
+
+// greedy aggregation (see the header); returns the aggregate of every row
+std::vector<int> aggregate(const Csr& A, int64_t& na) {
+  std::vector<int> agg((size_t)A.n, -1);
+  na = 0;
+  for (int64_t i = 0; i < A.n; ++i) {  // pass 1: seeds with all neighbours free
+    if (agg[i] >= 0) continue;
+    bool free = true;
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1] && free; ++k) free = agg[A.col[k]] < 0;
+    if (!free) continue;
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) agg[A.col[k]] = (int)na;
+    agg[i] = (int)na++;
+  }
+  std::vector<int> join((size_t)A.n, -1);
+  for (int64_t i = 0; i < A.n; ++i) {  // pass 2: join the first aggregated neighbour
+    if (agg[i] >= 0) continue;
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k)
+      if (agg[A.col[k]] >= 0) {
+        join[i] = agg[A.col[k]];
+        break;
+      }
+  }
+  for (int64_t i = 0; i < A.n; ++i)
+    if (join[i] >= 0) agg[i] = join[i];
+  for (int64_t i = 0; i < A.n; ++i) {  // pass 3: leftovers with their free neighbours
+    if (agg[i] >= 0) continue;
+    for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k)
+      if (agg[A.col[k]] < 0) agg[A.col[k]] = (int)na;
+    agg[i] = (int)na++;
+  }
+  return agg;
+}
+
+// P = (I - w D^-1 A) P0, P0 the aggregate indicator (columns sorted per row)
+Csr smoothed_p(const Csr& A, const std::vector<double>& dinv, const std::vector<int>& agg, int64_t na, double w) {
+  Csr P;
+  P.n = A.n;
+  P.m = na;
+  std::vector<int64_t> cnt((size_t)A.n + 1, 0);
+  std::vector<std::vector<int>> cols_t((size_t)n_workers());
+  std::vector<std::vector<double>> vals_t((size_t)n_workers());
+  std::vector<std::pair<int64_t, int64_t>> rng((size_t)n_workers(), {0, 0});
+  par_ranges(A.n, [&](int t, int64_t r0, int64_t r1) {
+    rng[t] = {r0, r1};
+    std::vector<std::pair<int, double>> e;
+    for (int64_t i = r0; i < r1; ++i) {
+      e.clear();
+      e.emplace_back(agg[i], 1.0);
+      for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) e.emplace_back(agg[A.col[k]], -w * dinv[i] * A.val[k]);
+      std::stable_sort(e.begin(), e.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+      int64_t c0 = 0;
+      for (size_t q = 0; q < e.size();) {  // merge equal aggregates (fixed order: deterministic sums)
+        size_t u = q;
+        double s = 0.0;
+        while (u < e.size() && e[u].first == e[q].first) s += e[u++].second;
+        cols_t[t].push_back(e[q].first);
+        vals_t[t].push_back(s);
+        ++c0;
+        q = u;
+      }
+      cnt[i + 1] = c0;
+    }
+  });
+  P.ptr.assign((size_t)A.n + 1, 0);
+  for (int64_t i = 0; i < A.n; ++i) P.ptr[i + 1] = P.ptr[i] + cnt[i + 1];
+  P.col.resize((size_t)P.ptr[A.n]);
+  P.val.resize((size_t)P.ptr[A.n]);
+  for (size_t t = 0; t < rng.size(); ++t) {
+    if (rng[t].second <= rng[t].first) continue;
+    std::copy(cols_t[t].begin(), cols_t[t].end(), P.col.begin() + P.ptr[rng[t].first]);
+    std::copy(vals_t[t].begin(), vals_t[t].end(), P.val.begin() + P.ptr[rng[t].first]);
+  }
+  return P;
+}
+
+Csr transpose(const Csr& P) {
+  Csr R;
+  R.n = P.m;
+  R.m = P.n;
+  R.ptr.assign((size_t)R.n + 1, 0);
+  for (int c : P.col) R.ptr[(size_t)c + 1]++;
+  for (int64_t r = 0; r < R.n; ++r) R.ptr[r + 1] += R.ptr[r];
+  R.col.resize(P.col.size());
+  R.val.resize(P.val.size());
+  std::vector<int64_t> fill(R.ptr.begin(), R.ptr.end() - 1);
+  for (int64_t i = 0; i < P.n; ++i)  // rows in order: each R row's columns ascend
+    for (int64_t k = P.ptr[i]; k < P.ptr[i + 1]; ++k) {
+      const int64_t q = fill[P.col[k]]++;
+      R.col[q] = (int)i;
+      R.val[q] = P.val[k];
+    }
+  return R;
+}
+
+// C = A B (rows in parallel, a dense accumulator per worker; columns sorted)
+Csr spgemm(const Csr& A, const Csr& B) {
+  Csr C;
+  C.n = A.n;
+  C.m = B.m;
+  const int nw = n_workers();
+  std::vector<std::vector<int>> cols_t((size_t)nw);
+  std::vector<std::vector<double>> vals_t((size_t)nw);
+  std::vector<std::pair<int64_t, int64_t>> rng((size_t)nw, {0, 0});
+  std::vector<int64_t> cnt((size_t)A.n + 1, 0);
+  par_ranges(A.n, [&](int t, int64_t r0, int64_t r1) {
+    rng[t] = {r0, r1};
+    std::vector<double> acc((size_t)B.m, 0.0);
+    std::vector<int> mark((size_t)B.m, -1), touched;
+    for (int64_t i = r0; i < r1; ++i) {
+      touched.clear();
+      for (int64_t k = A.ptr[i]; k < A.ptr[i + 1]; ++k) {
+        const double a = A.val[k];
+        const int j = A.col[k];
+        for (int64_t q = B.ptr[j]; q < B.ptr[j + 1]; ++q) {
+          const int c = B.col[q];
+          if (mark[c] != (int)i) {
+            mark[c] = (int)i;
+            acc[c] = 0.0;
+            touched.push_back(c);
+          }
+          acc[c] += a * B.val[q];
+        }
+      }
+      std::sort(touched.begin(), touched.end());
+      for (int c : touched) {
+        cols_t[t].push_back(c);
+        vals_t[t].push_back(acc[c]);
+      }
+      cnt[i + 1] = (int64_t)touched.size();
+    }
+  });
+  C.ptr.assign((size_t)A.n + 1, 0);
+  for (int64_t i = 0; i < A.n; ++i) C.ptr[i + 1] = C.ptr[i] + cnt[i + 1];
+  C.col.resize((size_t)C.ptr[A.n]);
+  C.val.resize((size_t)C.ptr[A.n]);
+  for (size_t t = 0; t < rng.size(); ++t) {
+    if (rng[t].second <= rng[t].first) continue;
+    std::copy(cols_t[t].begin(), cols_t[t].end(), C.col.begin() + C.ptr[rng[t].first]);
+    std::copy(vals_t[t].begin(), vals_t[t].end(), C.val.begin() + C.ptr[rng[t].first]);
+  }
+  return C;
+}
+
+template <class T>
+int amg_alloc(Ctx* c, size_t n, T** out) {
+  void* p = nullptr;
+  HIPC(hipMalloc(&p, sizeof(T) * std::max<size_t>(1, n)));
+  c->amg_bufs.push_back(p);
+  *out = static_cast<T*>(p);
+  return TV_OK;
+}
+
+template <class T>
+int amg_upload(Ctx* c, const std::vector<T>& h, T** out) {
+  if (int e = amg_alloc(c, h.size(), out)) return e;
+  if (!h.empty()) HIPC(hipMemcpy(*out, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  return TV_OK;
+}
+
+// stored entries of M in SELL-64 (padding included)
+int64_t sell_size(const Csr& M) {
+  int64_t t = 0;
+  for (int64_t s = 0; s * 64 < M.n; ++s) {
+    int64_t w = 0;
+    for (int64_t r = s * 64; r < std::min(M.n, s * 64 + 64); ++r) w = std::max(w, M.ptr[r + 1] - M.ptr[r]);
+    t += 64 * w;
+  }
+  return t;
+}
+
+// CSR -> SELL-64 on the device (padding: value 0, column 0)
+int upload_sell(Ctx* c, const Csr& M, Sell& out) {
+  const int64_t ns = (M.n + 63) / 64;
+  std::vector<int64_t> soff((size_t)ns + 1, 0);
+  for (int64_t s = 0; s < ns; ++s) {
+    int64_t w = 0;
+    for (int64_t r = s * 64; r < std::min(M.n, s * 64 + 64); ++r) w = std::max(w, M.ptr[r + 1] - M.ptr[r]);
+    soff[s + 1] = soff[s] + 64 * w;
+  }
+  std::vector<int> cols((size_t)soff[ns], 0);
+  std::vector<double> vals((size_t)soff[ns], 0.0);
+  for (int64_t r = 0; r < M.n; ++r) {
+    const int64_t s = r >> 6, lane = r & 63;
+    for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
+      const int64_t q = soff[s] + 64 * (k - M.ptr[r]) + lane;
+      cols[q] = M.col[k];
+      vals[q] = M.val[k];
+    }
+  }
+  int64_t* so;
+  int* co;
+  double* va;
+  if (int e = amg_upload(c, soff, &so)) return e;
+  if (int e = amg_upload(c, cols, &co)) return e;
+  if (int e = amg_upload(c, vals, &va)) return e;
+  out.nrow = M.n;
+  out.ncol = M.m;
+  out.nslice = ns;
+  out.soff = so;
+  out.cols = co;
+  out.val = va;
+  return TV_OK;
+}
+
+// the fine SELL-64 operator back on the host as CSR (padding entries dropped)
+int fine_csr(Ctx* c, Csr& A) {
+  const Sell S = um_operator(c->umg);
+  std::vector<int64_t> soff((size_t)S.nslice + 1);
+  HIPC(hipMemcpy(soff.data(), S.soff, sizeof(int64_t) * soff.size(), hipMemcpyDeviceToHost));
+  const int64_t nnz = soff[S.nslice];
+  std::vector<int> cols((size_t)nnz);
+  std::vector<double> vals((size_t)nnz);
+  HIPC(hipMemcpy(cols.data(), S.cols, sizeof(int) * (size_t)nnz, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(vals.data(), S.val, sizeof(double) * (size_t)nnz, hipMemcpyDeviceToHost));
+  A.n = S.nrow;
+  A.m = S.ncol;
+  A.ptr.assign((size_t)A.n + 1, 0);
+  for (int64_t r = 0; r < A.n; ++r) {
+    const int64_t s = r >> 6, lane = r & 63, w = (soff[s + 1] - soff[s]) >> 6;
+    int64_t k = 0;
+    for (int64_t q = 0; q < w; ++q)
+      if (vals[(size_t)(soff[s] + 64 * q + lane)] != 0.0) ++k;
+    A.ptr[r + 1] = A.ptr[r] + k;
+  }
+  A.col.resize((size_t)A.ptr[A.n]);
+  A.val.resize((size_t)A.ptr[A.n]);
+  for (int64_t r = 0; r < A.n; ++r) {
+    const int64_t s = r >> 6, lane = r & 63, w = (soff[s + 1] - soff[s]) >> 6;
+    int64_t k = A.ptr[r];
+    for (int64_t q = 0; q < w; ++q) {
+      const size_t e = (size_t)(soff[s] + 64 * q + lane);
+      if (vals[e] != 0.0) {
+        A.col[k] = cols[e];
+        A.val[k++] = vals[e];
+      }
+    }
+  }
+  return TV_OK;
+}
+
+}  // namespace
+
+// builds the hierarchy below the fine unstructured level (one partition)
+int amg_setup(Ctx* c) {
+  if (!c->um || c->n_parts > 1) return c->fail(TV_ERR_ARG, "AMG: unstructured meshes on one partition");
+  Csr A;
+  if (int e = fine_csr(c, A)) return e;
+  const int max_levels = c->O.mg_levels > 0 ? c->O.mg_levels : 12;
+  while ((int)c->amg.size() + 1 < max_levels && A.n > kAmgCoarseRows) {
+    const std::vector<double> dinv = diag_inv(A);
+    int64_t na = 0;
+    const std::vector<int> agg = aggregate(A, na);
+    if (na < 1 || na * 10 > A.n * 7) break;  // coarsening stalled
+    const double lam = lam_max(A, dinv, 15);
+    Csr P = smoothed_p(A, dinv, agg, na, 4.0 / (3.0 * lam));
+    Csr R = transpose(P);
+    Csr Ac;
+    {
+      const Csr AP = spgemm(A, P);
+      Ac = spgemm(R, AP);
+    }
+    c->amg.emplace_back();
+    AmgLevel& L = c->amg.back();
+    L.n = na;
+    if (int e = upload_sell(c, P, L.P)) return e;
+    if (int e = upload_sell(c, R, L.R)) return e;
+    if (int e = upload_sell(c, Ac, L.A)) return e;
+    L.p_nnz = sell_size(P);
+    L.r_nnz = sell_size(R);
+    L.a_nnz = sell_size(Ac);
+    const std::vector<double> dc = diag_inv(Ac);
+    for (double v : dc)
+      if (!(v > 0.0) || !std::isfinite(v)) return c->fail(TV_ERR_ARG, "AMG: coarse operator not positive definite");
+    L.omega = 2.0 / (1.1 * lam_max(Ac, dc, 20));
+    if (int e = amg_upload(c, dc, &L.dinv)) return e;
+    for (double** v : {&L.b, &L.x, &L.w})
+      if (int e = amg_alloc(c, (size_t)na, v)) return e;
+    A = std::move(Ac);
+  }
+  if (c->amg.empty()) return c->fail(TV_ERR_ARG, "AMG: the mesh is too small to coarsen");
+  HIPC(hipMalloc(&c->mgx, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
+  c->amg_on = true;
+  c->mg_on = true;
+  c->mg_omega0 = 0.0;  // the level-0 weight: lazily, at the temperature of the first solve (mg_dg_weight)
+  return TV_OK;
+}
+
+// the V-cycle on coarse level l >= 1 (c->amg[l - 1]); its pre-smoothing step
+// from 0 was formed by the restriction into it.  Returns the level's result.
+static const double* amg_level(Ctx* c, size_t l) {
+  AmgLevel& L = c->amg[l - 1];
+  if (l == c->amg.size()) return L.x;  // coarsest: one Jacobi step
+  AmgLevel& C = c->amg[l];
+  hipStream_t s = c->stream;
+  launch_amg_apply(L.A, c->st, L.x, L.w, s);
+  launch_amg_restrict(C.R, c->st, L.b, L.w, C.dinv, C.omega, C.b, C.x, s);
+  const double* xc = amg_level(c, l + 1);
+  launch_amg_prolong(C.P, c->st, xc, L.x, L.x, s);
+  launch_amg_post(L.A, c->st, L.x, L.b, L.dinv, L.omega, L.w, s);
+  return L.w;
+}
+
+// z = omega0 D^-1 r (x0 = c->mgx, formed by k_mg_update) + P_0 V_1(P_0^T r),
+// with the (z.z, z.r) records and the KSPCG tail
+int amg_apply0(Ctx* c, const RedTail* tail) {
+  AmgLevel& L1 = c->amg[0];
+  launch_amg_restrict(L1.R, c->st, c->r, nullptr, L1.dinv, L1.omega, L1.b, L1.x, c->stream);
+  const double* x1 = amg_level(c, 1);
+  return launch_amg_prolong0(L1.P, c->st, x1, c->mgx, c->r, c->z, c->partials, tail, c->stream);
+}
+
+// algorithmic bytes of one V-cycle (tv_kernel_bytes 11): the stored entries
+// of every launched operator (12 B: value + column, padding included) and the
+// vectors each launch streams once (gathered vectors counted once)
+double amg_cycle_bytes(const Ctx* c) {
+  const double n0 = (double)c->nT;
+  const AmgLevel& L1 = c->amg[0];
+  double b = 12.0 * (double)L1.r_nnz + 8.0 * n0 + 24.0 * (double)L1.n;  // R_0 (r in; b, x, dinv of level 1)
+  b += 12.0 * (double)L1.p_nnz + 8.0 * (double)L1.n + 24.0 * n0;        // P_0 (x_1 in; x0, r in, z out)
+  for (size_t l = 0; l + 1 < c->amg.size(); ++l) {
+    const AmgLevel& L = c->amg[l];
+    const AmgLevel& C = c->amg[l + 1];
+    const double n = (double)L.n, nc = (double)C.n;
+    b += 12.0 * (double)L.a_nnz + 16.0 * n;                      // w = A x
+    b += 12.0 * (double)C.r_nnz + 16.0 * n + 24.0 * nc;          // b_c = R (b - w), x_c
+    b += 12.0 * (double)C.p_nnz + 8.0 * nc + 16.0 * n;           // x += P x_c
+    b += 12.0 * (double)L.a_nnz + 32.0 * n;                      // post: x, b, dinv in, w out
+  }
+  return b;
+}
+
+}  // namespace tv

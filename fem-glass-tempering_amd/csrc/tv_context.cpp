@@ -578,6 +578,10 @@ int tv_create(const tv_mesh_desc* mesh, const tv_fe_config* fe, const tv_params*
     set_global_error("HIP stream/event creation failed");
     return TV_ERR_HIP;
   }
+  if (c->O.preconditioner == TV_PC_AMG) {
+    set_global_error("TV_PC_AMG: unstructured meshes (the box meshes take TV_PC_GMG)");
+    return TV_ERR_ARG;
+  }
   int rc = setup_mesh(c.get(), mesh);
   if (rc == TV_OK) rc = setup_fields(c.get());
   if (rc == TV_OK && c->O.preconditioner == TV_PC_GMG) rc = mg_setup(c.get());
@@ -701,12 +705,18 @@ static int create_unstructured(const tv_umesh_desc* mesh, const tv_upart_desc* p
     set_global_error("HIP stream/event creation failed");
     return TV_ERR_HIP;
   }
-  if (c->O.preconditioner != TV_PC_JACOBI) {
-    set_global_error("unstructured meshes: preconditioner TV_PC_JACOBI only");
+  if (c->O.preconditioner != TV_PC_JACOBI && c->O.preconditioner != TV_PC_AMG) {
+    set_global_error("unstructured meshes: preconditioner TV_PC_JACOBI or TV_PC_AMG (the box multigrid needs a "
+                     "rectilinear mesh)");
+    return TV_ERR_ARG;
+  }
+  if (c->O.preconditioner == TV_PC_AMG && part && part->n_parts > 1) {
+    set_global_error("unstructured meshes: TV_PC_AMG on one partition (partitioned: TV_PC_JACOBI)");
     return TV_ERR_ARG;
   }
   int rc = setup_umesh(c.get(), mesh, part);
   if (rc == TV_OK) rc = setup_fields(c.get());
+  if (rc == TV_OK && c->O.preconditioner == TV_PC_AMG) rc = amg_setup(c.get());
   if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
   if (rc != TV_OK) {
     set_global_error(c->err);
@@ -788,6 +798,7 @@ int tv_destroy(void* ctx) {
   um_free(c->umd);
   if (c->um_bmask) hipFree(c->um_bmask);
   if (c->um_sidx) hipFree(c->um_sidx);
+  for (void* p : c->amg_bufs) hipFree(p);
   if (c->um_sbuf) hipFree(c->um_sbuf);
   for (MgLevel& L : c->mg) {
     for (void* p : L.bufs) hipFree(p);
@@ -1064,6 +1075,8 @@ int tv_set_dirichlet(void* ctx, int enable, double value) {
   if (c->O.model_mode != TV_MODEL_PAPER)
     return c->fail(TV_ERR_STATE, "Dirichlet condition: only with model_mode = TV_MODEL_PAPER (the reference's "
                                  "own path cannot run, ThermoViscoProblem.py:236-243)");
+  if (enable && c->amg_on)
+    return c->fail(TV_ERR_STATE, "Dirichlet condition: not with TV_PC_AMG (Jacobi or the box multigrid)");
   hipSetDevice(c->device);
   c->dir_on = enable != 0;
   c->dir_value = value;

@@ -67,6 +67,16 @@ struct MgLevel {
   double* mask = nullptr;    // the level above the replicated ones: 1 owned / 0 ghost
 };
 
+// level l >= 1 of the algebraic multigrid (tv_amg.cpp): A_l, the prolongation
+// into level l - 1 (rows of that level) and R = P^T; the stored SELL entries
+struct AmgLevel {
+  int64_t n = 0;
+  Sell A, P, R;
+  int64_t a_nnz = 0, p_nnz = 0, r_nnz = 0;
+  double omega = 0.0;
+  double *dinv = nullptr, *b = nullptr, *x = nullptr, *w = nullptr;
+};
+
 struct Ctx {
   std::string err;
   int device = 0;
@@ -129,6 +139,10 @@ struct Ctx {
   std::vector<int64_t> um_cells;     // host copy: 2^dim per cell (input order)
   UmDevice* umd = nullptr;            // assembled operators, facet data (tv_um.hip)
   unsigned char* um_bmask = nullptr;  // boundary vertices (Dirichlet mode)
+  // algebraic multigrid (options.preconditioner = TV_PC_AMG, unstructured, tv_amg.cpp)
+  bool amg_on = false;
+  std::vector<AmgLevel> amg;
+  std::vector<void*> amg_bufs;
   // partitioned unstructured mesh (tv_create_unstructured_part): owned vertices
   // first, ghosts grouped by owner; per neighbour k: the ghosts received from
   // um_peer[k] at [nown + um_roff[k], + um_rcnt[k]), the owned values sent to it
@@ -201,6 +215,11 @@ struct Ctx {
 
 constexpr int64_t kCgsAutoMaxNodes = 3000000;  // AUTO Krylov form: single reduction up to this slab size
 constexpr int kTsCap = 1 << 15;                // timestamp slots of the in-solve kernel timing
+
+// ---- tv_amg.cpp ----
+int amg_setup(Ctx* c);
+int amg_apply0(Ctx* c, const RedTail* tail);
+double amg_cycle_bytes(const Ctx* c);
 
 // ---- tv_context.cpp ----
 void set_global_error(const std::string& m);

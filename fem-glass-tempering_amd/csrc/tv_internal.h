@@ -173,6 +173,34 @@ struct UmGrid {
   double T_amb, T_amb4;
 };
 
+// A sparse operator in SELL-64 on the device (entry k of row r: soff[r / 64] +
+// 64 k + r % 64; padding entries: value 0, column 0) -- the algebraic
+// multigrid's coarse operators, prolongations and restrictions (tv_amg.*)
+struct Sell {
+  int64_t nrow = 0, ncol = 0, nslice = 0;
+  const int64_t* soff = nullptr;
+  const int* cols = nullptr;
+  const double* val = nullptr;
+};
+int amg_num_blocks(const Sell& M);  // partial records of launch_amg_prolong0
+// y = A x
+void launch_amg_apply(const Sell& A, const PcgState* st, const double* x, double* y, hipStream_t s);
+// b_c = R (x - x2) (x2 may be null), x_c = omega_c dinv_c b_c (x_c may be null)
+void launch_amg_restrict(const Sell& R, const PcgState* st, const double* x, const double* x2, const double* dinv_c,
+                         double omega_c, double* b_c, double* x_c, hipStream_t s);
+// x_new = x_old + P x_c (x_new may alias x_old)
+void launch_amg_prolong(const Sell& P, const PcgState* st, const double* x_c, const double* x_old, double* x_new,
+                        hipStream_t s);
+// y = x + omega dinv (b - A x)
+void launch_amg_post(const Sell& A, const PcgState* st, const double* x, const double* b, const double* dinv,
+                     double omega, double* y, hipStream_t s);
+// z = x0 + P x_c, (z.z, z.r) records and the reduction tail; returns the record count
+int launch_amg_prolong0(const Sell& P, const PcgState* st, const double* x_c, const double* x0, const double* r,
+                        double* z, double* partials, const RedTail* tail, hipStream_t s);
+// the fine cell operator V = M + dt alpha K of an unstructured mesh, SELL-64
+// (device pointers of tv_um.hip's setup)
+Sell um_operator(const UmGrid& g);
+
 struct UmDevice;  // device allocations of one unstructured mesh (tv_um.hip)
 // builds the operators on the device (stream s, synchronised before return)
 int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, const int64_t* cells, UmGrid& g,

@@ -60,6 +60,10 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       break;
     case 11: {  // one multigrid V-cycle, per node of each level (streams counted once)
       if (!c->mg_on) return c->fail(TV_ERR_ARG, "kernel 11: preconditioner GMG not enabled");
+      if (c->amg_on) {  // the algebraic cycle: stored operator entries + vector streams
+        *bytes = amg_cycle_bytes(c);
+        break;
+      }
       // level 0: J x0 (16), restriction reads r, w (16), prolongation x0 -> x (16),
       // then CG: J x with the post-smoothing in its epilogue (x, r, dinv in, z out: 32),
       // DG: J x (16) + the cell-block post-smoothing (x0, r, w in, z out: 32)

@@ -73,9 +73,10 @@ int mg_dg_lambda(Ctx* c, const double* T, double* lam) {
   for (double& v : h) v /= std::sqrt(nrm);
   HIPC(hipMemcpyAsync(c->mgx, h.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
   if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
-  else launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
+  else if (!c->um) launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
   std::vector<double> part(1024);
   double l = 0.0;
+  if (c->um) op_diag(c, T, c->dinv, 1);  // the algebraic multigrid's level 0: point Jacobi of J(T)
   for (int it = 0; it < 30; ++it) {
     op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
     if (c->dggface) launch_dg_bsmooth(c->dg, nullptr, c->w, nullptr, c->dggface, 1.0, c->w, 0, c->stream);  // in place, per cell
@@ -97,10 +98,11 @@ int mg_dg_lambda(Ctx* c, const double* T, double* lam) {
 // temperature it will precondition -- the Robin term 4 a_rad T^3 of the cell
 // blocks vanishes at the T = 0 a freshly created context holds
 int mg_dg_weight(Ctx* c, const double* T) {
-  if (!c->mg_dg || c->mg_omega0 > 0.0) return TV_OK;
+  if (!(c->mg_dg || c->amg_on) || c->mg_omega0 > 0.0) return TV_OK;
   double lam = 0.0;
   if (int e = mg_dg_lambda(c, T, &lam)) return e;
-  c->mg_omega0 = 2.0 / (1.1 * 1.1 * lam);
+  // AMG level 0 (additive point Jacobi): the coarse levels' 2 / (1.1 lambda)
+  c->mg_omega0 = c->amg_on ? 2.0 / (1.1 * lam) : 2.0 / (1.1 * 1.1 * lam);
   return TV_OK;
 }
 
@@ -260,6 +262,7 @@ int mg_setup(Ctx* c) {
 // the cell-local values onto the CG level), coarse Jacobi diagonals
 
 void mg_prepare(Ctx* c, const double* T) {
+  if (c->amg_on) return;  // the algebraic hierarchy is T-independent (tv_amg.cpp)
   // after the first call (dinv interiors in place): the CG levels below the
   // base in two launches (launch_mg_prepare)
   const size_t base = c->mg_dg ? 1 : 0;  // DG: level 1 is the vertex mean of the DG field
@@ -349,6 +352,7 @@ void mg_level(Ctx* c, size_t l) {
 // level 0: x0 = omega dinv r is in c->mgx (k_mg_update); coarse correction,
 // post-smoothing into z with the (z.z, z.r) reduction tail
 int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
+  if (c->amg_on) return amg_apply0(c, tail);
   const int64_t n = c->nT;
   hipStream_t s = c->stream;
   const double* mask = c->dir_on ? c->dinv : nullptr;  // Dirichlet: the free subspace
@@ -392,7 +396,7 @@ int mg_iteration(Ctx* c, const double* T, int it) {
   int np = 0;
   if (!op_japply_fused(c, T, &np, &t1, it))  // p <- z + b p ; w <- J p ; p.w ; alpha
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;
-  const FaceAdd fa = c->mg_dg ? FaceAdd{} : cg_face_add(c->cg, 0);  // DG: w is complete
+  const FaceAdd fa = (c->mg_dg || c->um) ? FaceAdd{} : cg_face_add(c->cg, 0);  // DG, unstructured: w is complete
   if (c->dggface)
     launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
                       c->stream);
@@ -488,7 +492,7 @@ int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev) {
   // (dinv = 0 on the constrained rows, as k_bc_lift sets it before every solve;
   // the V-cycle masks its transfers with the same dinv)
   if (c->dir_on && c->fam_T == TV_CG) launch_bc_mask(c, c->dinv);
-  if (c->mg_dg)
+  if (c->mg_dg || c->amg_on)
     if (int e = mg_dg_weight(c, T)) return e;
   if (!c->mg_on) {
     launch_mg_jacobi(n, nullptr, r_dev, nullptr, nullptr, c->dinv, 1.0, z_dev, 0, s);  // z = dinv .* r

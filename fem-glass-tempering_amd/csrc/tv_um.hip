@@ -473,6 +473,16 @@ void launch_rows(const UmGrid& g, const double* T, const double* u, const double
 }  // namespace
 
 int um_num_blocks(const UmGrid& g) { return row_blocks(g); }
+Sell um_operator(const UmGrid& g) {
+  Sell m;
+  m.nrow = g.nrow;
+  m.ncol = g.nv;
+  m.nslice = g.nslice;
+  m.soff = g.soff;
+  m.cols = g.cols;
+  m.val = g.V;
+  return m;
+}
 void launch_um_pack(const int64_t* idx, int64_t n, const double* v, double* out, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_um_pack, dim3((unsigned)std::min<int64_t>(1024, (n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,

@@ -16,7 +16,7 @@ TV_OK, TV_ERR_ARG, TV_ERR_HIP, TV_ERR_NOT_CONVERGED, TV_ERR_KSP, TV_ERR_STATE, T
 TV_CG, TV_DG = 0, 1
 TV_PCG_AUTO, TV_PCG_KSPCG, TV_PCG_SINGLE_REDUCTION = 0, 1, 2
 TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
-TV_PC_JACOBI, TV_PC_GMG = 0, 1
+TV_PC_JACOBI, TV_PC_GMG, TV_PC_AMG = 0, 1, 2
 TV_DG_KERNEL_AUTO, TV_DG_KERNEL_TILE, TV_DG_KERNEL_CELLS = 0, 1, 2
 ABI_VERSION = 4
 

@@ -105,7 +105,8 @@ def ghosted_partition(mesh, part: np.ndarray, p: int, n_parts: int | None = None
     nv, nl = mesh.num_vertices, cells.shape[1]
     P = int(part.max()) + 1 if n_parts is None else int(n_parts)
     owner = np.full(nv, np.iinfo(np.int64).max, dtype=np.int64)
-    np.minimum.at(owner, cells.ravel(), np.repeat(part, nl))
+    for q in range(P - 1, -1, -1):  # lowest part last: owner = min over the cells around a vertex
+        owner[cells[part == q].ravel()] = q
     counts = np.bincount(owner, minlength=P)
     ocell = owner[cells]                                   # (nc, nl) owners of each cell's vertices
     own_c = np.flatnonzero(part == p)

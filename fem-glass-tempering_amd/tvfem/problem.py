@@ -139,9 +139,9 @@ class ThermoViscoProblem:
         self.write_output = self.WRITE_OUTPUT_DEFAULT if write_output is None else bool(write_output)
         self.output_dir = output_dir
         self._output_open = False
-        if preconditioner not in ("jacobi", "gmg"):
-            raise ValueError("preconditioner must be 'jacobi' (PETSc PCJACOBI, the oracle's) or 'gmg' "
-                             "(geometric multigrid on the box hierarchy)")
+        if preconditioner not in ("jacobi", "gmg", "amg"):
+            raise ValueError("preconditioner must be 'jacobi' (PETSc PCJACOBI, the oracle's), 'gmg' (geometric "
+                             "multigrid on the box hierarchy) or 'amg' (smoothed aggregation, unstructured meshes)")
         self.preconditioner = preconditioner
         self._mg_levels = int(mg_levels)
         if dg_kernel not in ("auto", "tile", "cells"):
@@ -233,7 +233,7 @@ class ThermoViscoProblem:
         opts.pcg_variant = {"auto": N.TV_PCG_AUTO, "kspcg": N.TV_PCG_KSPCG,
                             "single": N.TV_PCG_SINGLE_REDUCTION}[pcg_variant]
         opts.model_mode = N.TV_MODEL_PAPER if self.model_mode == "paper" else N.TV_MODEL_REFERENCE
-        opts.preconditioner = N.TV_PC_GMG if self.preconditioner == "gmg" else N.TV_PC_JACOBI
+        opts.preconditioner = {"jacobi": N.TV_PC_JACOBI, "gmg": N.TV_PC_GMG, "amg": N.TV_PC_AMG}[self.preconditioner]
         opts.mg_levels = self._mg_levels
         opts.dg_kernel = self._dg_kernel
         opts.dg_tile_chunk = self._dg_tile_chunk

@@ -159,7 +159,8 @@ typedef struct {
   int pcg_batch;          /* iterations launched between convergence polls  */
   int pcg_variant;        /* TV_PCG_AUTO / TV_PCG_KSPCG / TV_PCG_SINGLE_REDUCTION */
   int model_mode;         /* TV_MODEL_REFERENCE (default) / TV_MODEL_PAPER       */
-  int preconditioner;     /* TV_PC_JACOBI (default) / TV_PC_GMG                  */
+  int preconditioner;     /* TV_PC_JACOBI (default) / TV_PC_GMG (box meshes) /
+                             TV_PC_AMG (unstructured meshes, one partition)      */
   int mg_levels;          /* GMG: levels incl. the fine one (0: automatic)       */
   int dg_kernel;          /* 3D DG1 Jacobian: TV_DG_KERNEL_AUTO / _TILE / _CELLS */
   int dg_tile_chunk;      /* planes per marching DG tile (0: automatic = 5)      */
@@ -192,6 +193,7 @@ typedef struct {
  *           iterations per solve at C4. */
 #define TV_PC_JACOBI 0
 #define TV_PC_GMG 1
+#define TV_PC_AMG 2   /* smoothed-aggregation AMG (csrc/tv_amg.cpp), the PCGAMG of ThermoViscoProblem.py:344 */
 
 /* Model semantics.  REFERENCE reproduces the reference as it runs, quirks
  * included.  PAPER (opt-in, never the default) applies

@@ -1,0 +1,152 @@
+"""Smoothed-aggregation algebraic multigrid on the unstructured meshes
+(options.preconditioner = TV_PC_AMG, csrc/tv_amg.cpp + csrc/tv_amg_k.hip):
+the preconditioner the reference configures is PETSc's PCGAMG
+(ThermoViscoProblem.py:343-346); PETSc is not installed, so
+
+  * the V-cycle operator (tv_precond_apply, the PCApply of the solve) is
+    pinned to the numpy restatement oracle/amg.py -- same aggregation,
+    smoothed prolongation, Galerkin operators, weights and cycle -- built on
+    the oracle's own assembled cell operator, to 1e-10; symmetric, positive;
+  * the Newton solution is pinned to the oracle's (T <= 1e-10 per step,
+    equal Newton counts; the preconditioner only changes the Krylov counts,
+    which must fall well below Jacobi's).
+"""
+import numpy as np
+import pytest
+
+from oracle import amg as OA
+from oracle import tv_oracle as O
+from parity_util import check_field, relerr
+
+CG = {"element": "CG", "degree": 1}
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _mesh(n, L, seed=0, shuffle=True):
+    from tvfem import distorted_box_mesh
+    return distorted_box_mesh(L, n, amp=0.2, seed=seed, shuffle=shuffle)
+
+
+def _omesh(m):
+    return O.Mesh(dim=m.dim, x=m.x[:, :m.dim].copy(), cells=m.cells.copy())
+
+
+def test_amg_restatement_builds_a_spd_hierarchy():
+    """CPU: the numpy restatement on a distorted plate -- every coarse operator
+    symmetric positive definite, the additive cycle SPD (what CG needs)."""
+    m = _mesh((14, 12, 14), (2.0, 2.0, 1.0), seed=1, shuffle=False)
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    cell = O.HeatForm(O.Space(_omesh(m), "CG"), 0.1, O.ThermalParams.from_dict({**mp, "epsilon": 0.0, "htc": 0.0}))
+    V = cell.jacobian(np.full(m.num_vertices, 800.0))
+    levels = OA.build(V)
+    assert len(levels) >= 1
+    for A, P, R, d, om in levels:
+        assert abs(A - A.T).max() <= 1e-12 * abs(A).max()
+        assert np.all(A.diagonal() > 0) and 0.0 < om < 2.0 / 1.05
+    J = O.HeatForm(O.Space(_omesh(m), "CG"), 0.1, O.ThermalParams.from_dict(mp)).jacobian(np.full(m.num_vertices, 800.0))
+    d0 = 1.0 / J.diagonal()
+    om0 = 2.0 / (1.1 * OA.lam_max_device(J, d0))
+    rng = np.random.default_rng(0)
+    x, y = rng.standard_normal((2, m.num_vertices))
+    bx, by = OA.apply(levels, x, d0, om0), OA.apply(levels, y, d0, om0)
+    assert abs(y @ bx - x @ by) < 1e-12 * abs(y @ bx)
+    assert x @ bx > 0
+
+
+# the second case has > 2000 coarse rows on level 1: three levels
+VCYCLE_CASES = {"two_levels": ((16, 14, 12), (2.0, 2.0, 1.0)), "three_levels": ((40, 40, 36), (4.0, 4.0, 3.0))}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", list(VCYCLE_CASES))
+def test_amg_vcycle_matches_restatement(case):
+    torch = _torch()
+    from tvfem.problem import ThermoViscoProblem
+    n, L = VCYCLE_CASES[case]
+    m = _mesh(n, L, seed=2)
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    p = ThermoViscoProblem(m, (0.0, 1.0), 0.1, {"T": CG, "sigma": CG}, mp, verbose=False, preconditioner="amg")
+    p.setup()
+    nv = m.num_vertices
+    rng = np.random.default_rng(5)
+    T = 700.0 + rng.uniform(0.0, 150.0, nv)
+    p.set_field("T", T)
+    p._flush()
+    om = _omesh(m)
+    V = O.HeatForm(O.Space(om, "CG"), 0.1, O.ThermalParams.from_dict({**mp, "epsilon": 0.0, "htc": 0.0})).jacobian(T)
+    J = O.HeatForm(O.Space(om, "CG"), 0.1, O.ThermalParams.from_dict(mp)).jacobian(T)
+    levels = OA.build(V)
+    d0 = 1.0 / J.diagonal()
+    om0 = 2.0 / (1.1 * OA.lam_max_device(J, d0))
+    r, y = rng.standard_normal((2, nv))
+    out = []
+    for v in (r, y):
+        vd = torch.tensor(v, dtype=torch.float64, device="cuda")
+        zd = torch.empty_like(vd)
+        assert p._lib.tv_precond_apply(p._ctx, vd.data_ptr(), zd.data_ptr()) == 0, p._lib.tv_last_error(p._ctx)
+        out.append(zd.cpu().numpy())
+    z_r, z_y = out
+    e = relerr(z_r, OA.apply(levels, r, d0, om0))
+    sym = abs(y @ z_r - r @ z_y) / abs(y @ z_r)
+    print(f"[amg] V-cycle {case}: {len(levels) + 1} levels ({[lv[0].shape[0] for lv in levels]}), vs numpy {e:.2e}, "
+          f"symmetry {sym:.1e}")
+    assert len(levels) + 1 == (2 if case == "two_levels" else 3)
+    assert e < 1e-10, e
+    assert sym < 1e-12, sym
+    assert r @ z_r > 0.0
+    p.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["reference", "paper"])
+def test_amg_steps_match_oracle(mode):
+    """Coupled steps on a distorted plate with AMG-preconditioned KSPCG vs the
+    oracle (Jacobi-PCG): same Newton iterates to the Newton tolerance."""
+    _torch()
+    from tvfem.problem import ThermoViscoProblem
+    m = _mesh((16, 14, 12), (2.0, 2.0, 1.0), seed=4)
+    cfg = {"T": CG, "sigma": CG}
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    dev = ThermoViscoProblem(m, (0.0, 1.0), 0.1, cfg, mp, verbose=False, model_mode=mode, preconditioner="amg")
+    jac = ThermoViscoProblem(m, (0.0, 1.0), 0.1, cfg, mp, verbose=False, model_mode=mode)
+    ref = O.OracleProblem(_omesh(m), (0.0, 1.0), 0.1, cfg, mp, linear="pcg", model_mode=mode)
+    for q in (dev, jac, ref):
+        q.setup()
+    ka, kj = 0, 0
+    for s in range(3):
+        T_before = ref.functions_current["T"].copy()
+        for q in (dev, jac, ref):
+            q.solve_timestep()
+        assert relerr(dev.functions_current["T"].x.array, ref.functions_current["T"]) < 1e-10, s
+        assert dev.last_newton_iterations == ref.newton_history[-1][0]
+        ka += dev.last_krylov_iterations
+        kj += jac.last_krylov_iterations
+    mT = np.abs(ref.functions_current["T"] - T_before) > 1e-6
+    check_field(f"sigma[amg,{mode}]", dev.functions_next["sigma"].x.array, ref.functions_next["sigma"], mT, 9,
+                min_frac=0.9)
+    print(f"[amg] {mode}: Krylov its over 3 steps AMG {ka} vs Jacobi {kj}")
+    assert ka * 2 < kj, (ka, kj)
+    for q in (dev, jac):
+        q.close()
+
+
+@pytest.mark.gpu
+def test_amg_rejections():
+    _torch()
+    from tvfem import box_mesh
+    from tvfem.problem import ThermoViscoProblem
+    from tvfem._native import NativeError
+    cfg = {"T": CG, "sigma": CG}
+    with pytest.raises(NativeError):  # box meshes take the geometric hierarchy
+        ThermoViscoProblem(box_mesh([1.0, 1.0, 1.0], [4, 4, 4]), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
+                           verbose=False, preconditioner="amg")
+    m = _mesh((16, 14, 12), (2.0, 2.0, 1.0))
+    with pytest.raises(NativeError):  # partitioned: Jacobi only
+        ThermoViscoProblem(m, (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False, preconditioner="amg",
+                           n_parts=2, part=0)

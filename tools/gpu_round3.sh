@@ -36,6 +36,19 @@ if [ $PART = A ]; then
   line $OUT/bench_prof.json C4prof
   exit $rc
 fi
+if [ $PART = C ]; then  # the unstructured algebraic multigrid
+  step "amg tests"
+  timeout -k 10 600 python -u -m pytest tests/test_amg.py -m gpu -v -s -rs --timeout 300 --timeout-method thread > $OUT/amg_tests.log 2>&1
+  rc=$?; tail -3 $OUT/amg_tests.log; grep -h "^\[amg\]" $OUT/amg_tests.log
+  [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" $OUT/amg_tests.log | head -20; exit $rc; }
+  for spec in "UMamg --pc amg" "UMjac --pc jacobi"; do
+    set -- $spec; tag=$1; shift 1
+    step "bench distorted $tag"
+    timeout -k 10 600 python3 bench.py --mesh distorted --steps 5 --warmup 1 --kernel-reps 5 --no-cpu-baseline "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err || { tail -5 $OUT/bench_$tag.err; exit 1; }
+    line $OUT/bench_$tag.json $tag
+  done
+  exit 0
+fi
 step "bench C4 (CPU baseline: the C/OpenMP port with the same GMG)"
 timeout -k 10 600 python3 bench.py > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail -5 $OUT/bench_c4.err; exit 1; }
 cat $OUT/bench_c4.json
