@@ -131,6 +131,8 @@ def main():
                               write_output=a.output is not None, output_dir=a.output or "output", **kw)
     single = prob.pcg_variant == "single"
     lib, ctx = prob._lib, prob._ctx
+    if a.share > 1:  # the multi-rank launch sequence with the transport stubbed (tv_comm_init_stub)
+        N.check(lib.tv_comm_init_stub(ctx), ctx)
     if world > 1:
         from tvfem.parallel import init_host_comm, init_rccl
         if a.comm == "host":  # explicit opt-in only (rehearsal of several ranks on one GPU)

@@ -9,7 +9,18 @@ namespace tv {
 // --------------------------------------------------------------------------------------
 // communication
 // --------------------------------------------------------------------------------------
-bool multi_rank(const Ctx* c) { return c->nranks > 1 && (c->comm || c->host_sendrecv); }
+bool multi_rank(const Ctx* c) { return c->nranks > 1 && (c->comm || c->host_sendrecv || c->comm_stub); }
+
+// measurement stub (tv_comm_init_stub): the ghosts of the solver's vectors read
+// zero (each partition solves its own block: the operators stay SPD), the
+// temperature ghosts keep their initial value, reductions stay local
+static int stub_ghosts(Ctx* c, const CgGrid& g, double* v) {
+  if (v == c->f[TV_F_T].ptr || v == c->f[TV_F_T_PREV].ptr) return TV_OK;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  if (g.g_lo) HIPC(hipMemsetAsync(v + plane * (g.k_begin - 1), 0, plane * sizeof(double), c->stream));
+  if (g.g_hi) HIPC(hipMemsetAsync(v + plane * g.k_end, 0, plane * sizeof(double), c->stream));
+  return TV_OK;
+}
 
 // ghost planes of v on grid g (the fine grid or a distributed multigrid level:
 // one plane per interface, storage axis 2): send the first / last owned plane,
@@ -35,6 +46,7 @@ int halo_host(Ctx* c, const CgGrid& g, double* v) {
 
 int halo_grid(Ctx* c, const CgGrid& g, double* v) {
   if (!multi_rank(c)) return TV_OK;
+  if (c->comm_stub) return stub_ghosts(c, g, v);
   if (c->host_sendrecv) return halo_host(c, g, v);
   const int64_t plane = (int64_t)g.n0 * g.n1;
   NCCLC(ncclGroupStart());
@@ -58,6 +70,11 @@ int halo_um(Ctx* c, double* v) {
   const int64_t nown = c->ownT_n;
   const int64_t stot = c->um_soff.empty() ? 0 : c->um_soff.back() + c->um_scnt.back();
   const int64_t rtot = c->nT - nown;
+  if (c->comm_stub) {  // see stub_ghosts
+    if (rtot && v != c->f[TV_F_T].ptr && v != c->f[TV_F_T_PREV].ptr)
+      HIPC(hipMemsetAsync(v + nown, 0, rtot * sizeof(double), c->stream));
+    return TV_OK;
+  }
   launch_um_pack(c->um_sidx, stot, v, c->um_sbuf, c->stream);
   if (c->host_sendrecv) {
     double* hs = c->h_halo;
@@ -92,7 +109,7 @@ int halo(Ctx* c, double* v) {
 // levels of the partitioned multigrid: each rank contributes the coarse nodes
 // its owned fine nodes restrict to, zeros elsewhere)
 int allreduce_vec(Ctx* c, double* v, int64_t n) {
-  if (!multi_rank(c) || n <= 0) return TV_OK;
+  if (!multi_rank(c) || n <= 0 || c->comm_stub) return TV_OK;
   if (c->host_allreduce) {
     if (c->h_big_n < (size_t)n) {
       if (c->h_big) HIPC(hipHostFree(c->h_big));
@@ -112,7 +129,7 @@ int allreduce_vec(Ctx* c, double* v, int64_t n) {
 }
 
 int allreduce(Ctx* c, double* v, int n) {
-  if (!multi_rank(c)) return TV_OK;
+  if (!multi_rank(c) || c->comm_stub) return TV_OK;
   if (c->host_allreduce) {
     HIPC(hipMemcpyAsync(c->h_sums + 4, v, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
@@ -167,6 +184,7 @@ int cgs_exchange(Ctx* c, double* wout, const double* fout) {
   const CgGrid& g = c->cg;
   const int64_t plane = (int64_t)g.n0 * g.n1;
   const int blocks = (int)std::min<int64_t>(1024, (2 * plane + kBlock - 1) / kBlock);
+  if (c->comm_stub) return stub_ghosts(c, g, wout);
   hipLaunchKernelGGL(k_cgs_pack, dim3(blocks), dim3(kBlock), 0, c->stream, g, wout, fout, cgs_raxis(c), c->wsend);
   if (c->host_sendrecv) {
     if (int e = allreduce(c, c->sums, 3)) return e;
@@ -259,6 +277,21 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
     const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
     HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)plane));
   }
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_comm_init_stub(void* ctx) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (c->n_parts < 2) return c->fail(TV_ERR_ARG, "tv_comm_init_stub: a partition of a partitioned mesh only");
+  hipSetDevice(c->device);
+  c->nranks = c->n_parts;
+  c->rank = c->part;
+  c->comm_stub = true;
   if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
   if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
   HIPC(hipStreamSynchronize(c->stream));

@@ -171,6 +171,7 @@ struct Ctx {
   tv_host_allreduce_fn host_allreduce = nullptr;
   tv_host_sendrecv_fn host_sendrecv = nullptr;
   void* host_user = nullptr;
+  bool comm_stub = false;    // tv_comm_init_stub: measurement of one rank's share, no transport
   double* h_halo = nullptr;  // pinned staging: 2 send + 2 recv planes
   size_t h_halo_n = 0;
   // in-solve kernel timing (tv_kernel_timing): the fused matvec and the PCG

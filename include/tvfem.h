@@ -357,6 +357,12 @@ int tv_halo_exchange(void* ctx, int field);
 typedef int (*tv_host_allreduce_fn)(double* buf, int n, void* user);
 typedef int (*tv_host_sendrecv_fn)(const double* send, size_t n_send, int peer_send, double* recv,
                                    size_t n_recv, int peer_recv, void* user);
+/* Measurement only (bench.py --share): one rank's share of a partitioned run
+ * on one GPU with the transport stubbed -- the multi-rank launch sequence,
+ * every exchange fills the ghosts of the solver's vectors with zeros (the
+ * partition solves its own block, so the operators stay SPD), the
+ * temperature ghosts keep their values, every reduction stays local. */
+int tv_comm_init_stub(void* ctx);
 int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
                       tv_host_sendrecv_fn sendrecv_fn, void* user);
 

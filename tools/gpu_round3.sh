@@ -49,6 +49,15 @@ if [ $PART = C ]; then  # the unstructured algebraic multigrid
   done
   exit 0
 fi
+if [ $PART = S ]; then  # per-rank shares of C4 (the distributed GMG, transport stubbed)
+  for spec in "n2 400,400,50 --share 2" "n4 400,400,50 --share 4" "n8 400,400,50 --share 8" "n8j 400,400,50 --share 8 --pc jacobi"; do
+    set -- $spec; tag=$1; cells=$2; shift 2
+    step "bench $tag"
+    timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --cells $cells "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err || { tail -5 $OUT/bench_$tag.err; exit 1; }
+    line $OUT/bench_$tag.json $tag
+  done
+  exit 0
+fi
 step "bench C4 (CPU baseline: the C/OpenMP port with the same GMG)"
 timeout -k 10 600 python3 bench.py > $OUT/bench_c4.json 2> $OUT/bench_c4.err || { tail -5 $OUT/bench_c4.err; exit 1; }
 cat $OUT/bench_c4.json
