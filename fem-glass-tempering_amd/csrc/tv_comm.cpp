@@ -105,6 +105,31 @@ int halo(Ctx* c, double* v) {
   return halo_grid(c, c->cg, v);
 }
 
+// the all-reduce of n scalars and the ghost planes of v in ONE RCCL group (one
+// launch and one latency instead of two: the end of every KSPCG iteration on a
+// partitioned box -- the (z.z, z.r) sums and z for the next matvec)
+int allreduce_halo(Ctx* c, double* sums, int n, double* v) {
+  if (!multi_rank(c)) return TV_OK;
+  if (c->comm_stub || c->host_allreduce || c->um || c->fam_T != TV_CG) {
+    if (int e = allreduce(c, sums, n)) return e;
+    return halo(c, v);
+  }
+  const CgGrid& g = c->cg;
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  NCCLC(ncclGroupStart());
+  NCCLC(ncclAllReduce(sums, sums, n, ncclDouble, ncclSum, c->comm, c->stream));
+  if (g.g_lo) {
+    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclRecv(v, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+  }
+  if (g.g_hi) {
+    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
 // sum of a device vector over the ranks, in place (the agglomerated coarse
 // levels of the partitioned multigrid: each rank contributes the coarse nodes
 // its owned fine nodes restrict to, zeros elsewhere)

@@ -236,7 +236,8 @@ int transfer(Ctx* c, int field, double* host, size_t n, int dir);
 bool multi_rank(const Ctx* c);
 int halo(Ctx* c, double* v);  // ghost planes of a T-space vector of the fine grid
 int halo_grid(Ctx* c, const CgGrid& g, double* v);  // ghost planes of a vector of grid g (a GMG level)
-int allreduce_vec(Ctx* c, double* v, int64_t n);  // sum over the ranks of a device vector, in place
+int allreduce_vec(Ctx* c, double* v, int64_t n);
+int allreduce_halo(Ctx* c, double* sums, int n, double* v);  // one RCCL group: n-scalar sum + halo(v)  // sum over the ranks of a device vector, in place
 int allreduce(Ctx* c, double* v, int n);
 int reduce_logic(Ctx* c, int n, int W, int kind, int check_done);  // records -> (all-reduce) -> scalar logic
 int cgs_raxis(const Ctx* c);

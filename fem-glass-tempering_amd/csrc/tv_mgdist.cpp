@@ -395,10 +395,10 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
                    c->f[TV_F_DX].ptr + off, c->mgx + off, 0, 1, c->stream);  // x0 <- omega dinv r
   // the three collectives of an iteration close it: the (z.z, z.r) all-reduce
   // + KSPCG logic, and the ghost planes of z for the next fused matvec
-  auto close = [&](int kind) -> int {
-    if (int e = allreduce(c, c->sums, 2)) return e;
+  auto close = [&](int kind) -> int {  // one RCCL group: the sums and the ghosts of z
+    if (int e = allreduce_halo(c, c->sums, 2, c->z)) return e;
     launch_logic(c->st, c->sums, kind, c->stream);
-    return halo(c, c->z);
+    return TV_OK;
   };
   {
     RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};

@@ -105,11 +105,10 @@ int pcg_iteration(Ctx* c, const double* T, int it) {
   const FaceAdd fa = (c->fam_T == TV_CG && !c->um) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
                     c->z + off, c->partials, c->stream, &t2, &fa, it);
-  if (multi) {  // dp, beta, convergence
-    if (int e = allreduce(c, c->sums, 2)) return e;
+  if (multi) {  // dp, beta, convergence; the ghosts of z in the same RCCL group
+    if (int e = allreduce_halo(c, c->sums, 2, c->z)) return e;
     launch_logic(c->st, c->sums, 3, c->stream);
   }
-  if (int e = halo(c, c->z)) return e;
   return TV_OK;
 }
 
