@@ -50,6 +50,13 @@ if [ $PART = C ]; then  # the unstructured algebraic multigrid
   exit 0
 fi
 if [ $PART = S ]; then  # per-rank shares of C4 (the distributed GMG, transport stubbed)
+  if [ -x tools/probe/build/march_probe ]; then
+    step "march probe (flushed, warm)"
+    timeout -k 10 180 tools/probe/build/march_probe f > $OUT/probe_f.txt 2>&1 && timeout -k 10 180 tools/probe/build/march_probe > $OUT/probe_w.txt 2>&1 || { tail -5 $OUT/probe_f.txt; exit 1; }
+    grep -E "copy|R=8 store=1 xcd=1|D 2 rows|max" $OUT/probe_f.txt
+  fi
+  step "C3 GMG under rocprofv3 --kernel-trace"
+  timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof_c3g -o run --output-format csv -- python3 bench.py --cells 200,200,25 --pc gmg --steps 5 --warmup 1 --kernel-reps 3 --no-cpu-baseline > $OUT/bench_c3g_prof.json 2> $OUT/bench_c3g_prof.err || { tail -5 $OUT/bench_c3g_prof.err; exit 1; }
   for spec in "n2 400,400,50 --share 2" "n4 400,400,50 --share 4" "n8 400,400,50 --share 8" "n8j 400,400,50 --share 8 --pc jacobi"; do
     set -- $spec; tag=$1; cells=$2; shift 2
     step "bench $tag"

@@ -182,6 +182,77 @@ __global__ __launch_bounds__(R * W) void kA2(Grid g, const double* __restrict__ 
   }
 }
 
+// ---------------- D: two adjacent rows per wave (R waves, 2R-row tile) --------
+// rows rA = r0 + 2w and rB = rA + 1: rA's upper neighbour and rB's lower one are
+// in the wave's own registers; the slab carries the outer neighbours only
+// (halo rows 2R + 2 per 2R outputs, one barrier per plane for 2R rows)
+template <int R>
+__global__ __launch_bounds__(R * W) void kD(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                            int nseg, int qchunk) {
+  __shared__ double lds[2][2 * R + 2][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + 2 * R - 1) / (2 * R);
+  const int nch = (g.nQ + qchunk - 1) / qchunk;
+  const int b = remap(blockIdx.x, gridDim.x, true);
+  const int chunk = b % nch, t = b / nch, seg = t % nseg, rb = t / nseg;
+  const int r0 = rb * 2 * R, rA = r0 + 2 * wave, rB = rA + 1;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool wA = col_ok && lane >= 1 && lane <= SEG && rA < g.nR;
+  const bool wB = col_ok && lane >= 1 && lane <= SEG && rB < g.nR;
+  const bool halo = wave == 0 || wave == R - 1;
+  const int hrow = wave == 0 ? r0 - 1 : r0 + 2 * R;
+  const int hslot = wave == 0 ? 0 : 2 * R + 1;
+  const double da = 0.1;
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ; };
+  auto fetch = [&](int rr, int L) {
+    const long idx = okf(rr, L) ? (long)i + g.sR * rr + g.sQ * L : 0;
+    return in[idx];
+  };
+  double a[3], bq[3], cq[3];  // {rA, rB, halo} raw loads of three planes
+  a[0] = fetch(rA, q0 - 1); a[1] = fetch(rB, q0 - 1); a[2] = halo ? fetch(hrow, q0 - 1) : 0.0;
+  bq[0] = fetch(rA, q0); bq[1] = fetch(rB, q0); bq[2] = halo ? fetch(hrow, q0) : 0.0;
+  double uA_m = 0, uA_c = 0, vA_m = 0, vA_c = 0, uB_m = 0, uB_c = 0, vB_m = 0, vB_c = 0;
+  auto out1 = [&](int L, double us_m, double us_c, double us_p, double vs_m, double vs_c, double vs_p, int rr, bool wr) {
+    const double S1 = cM[0] * (us_m + da * vs_m) + cM[1] * (us_c + da * vs_c) + cM[2] * (us_p + da * vs_p) +
+                      da * (cK[0] * us_m + cK[1] * us_c + cK[2] * us_p);
+    const double S2 = da * (cM[0] * us_m + cM[1] * us_c + cM[2] * us_p);
+    const double y = cM[0] * shr1(S1) + cM[1] * S1 + cM[2] * shl1(S1) + cK[0] * shr1(S2) + cK[1] * S2 +
+                     cK[2] * shl1(S2);
+    if (wr) out[(long)i + g.sR * rr + g.sQ * (L - 1)] = y;
+  };
+  auto step = [&](int L, const double (&v)[3]) {
+    const int buf = L & 1;
+    const double xA = okf(rA, L) ? v[0] : 0.0, xB = okf(rB, L) ? v[1] : 0.0;
+    lds[buf][2 * wave + 1][lane] = xA;
+    lds[buf][2 * wave + 2][lane] = xB;
+    if (halo) lds[buf][hslot][lane] = okf(hrow, L) ? v[2] : 0.0;
+    __syncthreads();
+    const double xl = lds[buf][2 * wave][lane], xu = lds[buf][2 * wave + 3][lane];
+    const double uA = cM[0] * xl + cM[1] * xA + cM[2] * xB, vA = cK[0] * xl + cK[1] * xA + cK[2] * xB;
+    const double uB = cM[0] * xA + cM[1] * xB + cM[2] * xu, vB = cK[0] * xA + cK[1] * xB + cK[2] * xu;
+    if (L >= q0 + 1 && L <= q1) {
+      out1(L, uA_m, uA_c, uA, vA_m, vA_c, vA, rA, wA);
+      out1(L, uB_m, uB_c, uB, vB_m, vB_c, vB, rB, wB);
+    }
+    uA_m = uA_c; uA_c = uA; vA_m = vA_c; vA_c = vA;
+    uB_m = uB_c; uB_c = uB; vB_m = vB_c; vB_c = vB;
+  };
+  auto ld3 = [&](int L, double (&v)[3]) {
+    v[0] = fetch(rA, L); v[1] = fetch(rB, L); v[2] = halo ? fetch(hrow, L) : 0.0;
+  };
+  for (int L = q0 - 1; L <= q1; L += 3) {
+    ld3(L + 2, cq);
+    step(L, a);
+    ld3(L + 3, a);
+    step(L + 1, bq);
+    ld3(L + 4, bq);
+    step(L + 2, cq);
+  }
+}
+
 // ---------------- B: register march, waves independent ----------------------
 // WPB waves per block, consecutive rows; each wave loads rows r-1, r, r+1.
 template <int WPB, bool XCD>
@@ -337,6 +408,20 @@ int main(int argc, char** argv) {
     RUN_B(8, true)
     RUN_B(2, true)
   }
+  for (int minblk : {512, 768, 1024}) {  // D: 2 rows per wave, R = 8 / 4 waves (16 / 8-row tiles)
+#define RUN_D(RR)                                                                                          \
+  {                                                                                                        \
+    const int nrb = (g.nR + 2 * RR - 1) / (2 * RR);                                                        \
+    const int nch = chunks_for(nseg * nrb, g.nQ, minblk);                                                  \
+    const int qc = (g.nQ + nch - 1) / nch;                                                                 \
+    const int nb = nseg * nrb * ((g.nQ + qc - 1) / qc);                                                    \
+    char nm[96];                                                                                           \
+    snprintf(nm, sizeof nm, "D 2 rows/wave R=%d minblk=%d", RR, minblk);                                  \
+    rep(nm, timeit([&] { kD<RR><<<nb, RR * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nb);                 \
+  }
+    RUN_D(8)
+    RUN_D(4)
+  }
   {
     double* Bf;
     CK(hipMalloc(&Bf, 9L * g.n0 * g.nR * 8));
@@ -365,6 +450,13 @@ int main(int argc, char** argv) {
     double md = 0;
     for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
     printf("max |A-B| = %g\n", md);
+    CK(hipMemset(y, 0, N * 8));
+    const int nrbd = (g.nR + 15) / 16;
+    kD<8><<<nseg * nrbd, 8 * W>>>(g, x, y, nseg, g.nQ);
+    CK(hipMemcpy(yb.data(), y, N * 8, hipMemcpyDeviceToHost));
+    md = 0;
+    for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
+    printf("max |A-D| = %g\n", md);
   }
   return 0;
 }
