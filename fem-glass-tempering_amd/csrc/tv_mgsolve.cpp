@@ -4,6 +4,8 @@
 #include "tv_ctx.h"
 
 namespace tv {
+constexpr int64_t kMgFoldFacesNodes = 4000000;  // level 0: facet terms folded into the restriction below this
+
 // ---- geometric-multigrid preconditioned CG (options.preconditioner = GMG) ----
 // Gershgorin bound of D^-1 J on a rectilinear level: max over nodes of the
 // exact absolute row sum of the 27-point cell operator M + dt alpha K over its
@@ -371,10 +373,16 @@ int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
   const FaceAdd fa = cg_face_add(c->cg, 0);
   if (!c->mg.empty()) {
     MgLevel& C = c->mg[0];
-    // a complete J x (k_cg_addfaces) here: folding the facet terms into the
-    // restriction as on the coarse levels measured no gain on level 0
-    launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
-    launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
+    // below kMgFoldFacesNodes the restriction adds the face-workgroup facet
+    // terms itself, as on the coarse levels (one launch fewer where the V-cycle
+    // is launch-bound); at C4 a complete J x (k_cg_addfaces) measured the same
+    if (fa.on && mg_restrict_folds_faces(C.xf) && n < kMgFoldFacesNodes) {
+      launch_cg_japply_partial(c->cg, T, c->mgx, c->w, c->st, s);
+      launch_mg_restrict(C.xf, c->st, c->r, c->w, &fa, mask, C.b, C.dinv, C.omega, C.x, s);
+    } else {
+      launch_cg_japply(c->cg, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+      launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
+    }
     mg_level(c, 1);
     mg_prolong_from(c, 0, c->mgx, mask);
   }
