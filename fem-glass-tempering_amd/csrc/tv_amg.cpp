@@ -17,7 +17,9 @@
 //     aggregates of their free neighbours;
 //   * tentative prolongation: piecewise constant (the constant near-null
 //     space of the heat operator); smoothed P = (I - 4/3 / lambda D^-1 A) P0,
-//     lambda = lambda_max(D^-1 A) by power iteration; Galerkin A_c = P^T A P;
+//     lambda = lambda_max(D^-1 A) by power iteration, stored in float32 (P
+//     as CSR, R = P^T as SELL-64: the transfers are the cycle's largest
+//     streams); Galerkin A_c = P^T A P in double from the rounded P;
 //     until <= kAmgCoarseRows rows (or the options.mg_levels depth);
 //   * cycle: level 0 ADDITIVE -- z = omega0 D^-1 r + P_0 V_1(P_0^T r) -- so the
 //     preconditioner never applies the fine operator (a fine J x streams
@@ -272,37 +274,56 @@ int64_t sell_size(const Csr& M) {
   return t;
 }
 
-// CSR -> SELL-64 on the device (padding: value 0, column 0)
-int upload_sell(Ctx* c, const Csr& M, Sell& out) {
+// CSR -> the device: SELL-64 (padding: value 0, column 0) or CSR (as is);
+// values in float32 (the transfers) or double
+int upload_mat(Ctx* c, const Csr& M, Sell& out, bool csr, bool fp32) {
   const int64_t ns = (M.n + 63) / 64;
-  std::vector<int64_t> soff((size_t)ns + 1, 0);
-  for (int64_t s = 0; s < ns; ++s) {
-    int64_t w = 0;
-    for (int64_t r = s * 64; r < std::min(M.n, s * 64 + 64); ++r) w = std::max(w, M.ptr[r + 1] - M.ptr[r]);
-    soff[s + 1] = soff[s] + 64 * w;
-  }
-  std::vector<int> cols((size_t)soff[ns], 0);
-  std::vector<double> vals((size_t)soff[ns], 0.0);
-  for (int64_t r = 0; r < M.n; ++r) {
-    const int64_t s = r >> 6, lane = r & 63;
-    for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
-      const int64_t q = soff[s] + 64 * (k - M.ptr[r]) + lane;
-      cols[q] = M.col[k];
-      vals[q] = M.val[k];
+  std::vector<int64_t> soff;
+  std::vector<int> cols;
+  std::vector<double> vals;
+  if (csr) {
+    soff = M.ptr;
+    cols = M.col;
+    vals = M.val;
+  } else {
+    soff.assign((size_t)ns + 1, 0);
+    for (int64_t s = 0; s < ns; ++s) {
+      int64_t w = 0;
+      for (int64_t r = s * 64; r < std::min(M.n, s * 64 + 64); ++r) w = std::max(w, M.ptr[r + 1] - M.ptr[r]);
+      soff[s + 1] = soff[s] + 64 * w;
+    }
+    cols.assign((size_t)soff[ns], 0);
+    vals.assign((size_t)soff[ns], 0.0);
+    for (int64_t r = 0; r < M.n; ++r) {
+      const int64_t s = r >> 6, lane = r & 63;
+      for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
+        const int64_t q = soff[s] + 64 * (k - M.ptr[r]) + lane;
+        cols[q] = M.col[k];
+        vals[q] = M.val[k];
+      }
     }
   }
   int64_t* so;
   int* co;
-  double* va;
   if (int e = amg_upload(c, soff, &so)) return e;
   if (int e = amg_upload(c, cols, &co)) return e;
-  if (int e = amg_upload(c, vals, &va)) return e;
+  if (fp32) {
+    std::vector<float> vf(vals.begin(), vals.end());
+    float* va;
+    if (int e = amg_upload(c, vf, &va)) return e;
+    out.vals = va;
+  } else {
+    double* va;
+    if (int e = amg_upload(c, vals, &va)) return e;
+    out.vals = va;
+  }
   out.nrow = M.n;
   out.ncol = M.m;
   out.nslice = ns;
   out.soff = so;
   out.cols = co;
-  out.val = va;
+  out.csr = csr ? 1 : 0;
+  out.fp32 = fp32 ? 1 : 0;
   return TV_OK;
 }
 
@@ -315,7 +336,7 @@ int fine_csr(Ctx* c, Csr& A) {
   std::vector<int> cols((size_t)nnz);
   std::vector<double> vals((size_t)nnz);
   HIPC(hipMemcpy(cols.data(), S.cols, sizeof(int) * (size_t)nnz, hipMemcpyDeviceToHost));
-  HIPC(hipMemcpy(vals.data(), S.val, sizeof(double) * (size_t)nnz, hipMemcpyDeviceToHost));
+  HIPC(hipMemcpy(vals.data(), S.vals, sizeof(double) * (size_t)nnz, hipMemcpyDeviceToHost));
   A.n = S.nrow;
   A.m = S.ncol;
   A.ptr.assign((size_t)A.n + 1, 0);
@@ -357,6 +378,10 @@ int amg_setup(Ctx* c) {
     if (na < 1 || na * 10 > A.n * 7) break;  // coarsening stalled
     const double lam = lam_max(A, dinv, 15);
     Csr P = smoothed_p(A, dinv, agg, na, 4.0 / (3.0 * lam));
+    // the transfers are stored in float32 (half the bytes of the V-cycle's
+    // largest streams): round P first, so R = P^T and A_c = R (A P) are built
+    // from the very values the device applies (the cycle stays symmetric)
+    for (double& v : P.val) v = (double)(float)v;
     Csr R = transpose(P);
     Csr Ac;
     {
@@ -366,10 +391,11 @@ int amg_setup(Ctx* c) {
     c->amg.emplace_back();
     AmgLevel& L = c->amg.back();
     L.n = na;
-    if (int e = upload_sell(c, P, L.P)) return e;
-    if (int e = upload_sell(c, R, L.R)) return e;
-    if (int e = upload_sell(c, Ac, L.A)) return e;
-    L.p_nnz = sell_size(P);
+    // P: CSR (short rows of ~4 entries, no slice padding); R: SELL-64 (long rows)
+    if (int e = upload_mat(c, P, L.P, true, true)) return e;
+    if (int e = upload_mat(c, R, L.R, false, true)) return e;
+    if (int e = upload_mat(c, Ac, L.A, false, false)) return e;
+    L.p_nnz = (int64_t)P.col.size();
     L.r_nnz = sell_size(R);
     L.a_nnz = sell_size(Ac);
     const std::vector<double> dc = diag_inv(Ac);
@@ -414,20 +440,21 @@ int amg_apply0(Ctx* c, const RedTail* tail) {
 }
 
 // algorithmic bytes of one V-cycle (tv_kernel_bytes 11): the stored entries
-// of every launched operator (12 B: value + column, padding included) and the
+// of every launched operator (A: 12 B, value + column; P, R: 8 B, float value
+// + column; SELL padding included, P's CSR row pointer 8 B per row) and the
 // vectors each launch streams once (gathered vectors counted once)
 double amg_cycle_bytes(const Ctx* c) {
   const double n0 = (double)c->nT;
   const AmgLevel& L1 = c->amg[0];
-  double b = 12.0 * (double)L1.r_nnz + 8.0 * n0 + 24.0 * (double)L1.n;  // R_0 (r in; b, x, dinv of level 1)
-  b += 12.0 * (double)L1.p_nnz + 8.0 * (double)L1.n + 24.0 * n0;        // P_0 (x_1 in; x0, r in, z out)
+  double b = 8.0 * (double)L1.r_nnz + 8.0 * n0 + 24.0 * (double)L1.n;         // R_0 (r in; b, x, dinv of level 1)
+  b += 8.0 * (double)L1.p_nnz + 8.0 * n0 + 8.0 * (double)L1.n + 24.0 * n0;  // P_0 (x_1 in; x0, r in, z out)
   for (size_t l = 0; l + 1 < c->amg.size(); ++l) {
     const AmgLevel& L = c->amg[l];
     const AmgLevel& C = c->amg[l + 1];
     const double n = (double)L.n, nc = (double)C.n;
     b += 12.0 * (double)L.a_nnz + 16.0 * n;                      // w = A x
-    b += 12.0 * (double)C.r_nnz + 16.0 * n + 24.0 * nc;          // b_c = R (b - w), x_c
-    b += 12.0 * (double)C.p_nnz + 8.0 * nc + 16.0 * n;           // x += P x_c
+    b += 8.0 * (double)C.r_nnz + 16.0 * n + 24.0 * nc;           // b_c = R (b - w), x_c
+    b += 8.0 * (double)C.p_nnz + 8.0 * n + 8.0 * nc + 16.0 * n;  // x += P x_c
     b += 12.0 * (double)L.a_nnz + 32.0 * n;                      // post: x, b, dinv in, w out
   }
   return b;

@@ -27,24 +27,37 @@ enum AmgMode {
 
 constexpr int kAmgBlocksMax = 2048;
 
-// the sum over a row of M of val * x[col]: U entries in flight per lane
-__device__ __forceinline__ double sell_row(const Sell& M, int64_t s, int lane, const double* __restrict__ x,
-                                           const double* __restrict__ x2) {
-  const int64_t so = M.soff[s];
-  const int wdt = (int)((M.soff[s + 1] - so) >> 6);
-  const int* __restrict__ cs = M.cols + so + lane;
-  const double* __restrict__ vs = M.val + so + lane;
+// the sum over row r of M of val * (x - x2)[col] (x2 optional): SELL-64 (lane
+// = row of the wave's slice, column-major entries) or CSR (one row per lane,
+// the transfers' short rows: no slice padding); U entries in flight per lane
+template <typename V>
+__device__ __forceinline__ double row_sum(const Sell& M, int64_t r, const double* __restrict__ x,
+                                          const double* __restrict__ x2) {
+  int64_t k0, step;
+  int len;
+  if (M.csr) {
+    k0 = M.soff[r];
+    len = (int)(M.soff[r + 1] - k0);
+    step = 1;
+  } else {
+    const int64_t s = r >> 6;
+    k0 = M.soff[s] + (r & 63);
+    len = (int)((M.soff[s + 1] - M.soff[s]) >> 6);
+    step = 64;
+  }
+  const int* __restrict__ cs = M.cols + k0;
+  const V* __restrict__ vs = reinterpret_cast<const V*>(M.vals) + k0;
   constexpr int U = 8;
   double acc = 0.0;
-  for (int k = 0; k < wdt; k += U) {
+  for (int k = 0; k < len; k += U) {
     int c[U];
     double a[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const bool ok = k + j < wdt;
-      const int o = 64 * (ok ? k + j : 0);
+      const bool ok = k + j < len;
+      const int64_t o = step * (ok ? k + j : 0);
       c[j] = __builtin_nontemporal_load(&cs[o]);
-      a[j] = __builtin_nontemporal_load(&vs[o]);
+      a[j] = (double)__builtin_nontemporal_load(&vs[o]);
       if (!ok) a[j] = 0.0;
     }
 #pragma unroll
@@ -53,7 +66,7 @@ __device__ __forceinline__ double sell_row(const Sell& M, int64_t s, int lane, c
   return acc;
 }
 
-template <int MODE>
+template <int MODE, typename V>
 __global__ __launch_bounds__(kBlock) void k_amg_rows(Sell M, const PcgState* __restrict__ st,
                                                      const double* __restrict__ x, const double* x2,
                                                      const double* __restrict__ b, const double* __restrict__ dinv,
@@ -63,15 +76,9 @@ __global__ __launch_bounds__(kBlock) void k_amg_rows(Sell M, const PcgState* __r
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   constexpr int WPB = kBlock / 64;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t nw = (int64_t)gridDim.x * WPB;
-  const int64_t gw = (int64_t)blk * WPB + wave;
-  const int64_t chunk = (M.nslice + nw - 1) / nw;
-  const int64_t s0 = gw * chunk, s1 = std::min<int64_t>(s0 + chunk, M.nslice);
   double zz = 0.0, zb = 0.0;
-  for (int64_t s = s0; s < s1; ++s) {
-    const int64_t r = s * 64 + lane;
-    const double acc = sell_row(M, s, lane, (MODE == AMG_POST) ? x2 : x, (MODE == AMG_RESTRICT) ? x2 : nullptr);
-    if (r >= M.nrow) continue;
+  auto row = [&](int64_t r) {
+    const double acc = row_sum<V>(M, r, (MODE == AMG_POST) ? x2 : x, (MODE == AMG_RESTRICT) ? x2 : nullptr);
     if (MODE == AMG_APPLY) {
       y[r] = acc;
     } else if (MODE == AMG_RESTRICT) {
@@ -86,6 +93,20 @@ __global__ __launch_bounds__(kBlock) void k_amg_rows(Sell M, const PcgState* __r
       y[r] = z;
       zz += z * z;
       zb += z * b[r];
+    }
+  };
+  if (M.csr) {  // a contiguous row range per workgroup (XCD-remapped)
+    const int64_t per = (M.nrow + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = (int64_t)blk * per, r1 = std::min<int64_t>(r0 + per, M.nrow);
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kBlock) row(r);
+  } else {  // a contiguous slice range per wave
+    const int64_t nw = (int64_t)gridDim.x * WPB;
+    const int64_t gw = (int64_t)blk * WPB + wave;
+    const int64_t chunk = (M.nslice + nw - 1) / nw;
+    const int64_t s0 = gw * chunk, s1 = std::min<int64_t>(s0 + chunk, M.nslice);
+    for (int64_t s = s0; s < s1; ++s) {
+      const int64_t r = s * 64 + lane;
+      if (r < M.nrow) row(r);
     }
   }
   if (MODE == AMG_PROLONG0) {
@@ -103,15 +124,22 @@ __global__ __launch_bounds__(kBlock) void k_amg_rows(Sell M, const PcgState* __r
   }
 }
 
-int amg_blocks(const Sell& M) { return (int)std::max<int64_t>(1, std::min<int64_t>((M.nslice + 3) / 4, kAmgBlocksMax)); }
+int amg_blocks(const Sell& M) {
+  const int64_t units = M.csr ? (M.nrow + kBlock - 1) / kBlock : (M.nslice + 3) / 4;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(units, kAmgBlocksMax));
+}
 
 template <int MODE>
 int launch(const Sell& M, const PcgState* st, const double* x, const double* x2, const double* b, const double* dinv,
            double omega, double* y, double* y2, double* partials, const RedTail* tail, hipStream_t s) {
   const int nb = amg_blocks(M);
   const RedTail rt = tail ? *tail : RedTail{};
-  hipLaunchKernelGGL((k_amg_rows<MODE>), dim3(nb), dim3(kBlock), 0, s, M, st, x, x2, b, dinv, omega, y, y2, partials,
-                     rt);
+  if (M.fp32)
+    hipLaunchKernelGGL((k_amg_rows<MODE, float>), dim3(nb), dim3(kBlock), 0, s, M, st, x, x2, b, dinv, omega, y, y2,
+                       partials, rt);
+  else
+    hipLaunchKernelGGL((k_amg_rows<MODE, double>), dim3(nb), dim3(kBlock), 0, s, M, st, x, x2, b, dinv, omega, y, y2,
+                       partials, rt);
   return nb;
 }
 

@@ -173,14 +173,17 @@ struct UmGrid {
   double T_amb, T_amb4;
 };
 
-// A sparse operator in SELL-64 on the device (entry k of row r: soff[r / 64] +
-// 64 k + r % 64; padding entries: value 0, column 0) -- the algebraic
-// multigrid's coarse operators, prolongations and restrictions (tv_amg.*)
+// A sparse operator on the device: SELL-64 (entry k of row r: soff[r / 64] +
+// 64 k + r % 64; padding entries: value 0, column 0) or, csr = 1, CSR (soff =
+// the row pointer) -- the fine unstructured operator and the algebraic
+// multigrid's coarse operators (double), prolongations (CSR) and restrictions
+// (SELL), the transfers with float32 values (fp32 = 1: vals is a float array)
 struct Sell {
   int64_t nrow = 0, ncol = 0, nslice = 0;
   const int64_t* soff = nullptr;
   const int* cols = nullptr;
-  const double* val = nullptr;
+  const void* vals = nullptr;
+  int csr = 0, fp32 = 0;
 };
 int amg_num_blocks(const Sell& M);  // partial records of launch_amg_prolong0
 // y = A x

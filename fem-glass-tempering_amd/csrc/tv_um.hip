@@ -480,7 +480,7 @@ Sell um_operator(const UmGrid& g) {
   m.nslice = g.nslice;
   m.soff = g.soff;
   m.cols = g.cols;
-  m.val = g.V;
+  m.vals = g.V;
   return m;
 }
 void launch_um_pack(const int64_t* idx, int64_t n, const double* v, double* out, hipStream_t s) {

@@ -14,7 +14,8 @@ Algorithm (each step as tv_amg.cpp states it):
   * A = the T-independent cell operator M + dt alpha K, exact zeros dropped;
   * greedy aggregation over every off-diagonal nonzero, three passes;
   * P = (I - 4 / (3 lambda) D^-1 A) P0, lambda by 15 power iterations of
-    D^-1 A from the fixed xorshift start vector; R = P^T; A_c = R (A P);
+    D^-1 A from the fixed xorshift start vector, rounded to float32 (the
+    device's storage of the transfers); R = P^T; A_c = R (A P) in double;
   * coarse weights omega_l = 2 / (1.1 lambda_max(D^-1 A_l)) (20 iterations);
     level-0 weight 2 / (1.1 lambda_max(D^-1 J(T))) (30 iterations, the
     device's mg_dg_lambda);
@@ -112,6 +113,7 @@ def build(V, max_levels=12):
         lam = lam_max_host(A, dinv, 15)
         P0 = sp.csr_matrix((np.ones(A.shape[0]), (np.arange(A.shape[0]), agg)), shape=(A.shape[0], na))
         P = sp.csr_matrix(P0 - (4.0 / (3.0 * lam)) * (sp.diags(dinv) @ (A @ P0)))
+        P.data = P.data.astype(np.float32).astype(np.float64)  # the device stores the transfers in float32
         R = sp.csr_matrix(P.T)
         Ac = sp.csr_matrix(R @ (A @ P))
         Ac.sort_indices()
