@@ -130,13 +130,15 @@ def _torch():
 MESHES = {
     "quad": ((9, 5), (3.0, 1.0)),
     "hex": ((7, 5, 4), (2.0, 2.0, 1.0)),
+    # numbered plane by plane (not shuffled): the 16-bit column-offset operator
+    "hex_ordered": ((7, 5, 4), (2.0, 2.0, 1.0)),
 }
 
 
 def make_pair(name, mode="reference", seed=0, **kw):
     from tvfem.problem import ThermoViscoProblem
     n, L = MESHES[name]
-    m = distorted_mesh(n, L, seed=seed)
+    m = distorted_mesh(n, L, seed=seed, shuffle=not name.endswith("_ordered"))
     cfg = {"T": CG, "sigma": CG}
     dev = ThermoViscoProblem(m, (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False, model_mode=mode, **kw)
     ref = O.OracleProblem(oracle_mesh(m), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), linear="pcg",

@@ -38,7 +38,7 @@ if [ $PART = A ]; then
 fi
 if [ $PART = C ]; then  # the unstructured algebraic multigrid
   step "amg tests"
-  timeout -k 10 600 python -u -m pytest tests/test_amg.py -m gpu -v -s -rs --timeout 300 --timeout-method thread > $OUT/amg_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests/test_amg.py tests/test_unstructured.py tests/test_upartition.py -m gpu -v -s -rs --timeout 300 --timeout-method thread > $OUT/amg_tests.log 2>&1
   rc=$?; tail -3 $OUT/amg_tests.log; grep -h "^\[amg\]" $OUT/amg_tests.log
   [ $rc -ne 0 ] && { grep -E "Error|assert|FAILED" $OUT/amg_tests.log | head -20; exit $rc; }
   for spec in "UMamg --pc amg" "UMjac --pc jacobi"; do
