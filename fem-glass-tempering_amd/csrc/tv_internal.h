@@ -158,7 +158,6 @@ struct UmGrid {
   // assembled cell operators (entry k of row r: soff[r / 64] + 64 k + r % 64)
   const int64_t* soff;   // nslice + 1
   const int* cols;
-  const short* dcols;    // col - row as 16 bits (nullptr: bandwidth > 32767, cols only)
   const double* V;       // M + dt alpha K  (J x)
   const double* M;       // mass            (residual)
   const double* K;       // dt alpha K      (residual)

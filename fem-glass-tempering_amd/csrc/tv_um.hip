@@ -360,7 +360,7 @@ __device__ __forceinline__ double robin_row(const UmGrid& g, int64_t r, const do
 //             + the reduction tail (PETSc's dpi and alpha)
 //   UM_RES:   out = M (u - up) + K u - dt f b + Robin(u)      (u = T, up = T_prev)
 //   UM_DIAG:  out = diag V + Robin diagonal (inverted if `invert`)
-template <int D, int MODE, bool IDX16>
+template <int D, int MODE>
 __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __restrict__ T,
                                                     const double* __restrict__ u, const double* __restrict__ up,
                                                     double* __restrict__ out, const PcgState* __restrict__ st,
@@ -380,20 +380,12 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
     const int64_t so = g.soff[s];
     const int wdt = (int)((g.soff[s + 1] - so) >> 6);
     const int* __restrict__ cs = g.cols + so + lane;  // entry k of this row: cs[64 k]
-    // IDX16: the columns as 16-bit offsets from the row (10 instead of 12 bytes
-    // per stored entry of J x, 18 instead of 20 of the residual)
-    // (the padding lanes past the last row read vertex 0, as their int32 columns do)
-    const short* __restrict__ ds = g.dcols + so + lane;
-    const int rbase = r < g.nrow ? (int)r : 0;
-    auto col = [&](int o) -> int {
-      return IDX16 ? rbase + (int)__builtin_nontemporal_load(&ds[o]) : __builtin_nontemporal_load(&cs[o]);
-    };
     double acc = 0.0, acc2 = 0.0;
     if (MODE == UM_RES) {
       const double* __restrict__ ms = g.M + so + lane;
       const double* __restrict__ ks = g.K + so + lane;
       for (int k = 0; k < wdt; ++k) {
-        const int c = col(64 * k);
+        const int c = __builtin_nontemporal_load(&cs[64 * k]);
         const double xc = u[c];
         acc += __builtin_nontemporal_load(&ms[64 * k]) * (xc - up[c]);
         acc2 += __builtin_nontemporal_load(&ks[64 * k]) * xc;
@@ -413,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
         for (int j = 0; j < U; ++j) {
           const bool ok = k + j < wdt;
           const int o = 64 * (ok ? k + j : 0);
-          c[j] = col(o);
+          c[j] = __builtin_nontemporal_load(&cs[o]);
           a[j] = __builtin_nontemporal_load(&vs[o]);
           if (!ok) a[j] = 0.0;
         }
@@ -472,17 +464,10 @@ template <int MODE>
 void launch_rows(const UmGrid& g, const double* T, const double* u, const double* up, double* out,
                  const PcgState* st, double* partials, const RedTail& rt, int invert, hipStream_t s) {
   const dim3 grid(row_blocks(g)), block(kBlock);
-#define TV_UMR(D, I16) \
-  hipLaunchKernelGGL((k_um_rows<D, MODE, I16>), grid, block, 0, s, g, T, u, up, out, st, partials, rt, invert)
-  const bool i16 = g.dcols != nullptr && MODE != UM_DIAG;
-  if (g.dim == 2) {
-    if (i16) TV_UMR(2, true);
-    else TV_UMR(2, false);
-  } else {
-    if (i16) TV_UMR(3, true);
-    else TV_UMR(3, false);
-  }
-#undef TV_UMR
+  if (g.dim == 2)
+    hipLaunchKernelGGL((k_um_rows<2, MODE>), grid, block, 0, s, g, T, u, up, out, st, partials, rt, invert);
+  else
+    hipLaunchKernelGGL((k_um_rows<3, MODE>), grid, block, 0, s, g, T, u, up, out, st, partials, rt, invert);
 }
 
 }  // namespace
@@ -708,26 +693,6 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   }
   // padding lanes of the last slice (rows >= nrow) keep column 0, value 0
   std::vector<std::vector<int>>().swap(part);
-  // 16-bit column offsets from the row where the bandwidth allows (a mesh
-  // numbered plane by plane, as gmsh / box meshes are: |col - row| <= one plane
-  // + one row + 1); padding entries point at the row itself (offset 0)
-  std::vector<short> dcols;
-  {
-    int64_t bw = 0;
-    for (int64_t sl = 0; sl < nslice; ++sl)
-      for (int64_t q = soff[(size_t)sl]; q < soff[(size_t)sl + 1]; ++q) {
-        const int64_t r = sl * 64 + (q - soff[(size_t)sl]) % 64;
-        if (r < nrow) bw = std::max<int64_t>(bw, std::llabs((int64_t)cols[(size_t)q] - r));
-      }
-    if (bw <= 32767) {
-      dcols.resize((size_t)nnz);
-      for (int64_t sl = 0; sl < nslice; ++sl)
-        for (int64_t q = soff[(size_t)sl]; q < soff[(size_t)sl + 1]; ++q) {
-          const int64_t r = sl * 64 + (q - soff[(size_t)sl]) % 64;
-          dcols[(size_t)q] = (short)(r < nrow ? (int64_t)cols[(size_t)q] - r : 0);
-        }
-    }
-  }
   d->nnz = nnz;
   // -- boundary facet data (host): incidences of the boundary rows
   const int nfv = nl / 2;
@@ -785,9 +750,6 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
       um_upload(d, fcell, &fcell_d, err) || um_upload(d, flf, &flf_d, err) || um_upload(d, boff, &boff_d, err) ||
       um_upload(d, binc, &binc_d, err))
     return 1;
-  short* dcols_d = nullptr;
-  if (!dcols.empty() && um_upload(d, dcols, &dcols_d, err)) return 1;
-  std::vector<short>().swap(dcols);
   std::vector<int>().swap(cell_h);
   std::vector<int>().swap(cols);
   std::vector<int64_t>().swap(inc);
@@ -827,7 +789,6 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   g.nslice = nslice;
   g.soff = soff_d;
   g.cols = cols_d;
-  g.dcols = dcols_d;
   g.V = V;
   g.M = M;
   g.K = K;
