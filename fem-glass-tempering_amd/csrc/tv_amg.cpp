@@ -17,8 +17,8 @@
 //     aggregates of their free neighbours;
 //   * tentative prolongation: piecewise constant (the constant near-null
 //     space of the heat operator); smoothed P = (I - 4/3 / lambda D^-1 A) P0,
-//     lambda = lambda_max(D^-1 A) by power iteration, stored in float32 (P
-//     as CSR, R = P^T as SELL-64: the transfers are the cycle's largest
+//     lambda = lambda_max(D^-1 A) by power iteration, stored in float32
+//     (SELL-64, like R = P^T: the transfers are the cycle's largest
 //     streams); Galerkin A_c = P^T A P in double from the rounded P;
 //     until <= kAmgCoarseRows rows (or the options.mg_levels depth);
 //   * cycle: level 0 ADDITIVE -- z = omega0 D^-1 r + P_0 V_1(P_0^T r) -- so the
@@ -391,11 +391,12 @@ int amg_setup(Ctx* c) {
     c->amg.emplace_back();
     AmgLevel& L = c->amg.back();
     L.n = na;
-    // P: CSR (short rows of ~4 entries, no slice padding); R: SELL-64 (long rows)
-    if (int e = upload_mat(c, P, L.P, true, true)) return e;
+    // P and R: SELL-64 with float32 values (one row per lane in CSR left the
+    // wave's loads uncoalesced: measured slower, 475 vs 411 us per V-cycle)
+    if (int e = upload_mat(c, P, L.P, false, true)) return e;
     if (int e = upload_mat(c, R, L.R, false, true)) return e;
     if (int e = upload_mat(c, Ac, L.A, false, false)) return e;
-    L.p_nnz = (int64_t)P.col.size();
+    L.p_nnz = sell_size(P);
     L.r_nnz = sell_size(R);
     L.a_nnz = sell_size(Ac);
     const std::vector<double> dc = diag_inv(Ac);
@@ -441,20 +442,20 @@ int amg_apply0(Ctx* c, const RedTail* tail) {
 
 // algorithmic bytes of one V-cycle (tv_kernel_bytes 11): the stored entries
 // of every launched operator (A: 12 B, value + column; P, R: 8 B, float value
-// + column; SELL padding included, P's CSR row pointer 8 B per row) and the
+// + column; SELL padding included) and the
 // vectors each launch streams once (gathered vectors counted once)
 double amg_cycle_bytes(const Ctx* c) {
   const double n0 = (double)c->nT;
   const AmgLevel& L1 = c->amg[0];
   double b = 8.0 * (double)L1.r_nnz + 8.0 * n0 + 24.0 * (double)L1.n;         // R_0 (r in; b, x, dinv of level 1)
-  b += 8.0 * (double)L1.p_nnz + 8.0 * n0 + 8.0 * (double)L1.n + 24.0 * n0;  // P_0 (x_1 in; x0, r in, z out)
+  b += 8.0 * (double)L1.p_nnz + 8.0 * (double)L1.n + 24.0 * n0;  // P_0 (x_1 in; x0, r in, z out)
   for (size_t l = 0; l + 1 < c->amg.size(); ++l) {
     const AmgLevel& L = c->amg[l];
     const AmgLevel& C = c->amg[l + 1];
     const double n = (double)L.n, nc = (double)C.n;
     b += 12.0 * (double)L.a_nnz + 16.0 * n;                      // w = A x
     b += 8.0 * (double)C.r_nnz + 16.0 * n + 24.0 * nc;           // b_c = R (b - w), x_c
-    b += 8.0 * (double)C.p_nnz + 8.0 * n + 8.0 * nc + 16.0 * n;  // x += P x_c
+    b += 8.0 * (double)C.p_nnz + 8.0 * nc + 16.0 * n;            // x += P x_c
     b += 12.0 * (double)L.a_nnz + 32.0 * n;                      // post: x, b, dinv in, w out
   }
   return b;
