@@ -130,7 +130,7 @@ def _torch():
 MESHES = {
     "quad": ((9, 5), (3.0, 1.0)),
     "hex": ((7, 5, 4), (2.0, 2.0, 1.0)),
-    # numbered plane by plane (not shuffled): the 16-bit column-offset operator
+    # numbered plane by plane (not shuffled), as gmsh and the box meshes number them
     "hex_ordered": ((7, 5, 4), (2.0, 2.0, 1.0)),
 }
 
