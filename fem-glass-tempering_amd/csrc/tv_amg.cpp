@@ -39,6 +39,7 @@ namespace tv {
 namespace {
 
 constexpr int64_t kAmgCoarseRows = 2000;
+constexpr int64_t kAmgSortWindow = 4096;  // rows per length-sorting window of the transfers' SELL layout
 
 struct Csr {
   int64_t n = 0, m = 0;  // rows, columns
@@ -263,46 +264,49 @@ int amg_upload(Ctx* c, const std::vector<T>& h, T** out) {
   return TV_OK;
 }
 
-// stored entries of M in SELL-64 (padding included)
-int64_t sell_size(const Csr& M) {
-  int64_t t = 0;
-  for (int64_t s = 0; s * 64 < M.n; ++s) {
-    int64_t w = 0;
-    for (int64_t r = s * 64; r < std::min(M.n, s * 64 + 64); ++r) w = std::max(w, M.ptr[r + 1] - M.ptr[r]);
-    t += 64 * w;
-  }
-  return t;
-}
-
 // CSR -> the device: SELL-64 (padding: value 0, column 0) or CSR (as is);
 // values in float32 (the transfers) or double
-int upload_mat(Ctx* c, const Csr& M, Sell& out, bool csr, bool fp32) {
+int upload_mat(Ctx* c, const Csr& M, Sell& out, bool csr, bool fp32, int64_t sort_window, int64_t* stored) {
   const int64_t ns = (M.n + 63) / 64;
   std::vector<int64_t> soff;
   std::vector<int> cols;
   std::vector<double> vals;
+  std::vector<int> perm;
   if (csr) {
     soff = M.ptr;
     cols = M.col;
     vals = M.val;
   } else {
+    // sort_window > 0: rows ordered by decreasing length inside windows of that
+    // many rows (stable), so each 64-row slice pads to a similar length
+    perm.resize((size_t)M.n);
+    std::iota(perm.begin(), perm.end(), 0);
+    if (sort_window > 0)
+      for (int64_t w0 = 0; w0 < M.n; w0 += sort_window) {
+        const int64_t w1 = std::min(M.n, w0 + sort_window);
+        std::stable_sort(perm.begin() + w0, perm.begin() + w1, [&](int a, int b) {
+          return M.ptr[a + 1] - M.ptr[a] > M.ptr[b + 1] - M.ptr[b];
+        });
+      }
+    auto len = [&](int64_t q) { return M.ptr[perm[q] + 1] - M.ptr[perm[q]]; };
     soff.assign((size_t)ns + 1, 0);
     for (int64_t s = 0; s < ns; ++s) {
       int64_t w = 0;
-      for (int64_t r = s * 64; r < std::min(M.n, s * 64 + 64); ++r) w = std::max(w, M.ptr[r + 1] - M.ptr[r]);
+      for (int64_t q = s * 64; q < std::min(M.n, s * 64 + 64); ++q) w = std::max(w, len(q));
       soff[s + 1] = soff[s] + 64 * w;
     }
     cols.assign((size_t)soff[ns], 0);
     vals.assign((size_t)soff[ns], 0.0);
-    for (int64_t r = 0; r < M.n; ++r) {
-      const int64_t s = r >> 6, lane = r & 63;
+    for (int64_t q = 0; q < M.n; ++q) {
+      const int64_t s = q >> 6, lane = q & 63, r = perm[q];
       for (int64_t k = M.ptr[r]; k < M.ptr[r + 1]; ++k) {
-        const int64_t q = soff[s] + 64 * (k - M.ptr[r]) + lane;
-        cols[q] = M.col[k];
-        vals[q] = M.val[k];
+        const int64_t o = soff[s] + 64 * (k - M.ptr[r]) + lane;
+        cols[o] = M.col[k];
+        vals[o] = M.val[k];
       }
     }
   }
+  if (stored) *stored = (int64_t)cols.size();
   int64_t* so;
   int* co;
   if (int e = amg_upload(c, soff, &so)) return e;
@@ -316,6 +320,12 @@ int upload_mat(Ctx* c, const Csr& M, Sell& out, bool csr, bool fp32) {
     double* va;
     if (int e = amg_upload(c, vals, &va)) return e;
     out.vals = va;
+  }
+  out.perm = nullptr;
+  if (!csr && sort_window > 0) {
+    int* pd;
+    if (int e = amg_upload(c, perm, &pd)) return e;
+    out.perm = pd;
   }
   out.nrow = M.n;
   out.ncol = M.m;
@@ -391,14 +401,14 @@ int amg_setup(Ctx* c) {
     c->amg.emplace_back();
     AmgLevel& L = c->amg.back();
     L.n = na;
-    // P and R: SELL-64 with float32 values (one row per lane in CSR left the
-    // wave's loads uncoalesced: measured slower, 475 vs 411 us per V-cycle)
-    if (int e = upload_mat(c, P, L.P, false, true)) return e;
-    if (int e = upload_mat(c, R, L.R, false, true)) return e;
-    if (int e = upload_mat(c, Ac, L.A, false, false)) return e;
-    L.p_nnz = sell_size(P);
-    L.r_nnz = sell_size(R);
-    L.a_nnz = sell_size(Ac);
+    // P and R: SELL-64 with float32 values; R's rows (one per aggregate, their
+    // lengths vary with the aggregate) sorted by length inside windows of
+    // kAmgSortWindow rows, P's kept in order (its outputs are the fine vectors:
+    // a sorted P would scatter three fine streams).  One row per lane in CSR
+    // left the wave's loads uncoalesced (measured slower, 475 vs 411 us per V-cycle)
+    if (int e = upload_mat(c, P, L.P, false, true, 0, &L.p_nnz)) return e;
+    if (int e = upload_mat(c, R, L.R, false, true, kAmgSortWindow, &L.r_nnz)) return e;
+    if (int e = upload_mat(c, Ac, L.A, false, false, 0, &L.a_nnz)) return e;
     const std::vector<double> dc = diag_inv(Ac);
     for (double v : dc)
       if (!(v > 0.0) || !std::isfinite(v)) return c->fail(TV_ERR_ARG, "AMG: coarse operator not positive definite");

@@ -77,8 +77,11 @@ __global__ __launch_bounds__(kBlock) void k_amg_rows(Sell M, const PcgState* __r
   constexpr int WPB = kBlock / 64;
   const int blk = xcd_remap(blockIdx.x, gridDim.x);
   double zz = 0.0, zb = 0.0;
-  auto row = [&](int64_t r) {
-    const double acc = row_sum<V>(M, r, (MODE == AMG_POST) ? x2 : x, (MODE == AMG_RESTRICT) ? x2 : nullptr);
+  // q: the row's position in the stored layout; r: the row (perm: SELL rows
+  // sorted by length inside windows, so a slice's rows have similar lengths)
+  auto row = [&](int64_t q) {
+    const double acc = row_sum<V>(M, q, (MODE == AMG_POST) ? x2 : x, (MODE == AMG_RESTRICT) ? x2 : nullptr);
+    const int64_t r = M.perm ? (int64_t)M.perm[q] : q;
     if (MODE == AMG_APPLY) {
       y[r] = acc;
     } else if (MODE == AMG_RESTRICT) {

@@ -183,6 +183,7 @@ struct Sell {
   const int64_t* soff = nullptr;
   const int* cols = nullptr;
   const void* vals = nullptr;
+  const int* perm = nullptr;  // SELL: stored position -> row (nullptr: identity)
   int csr = 0, fp32 = 0;
 };
 int amg_num_blocks(const Sell& M);  // partial records of launch_amg_prolong0
