@@ -157,6 +157,17 @@ def test_partitioned_gmg_matches_single_partition(world, rep):
 
 
 @pytest.mark.gpu
+def test_partitioned_output_series():
+    """The writers on a slab-partitioned box, one directory per part holding
+    its owned planes: the written T and sigma equal the gathered state."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _partition_check(2, 29748, ("--steps", "2", "--output"))
+    assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
 def test_auto_krylov_form_agrees_across_ranks():
     """pcg_variant AUTO must pick the same Krylov form on every rank (the two
     forms issue different collectives).  A 400 x 292 x 50 plate on 2 ranks gives

@@ -132,6 +132,20 @@ def test_partitioned_unstructured_matches_single_partition(world):
 
 
 @pytest.mark.gpu
+def test_partitioned_unstructured_output():
+    """The writers on a partitioned unstructured mesh (ThermoViscoProblem.py:
+    246-276, one directory per part): each part writes its own cells over its
+    local vertices, and the written T and sigma -- ghost vertices included,
+    whose visco state evolves on the part itself -- equal the gathered
+    owners' values exactly."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _partition_check(2, 29817, ("--cells", "10,30,5", "--steps", "2", "--output"))
+    assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
 def test_partitioned_unstructured_host_edit():
     """A host edit of T on the owning rank only, then the collective ghost
     refresh at the start of the step (as the box partition does)."""

@@ -30,10 +30,11 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
 
-def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0):
+def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0,
+        outdir=None):
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
-                           verbose=False, pcg_variant=pcg, write_output=False, preconditioner=pc,
-                           mg_replicate_nodes=mg_rep)
+                           verbose=False, pcg_variant=pcg, write_output=outdir is not None,
+                           output_dir=outdir or "output", preconditioner=pc, mg_replicate_nodes=mg_rep)
     if comm is not None:
         comm(p)
     p.setup()
@@ -53,6 +54,13 @@ def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False,
     if up is not None:  # unstructured partition: owned vertices -> global ids
         out["l2g"] = up["l2g"][:up["n_owned"]]
     p.close()
+    if outdir is not None:  # the last step of the written T and sigma series (this part's directory)
+        from tvfem.xdmf import read_series
+        d = os.path.join(outdir, f"part{part}") if n_parts > 1 else outdir
+        out["outT"] = np.asarray(read_series(os.path.join(d, "T.xdmf"))["values"][-1]).ravel()
+        out["outS"] = np.asarray(read_series(os.path.join(d, "sigma.xdmf"))["values"][-1]).ravel()
+        if up is not None:
+            out["l2g_local"] = up["l2g"]
     return out, its
 
 
@@ -66,6 +74,8 @@ def main():
     ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi")
     ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
                     help="distorted: the box as a general hexahedral mesh (tv_um.hip), RCB cell partition + ghost layer")
+    ap.add_argument("--output", action="store_true",
+                    help="write the five series (per-part directories) and check them against the gathered state")
     ap.add_argument("--mg-replicate", type=int, default=0,
                     help="GMG: coarse levels of at most this many nodes replicated (0: the library default)")
     a = ap.parse_args()
@@ -76,14 +86,18 @@ def main():
     nc = [int(v) for v in a.cells.split(",")]
     mesh = (distorted_box_mesh if a.mesh == "distorted" else box_mesh)([2.0, 6.0, 1.0], nc)
     steps = a.steps
+    outdir = None
+    if a.output:
+        import tempfile
+        outdir = tempfile.mkdtemp(prefix=f"pcheck{rank}_")
     if a.comm == "rccl":
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
-                       pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate)
+                       pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir)
     else:
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
-                       edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate)
+                       edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
@@ -99,6 +113,15 @@ def main():
                 full = np.concatenate([np.asarray(g[k]) for g in gathered])
             e = np.linalg.norm(full - ref[k]) / np.linalg.norm(ref[k])
             res[k] = float(e)
+            if a.output and k in ("T", "sigma"):  # every part's written series vs the gathered state
+                key = "outT" if k == "T" else "outS"
+                if "l2g_local" in gathered[0]:  # unstructured: the part's local vertices, ghosts included
+                    fr = full.reshape(mesh.num_vertices, -1)
+                    errs = [np.abs(np.asarray(g[key]) - fr[np.asarray(g["l2g_local"], dtype=np.int64)].ravel()).max()
+                            for g in gathered]
+                else:  # box: the owned planes, in partition order
+                    errs = [np.abs(np.concatenate([np.asarray(g[key]) for g in gathered]) - full).max()]
+                res["output_" + k] = float(max(errs) / np.abs(full).max())
         print("PARTITION_CHECK " + json.dumps(res), flush=True)
     dist.barrier()
 
