@@ -12,6 +12,14 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 step() { echo "[gpu_round3] $*"; }
 line() { python3 -c "import json;d=json.load(open('$1'));print('$2', round(d['ms_per_step'],3), 'ms/step', d['config'].get('newton_its_per_step'), d['config']['krylov_its_per_step'], 'its', {k:round(v['ms']*1e3,1) for k,v in d['kernels'].items()}, 'frac', round(d['roofline']['frac'],3))"; }
+if [ $PART = T ]; then  # the GPU suite only
+  step tests
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -s -rs --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
+  rc=$?; tail -3 $OUT/tests.log
+  grep -h "^\[parity\]\|^\[c3\|^\[fullsize\]\|^\[amg\]\|upartition\]" $OUT/tests.log > $OUT/parity_lines.txt
+  grep -E "FAILED|ERROR" $OUT/tests.log | head -20
+  exit $rc
+fi
 if [ $PART = A ]; then
   step tests
   timeout -k 10 900 python -u -m pytest tests -m gpu -v -s -rs --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
