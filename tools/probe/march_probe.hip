@@ -253,6 +253,80 @@ __global__ __launch_bounds__(R * W) void kD(Grid g, const double* __restrict__ i
   }
 }
 
+// ---------------- G: S planes per barrier, prefetch PF steps ahead ----------
+template <int R, int S, int PF>
+__global__ __launch_bounds__(R * W) void kG(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                            int nseg, int qchunk) {
+  __shared__ double lds[2][S][R + 2][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int nch = (g.nQ + qchunk - 1) / qchunk;
+  const int b = remap(blockIdx.x, gridDim.x, true);
+  const int chunk = b % nch, t0 = b / nch, seg = t0 % nseg, rb = t0 / nseg;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool writer = col_ok && lane >= 1 && lane <= SEG && r < g.nR;
+  const bool halo = wave == 0 || wave == R - 1;
+  const int hrow = wave == 0 ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
+  const int hslot = wave == 0 ? 0 : R + 1;
+  const double da = 0.1;
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ; };
+  auto fetch = [&](int rr, int L) {
+    const long idx = okf(rr, L) ? (long)i + g.sR * rr + g.sQ * L : 0;
+    return in[idx];
+  };
+  double rv[PF + 1][S], rh[PF + 1][S];
+  auto ld = [&](int t, double (&v)[S], double (&h)[S]) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int L = q0 - 1 + t * S + s;
+      v[s] = fetch(r, L);
+      h[s] = halo ? fetch(hrow, L) : 0.0;
+    }
+  };
+  const int nsteps = (q1 - q0 + 2 + S - 1) / S;
+#pragma unroll
+  for (int u = 0; u < PF; ++u) ld(u, rv[u], rh[u]);
+  double us_m = 0, us_c = 0, vs_m = 0, vs_c = 0;
+  auto step = [&](int t, const double (&v)[S], const double (&h)[S]) {
+    const int buf = t & 1;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int L = q0 - 1 + t * S + s;
+      lds[buf][s][wave + 1][lane] = okf(r, L) ? v[s] : 0.0;
+      if (halo) lds[buf][s][hslot][lane] = okf(hrow, L) ? h[s] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int L = q0 - 1 + t * S + s;
+      const double x0 = lds[buf][s][wave][lane], x1 = lds[buf][s][wave + 1][lane], x2 = lds[buf][s][wave + 2][lane];
+      const double us_p = cM[0] * x0 + cM[1] * x1 + cM[2] * x2;
+      const double vs_p = cK[0] * x0 + cK[1] * x1 + cK[2] * x2;
+      if (L >= q0 + 1 && L <= q1) {
+        const double S1 = cM[0] * (us_m + da * vs_m) + cM[1] * (us_c + da * vs_c) + cM[2] * (us_p + da * vs_p) +
+                          da * (cK[0] * us_m + cK[1] * us_c + cK[2] * us_p);
+        const double S2 = da * (cM[0] * us_m + cM[1] * us_c + cM[2] * us_p);
+        const double y = cM[0] * shr1(S1) + cM[1] * S1 + cM[2] * shl1(S1) + cK[0] * shr1(S2) + cK[1] * S2 +
+                         cK[2] * shl1(S2);
+        if (writer) out[(long)i + g.sR * r + g.sQ * (L - 1)] = y;
+      }
+      us_m = us_c; us_c = us_p; vs_m = vs_c; vs_c = vs_p;
+    }
+  };
+  for (int t = 0; t < nsteps; t += PF + 1) {
+#pragma unroll
+    for (int u = 0; u <= PF; ++u) {
+      const int sf = (u + PF) % (PF + 1);
+      ld(t + u + PF, rv[sf], rh[sf]);
+      step(t + u, rv[u], rh[u]);
+    }
+  }
+}
+
 // ---------------- B: register march, waves independent ----------------------
 // WPB waves per block, consecutive rows; each wave loads rows r-1, r, r+1.
 template <int WPB, bool XCD>
@@ -408,6 +482,23 @@ int main(int argc, char** argv) {
     RUN_B(8, true)
     RUN_B(2, true)
   }
+  for (int minblk : {512, 1024}) {  // G: S planes per barrier step, prefetch PF steps
+#define RUN_G(SS, PP)                                                                                      \
+  {                                                                                                        \
+    const int nrb = (g.nR + 7) / 8;                                                                        \
+    const int nch = chunks_for(nseg * nrb, g.nQ, minblk);                                                  \
+    const int qc = (g.nQ + nch - 1) / nch;                                                                 \
+    const int nb = nseg * nrb * ((g.nQ + qc - 1) / qc);                                                    \
+    char nm[96];                                                                                           \
+    snprintf(nm, sizeof nm, "G R=8 S=%d PF=%d minblk=%d", SS, PP, minblk);                                \
+    rep(nm, timeit([&] { kG<8, SS, PP><<<nb, 8 * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nb);           \
+  }
+    RUN_G(1, 2)
+    RUN_G(1, 4)
+    RUN_G(2, 1)
+    RUN_G(2, 2)
+    RUN_G(4, 1)
+  }
   for (int minblk : {512, 768, 1024}) {  // D: 2 rows per wave, R = 8 / 4 waves (16 / 8-row tiles)
 #define RUN_D(RR)                                                                                          \
   {                                                                                                        \
@@ -457,6 +548,12 @@ int main(int argc, char** argv) {
     md = 0;
     for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
     printf("max |A-D| = %g\n", md);
+    CK(hipMemset(y, 0, N * 8));
+    kG<8, 2, 2><<<nseg * nrb8, 8 * W>>>(g, x, y, nseg, g.nQ);
+    CK(hipMemcpy(yb.data(), y, N * 8, hipMemcpyDeviceToHost));
+    md = 0;
+    for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
+    printf("max |A-G| = %g\n", md);
   }
   return 0;
 }
