@@ -163,7 +163,7 @@ def test_partitioned_output_series():
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    res = _partition_check(2, 29748, ("--steps", "2", "--output"))
+    res = _partition_check(2, "host", 29748, ("--steps", "2", "--output"))
     assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
 
 
