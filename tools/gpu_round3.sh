@@ -20,6 +20,17 @@ if [ $PART = T ]; then  # the GPU suite only
   grep -E "FAILED|ERROR" $OUT/tests.log | head -20
   exit $rc
 fi
+if [ $PART = P ]; then  # march probe, a focused test, the C3 GMG line
+  timeout -k 10 180 tools/probe/build/march_probe f > $OUT/probe_f.txt 2>&1 || { tail -5 $OUT/probe_f.txt; exit 1; }
+  grep -E "copy|G R=8|A R=8 store=1 xcd=1|max" $OUT/probe_f.txt
+  timeout -k 10 300 python -u -m pytest tests/test_partition.py -m gpu -k output -v -s --timeout 200 --timeout-method thread > $OUT/ftest.log 2>&1; tail -2 $OUT/ftest.log
+  for spec in "C3g 200,200,25 --pc gmg" "C3 200,200,25"; do
+    set -- $spec; tag=$1; cells=$2; shift 2
+    timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --cells $cells "$@" > $OUT/bench_$tag.json 2> $OUT/bench_$tag.err || { tail -5 $OUT/bench_$tag.err; exit 1; }
+    line $OUT/bench_$tag.json $tag
+  done
+  exit 0
+fi
 if [ $PART = A ]; then
   step tests
   timeout -k 10 900 python -u -m pytest tests -m gpu -v -s -rs --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
