@@ -28,6 +28,10 @@
 #include <cstdlib>
 
 #include "tv_device.h"
+
+#ifndef TV_MARCH_ORDER
+#define TV_MARCH_ORDER 0  // tile order of k_cg_march (A/B builds only; 0 = production)
+#endif
 #include <cstdio>
 #include <vector>
 
@@ -742,10 +746,23 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   // (first / last chunk, first / last segment) spread evenly over the XCDs
   const int nch = (nQ + qchunk - 1) / qchunk;
   const int b = xcd_remap(bid, nmarch);
+#if TV_MARCH_ORDER == 1  // A/B build only: segment fastest, then chunk
+  const int seg = b % nseg;
+  const int t = b / nseg;
+  const int chunk = t % nch;
+  const int rb = t / nch;
+#elif TV_MARCH_ORDER == 2  // A/B build only: segment fastest, then row block
+  const int seg = b % nseg;
+  const int t = b / nseg;
+  const int nrbk = (nR + R - 1) / R;
+  const int rb = t % nrbk;
+  const int chunk = t / nrbk;
+#else
   const int chunk = b % nch;
   const int t = b / nch;
   const int seg = t % nseg;
   const int rb = t / nseg;
+#endif
   const int r0 = rb * R;
   const int r = r0 + wave;
   const bool row_ok = r < nR;
