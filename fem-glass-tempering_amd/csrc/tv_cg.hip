@@ -1596,7 +1596,10 @@ int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 
 // march chunking: split the march axis until the grid has kMarchMinBlocks
 // tiles (256 CUs x 4), down to kMarchMinQ planes per chunk; tiny grids further
-constexpr int kMarchMinBlocks = 1024;
+#ifndef TV_EXP_MINBLK
+#define TV_EXP_MINBLK 1024
+#endif
+constexpr int kMarchMinBlocks = TV_EXP_MINBLK;
 constexpr int kMarchMinQ = 6;
 constexpr int kMarchSmallTiles = 256;  // one marching tile per CU
 

@@ -31,12 +31,15 @@ if [ $PART = P ]; then  # march probe, a focused test, the C3 GMG line
   done
   exit 0
 fi
-if [ $PART = X ]; then  # A/B of library builds (TVFEM_LIB), interleaved, C4 bench lines
+if [ $PART = X ]; then  # A/B of library builds (TVFEM_LIB), interleaved: "lib-suffix config" pairs in $XPAIRS
   for rep in 1 2; do
-    for v in "" _exp1 _exp2; do
+    for pair in $XPAIRS; do
+      v=${pair%%:*}; cfg=${pair##*:}; [ "$v" = base ] && v=""
+      case $cfg in C4) args="";; C5) args="--family DG --cells 200,200,25";; C3) args="--cells 200,200,25 --pc gmg";; esac
       [ -f fem-glass-tempering_amd/tvfem/libtvfem$v.so ] || continue
-      TVFEM_LIB=$PWD/fem-glass-tempering_amd/tvfem/libtvfem$v.so timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_x$v.$rep.json 2> $OUT/bench_x$v.$rep.err || { tail -5 $OUT/bench_x$v.$rep.err; exit 1; }
-      python3 -c "import json;d=json.load(open('$OUT/bench_x$v.$rep.json'));r=d['roofline'];print('lib$v', round(d['ms_per_step'],3), {k:round(v['ms']*1e3,1) for k,v in d['kernels'].items()}, 'flushed', round(r['hbm_flushed']['ms_per_launch']*1e3,1))"
+      o=$OUT/bench_x$v.$cfg.$rep
+      TVFEM_LIB=$PWD/fem-glass-tempering_amd/tvfem/libtvfem$v.so timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline $args > $o.json 2> $o.err || { tail -5 $o.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$o.json'));r=d['roofline'];print('lib$v $cfg', round(d['ms_per_step'],3), {k:round(v['ms']*1e3,1) for k,v in d['kernels'].items()}, 'flushed', round(r['hbm_flushed']['ms_per_launch']*1e3,1))"
     done
   done
   exit 0
