@@ -21,10 +21,6 @@
 
 #include "tv_device.h"
 
-#ifndef TV_EXP_DGORDER
-#define TV_EXP_DGORDER 0
-#endif
-
 namespace tv {
 namespace {
 
@@ -491,18 +487,11 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
   // chunk fastest: the chunks of one column of tiles share their boundary
   // planes and land on one XCD (contiguous range after the remap)
   const int b = xcd_remap((int)blockIdx.x, (int)gridDim.x);
-#if TV_EXP_DGORDER == 1
-  const int seg = b % nseg;
-  const int t = b / nseg;
-  const int nrbk = (int)((gridDim.x / nch) / nseg);
-  const int rb = t % nrbk;
-  const int chunk = t / nrbk;
-#else
+  // (segment fastest, as the CG march: the same at C5, measured)
   const int chunk = b % nch;
   const int t = b / nch;
   const int seg = t % nseg;
   const int rb = t / nseg;
-#endif
   const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, npl);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
   const int r = HL ? rb * R + wave : rb * R - 1 + wave;  // row along ra (!HL: waves 0 and R + 1 are halo rows)
