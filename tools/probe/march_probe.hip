@@ -327,6 +327,83 @@ __global__ __launch_bounds__(R * W) void kG(Grid g, const double* __restrict__ i
   }
 }
 
+// ---------------- H: NS x-segments per wave (longer contiguous row runs) -----
+// as A (R waves = R rows, LDS slab, PF 2), each wave covering NS consecutive
+// 62-output segments of its row per plane: NS loads of 512 B per row per plane
+template <int R, int NS>
+__global__ __launch_bounds__(R * W) void kH(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                            int nsegw, int qchunk) {
+  __shared__ double lds[2][R + 2][NS][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int b = remap(blockIdx.x, gridDim.x, true);
+  const int sw = b % nsegw, t = b / nsegw, rb = t % nrb, chunk = t / nrb;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const bool halo = wave == 0 || wave == R - 1;
+  const int hrow = wave == 0 ? r0 - 1 : (wave == R - 1 ? r0 + R : r);
+  const int hslot = wave == 0 ? 0 : R + 1;
+  const double da = 0.1;
+  int ii[NS];
+  bool cok[NS], wr[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    ii[k] = (sw * NS + k) * SEG - 1 + lane;
+    cok[k] = ii[k] >= 0 && ii[k] < g.n0;
+    wr[k] = cok[k] && lane >= 1 && lane <= SEG && r < g.nR;
+  }
+  auto okf = [&](int k, int rr, int L) { return cok[k] && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ; };
+  auto fetch = [&](int k, int rr, int L) {
+    const long idx = okf(k, rr, L) ? (long)ii[k] + g.sR * rr + g.sQ * L : 0;
+    return in[idx];
+  };
+  double a[NS], ah[NS], bb[NS], bh[NS], c[NS], ch[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    a[k] = fetch(k, r, q0 - 1); ah[k] = halo ? fetch(k, hrow, q0 - 1) : 0.0;
+    bb[k] = fetch(k, r, q0); bh[k] = halo ? fetch(k, hrow, q0) : 0.0;
+  }
+  double us_m[NS], us_c[NS], vs_m[NS], vs_c[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) us_m[k] = us_c[k] = vs_m[k] = vs_c[k] = 0.0;
+  auto step = [&](int L, const double (&v)[NS], const double (&hv)[NS]) {
+    const int buf = L & 1;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      lds[buf][wave + 1][k][lane] = okf(k, r, L) ? v[k] : 0.0;
+      if (halo) lds[buf][hslot][k][lane] = okf(k, hrow, L) ? hv[k] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const double x0 = lds[buf][wave][k][lane], x1 = lds[buf][wave + 1][k][lane], x2 = lds[buf][wave + 2][k][lane];
+      const double us_p = cM[0] * x0 + cM[1] * x1 + cM[2] * x2;
+      const double vs_p = cK[0] * x0 + cK[1] * x1 + cK[2] * x2;
+      if (L >= q0 + 1 && L <= q1) {
+        const double S1 = cM[0] * (us_m[k] + da * vs_m[k]) + cM[1] * (us_c[k] + da * vs_c[k]) +
+                          cM[2] * (us_p + da * vs_p) + da * (cK[0] * us_m[k] + cK[1] * us_c[k] + cK[2] * us_p);
+        const double S2 = da * (cM[0] * us_m[k] + cM[1] * us_c[k] + cM[2] * us_p);
+        const double y = cM[0] * shr1(S1) + cM[1] * S1 + cM[2] * shl1(S1) + cK[0] * shr1(S2) + cK[1] * S2 +
+                         cK[2] * shl1(S2);
+        if (wr[k]) out[(long)ii[k] + g.sR * r + g.sQ * (L - 1)] = y;
+      }
+      us_m[k] = us_c[k]; us_c[k] = us_p; vs_m[k] = vs_c[k]; vs_c[k] = vs_p;
+    }
+  };
+  for (int L = q0 - 1; L <= q1; L += 3) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) { c[k] = fetch(k, r, L + 2); ch[k] = halo ? fetch(k, hrow, L + 2) : 0.0; }
+    step(L, a, ah);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) { a[k] = fetch(k, r, L + 3); ah[k] = halo ? fetch(k, hrow, L + 3) : 0.0; }
+    step(L + 1, bb, bh);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) { bb[k] = fetch(k, r, L + 4); bh[k] = halo ? fetch(k, hrow, L + 4) : 0.0; }
+    step(L + 2, c, ch);
+  }
+}
+
 // ---------------- B: register march, waves independent ----------------------
 // WPB waves per block, consecutive rows; each wave loads rows r-1, r, r+1.
 template <int WPB, bool XCD>
@@ -482,6 +559,23 @@ int main(int argc, char** argv) {
     RUN_B(8, true)
     RUN_B(2, true)
   }
+  for (int minblk : {256, 512, 1024}) {  // H: NS x-segments per wave, segment-group fastest
+#define RUN_H(NSS)                                                                                         \
+  {                                                                                                        \
+    const int nrb = (g.nR + 7) / 8;                                                                        \
+    const int nsw = (nseg + NSS - 1) / NSS;                                                                \
+    const int nch = chunks_for(nsw * nrb, g.nQ, minblk);                                                   \
+    const int qc = (g.nQ + nch - 1) / nch;                                                                 \
+    const int nb = nsw * nrb * ((g.nQ + qc - 1) / qc);                                                     \
+    char nm[96];                                                                                           \
+    snprintf(nm, sizeof nm, "H R=8 NS=%d minblk=%d", NSS, minblk);                                        \
+    rep(nm, timeit([&] { kH<8, NSS><<<nb, 8 * W>>>(g, x, y, nsw, qc); }, reps, e0, e1), nb);               \
+  }
+    RUN_H(1)
+    RUN_H(2)
+    RUN_H(4)
+    RUN_H(7)
+  }
   for (int minblk : {512, 1024}) {  // G: S planes per barrier step, prefetch PF steps
 #define RUN_G(SS, PP)                                                                                      \
   {                                                                                                        \
@@ -554,6 +648,12 @@ int main(int argc, char** argv) {
     md = 0;
     for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
     printf("max |A-G| = %g\n", md);
+    CK(hipMemset(y, 0, N * 8));
+    kH<8, 4><<<((nseg + 3) / 4) * nrb8, 8 * W>>>(g, x, y, (nseg + 3) / 4, g.nQ);
+    CK(hipMemcpy(yb.data(), y, N * 8, hipMemcpyDeviceToHost));
+    md = 0;
+    for (long k = 0; k < N; ++k) md = fmax(md, fabs(ya[k] - yb[k]));
+    printf("max |A-H| = %g\n", md);
   }
   return 0;
 }
