@@ -1597,10 +1597,7 @@ int dim_of(const CgGrid& g) { return g.deg2 ? 1 : (g.deg1 ? 2 : 3); }
 // march chunking: split the march axis until the grid has kMarchMinBlocks
 // tiles (256 CUs x 4), down to kMarchMinQ planes per chunk; tiny grids further
 constexpr int kMarchMinBlocks = 1024;  // 512: the same at C4, 2048: 7 % slower (measured)
-#ifndef TV_EXP_MINQ
-#define TV_EXP_MINQ 6
-#endif
-constexpr int kMarchMinQ = TV_EXP_MINQ;
+constexpr int kMarchMinQ = 6;  // 3 / 4: the same at C4, 1-3 % slower at C3 (measured)
 constexpr int kMarchSmallTiles = 256;  // one marching tile per CU
 
 struct Launch {
