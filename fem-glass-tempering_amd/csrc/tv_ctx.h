@@ -191,6 +191,12 @@ struct Ctx {
   int last_newton = 0, last_krylov = 0;
   double last_dx = 0.0;
   int pcg_hint = 0;
+  // multigrid solves: the Krylov count of the Newton iteration with the same
+  // index in the previous time step (the solves of a step take a repeating
+  // pattern of counts, e.g. 6 5 5 4: the previous solve's count over-queues
+  // early-exit iterations, ~25 launches each), and the index of the current one
+  int mg_hint[16] = {0};
+  int newton_k = 0;
 
   int fail(int code, const std::string& m) {
     err = m;

@@ -422,7 +422,8 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipEventRecord(c->evp[0], c->stream));
     return TV_OK;
   };
-  if (int e = enqueue(std::max(1, c->pcg_hint))) return e;
+  const int hk = std::min(c->newton_k, 15);  // every rank polls the same all-reduced state: same decisions
+  if (int e = enqueue(std::max(1, c->mg_hint[hk] > 0 ? c->mg_hint[hk] : c->pcg_hint))) return e;
   for (;;) {
     HIPC(hipEventSynchronize(c->evp[0]));
     if (c->h_st[0].done) break;
@@ -433,6 +434,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
   *reason = c->h_st[0].reason;
   launch_mg_dx_finish(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
   c->pcg_hint = std::max(1, c->h_st[0].it);
+  c->mg_hint[hk] = c->pcg_hint;
   if (c->ktime) {
     for (int it = 0; it < *its; it += c->kstride)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);

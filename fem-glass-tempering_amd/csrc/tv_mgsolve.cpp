@@ -451,7 +451,8 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipEventRecord(c->evp[0], c->stream));
     return TV_OK;
   };
-  if (int e = enqueue(std::max(1, c->pcg_hint))) return e;
+  const int hk = std::min(c->newton_k, 15);
+  if (int e = enqueue(std::max(1, c->mg_hint[hk] > 0 ? c->mg_hint[hk] : c->pcg_hint))) return e;
   for (;;) {
     HIPC(hipEventSynchronize(c->evp[0]));
     if (c->h_st[0].done) break;
@@ -464,6 +465,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   // k_dg_bupdate DXU): solves of 0 / 1 iterations and the last step of an odd-length one
   launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
   c->pcg_hint = std::max(1, c->h_st[0].it);
+  c->mg_hint[hk] = c->pcg_hint;
   if (c->ktime) {
     for (int it = 0; it < *its; it += c->kstride)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);

@@ -353,6 +353,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;
     int k = 0, reason = 0;
+    c->newton_k = its;  // the multigrid solves queue the count this Newton index took last step
     if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason) : pcg_solve_mg(c, T, &k, &reason))
                           : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
       return e;
