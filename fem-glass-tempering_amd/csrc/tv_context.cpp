@@ -935,6 +935,8 @@ int tv_field_device_ptr(void* ctx, int field, void** dev_ptr, int64_t* comp_stri
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || field < 0 || field >= TV_NUM_FIELDS) return TV_ERR_ARG;
   if (!c->f[field].ptr) return c->fail(TV_ERR_STATE, "field not materialized");
+  hipSetDevice(c->device);
+  HIPC(hipStreamSynchronize(c->stream));  // the queued steps are complete when the consumer reads
   if (dev_ptr) *dev_ptr = c->f[field].ptr;
   if (comp_stride) *comp_stride = c->f[field].space == 0 ? c->nT : c->nS;
   return TV_OK;

@@ -185,6 +185,7 @@ struct Ctx {
   std::vector<int> ts_pending;       // slots of productive iterations not yet read back
   double ts_khz = 0.0;               // REALTIME clock (hipDeviceAttributeWallClockRate)
   hipEvent_t vev[2] = {nullptr, nullptr};
+  bool vev_pending = false;          // the last step's visco events not yet read
   double ksum[3] = {0.0, 0.0, 0.0};  // ms: fused matvec, PCG update, visco update
   int64_t kcnt[3] = {0, 0, 0};
   // stats
@@ -243,7 +244,8 @@ bool multi_rank(const Ctx* c);
 int halo(Ctx* c, double* v);  // ghost planes of a T-space vector of the fine grid
 int halo_grid(Ctx* c, const CgGrid& g, double* v);  // ghost planes of a vector of grid g (a GMG level)
 int allreduce_vec(Ctx* c, double* v, int64_t n);
-int allreduce_halo(Ctx* c, double* sums, int n, double* v);  // one RCCL group: n-scalar sum + halo(v)  // sum over the ranks of a device vector, in place
+int allreduce_halo(Ctx* c, double* sums, int n, double* v);
+int visco_timing_flush(Ctx* c);  // tv_solver.cpp  // one RCCL group: n-scalar sum + halo(v)  // sum over the ranks of a device vector, in place
 int allreduce(Ctx* c, double* v, int n);
 int reduce_logic(Ctx* c, int n, int W, int kind, int check_done);  // records -> (all-reduce) -> scalar logic
 int cgs_raxis(const Ctx* c);

@@ -232,6 +232,7 @@ int tv_kernel_timing(void* ctx, int on) {
   c->ts_pending.clear();
   c->ts_next = kTsCap;  // zeroes the stamps
   if (int e = ts_flush(c)) return e;
+  if (int e = visco_timing_flush(c)) return e;  // a pending visco pair belongs to the old window
   c->ktime = on > 0;
   c->kstride = on > 1 ? on : 1;
   for (int k = 0; k < 3; ++k) {
@@ -249,6 +250,7 @@ int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches) {
   if (k < 0) return c->fail(TV_ERR_ARG, "tv_kernel_stats: kernel 3 (fused matvec), 4 (PCG update) or 1 (visco)");
   hipSetDevice(c->device);
   if (int e = ts_flush(c)) return e;
+  if (int e = visco_timing_flush(c)) return e;
   *ms_avg = c->kcnt[k] ? c->ksum[k] / (double)c->kcnt[k] : 0.0;
   if (launches) *launches = c->kcnt[k];
   return TV_OK;

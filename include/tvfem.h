@@ -287,7 +287,9 @@ int tv_dof_coordinates(void* ctx, int space, double* xyz, size_t n_dofs);
 /* host <-> device field transfer, owned dofs, interleaved reference layout */
 int tv_set_field(void* ctx, int field, const double* host, size_t n_values);
 int tv_get_field(void* ctx, int field, double* host, size_t n_values);
-/* device address of a field's storage (component-major: comp*stride + dof) */
+/* device address of a field's storage (component-major: comp*stride + dof);
+ * waits for the context's queued work first (tv_step returns with the visco
+ * update possibly still running on the context's stream) */
 int tv_field_device_ptr(void* ctx, int field, void** dev_ptr, int64_t* comp_stride);
 
 int tv_set_initial_condition(void* ctx, double T0);
@@ -318,6 +320,10 @@ int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev);
 /* ---- solvers -------------------------------------------------------------- */
 int tv_solve_T(void* ctx, int* newton_its, int* krylov_its, int* converged);
 int tv_visco_update(void* ctx);
+/* one time step (solve_timestep minus I/O); returns once the Newton solve has
+ * converged, with the visco update still queued on the context's stream:
+ * tv_get_field / tv_set_field / the operator calls / tv_field_device_ptr order
+ * themselves behind it, tv_sync waits for it */
 int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its);
 
 /* ---- time-series output -------------------------------------------------------
