@@ -198,6 +198,7 @@ struct Ctx {
   // early-exit iterations, ~25 launches each), and the index of the current one
   int mg_hint[16] = {0};
   int newton_k = 0;
+  int newton_pred = 0;  // the previous step's Newton count (speculative residual, newton())
 
   int fail(int code, const std::string& m) {
     err = m;
