@@ -61,8 +61,6 @@ def parse():
                          "one GPU), jacobi, or auto (gmg where it applies and the mesh has >= 4M T-dofs, at "
                          "every rank count; amg for --mesh distorted on one GPU)")
     ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
-    ap.add_argument("--mg-fused-nodes", type=int, default=0,
-                    help="GMG: coarse levels up to this size in one persistent launch (0: automatic, -1: off)")
     ap.add_argument("--share", type=int, default=0, metavar="N",
                     help="time ONE rank's share of an N-way partition of the mesh on this GPU with the "
                          "communication stubbed (halos and all-reduces are no-ops) and the iteration counts "
@@ -131,7 +129,7 @@ def main():
         kw = {"n_parts": a.share, "part": a.share // 2, "part_axis": 1, "newton_fixed_its": nn,
               "ksp_fixed_its": kk}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
-                              verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels, mg_fused_nodes=a.mg_fused_nodes,
+                              verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,
                               write_output=a.output is not None, output_dir=a.output or "output", **kw)
     single = prob.pcg_variant == "single"
     lib, ctx = prob._lib, prob._ctx

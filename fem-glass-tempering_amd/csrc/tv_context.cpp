@@ -513,7 +513,6 @@ void tv_default_options(tv_options* o) {
   o->dg_tile_chunk = 0;
   o->mg_replicate_nodes = 0;
   o->ksp_fixed_its = 0;
-  o->mg_fused_nodes = 0;
 }
 
 
@@ -830,8 +829,6 @@ int tv_destroy(void* ctx) {
   if (c->h_halo) hipHostFree(c->h_halo);
   if (c->h_big) hipHostFree(c->h_big);
   if (c->mg_mask0) hipFree(c->mg_mask0);
-  if (c->mg_bar) hipFree(c->mg_bar);
-  if (c->h_bar) hipHostFree(c->h_bar);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);

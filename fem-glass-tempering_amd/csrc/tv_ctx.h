@@ -56,7 +56,6 @@ struct MgLevel {
   double* ffbuf[2] = {nullptr, nullptr};
   std::vector<void*> bufs;   // T, b, x, w, dinv and the transfer maps
   bool dinv_interior = false;  // dinv holds the T-independent interior diagonal
-  bool w_complete = false;     // w = the complete J x (facets included: the fused launch's first level)
   // partitioned contexts (tv_mgdist.cpp): a distributed level is this rank's
   // slab of the global level with one ghost plane per interface (dist); a
   // replicated level is the whole global level on every rank.  first2 = global
@@ -126,14 +125,6 @@ struct Ctx {
   std::vector<MgLevel> mg;
   double mg_omega0 = 0.0;
   double* mgx = nullptr;    // level-0 V-cycle iterate
-  // levels mg_fused_from .. the coarsest (1-based; 0 = none) run as one
-  // persistent launch (k_mg_fused) of mg_fused_nwg workgroups; mg_bar = its
-  // grid-barrier words (arrivals, generation, timeout flag), h_bar = a pinned
-  // copy of the timeout flag read after every multigrid solve
-  int mg_fused_from = 0;
-  int mg_fused_nwg = 0;
-  unsigned* mg_bar = nullptr;
-  unsigned* h_bar = nullptr;
   double* dggface = nullptr; // DG level 0: facet means of dg(T) for the cell-block Jacobi smoother
   // partitioned GMG (tv_mgdist.cpp): levels 0 .. mg_A - 1 are distributed over
   // the partitions, mg_A .. the coarsest are replicated on every rank
@@ -287,8 +278,6 @@ int mg_level_vectors(Ctx* c, MgLevel& L);
 double mg_gershgorin(const std::vector<double> (&X)[3], double dt_alpha);
 double mg_omega(double b);
 void mg_level(Ctx* c, size_t l);
-int mg_fused_setup(Ctx* c);
-MgFused mg_fused_args(Ctx* c, int m);  // the fused launch's arguments from level m (1-based) down
 template <class T>
 int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
   void* p = nullptr;

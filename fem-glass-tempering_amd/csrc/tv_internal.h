@@ -401,34 +401,6 @@ struct MgPrep {
   int64_t off_b[kMgPrepMax + 1];
 };
 void launch_mg_prepare(const MgPrep& p, hipStream_t s);
-// The small coarse levels of one V-cycle as ONE persistent launch (tv_mg.hip
-// k_mg_fused): entry 0 is level m (b and x = omega dinv b in place, from the
-// restriction into it), entries 1 .. nl-1 the levels below it.  Phases per
-// level pair: complete J x (facets inline), restriction with the coarse
-// pre-smoothing; then upwards the prolongation (the coarse post-smoothing
-// applied on the fly) and J x -- separated by grid barriers.  On exit entry 0
-// holds x (before its post-smoothing) and the COMPLETE w = J x.
-constexpr int kMgFusedMax = 4;
-struct MgFusedLevel {
-  CgGrid g;
-  const double* T;
-  const double* dinv;
-  double* b;
-  double* x;
-  double* w;
-  double omega;
-  MgXfer xf;                  // finer entry -> this entry (entries >= 1)
-};
-struct MgFused {
-  int nl;
-  MgFusedLevel L[kMgFusedMax];
-  unsigned* bar;              // barrier words: arrivals, generation, timeout flag (zeroed once)
-  const PcgState* st;
-};
-constexpr int kMgFusedBlock = 512;
-// workgroups of the launch (all co-resident: at most one per CU is asked for)
-int mg_fused_blocks(const MgFused& f, int n_cu);
-void launch_mg_fused(const MgFused& f, int nwg, hipStream_t s);
 bool cg_uses_march(const CgGrid& g);  // the 3D marching kernels (not the x-row kernel) serve this grid
 // DG1 level 0 -> CG1 level 1 of the same box (3D; cells c0 x c1 x c2, DG dof
 // (l, cell) at l * ncell + cell, l = a + 2b + 4c over the storage axes):

@@ -555,280 +555,8 @@ int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((
 // measured 24 us at 143k coarse nodes)
 int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kBlock - 1) / kBlock); }
 
-// ---- the small coarse levels as ONE persistent launch (k_mg_fused) -------------
-// Below ~1M nodes a V-cycle level is a chain of dependent launches of 5-14 us
-// each (launch ramp, a few dependent memory round trips, drain) for < 1 us of
-// HBM traffic.  Here the levels m .. coarsest run inside one launch of at most
-// one 512-thread workgroup per CU, their phases separated by grid barriers.
-// Hand-off form (MI355X_MICROARCH.md "Workgroup dispatch ... visibility",
-// cdna_hip_programming.md Guideline 16 R1): every phase output is stored
-// WRITE-THROUGH (sc1, agent-scope relaxed atomic stores) and drained by every
-// storing wave before the workgroup barrier; one lane then arrives on the
-// arrival counter; the last arriver re-arms it and bumps the generation word;
-// the others poll the generation (relaxed agent loads, s_sleep, bounded); one
-// agent-scope acquire per workgroup after the match, then plain loads.
-
-__device__ __forceinline__ void st_wt(double* p, double v) {  // write-through (sc1) store
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// grid barrier; false (and the timeout word set) when a workgroup gave up
-// waiting -- every workgroup then still reaches the end of the launch
-__device__ bool fused_sync(unsigned* bar, unsigned nwg) {
-  __shared__ int ok;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ok = 1;
-    // the generation cannot advance before this workgroup's arrival below
-    const unsigned gen = __hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(&bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == nwg - 1) {  // last arrival: re-arm, then release the others
-      __hip_atomic_store(&bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&bar[1], gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      unsigned spins = 0;
-      while (__hip_atomic_load(&bar[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 23)) {  // ~seconds: a lost workgroup; report instead of hanging
-          __hip_atomic_store(&bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1 holds no line of the last phase
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  return ok != 0;
-}
-
-// complete J(T) x at node (i, j, k) of a level: the 27-point tensor-product
-// cell operator (per-node 1D rows, as the march) plus the Robin facet terms of
-// every boundary face the node lies on (3 x 3 Gauss per facet, as diag_value)
-__device__ __forceinline__ double fused_jx(const MgFusedLevel& L, int i, int j, int k) {
-  const CgGrid& g = L.g;
-  const int n0 = g.n0, n1 = g.n1, n2 = g.n2;
-  const int64_t pl = (int64_t)n0 * n1;
-  const int64_t n = (int64_t)i + (int64_t)n0 * j + pl * k;
-  double X[3][3][3];  // [c: k][b: j][a: i]
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const bool ok = i + a - 1 >= 0 && i + a - 1 < n0 && j + b - 1 >= 0 && j + b - 1 < n1 && k + c - 1 >= 0 &&
-                        k + c - 1 < n2;
-        X[c][b][a] = ok ? L.x[n + (a - 1) + (int64_t)n0 * (b - 1) + pl * (c - 1)] : 0.0;
-      }
-  const double* cx = g.coef[0] + (int64_t)i * C_NCOEF;
-  const double* cy = g.coef[1] + (int64_t)j * C_NCOEF;
-  const double* cz = g.coef[2] + (int64_t)k * C_NCOEF;
-  const double Mx[3] = {cx[C_MLO], cx[C_MDI], cx[C_MUP]}, Kx[3] = {cx[C_KLO], cx[C_KDI], cx[C_KUP]};
-  const double My[3] = {cy[C_MLO], cy[C_MDI], cy[C_MUP]}, Ky[3] = {cy[C_KLO], cy[C_KDI], cy[C_KUP]};
-  const double Mz[3] = {cz[C_MLO], cz[C_MDI], cz[C_MUP]}, Kz[3] = {cz[C_KLO], cz[C_KDI], cz[C_KUP]};
-  const double da = g.dt_alpha;
-  double y = 0.0;
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const double rM = (Mx[0] * X[c][b][0] + Mx[1] * X[c][b][1]) + Mx[2] * X[c][b][2];
-      const double rK = (Kx[0] * X[c][b][0] + Kx[1] * X[c][b][1]) + Kx[2] * X[c][b][2];
-      const double myz = My[b] * Mz[c];
-      y += myz * (rM + da * rK) + da * (Ky[b] * Mz[c] + My[b] * Kz[c]) * rM;
-    }
-  // Robin facets: patches over the face's two tangential axes
-  auto tpatch = [&](int64_t sa, int64_t sb, int ia, int na, int ib, int nb, double (&P)[3][3]) {
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        const bool ok = ia + u - 1 >= 0 && ia + u - 1 < na && ib + v - 1 >= 0 && ib + v - 1 < nb;
-        P[u][v] = ok ? L.T[n + (int64_t)(u - 1) * sa + (int64_t)(v - 1) * sb] : 0.0;
-      }
-  };
-  double Tp[3][3], Xp[3][3];
-  if ((i == 0 && g.bnd[0][0]) || (i == n0 - 1 && g.bnd[0][1])) {  // tangential (j, k)
-    tpatch(n0, pl, j, n1, k, n2, Tp);
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) Xp[u][v] = X[v][u][1];
-    y += facet_sum<MODE_JAC, false, false, false>(g, cy[C_HLO], cy[C_HHI], cz[C_HLO], cz[C_HHI], Tp, Xp);
-  }
-  if ((j == 0 && g.bnd[1][0]) || (j == n1 - 1 && g.bnd[1][1])) {  // tangential (i, k)
-    tpatch(1, pl, i, n0, k, n2, Tp);
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) Xp[u][v] = X[v][1][u];
-    y += facet_sum<MODE_JAC, false, false, false>(g, cx[C_HLO], cx[C_HHI], cz[C_HLO], cz[C_HHI], Tp, Xp);
-  }
-  if ((k == 0 && g.bnd[2][0]) || (k == n2 - 1 && g.bnd[2][1])) {  // tangential (i, j)
-    tpatch(1, n0, i, n0, j, n1, Tp);
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) Xp[u][v] = X[1][v][u];
-    y += facet_sum<MODE_JAC, false, false, false>(g, cx[C_HLO], cx[C_HHI], cy[C_HLO], cy[C_HHI], Tp, Xp);
-  }
-  return y;
-}
-
-// w <- J x on every node of entry e
-__device__ void fused_phase_jx(const MgFusedLevel& L) {
-  const int64_t n = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
-  const int64_t stride = (int64_t)gridDim.x * kMgFusedBlock;
-  for (int64_t t = (int64_t)blockIdx.x * kMgFusedBlock + threadIdx.x; t < n; t += stride) {
-    int i, j, k;
-    decode_node(t, L.g, i, j, k);
-    st_wt(L.w + t, fused_jx(L, i, j, k));
-  }
-}
-
-// C.b <- P^T (F.b - F.w), C.x <- omega_C dinv_C C.b (the coarse pre-smoothing from 0)
-__device__ void fused_phase_restrict(const MgFusedLevel& F, const MgFusedLevel& C) {
-  const MgXfer& x = C.xf;
-  const int cn0 = x.cn[0], cn1 = x.cn[1];
-  const int64_t n = (int64_t)cn0 * cn1 * x.cn[2];
-  const int64_t fpl = (int64_t)x.fn[0] * x.fn[1];
-  const int64_t stride = (int64_t)gridDim.x * kMgFusedBlock;
-  for (int64_t t = (int64_t)blockIdx.x * kMgFusedBlock + threadIdx.x; t < n; t += stride) {
-    int i, j, k;
-    decode_node(t, C.g, i, j, k);
-    int fi[3], fj[3], fk[3];
-    rmap(x, 0, i, fi[0], fi[1], fi[2]);
-    rmap(x, 1, j, fj[0], fj[1], fj[2]);
-    rmap(x, 2, k, fk[0], fk[1], fk[2]);
-    double acc = 0.0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      double pln = 0.0;
-#pragma unroll
-      for (int b = 0; b < 3; ++b) {
-        const int64_t base = (int64_t)fj[b] * x.fn[0] + fpl * fk[c];
-        double row = 0.0;
-#pragma unroll
-        for (int a = 0; a < 3; ++a) row += x.rw[0][3 * i + a] * (F.b[base + fi[a]] - F.w[base + fi[a]]);
-        pln += x.rw[1][3 * j + b] * row;
-      }
-      acc += x.rw[2][3 * k + c] * pln;
-    }
-    st_wt(C.b + t, acc);
-    st_wt(C.x + t, C.omega * C.dinv[t] * acc);
-  }
-}
-
-// F.x <- F.x + P xt, xt = C.x (the coarsest entry) or its post-smoothing step
-// C.x + omega_C dinv_C (C.b - C.w) formed on the fly
-__device__ void fused_phase_prolong(const MgFusedLevel& F, const MgFusedLevel& C, bool smooth) {
-  const MgXfer& x = C.xf;
-  const int64_t n = (int64_t)x.fn[0] * x.fn[1] * x.fn[2];
-  const int64_t cpl = (int64_t)x.cn[0] * x.cn[1];
-  const int64_t stride = (int64_t)gridDim.x * kMgFusedBlock;
-  for (int64_t t = (int64_t)blockIdx.x * kMgFusedBlock + threadIdx.x; t < n; t += stride) {
-    int i, j, k;
-    decode_node(t, F.g, i, j, k);
-    int ci[2], cj[2], ck[2];
-    pmap(x, 0, i, ci[0], ci[1]);
-    pmap(x, 1, j, cj[0], cj[1]);
-    pmap(x, 2, k, ck[0], ck[1]);
-    double v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int64_t o = ci[q & 1] + (int64_t)x.cn[0] * cj[(q >> 1) & 1] + cpl * ck[q >> 2];
-      double xv = C.x[o];
-      if (smooth) xv += C.omega * C.dinv[o] * (C.b[o] - C.w[o]);
-      v[q] = xv;
-    }
-    const double wi0 = x.pw[0][2 * i], wi1 = x.pw[0][2 * i + 1];
-    const double wj0 = x.pw[1][2 * j], wj1 = x.pw[1][2 * j + 1];
-    const double wk0 = x.pw[2][2 * k], wk1 = x.pw[2][2 * k + 1];
-    const double p0 = wj0 * (wi0 * v[0] + wi1 * v[1]) + wj1 * (wi0 * v[2] + wi1 * v[3]);
-    const double p1 = wj0 * (wi0 * v[4] + wi1 * v[5]) + wj1 * (wi0 * v[6] + wi1 * v[7]);
-    st_wt(F.x + t, F.x[t] + (wk0 * p0 + wk1 * p1));
-  }
-}
-
-#ifdef TV_FUSED_TRACE  // experiment builds only: phase timestamps of workgroups 0 and nwg - 1, printed once
-__device__ unsigned g_fused_launch, g_fused_launch2;
-#define FTS(q) do { if (threadIdx.x == 0 && q < 24) ts[q] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define FTS(q) do { } while (0)
-#endif
-
-__global__ __launch_bounds__(kMgFusedBlock) void k_mg_fused(MgFused f) {
-  if (f.st != nullptr && f.st->done) return;  // uniform: the solve state does not change during the launch
-  const unsigned nwg = gridDim.x;
-  bool ok = true;
-#ifdef TV_FUSED_TRACE
-  uint64_t ts[24] = {0};
-#endif
-  int q = 0;
-  FTS(q); ++q;
-  for (int e = 0; e + 1 < f.nl; ++e) {  // down: J x, restriction (+ the coarse pre-smoothing)
-    fused_phase_jx(f.L[e]);
-    FTS(q); ++q;
-    ok = ok && fused_sync(f.bar, nwg);
-    FTS(q); ++q;
-    fused_phase_restrict(f.L[e], f.L[e + 1]);
-    FTS(q); ++q;
-    ok = ok && fused_sync(f.bar, nwg);
-    FTS(q); ++q;
-  }
-  for (int e = f.nl - 2; e >= 0; --e) {  // up: prolongation (+ the coarse post-smoothing), J x
-    fused_phase_prolong(f.L[e], f.L[e + 1], e + 2 < f.nl);
-    FTS(q); ++q;
-    ok = ok && fused_sync(f.bar, nwg);
-    FTS(q); ++q;
-    fused_phase_jx(f.L[e]);
-    FTS(q); ++q;
-    if (e > 0) {
-      ok = ok && fused_sync(f.bar, nwg);
-      FTS(q); ++q;
-    }
-  }
-  (void)ok;
-#ifdef TV_FUSED_TRACE
-  __shared__ unsigned launch;
-  if (threadIdx.x == 0) {
-    if (blockIdx.x == 0) launch = atomicAdd(&g_fused_launch, 1u);
-    else if (blockIdx.x == nwg - 1) launch = atomicAdd(&g_fused_launch2, 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == nwg - 1) && launch >= 40 && launch < 43) {
-    double d[24];
-    for (int p = 0; p < 24; ++p) d[p] = (p < q && p > 0) ? (ts[p] - ts[0]) * 0.01 : 0.0;
-    printf("[fused] launch %u wg %u/%u nl %d: %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f %.2f\n",
-           launch, blockIdx.x, nwg, f.nl, d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11], d[12],
-           d[13], d[14], d[15], d[16]);
-  }
-#endif
-}
-
 }  // namespace
 
-int mg_fused_blocks(const MgFused& f, int n_cu) {
-  int64_t nmax = 0;
-  for (int e = 0; e < f.nl; ++e) nmax = std::max<int64_t>(nmax, (int64_t)f.L[e].g.n0 * f.L[e].g.n1 * f.L[e].g.n2);
-  // about two nodes per thread on the largest level, at most one workgroup per CU
-  const int64_t want = (nmax + 2 * kMgFusedBlock - 1) / (2 * kMgFusedBlock);
-  // the grid barrier needs every workgroup resident at once: one per CU at most,
-  // and the occupancy query must admit at least one per CU
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mg_fused, kMgFusedBlock, 0) != hipSuccess || per_cu < 1)
-    return 0;
-  return (int)std::max<int64_t>(8, std::min<int64_t>(want, n_cu));
-}
-
-void launch_mg_fused(const MgFused& f, int nwg, hipStream_t s) {
-  hipLaunchKernelGGL(k_mg_fused, dim3(nwg), dim3(kMgFusedBlock), 0, s, f);
-}
 
 
 void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, const double* wf, const FaceAdd* fa,

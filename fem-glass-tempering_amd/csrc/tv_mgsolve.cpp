@@ -5,7 +5,6 @@
 
 namespace tv {
 constexpr int64_t kMgFoldFacesNodes = 4000000;  // level 0: facet terms folded into the restriction below this
-constexpr int64_t kMgFusedNodes = 1200000;      // coarse levels up to this size: one persistent launch (k_mg_fused)
 
 // ---- geometric-multigrid preconditioned CG (options.preconditioner = GMG) ----
 // Gershgorin bound of D^-1 J on a rectilinear level: max over nodes of the
@@ -258,56 +257,7 @@ int mg_setup(Ctx* c) {
     for (int s = 0; s < 3; ++s) Xp[s] = L.X[s];
   }
   c->mg_on = true;
-  return mg_fused_setup(c);
-}
-
-// The coarse levels of at most kMgFusedNodes nodes (tv_options.mg_fused_nodes)
-// run as one persistent launch per V-cycle (k_mg_fused, tv_mg.hip): the first
-// level m of that range has all levels below it inside the range; at least two
-// levels, at most kMgFusedMax
-int mg_fused_setup(Ctx* c) {
-  c->mg_fused_from = 0;
-  if (c->O.mg_fused_nodes < 0 || c->n_parts > 1 || c->mg.size() < 2) return TV_OK;
-  const int64_t lim = c->O.mg_fused_nodes > 0 ? c->O.mg_fused_nodes : kMgFusedNodes;
-  const int size = (int)c->mg.size();
-  int m = size;  // 1-based level index: level l is c->mg[l - 1]
-  while (m > 1 && c->mg[m - 2].n <= lim && size - (m - 1) + 1 <= kMgFusedMax) --m;
-  if (m >= size || c->mg[m - 1].n > lim) return TV_OK;  // fewer than two small levels
-  MgFused f = mg_fused_args(c, m);
-  int ncu = 0;
-  HIPC(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device));
-  const int nwg = mg_fused_blocks(f, ncu);
-  if (nwg <= 0) return TV_OK;  // not co-resident (occupancy query): one launch per kernel
-  if (!c->mg_bar) {
-    HIPC(hipMalloc(&c->mg_bar, 64));
-    HIPC(hipMemset(c->mg_bar, 0, 64));
-    HIPC(hipHostMalloc(&c->h_bar, sizeof(unsigned)));
-    *c->h_bar = 0;
-  }
-  c->mg_fused_from = m;
-  c->mg_fused_nwg = nwg;
-  c->mg[m - 1].w_complete = true;
   return TV_OK;
-}
-
-MgFused mg_fused_args(Ctx* c, int m) {
-  MgFused f{};
-  f.nl = (int)c->mg.size() - m + 1;
-  for (int e = 0; e < f.nl; ++e) {
-    const MgLevel& L = c->mg[(size_t)(m - 1 + e)];
-    MgFusedLevel& F = f.L[e];
-    F.g = L.g;
-    F.T = L.T;
-    F.dinv = L.dinv;
-    F.b = L.b;
-    F.x = L.x;
-    F.w = L.w;
-    F.omega = L.omega;
-    F.xf = L.xf;
-  }
-  f.bar = c->mg_bar;
-  f.st = c->st;
-  return f;
 }
 
 // per Newton iteration: T injected down the hierarchy (DG: the vertex mean of
@@ -372,8 +322,7 @@ void mg_prolong_from(Ctx* c, size_t ci, double* xf, const double* mask) {
   MgLevel& C = c->mg[ci];
   const bool smoothed = ci + 1 < c->mg.size() && mg_prolong_smooths(C.xf);
   if (smoothed) {
-    // the fused launch's first level leaves the complete J x in w (no facet terms to add)
-    const CoarsePost cp{C.b, C.w, C.dinv, C.omega, C.w_complete ? FaceAdd{} : cg_face_add(C.g, 0)};
+    const CoarsePost cp{C.b, C.w, C.dinv, C.omega, cg_face_add(C.g, 0)};
     launch_mg_prolong(C.xf, c->st, xf, C.x, mask, c->stream, &cp);
   } else {
     launch_mg_prolong(C.xf, c->st, xf, C.x, mask, c->stream);
@@ -383,12 +332,6 @@ void mg_prolong_from(Ctx* c, size_t ci, double* xf, const double* mask) {
 void mg_level(Ctx* c, size_t l) {
   MgLevel& L = c->mg[l - 1];
   hipStream_t s = c->stream;
-  if ((int)l == c->mg_fused_from) {  // this level and every one below it: one persistent launch
-    launch_mg_fused(mg_fused_args(c, (int)l), c->mg_fused_nwg, s);
-    if (!mg_prolong_smooths(L.xf))  // the post-smoothing the prolongation out of this level cannot fuse
-      launch_mg_jacobi(L.n, c->st, L.b, L.w, nullptr, L.dinv, L.omega, L.x, 1, s);
-    return;
-  }
   if (l < c->mg.size()) {
     const MgLevel& C = c->mg[l];
     const FaceAdd fa = cg_face_add(L.g, 0);
@@ -505,8 +448,6 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
     launched += nb;
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
-    if (c->mg_fused_from)  // the fused launch's barrier timeout flag
-      HIPC(hipMemcpyAsync(c->h_bar, c->mg_bar + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
     HIPC(hipEventRecord(c->evp[0], c->stream));
     return TV_OK;
   };
@@ -518,8 +459,6 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
     if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
     if (int e = enqueue(1)) return e;
   }
-  if (c->mg_fused_from && *c->h_bar)
-    return c->fail(TV_ERR_HIP, "GMG: a grid barrier of the fused coarse-level launch timed out");
   *its = c->h_st[0].it;
   *reason = c->h_st[0].reason;
   // level 0 updates dx in pairs of iterations from iteration 1 on (k_mg_update /

@@ -18,7 +18,7 @@ TV_PCG_AUTO, TV_PCG_KSPCG, TV_PCG_SINGLE_REDUCTION = 0, 1, 2
 TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
 TV_PC_JACOBI, TV_PC_GMG, TV_PC_AMG = 0, 1, 2
 TV_DG_KERNEL_AUTO, TV_DG_KERNEL_TILE, TV_DG_KERNEL_CELLS = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 4
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -91,7 +91,7 @@ class Options(C.Structure):
                 ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
                 ("model_mode", C.c_int), ("preconditioner", C.c_int), ("mg_levels", C.c_int),
                 ("dg_kernel", C.c_int), ("dg_tile_chunk", C.c_int), ("mg_replicate_nodes", C.c_int),
-                ("ksp_fixed_its", C.c_int), ("mg_fused_nodes", C.c_int)]
+                ("ksp_fixed_its", C.c_int)]
 
 
 _lib = None

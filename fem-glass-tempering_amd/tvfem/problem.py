@@ -111,7 +111,7 @@ class ThermoViscoProblem:
                  verbose: bool = True, pcg_variant: str = "auto", model_mode: str = "reference",
                  write_output: bool | None = None, output_dir: str = "output", preconditioner: str = "jacobi",
                  mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0,
-                 mg_replicate_nodes: int = 0, mg_fused_nodes: int = 0, ksp_fixed_its: int = 0, newton_fixed_its: int = 0,
+                 mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0, newton_fixed_its: int = 0,
                  cell_parts=None) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
@@ -151,7 +151,6 @@ class ThermoViscoProblem:
                            "cells": N.TV_DG_KERNEL_CELLS}[dg_kernel]
         self._dg_tile_chunk = int(dg_tile_chunk)
         self._mg_replicate_nodes = int(mg_replicate_nodes)
-        self._mg_fused_nodes = int(mg_fused_nodes)
         self._ksp_fixed_its = int(ksp_fixed_its)
         self._newton_fixed_its = int(newton_fixed_its)
         # partitioned unstructured mesh: cell -> part ids (default: tv_partition_rcb)
@@ -239,7 +238,6 @@ class ThermoViscoProblem:
         opts.dg_kernel = self._dg_kernel
         opts.dg_tile_chunk = self._dg_tile_chunk
         opts.mg_replicate_nodes = self._mg_replicate_nodes
-        opts.mg_fused_nodes = self._mg_fused_nodes
         opts.ksp_fixed_its = self._ksp_fixed_its
         if self._newton_fixed_its > 0:  # timing runs only: exactly this many Newton iterations per step
             opts.newton_rtol = 0.0

@@ -51,10 +51,9 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 5  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+#define TV_ABI_VERSION 4  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
                             3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its;
-                            4: tv_upart_desc / tv_create_unstructured_part;
-                            5: tv_options.mg_fused_nodes */
+                            4: tv_upart_desc / tv_create_unstructured_part */
 
 /* status codes */
 #define TV_OK 0
@@ -171,9 +170,6 @@ typedef struct {
                              iterations, with no convergence test (PETSc
                              KSP_NORM_NONE + max_it; timing of partition shares
                              with the communication stubbed)                    */
-  int mg_fused_nodes;     /* GMG, one partition: the coarse levels of at most this
-                             many nodes run as ONE persistent launch per V-cycle
-                             (0: automatic = 1200000; < 0: one launch per kernel) */
 } tv_options;
 
 /* 3D DG1 Jacobian kernel: AUTO = TILE, the marching tile kernel (production);
