@@ -202,12 +202,26 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
   const bool pair = f1 + 1 < nf;
   const double wl = x.rw[0][3 * II], wr = x.rw[0][3 * II + 2];
   const int64_t fpl = (int64_t)nf * x.fn[1];
+  const int64_t o = (int64_t)I + (int64_t)cn * (J + (int64_t)x.cn[1] * K);
+  // the output's coarse diagonal first: its load overlaps the gathers below
+  const double dci = (xc != nullptr && ok) ? dinv_c[o] : 0.0;
+  // fine rows / planes of the 3 x 3 gather: closed form along axis 1 (always a
+  // whole axis) and, on a whole-box level, along axis 2 -- no table load ahead
+  // of the gathers (a partitioned level's local axis-2 window keeps its table)
+  int fjr[3], fkr[3];
+  rmap(x, 1, J, fjr[0], fjr[1], fjr[2]);
+  if (x.aligned) {
+    rmap(x, 2, K, fkr[0], fkr[1], fkr[2]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) fkr[c] = x.ri[2][3 * K + c];
+  }
   double dc[9], dr[9], wq[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const int c = q / 3, b = q % 3;
     wq[q] = x.rw[2][3 * K + c] * x.rw[1][3 * J + b];
-    const int fj = x.ri[1][3 * J + b], fk = x.ri[2][3 * K + c];
+    const int fj = fjr[b], fk = fkr[c];
     const int64_t f = (int64_t)fj * nf + fpl * fk + f1;
     if (pair) {
       const d2a8 r = ld_pair(bf + f);
@@ -240,9 +254,8 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
     acc += wq[q] * ((wl * dl + dc[q]) + wr * dr[q]);
   }
   if (!ok) return;
-  const int64_t o = (int64_t)I + (int64_t)cn * (J + (int64_t)x.cn[1] * K);
   bc[o] = acc;
-  if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;  // the coarse pre-smoothing step from 0
+  if (xc != nullptr) xc[o] = omega_c * dci * acc;  // the coarse pre-smoothing step from 0
 }
 
 // Prolongation, one wave per (fine row, 63-pair segment); lane l owns the fine
