@@ -459,35 +459,11 @@ __device__ __forceinline__ void facet_corners(const CgGrid& g, bool ok, double h
 // PCG, else p = x) of the R + 1 node rows r0-1 .. r0+R-1 are staged in LDS;
 // waves 1..R-1 write node rows r0 .. r0+R-2 of fface and the workgroup's
 // p.(facet terms) record, then the tile takes part in the reduction tail.
-// (P xc)(i, j, k): the prolongation of the next coarser level's vector xc at a
-// fine node (2 x 2 x 2 coarse nodes, the transfer tables' weights) -- the PROL
-// march's x = x0 + P xc at the few nodes it loads outside its own rows
-__device__ __forceinline__ double prol_at(const PostArgs& pa, int i, int j, int k) {
-  const MgXfer& X = pa.xf;
-  int ci[2], cj[2], ck[2];
-  pmap(X, 0, i, ci[0], ci[1]);
-  pmap(X, 1, j, cj[0], cj[1]);
-  pmap(X, 2, k, ck[0], ck[1]);
-  const int64_t cpl = (int64_t)X.cn[0] * X.cn[1];
-  double acc = 0.0;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    double pl = 0.0;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int64_t o = (int64_t)X.cn[0] * cj[b] + cpl * ck[c];
-      pl += X.pw[1][2 * j + b] * (X.pw[0][2 * i] * pa.xc[o + ci[0]] + X.pw[0][2 * i + 1] * pa.xc[o + ci[1]]);
-    }
-    acc += X.pw[2][2 * k + c] * pl;
-  }
-  return acc;
-}
-
-template <bool FUSEP, int R, bool PROL = false>
+template <bool FUSEP, int R>
 __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const double* __restrict__ in0,
                            const double* pA, const double* pB, const PcgState* __restrict__ st,
                            double* __restrict__ partials, const RedTail& rt, int nrec, int fb,
-                           const FaceOff& fo, double* sm, double* redf, int it_host, const PostArgs& pa) {
+                           const FaceOff& fo, double* sm, double* redf, int it_host) {
   // LDS carved from the kernel's shared buffer (the marching tiles use it for
   // their own face planes): T and p of R + 1 node rows, and the upper-corner
   // contributions (c: c1, d: c1 + 1) of each facet row
@@ -527,15 +503,7 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
   auto stage = [&](int row, int cc2) {
     const bool ok = ok1 && cc2 >= 0 && cc2 < n2;
     const int o = ok ? node_of(c1, cc2) : 0;
-    const double tt = T[o];
-    double zz = in0[o];
-    if (PROL && ok) {  // x = x0 + P xc
-      int c[3];
-      c[t1] = c1;
-      c[t2] = cc2;
-      c[a] = side ? n[a] - 1 : 0;
-      zz += prol_at(pa, c[0], c[1], c[2]);
-    }
+    const double tt = T[o], zz = in0[o];
     const double oo = FUSEP ? pold[o] : 0.0;
     sT[row][lane] = ok ? tt : 0.0;
     sP[row][lane] = ok ? ((FUSEP && !first) ? zz + bcoef * oo : zz) : 0.0;
@@ -650,12 +618,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, double* __rest
 // of the output plane in the prefetch ring, and (z.z, z.r) per tile as records
 // 2 tile, 2 tile + 1; the facet terms of the face workgroups (faces along the
 // march) are applied afterwards by k_mg_post_faces, which also runs the tail.
-// PROL (POST, PF = 1, chunks starting at even planes): in0 is the pre-smoothed
-// x0 and x = x0 + P xc is formed where x is loaded -- per coarse plane two
-// loads per row (the coarse rows either side), the x neighbour from the next
-// lane (DPP), interpolated along x and the row axis once per coarse plane and
-// carried in registers for the three fine planes that read it
-template <int MODE, bool FUSEP, int R, int WPE, int PF, bool POST = false, bool PROL = false>
+template <int MODE, bool FUSEP, int R, int WPE, int PF, bool POST = false>
 __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))) void k_cg_march(CgGrid g, const double* __restrict__ T,
                                                         const double* __restrict__ in0, const double* in1,
                                                         double* __restrict__ out, double* pout,
@@ -664,7 +627,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
                                                         int qchunk, RedTail rt, int nrec, int nmarch,
                                                         FaceOff fo, int it_host, PostArgs pa) {
   static_assert(!POST || (MODE == MODE_JAC && !FUSEP), "POST: plain Jacobian march only");
-  static_assert(!PROL || (POST && PF == 1), "PROL: the post-smoothing march with a two-plane step pattern");
   stamp_start(rt);
   constexpr int NA = (MODE == MODE_RES) ? 2 : 1;  // LDS arrays: stiffness input (+ mass input)
   __shared__ double lds[NA][2][R + 2][kWave];  // double-buffered plane slab (one barrier per plane)
@@ -682,8 +644,8 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const int fidx = (MODE == MODE_JAC && bid >= nmarch) ? bid - nmarch : -1;
   if (fidx >= 0) {
     if (st != nullptr && st->done) return;
-    face_block<FUSEP, R, PROL>(g, T, in0, in1, pout, st, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx,
-                               fo, fsm, red, it_host, pa);
+    face_block<FUSEP, R>(g, T, in0, in1, pout, st, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx, fo,
+                         fsm, red, it_host);
     return;
   }
   const int lane = threadIdx.x & (kWave - 1);
@@ -792,59 +754,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     a_r = bload(rsr, o);
     a_d = bload(rsd, o);
   };
-  // PROL: x = x0 + P xc.  Per lane the coarse x node floor(i / 2) (the next one
-  // from lane + 1), per row (own, halo) the coarse rows floor(r / 2) and the one
-  // after, per fine plane L the coarse planes floor(L / 2) and the one after;
-  // weights from the transfer tables (even node: (1, 0), odd tail: (0, 1)),
-  // 0 outside the grid so those x stay 0
-  double wxa = 0.0, wxb = 0.0, wra = 0.0, wrb = 0.0, wha = 0.0, whb = 0.0;
-  uint32_t co_lane = kBadOff, co_hl = kBadOff, co_ra = 0, co_rb = 0, co_ha = 0, co_hb = 0, sQc8 = 0;
-  int cnQ = 0;
-  buf_t rsc = mk_rsrc(in0, 0u);
-  auto wpair = [&](int ax, int f, int nf, double& w0, double& w1) {
-    w0 = w1 = 0.0;
-    if (f < 0 || f >= nf) return;
-    if (!(f & 1)) {
-      w0 = 1.0;
-    } else if (f == nf - 1) {
-      w1 = 1.0;
-    } else {
-      w0 = pa.xf.pw[ax][2 * f];
-      w1 = pa.xf.pw[ax][2 * f + 1];
-    }
-  };
-  if constexpr (PROL) {
-    const int cn0 = pa.xf.cn[0], cnR = pa.xf.cn[raxis];
-    cnQ = pa.xf.cn[qaxis];
-    const int64_t sRc = (raxis == 1) ? (int64_t)cn0 : (int64_t)cn0 * pa.xf.cn[1];
-    sQc8 = (uint32_t)(((raxis == 1) ? (int64_t)cn0 * pa.xf.cn[1] : (int64_t)cn0) * 8);
-    rsc = mk_rsrc(pa.xc, (uint32_t)cn0 * (uint32_t)pa.xf.cn[1] * (uint32_t)pa.xf.cn[2] * 8u);
-    wpair(0, i, n0, wxa, wxb);
-    // the lane just past the grid loads too: an odd-tail lane takes its value
-    co_lane = (i >= 0 && i <= n0) ? (uint32_t)min(i >> 1, cn0 - 1) * 8u : kBadOff;
-    co_hl = halo ? co_lane : kBadOff;
-    auto rows = [&](int rr, double& w0, double& w1, uint32_t& oa, uint32_t& ob) {
-      wpair(raxis, rr, nR, w0, w1);
-      const int ca = (rr >= 0 && rr < nR) ? min(rr >> 1, cnR - 1) : 0;
-      oa = (uint32_t)(ca * sRc) * 8u;
-      ob = (uint32_t)(min(ca + 1, cnR - 1) * sRc) * 8u;
-    };
-    rows(r, wra, wrb, co_ra, co_rb);
-    rows(hrow, wha, whb, co_ha, co_hb);
-  }
-  // raw loads of coarse plane m: own row (coarse rows a, b), halo row (a, b)
-  auto cfetch = [&](int m, double (&A)[4]) {
-    const uint32_t po = (m >= 0 && m < cnQ) ? (uint32_t)m * sQc8 : kBadOff;
-    A[0] = bload(rsc, co_lane + co_ra + po);
-    A[1] = bload(rsc, co_lane + co_rb + po);
-    A[2] = bload(rsc, co_hl + co_ha + po);
-    A[3] = bload(rsc, co_hl + co_hb + po);
-  };
-  // ... interpolated along x and the row axis (every lane: DPP)
-  auto cval = [&](const double (&A)[4], double& vo, double& vh) {
-    vo = wra * (wxa * A[0] + wxb * shl1(A[0])) + wrb * (wxa * A[1] + wxb * shl1(A[1]));
-    vh = wha * (wxa * A[2] + wxb * shl1(A[2])) + whb * (wxa * A[3] + wxb * shl1(A[3]));
-  };
 
   auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
     v = a0;
@@ -867,14 +776,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     fetch(vo_halo, q0 - 1 + s, rh0[s], rh1[s]);
     fetch_post(q0 - 1 + s, rr[s], rd[s]);
   }
-  // PROL: the two coarse planes of the first step (L = q0 - 1, odd: q0 is even)
-  double Vco = 0.0, Vch = 0.0, Vno = 0.0, Vnh = 0.0;  // coarse planes floor(L / 2), floor(L / 2) + 1
-  double Cr[4] = {0.0, 0.0, 0.0, 0.0};                 // raw loads of the coarse plane two ahead
-  double Cp0[4] = {0.0, 0.0, 0.0, 0.0}, Cp1[4] = {0.0, 0.0, 0.0, 0.0};
-  if constexpr (PROL) {
-    cfetch(q0 / 2 - 1, Cp0);
-    cfetch(q0 / 2, Cp1);
-  }
   // the solver state is read only now, so its latency overlaps the prefetch;
   // once the PCG has converged every launch of the batch exits here
   if (FUSEP) {
@@ -893,23 +794,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       fZ[f][0] = bload(rsZ, vo_own + po); fZ[f][1] = bload(rsZ, vo_halo + po);
       fO[f][0] = FUSEP ? bload(rsO, vo_own + po) : 0.0;
       fO[f][1] = FUSEP ? bload(rsO, vo_halo + po) : 0.0;
-    }
-  }
-  if constexpr (PROL) {  // x = x0 + P xc on the face planes (block-uniform branches: every lane runs the DPP)
-    if (fq0 || fq1) {
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if (!(f == 0 ? fq0 : fq1)) continue;
-        const int Lf = (f == 0) ? 0 : nQ - 1;
-        double w0, w1, A0[4], A1[4], v0o, v0h, v1o, v1h;
-        wpair(qaxis, Lf, nQ, w0, w1);
-        cfetch(Lf >> 1, A0);
-        cfetch((Lf >> 1) + 1, A1);
-        cval(A0, v0o, v0h);
-        cval(A1, v1o, v1h);
-        fZ[f][0] += w0 * v0o + w1 * v1o;
-        fZ[f][1] += w0 * v0h + w1 * v1h;
-      }
     }
   }
   // march-axis coefficients of the chunk, pre-scaled per plane q into
@@ -992,19 +876,16 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   double us_m = 0.0, us_c = 0.0, t_m = 0.0, t_c = 0.0;
   double xc = 0.0;  // own-row value of the centre plane (p of the output node)
   double dot = 0.0, zz = 0.0, zr = 0.0;
-  // xo, xh (PROL): P xc at plane L of the own / halo row
-  auto step = [&](int L, double c0, double c1, double h0, double h1, double pr, double pd, double xo, double xh) {
+  auto step = [&](int L, double c0, double c1, double h0, double h1, double pr, double pd) {
     const int buf = L & 1;
     double v, vm;
     combine(vo_own, L, c0, c1, v, vm);
-    if (PROL) v += xo;
     if (FUSEP) bstore(rsp, vo_wr + ((L >= q0 && L < q1) ? plane_off(L) : kBadOff), v);
     lds[0][buf][wave + 1][lane] = v;
     if (MODE == MODE_RES) lds[NA - 1][buf][wave + 1][lane] = vm;
     if (halo) {
       double hv, hvm;
       combine(vo_halo, L, h0, h1, hv, hvm);
-      if (PROL) hv += xh;
       lds[0][buf][hslot][lane] = hv;
       if (MODE == MODE_RES) lds[NA - 1][buf][hslot][lane] = hvm;
     }
@@ -1052,10 +933,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   };
   // no early exits: steps past q1 only touch LDS (their stores are masked), so
   // the register sets keep fixed registers across the back edge
-  if constexpr (PROL) {  // the first step's coarse planes (loaded with the prologue)
-    cval(Cp0, Vco, Vch);
-    cval(Cp1, Vno, Vnh);
-  }
   for (int L = q0 - 1; L <= q1; L += PF + 1) {
 #pragma unroll
     for (int s = 0; s <= PF; ++s) {
@@ -1063,23 +940,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       fetch(vo_own, L + s + PF, ra0[sf], ra1[sf]);
       fetch(vo_halo, L + s + PF, rh0[sf], rh1[sf]);
       fetch_post(L + s + PF, rr[sf], rd[sf]);
-      double xo = 0.0, xh = 0.0;
-      if constexpr (PROL) {
-        // s = 0: L odd (q0 even), coarse planes (L - 1) / 2 and the next; s = 1: L + 1 even, that next one
-        if (s == 0) cfetch((L - 1) / 2 + 2, Cr);  // the plane the next odd step adds
-        double w0, w1;
-        wpair(qaxis, L + s, nQ, w0, w1);
-        xo = (s == 0) ? w0 * Vco + w1 * Vno : w0 * Vno;
-        xh = (s == 0) ? w0 * Vch + w1 * Vnh : w0 * Vnh;
-      }
-      step(L + s, ra0[s], ra1[s], rh0[s], rh1[s], POST ? rr[s] : 0.0, POST ? rd[s] : 0.0, xo, xh);
-      if constexpr (PROL) {
-        if (s == 1) {
-          Vco = Vno;
-          Vch = Vnh;
-          cval(Cr, Vno, Vnh);
-        }
-      }
+      step(L + s, ra0[s], ra1[s], rh0[s], rh1[s], POST ? rr[s] : 0.0, POST ? rd[s] : 0.0);
     }
   }
   if (POST) {  // (z.z, z.r) records of the tile; k_mg_post_faces reduces them
@@ -1097,10 +958,8 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
         a += red[w];
         c += fsm[w];
       }
-      if (partials != nullptr) {  // null: a coarse level's smoothing (no records)
-        store_partial(&partials[2 * (int64_t)bid], a);
-        store_partial(&partials[2 * (int64_t)bid + 1], c);
-      }
+      store_partial(&partials[2 * (int64_t)bid], a);
+      store_partial(&partials[2 * (int64_t)bid + 1], c);
     }
     return;
   }
@@ -1824,7 +1683,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
     red[1][wave] = a1;
   }
   __syncthreads();
-  if (threadIdx.x < 2 && partials != nullptr) {  // null: a coarse level's smoothing (no records, no tail)
+  if (threadIdx.x < 2) {
     const int w = threadIdx.x;
     store_partial(&partials[2 * ((int64_t)rec0 + blockIdx.x) + w], (red[w][0] + red[w][1]) + (red[w][2] + red[w][3]));
   }
@@ -1870,41 +1729,18 @@ __global__ __launch_bounds__(kBlock) void k_mg_prep_diag(MgPrep p) {
 
 }  // namespace
 
-#ifndef TV_PROL_WPE
-#define TV_PROL_WPE 1
-#endif
-bool cg_post_supported(const CgGrid& g) {
-  const Launch L = plan(g, false);
-  return L.march && g.n0 >= 3 && g.k_begin == 0 && g.k_end == g.n2;
-}
-
 int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
                           double omega, double* z, const PcgState* st, double* partials, const RedTail* tail,
-                          hipStream_t s, const double* xc, const MgXfer* xf) {
-  Launch L = plan(g, false);
+                          hipStream_t s) {
+  const Launch L = plan(g, false);
   // the production march configuration only (experiment switches fall back)
-  if (!cg_post_supported(g)) return -1;
+  if (!L.march || g.n0 < 3 || g.k_begin != 0 || g.k_end != g.n2) return -1;
   const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
-  PostArgs pa{r, dinv, omega};
-  if (xc != nullptr) {
-    // PROL: x = x (= x0) + P xc; its two-plane step pattern needs chunks that
-    // start at even planes (at most kFaceChunk planes: the LDS coefficient stage)
-    const int nQ = (L.raxis == 1) ? g.n2 : g.n1;
-    L.qchunk += L.qchunk & 1;
-    if (L.qchunk > kFaceChunk) L.qchunk = kFaceChunk;
-    L.blocks = L.nseg * ((((L.raxis == 1) ? g.n1 : g.n2) + L.rows - 1) / L.rows) * ((nQ + L.qchunk - 1) / L.qchunk);
-    pa.xc = xc;
-    pa.xf = *xf;
-  }
   const int grid = L.blocks + fo.off[6];
-  if (xc != nullptr)
-    hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, TV_PROL_WPE, 1, true, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T,
-                       x, nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks,
-                       fo, 0, pa);
-  else
-    hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, 1, 2, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T, x,
-                       nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks, fo,
-                       0, pa);
+  const PostArgs pa{r, dinv, omega};
+  hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, 1, 2, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T, x,
+                     nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks, fo,
+                     0, pa);
   const FaceAdd fa = cg_face_add(g, 0);
   const int nO = (L.raxis == 2) ? g.n1 : g.n2;
   const int64_t nodes = 2 * (int64_t)g.n1 * g.n2 + 2 * (int64_t)(g.n0 - 2) * nO;

@@ -125,9 +125,6 @@ struct Ctx {
   std::vector<MgLevel> mg;
   double mg_omega0 = 0.0;
   double* mgx = nullptr;    // level-0 V-cycle iterate
-  // the prolongation into level 0 fused into its post-smoothing march (PROL:
-  // x = x0 + P xc formed on the fly); level 1 then smooths into its w buffer
-  bool mg_prol = false;
   double* dggface = nullptr; // DG level 0: facet means of dg(T) for the cell-block Jacobi smoother
   // partitioned GMG (tv_mgdist.cpp): levels 0 .. mg_A - 1 are distributed over
   // the partitions, mg_A .. the coarsest are replicated on every rank

@@ -24,6 +24,14 @@ enum { C_MLO = 0, C_MDI, C_MUP, C_KLO, C_KDI, C_KUP, C_HLO, C_HHI, C_NCOEF };
 // 0 is physical x (fastest), storage axis 2 is the partition axis (slowest);
 // local node index = i + n0*(j + n1*k).  Along axis 2 the local array holds the
 // owned planes plus one ghost plane towards each neighbouring partition.
+// Operands of the multigrid post-smoothing fused into the Jacobian march
+// (k_cg_march POST): z = x + omega dinv (r - J x)
+struct PostArgs {
+  const double* r;
+  const double* dinv;
+  double omega;
+};
+
 struct CgGrid {
   int n0, n1, n2;             // local node counts per storage axis (n2 incl. ghosts)
   int k_begin, k_end;         // owned planes along axis 2, local indexing
@@ -341,19 +349,6 @@ struct MgXfer {
   // applies); 0 on a partitioned level, whose local planes start anywhere
   int aligned;
 };
-// Operands of the multigrid post-smoothing fused into the Jacobian march
-// (k_cg_march POST): z = x + omega dinv (r - J x).  PROL (xc != nullptr): the
-// march input is the pre-smoothed x0 and x = x0 + P xc is formed on the fly, P
-// the prolongation of xf (the next coarser level -> this one): the separate
-// prolongation pass (16 B per fine node) disappears
-struct PostArgs {
-  const double* r;
-  const double* dinv;
-  double omega;
-  const double* xc;
-  MgXfer xf;
-};
-
 // bc <- P^T (bf - (wf + facet terms fa)) on the coarse owned nodes (mask:
 // level-0 dinv, 0 = excluded node); xc != nullptr: also the coarse level's
 // pre-smoothing from 0, xc <- omega_c dinv_c bc
@@ -435,13 +430,9 @@ void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const dou
 // (k_mg_post_faces, which runs the reduction tail); z <- x + omega dinv (r - J x),
 // w untouched.  Returns the record count, or -1 where the march path does not
 // apply (the caller then runs J x + launch_mg_post)
-// xc != nullptr (PROL): x is the pre-smoothed x0 and the march forms x0 + P xc
-// (P of the transfer xf, the next coarser level -> g); partials == nullptr: no
-// records, no tail (a coarse level's post-smoothing into z)
 int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
                           double omega, double* z, const PcgState* st, double* partials, const RedTail* tail,
-                          hipStream_t s, const double* xc = nullptr, const MgXfer* xf = nullptr);
-bool cg_post_supported(const CgGrid& g);  // launch_cg_japply_post applies (3D march, one partition)
+                          hipStream_t s);
 // z <- x0 + omega dinv (r - (w + facet terms)) (post-smoothing), (z.z, z.r) records + reduction tail;
 // returns the record count
 int launch_mg_post(int64_t n, const PcgState* st, const double* x0, const double* r, const double* w,

@@ -257,14 +257,6 @@ int mg_setup(Ctx* c) {
     for (int s = 0; s < 3; ++s) Xp[s] = L.X[s];
   }
   c->mg_on = true;
-  // level 0's prolongation fused into its post-smoothing march (single
-  // partition, CG1 level 0, whole-box 2 x 2 x 2 transfers, both levels on the
-  // march path)
-  c->mg_prol = !dg && !c->mg.empty() && mg_prolong_smooths(c->mg[0].xf) && cg_post_supported(c->cg) &&
-               (c->mg.size() < 2 || cg_post_supported(c->mg[0].g));
-#ifdef TV_NO_PROL  // A/B experiment builds only
-  c->mg_prol = false;
-#endif
   return TV_OK;
 }
 
@@ -352,13 +344,6 @@ void mg_level(Ctx* c, size_t l) {
     }
     mg_level(c, l + 1);
     mg_prolong_from(c, l, L.x, nullptr);
-    if (l == 1 && c->mg_prol && !c->dir_on) {
-      // level 0 prolongates the smoothed correction inside its own post-smoothing
-      // march: the post-smoothing step of level 1 into its w buffer (the POST
-      // march + the side-face pass, no records)
-      launch_cg_japply_post(L.g, L.T, L.x, L.b, L.dinv, L.omega, L.w, c->st, nullptr, nullptr, s);
-      return;
-    }
     launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
     // post-smoothing, unless the prolongation out of this level applies it (mg_prolong_from)
     if (!mg_prolong_smooths(L.xf))
@@ -399,14 +384,6 @@ int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
       launch_mg_restrict(C.xf, c->st, c->r, c->w, nullptr, mask, C.b, C.dinv, C.omega, C.x, s);
     }
     mg_level(c, 1);
-    if (c->mg_prol && !c->dir_on) {
-      // x = x0 + P xc inside the post-smoothing march: xc = level 1's smoothed
-      // iterate (its w buffer, mg_level) or, a coarsest level 1, its x
-      MgLevel& C1 = c->mg[0];
-      const double* xc = c->mg.size() >= 2 ? C1.w : C1.x;
-      return launch_cg_japply_post(c->cg, T, c->mgx, c->r, c->dinv, c->mg_omega0, c->z, c->st, c->partials, tail, s,
-                                   xc, &C1.xf);
-    }
     mg_prolong_from(c, 0, c->mgx, mask);
   }
   // J x, post-smoothing and (z.z, z.r) in the march epilogue (+ the side-face pass)
