@@ -1632,10 +1632,13 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
 // tiles wrote records 0 .. rec0 - 1); the last block reduces all of them and
 // runs the KSPCG logic.  Nodes on both face families are visited once (the
 // row-axis faces skip i = 0 and i = n0 - 1; face_at sums every face of a node).
+// [kb, ke): the owned planes of storage axis 2 (a partition's ghost planes are
+// neither rewritten nor counted)
 __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis, const double* __restrict__ r,
                                                          const double* __restrict__ dinv, double omega,
                                                          double* __restrict__ z, double* __restrict__ partials,
-                                                         int rec0, RedTail rt, const PcgState* __restrict__ st) {
+                                                         int rec0, RedTail rt, const PcgState* __restrict__ st, int kb,
+                                                         int ke) {
   if (st->done) return;  // uniform: a converged solve's queued launch
   const int n0 = fa.n0, n1 = fa.n1, n2 = fa.n2;
   const int64_t nA = 2 * (int64_t)n1 * n2;
@@ -1665,6 +1668,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
         j = side ? n1 - 1 : 0;
       }
     }
+    if (k < kb || k >= ke) continue;  // a ghost plane
     const int64_t q = i + (int64_t)n0 * (j + (int64_t)n1 * k);
     // the node's three loads first, independent of the face lookups (one round trip)
     const double zo = z[q], dq = dinv[q], rq = r[q];
@@ -1733,8 +1737,10 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
                           double omega, double* z, const PcgState* st, double* partials, const RedTail* tail,
                           hipStream_t s) {
   const Launch L = plan(g, false);
-  // the production march configuration only (experiment switches fall back)
-  if (!L.march || g.n0 < 3 || g.k_begin != 0 || g.k_end != g.n2) return -1;
+  // the production march configuration only; a partition's slab too (the march
+  // writes z and its records on the owned planes only, the side-face pass skips
+  // the ghost planes)
+  if (!L.march || g.n0 < 3) return -1;
   const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
   const int grid = L.blocks + fo.off[6];
   const PostArgs pa{r, dinv, omega};
@@ -1750,7 +1756,7 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, cap));
   const RedTail rt = tail ? *tail : RedTail{};
   hipLaunchKernelGGL(k_mg_post_faces, dim3(nb), dim3(kBlock), 0, s, fa, L.raxis, r, dinv, omega, z, partials,
-                     L.blocks, rt, st);
+                     L.blocks, rt, st, g.k_begin, g.k_end);
   return L.blocks + nb;
 }
 

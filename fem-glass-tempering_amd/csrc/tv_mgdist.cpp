@@ -338,6 +338,10 @@ int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
     MgLevel& C = c->mg[l];
     // every local fine plane, ghost planes included (their inputs are local)
     launch_mg_prolong(C.xf, c->st, r.x, C.x, l == 0 ? dmask : nullptr, s);
+    // level 0: J x, the post-smoothing and the (z.z, z.r) records in the march
+    // epilogue (+ the side-face pass with the reduction tail), as on one partition
+    if (l == 0 && launch_cg_japply_post(*r.g, r.T, r.x, r.b, r.dinv, r.omega, c->z, c->st, c->partials, tail, s) >= 0)
+      return TV_OK;
     launch_cg_japply_partial(*r.g, r.T, r.x, r.w, c->st, s);
     const FaceAdd fa = cg_face_add(*r.g, r.off);
     if (l > 0) {
