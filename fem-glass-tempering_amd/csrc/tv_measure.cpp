@@ -1,6 +1,8 @@
 // Measurement entry points: in-solve kernel timing from device clock stamps,
 // algorithmic bytes per launch and timed launches of the
 // hot kernels (HIP events), including the Infinity-Cache-flushed J x.
+#include <algorithm>
+
 #include "tv_ctx.h"
 
 namespace tv {
@@ -175,8 +177,10 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     // J x with the Infinity Cache flushed before every launch: a 512 MiB write
     // (2x the 256 MiB L3) then a read sweep of the same buffer, so the cache
     // holds clean lines (no write-backs of the flush competing with the timed
-    // launch), HIP events around each launch alone (SURVEY.md section 8(d) H7:
-    // the HBM figure, not the cache-assisted one)
+    // launch), HIP events around each launch alone; the MEDIAN over the reps
+    // (the HBM figure, not
+    // the cache-assisted one).  The events include the dispatch (~6 us before
+    // the first workgroup in a kernel trace).
     const size_t fl = (size_t)512 << 20;
     void* flush = nullptr;
     HIPC(hipMalloc(&flush, fl));
@@ -192,15 +196,16 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
       HIPC(hipEventRecord(ev[2 * i + 1], c->stream));
     }
     HIPC(hipEventSynchronize(ev.back()));
-    double sum = 0.0;
+    std::vector<double> t((size_t)reps);
     for (int i = 0; i < reps; ++i) {
-      float t = 0.f;
-      HIPC(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
-      sum += t;
+      float f = 0.f;
+      HIPC(hipEventElapsedTime(&f, ev[2 * i], ev[2 * i + 1]));
+      t[(size_t)i] = f;
     }
     for (auto& e : ev) hipEventDestroy(e);
     HIPC(hipFree(flush));
-    *ms = sum / reps;
+    std::sort(t.begin(), t.end());
+    *ms = (reps & 1) ? t[(size_t)reps / 2] : 0.5 * (t[(size_t)reps / 2 - 1] + t[(size_t)reps / 2]);
     return TV_OK;
   }
   if (int e = one()) return e;  // warm-up

@@ -377,8 +377,9 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
  * kernel: 0 = Jacobian apply (matvec), 1 = fused viscoelastic update,
  * 2 = residual, 3 = fused PCG matvec (p <- z + b p; w <- J p; p.w),
  * 4 = PCG vector update, 10 = Jacobian apply with the 256 MiB Infinity Cache
- * flushed (512 MiB write) before every launch, events around the launch alone.
- * Writes the mean duration per launch in ms. */
+ * flushed (512 MiB write) before every launch, events around the launch alone,
+ * the MEDIAN over the reps.  Writes the duration per launch in ms (the mean,
+ * except 10). */
 int tv_time_kernel(void* ctx, int kernel, int reps, double* ms_per_launch);
 /* algorithmic bytes moved by one launch of `kernel` */
 int tv_kernel_bytes(void* ctx, int kernel, double* bytes);
