@@ -512,17 +512,45 @@ static void axis_tables(const double* Xf, int nf, const char* is_c, int* pi, dou
   free(fpos);
 }
 
+/* Deterministic dot products: fixed chunks of DCHUNK entries summed in order,
+ * the chunk sums added in chunk order -- the same bits for any thread count
+ * or schedule (OpenMP's reduction(+) combines the threads' partial sums in
+ * arrival order, so Krylov counts at a convergence threshold could differ
+ * between runs).  s2 / a2 may be NULL. */
+#define DCHUNK 4096
+static void dots(long long N, const double* a1, const double* b1, const double* a2, const double* b2, double* s1,
+                 double* s2) {
+  const long long nc = (N + DCHUNK - 1) / DCHUNK;
+  double* part = (double*)malloc(sizeof(double) * 2 * (size_t)(nc > 0 ? nc : 1));
+#pragma omp parallel for schedule(static)
+  for (long long c = 0; c < nc; ++c) {
+    const long long t1 = (c + 1) * DCHUNK < N ? (c + 1) * DCHUNK : N;
+    double x = 0.0, y = 0.0;
+    for (long long t = c * DCHUNK; t < t1; ++t) {
+      x += a1[t] * b1[t];
+      if (a2) y += a2[t] * b2[t];
+    }
+    part[2 * c] = x;
+    part[2 * c + 1] = y;
+  }
+  double x = 0.0, y = 0.0;
+  for (long long c = 0; c < nc; ++c) {
+    x += part[2 * c];
+    y += part[2 * c + 1];
+  }
+  free(part);
+  *s1 = x;
+  if (s2) *s2 = y;
+}
+
 static int pcg(tvcpu* h, double rtol) {
   const long long N = h->N;
   double zz = 0, zr = 0;
   if (h->nlev > 0) mg_prepare(h);
   precond(h, h->r, h->z);
-#pragma omp parallel for reduction(+ : zz, zr)
-  for (long long t = 0; t < N; ++t) {
-    h->dx[t] = 0.0;
-    zz += h->z[t] * h->z[t];
-    zr += h->z[t] * h->r[t];
-  }
+#pragma omp parallel for
+  for (long long t = 0; t < N; ++t) h->dx[t] = 0.0;
+  dots(N, h->z, h->z, h->z, h->r, &zz, &zr);
   double dp = sqrt(zz), ttol = fmax(rtol * dp, 1e-50), rnorm0 = dp;
   if (dp <= ttol) return 0;
   double beta = zr, betaold = 1.0, dpiold = 0.0;
@@ -532,8 +560,7 @@ static int pcg(tvcpu* h, double rtol) {
     for (long long t = 0; t < N; ++t) h->p[t] = it ? h->z[t] + b * h->p[t] : h->z[t];
     op_apply(h, 1, h->p, h->w);
     double dpi = 0;
-#pragma omp parallel for reduction(+ : dpi)
-    for (long long t = 0; t < N; ++t) dpi += h->p[t] * h->w[t];
+    dots(N, h->p, h->w, NULL, NULL, &dpi, NULL);
     if (dpi == 0.0 || (it > 0 && (dpi > 0) != (dpiold > 0))) return -it - 1;
     dpiold = dpi;
     betaold = beta;
@@ -545,11 +572,7 @@ static int pcg(tvcpu* h, double rtol) {
       h->r[t] -= a * h->w[t];
     }
     precond(h, h->r, h->z);
-#pragma omp parallel for reduction(+ : zz, zr)
-    for (long long t = 0; t < N; ++t) {
-      zz += h->z[t] * h->z[t];
-      zr += h->z[t] * h->r[t];
-    }
+    dots(N, h->z, h->z, h->z, h->r, &zz, &zr);
     dp = sqrt(zz);
     if (dp <= ttol) return it + 1;
     if (dp >= 1e5 * rnorm0 || !isfinite(dp)) return -it - 1;
@@ -569,11 +592,9 @@ static int newton(tvcpu* h) {
     if (k < 0) return -1;
     kits += k;
     double nn = 0;
-#pragma omp parallel for reduction(+ : nn)
-    for (long long t = 0; t < N; ++t) {
-      h->T[t] -= h->dx[t];
-      nn += h->dx[t] * h->dx[t];
-    }
+#pragma omp parallel for
+    for (long long t = 0; t < N; ++t) h->T[t] -= h->dx[t];
+    dots(N, h->dx, h->dx, NULL, NULL, &nn, NULL);
     double rn = sqrt(nn);
     ++its;
     if (its == 1) r0 = rn;
