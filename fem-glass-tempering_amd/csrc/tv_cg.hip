@@ -610,6 +610,41 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, double* __rest
   }
 }
 
+// Tile of marching workgroup bid.  Each XCD (bid & 7) takes a contiguous
+// share of the tile sequence (as xcd_remap), and that share BEGINS with its
+// part of the face-chunk tiles: the first and the last chunk along the march
+// axis integrate the Robin facets of the faces normal to it in their
+// prologue, so those tiles run longer.  In plain chunk order they sat on the
+// XCDs holding the first and last chunks (C4: 4 chunks, XCDs 0-1 and 6-7) and
+// ran last there; here every XCD gets the same number of them, first (C4:
+// fused matvec 74.1 -> 72.0 us, J x 41.8 -> 40.5 us, flushed J x 52.5 ->
+// 50.9 us, interleaved A/B on one box).  Face tiles: seg fastest, then row
+// block, then face chunk; the others: seg, row block, chunk 1 .. nch - 2 --
+// XCD x works on the same band of row blocks in both parts.
+__device__ __forceinline__ void march_tile(int bid, int nmarch, int nseg, int nrbk, int nch, int& seg, int& rb,
+                                           int& chunk) {
+  const int x = bid & 7, p = bid >> 3;
+  const int q = nmarch >> 3, r = nmarch & 7;
+  const int start = x * q + min(x, r);
+  const int per_chunk = nseg * nrbk;
+  const int nF = (nch > 1 ? 2 : 1) * per_chunk;
+  const int fq = nF >> 3, fr = nF & 7;
+  const int fsize = fq + (x < fr ? 1 : 0), fstart = x * fq + min(x, fr);
+  int t, c;
+  if (p < fsize) {
+    t = fstart + p;
+    c = t / per_chunk;
+    chunk = c ? nch - 1 : 0;
+  } else {
+    t = (start - fstart) + (p - fsize);
+    c = t / per_chunk;
+    chunk = 1 + c;
+  }
+  t -= c * per_chunk;
+  seg = t % nseg;
+  rb = t / nseg;
+}
+
 // WPE: minimum waves per SIMD the register allocation must allow (8: <= 64
 // VGPRs, four 8-wave tiles per CU, at the price of a few spills)
 // PF: prefetch depth (planes whose loads are in flight while one is computed)
@@ -656,20 +691,16 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
   const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
   const int qaxis = 3 - raxis;
-  // tile order: x segment fastest, then row block, then chunk; each XCD takes a
-  // contiguous run of tiles (xcd_remap), i.e. whole x-rows of a band of row
+  // tile order (march_tile): x segment fastest, then row block, then chunk;
+  // each XCD takes a contiguous run of tiles, i.e. whole x-rows of a band of row
   // blocks in one chunk -- the concurrent tiles of an XCD read long contiguous
   // runs and share their halo rows in L2 (measured at C4 against chunk-fastest:
   // step 11.22 / 11.34 -> 10.99 / 10.85 ms, flushed J x 53.5 -> 50.9-52.6 us;
   // segment, then chunk: 11.08 / 11.17 ms)
   const int nch = (nQ + qchunk - 1) / qchunk;
-  const int b = xcd_remap(bid, nmarch);
-  const int seg = b % nseg;
-  const int t = b / nseg;
   const int nrbk = (nR + R - 1) / R;
-  const int rb = t % nrbk;
-  const int chunk = t / nrbk;
-  (void)nch;
+  int seg, rb, chunk;
+  march_tile(bid, nmarch, nseg, nrbk, nch, seg, rb, chunk);
   const int r0 = rb * R;
   const int r = r0 + wave;
   const bool row_ok = r < nR;

@@ -12,7 +12,7 @@ for rep in 1 2; do
       IFS=' ' read -r -a argv <<< "$args"
       o=$OUT/b${v}_${tag}_$rep
       TVFEM_LIB=$PWD/fem-glass-tempering_amd/tvfem/libtvfem$v.so timeout -k 10 300 python3 bench.py --no-cpu-baseline "${argv[@]}" > $o.json 2> $o.err || { tail -5 $o.err; exit 1; }
-      python3 -c "import json;d=json.load(open('$o.json'));print('lib$v', '$tag', round(d['ms_per_step'],3), d['config'].get('krylov_its_per_step'), {k:round(v['ms']*1e3,1) for k,v in d['kernels'].items()})"
+      python3 -c "import json;d=json.load(open('$o.json'));print('lib$v', '$tag', round(d['ms_per_step'],3), d['config'].get('krylov_its_per_step'), {k:round(v['ms']*1e3,1) for k,v in d['kernels'].items()}, 'flushed', round(d['roofline']['hbm_flushed']['ms_per_launch']*1e3,1))"
     done
   done
 done
