@@ -379,12 +379,15 @@ int setup_fields(Ctx* c) {
     return c->fail(TV_ERR_ARG, "pcg_variant SINGLE_REDUCTION needs a 3D CG1 temperature space");
   // AUTO: the single-reduction form where the mesh is partitioned into slabs
   // of at most kCgsAutoMaxNodes owned nodes (one RCCL group per iteration
-  // instead of two all-reduces + a halo + two logic launches); on one
-  // partition, and on larger slabs where its heavier launch is bandwidth-bound,
-  // KSPCG's two lighter launches are faster (measured on the C4 per-rank
-  // shares, DESIGN.md §5: 4.1M nodes 13.2 vs 18.3 ms/step, against ~2.7 ms of
-  // communication the single reduction saves; 2M nodes 7.6 vs 8.6 ms; 1M
-  // nodes 6.5 vs 6.7 ms)
+  // instead of two all-reduces + a halo + two logic launches), and on one
+  // partition of at most kCgsAutoMaxNodes1 nodes, where an iteration is
+  // launch-latency bound and one launch beats two (round 3, one box, same
+  // Krylov counts: C3 1.05M nodes 2.97 vs 3.14 ms/step, C2 112K nodes 1.02-1.05
+  // vs 1.06 ms; profiles/r03_single_reduction_c2_c3.txt); on larger grids its
+  // heavier launch is bandwidth-bound and KSPCG's two lighter launches are
+  // faster (measured on the C4 per-rank shares, DESIGN.md §5: 4.1M nodes 13.2
+  // vs 18.3 ms/step, against ~2.7 ms of communication the single reduction
+  // saves; 2M nodes 7.6 vs 8.6 ms)
   // The choice must agree on every rank (the two forms issue different
   // collectives): it is taken on the LARGEST slab of the partition, which every
   // rank computes identically from the global mesh, not on this rank's own slab
@@ -399,7 +402,8 @@ int setup_fields(Ctx* c) {
     }
   }
   c->cgs = can && (var == TV_PCG_SINGLE_REDUCTION ||
-                   (var == TV_PCG_AUTO && c->n_parts > 1 && max_slab <= kCgsAutoMaxNodes &&
+                   (var == TV_PCG_AUTO &&
+                    (c->n_parts > 1 ? max_slab <= kCgsAutoMaxNodes : c->nT <= kCgsAutoMaxNodes1) &&
                     c->O.preconditioner != TV_PC_GMG));  // the multigrid solve runs in the KSPCG form
   if (c->cgs) {
     for (double** q : {&c->cr[0], &c->cr[1], &c->cs[0], &c->cs[1], &c->cw1}) {

@@ -223,6 +223,7 @@ struct Ctx {
   } while (0)
 
 constexpr int64_t kCgsAutoMaxNodes = 3000000;  // AUTO Krylov form: single reduction up to this slab size
+constexpr int64_t kCgsAutoMaxNodes1 = 1500000;  // ... and on one partition up to this size (Jacobi)
 constexpr int kTsCap = 1 << 15;                // timestamp slots of the in-solve kernel timing
 
 // ---- tv_amg.cpp ----
