@@ -1210,12 +1210,9 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
   const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
   const int qaxis = 3 - raxis;
   // tile order as k_cg_march: x segment fastest, then row block, then chunk
-  const int b = xcd_remap((int)blockIdx.x, nmarch);
-  const int seg = b % nseg;
-  const int t = b / nseg;
   const int nrbk = (nR + R - 1) / R;
-  const int rb = t % nrbk;
-  const int chunk = t / nrbk;
+  int seg, rb, chunk;  // face-chunk tiles spread over the XCDs, first (march_tile)
+  march_tile((int)blockIdx.x, nmarch, nseg, nrbk, (nQ + qchunk - 1) / qchunk, seg, rb, chunk);
   const int r0 = rb * R;
   const int r = r0 + wave;
   const bool row_ok = r < nR;
