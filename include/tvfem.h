@@ -211,8 +211,10 @@ typedef struct {
  *                     (p.w, then z.z and z.r), a fused matvec and an update launch;
  *   SINGLE_REDUCTION  Chronopoulos-Gear form: one launch and one reduction per
  *                     iteration (3D CG1 temperature only);
- *   AUTO              SINGLE_REDUCTION on partitioned 3D CG1 meshes (one
- *                     communication round per iteration), else KSPCG. */
+ *   AUTO              SINGLE_REDUCTION (Jacobi) on 3D CG1 box meshes partitioned
+ *                     into slabs of <= 3M owned nodes (one communication round
+ *                     per iteration) or on one partition of <= 1.5M nodes (one
+ *                     launch per iteration), else KSPCG. */
 #define TV_PCG_AUTO 0
 #define TV_PCG_KSPCG 1
 #define TV_PCG_SINGLE_REDUCTION 2
