@@ -61,6 +61,10 @@ def parse():
                          "one GPU), jacobi, or auto (gmg where it applies and the mesh has >= 4M T-dofs, at "
                          "every rank count; amg for --mesh distorted on one GPU)")
     ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
+    ap.add_argument("--mg-coupling", choices=["auto", "global", "local"], default="auto",
+                    help="partitioned GMG: global = the distributed V-cycle of the whole box (the N = 1 "
+                         "preconditioner), local = each slab's own V-cycle (block Jacobi, no exchange inside the "
+                         "preconditioner, ~2.4x the Krylov iterations); auto = global")
     ap.add_argument("--share", type=int, default=0, metavar="N",
                     help="time ONE rank's share of an N-way partition of the mesh on this GPU with the "
                          "communication stubbed (halos and all-reduces are no-ops) and the iteration counts "
@@ -130,6 +134,7 @@ def main():
               "ksp_fixed_its": kk}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
                               verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,
+                              mg_coupling=a.mg_coupling,
                               write_output=a.output is not None, output_dir=a.output or "output", **kw)
     single = prob.pcg_variant == "single"
     lib, ctx = prob._lib, prob._ctx
@@ -146,6 +151,14 @@ def main():
             except Exception as e:
                 print(f"[bench rank {rank}] RCCL init failed: {e}", file=sys.stderr, flush=True)
                 raise SystemExit(3)
+        # pre-flight: every exchange pattern of the solve on id-valued vectors
+        # (tv_comm_check, collective); a wrong ghost or sum ends the run here
+        nchk, nbad = C.c_int64(), C.c_int64()
+        rc = lib.tv_comm_check(ctx, C.byref(nchk), C.byref(nbad))
+        if rc != 0 or nbad.value:
+            print(f"[bench rank {rank}] transport check failed: rc {rc}, {nbad.value} of {nchk.value} wrong: "
+                  f"{lib.tv_last_error(ctx)}", file=sys.stderr, flush=True)
+            raise SystemExit(3)
     prob.setup()
     n_owned, _ = prob.num_dofs(0)
     n_global = int(np.prod([n + 1 for n in nc])) if a.family == "CG" else 8 * int(np.prod(nc))

@@ -11,6 +11,44 @@ namespace tv {
 // --------------------------------------------------------------------------------------
 bool multi_rank(const Ctx* c) { return c->nranks > 1 && (c->comm || c->host_sendrecv || c->comm_stub); }
 
+int require_comm(Ctx* c, const char* what) {
+  if (c->n_parts > 1 && !multi_rank(c))
+    return c->fail(TV_ERR_STATE, std::string(what) + ": a partition of a partitioned mesh needs its communicator "
+                                 "(tv_comm_init / tv_comm_init_host) before it solves");
+  return TV_OK;
+}
+
+int refresh_dirty_ghosts(Ctx* c) {
+  if (!(c->um && c->n_parts > 1) || !multi_rank(c) || c->comm_stub) return TV_OK;
+  // T and T_prev are exchanged every step anyway (newton); the other fields
+  // only when a rank wrote them.  Every rank learns the union of the writes
+  // through one all-reduce of a flag per field.
+  if (!c->d_dirty) HIPC(hipMalloc(&c->d_dirty, sizeof(double) * TV_NUM_FIELDS));
+  double fl[TV_NUM_FIELDS];
+  for (int f = 0; f < TV_NUM_FIELDS; ++f) fl[f] = (c->ghost_dirty >> f) & 1u ? 1.0 : 0.0;
+  HIPC(hipMemcpyAsync(c->d_dirty, fl, sizeof(fl), hipMemcpyHostToDevice, c->stream));
+  if (int e = allreduce_vec(c, c->d_dirty, TV_NUM_FIELDS)) return e;
+  HIPC(hipMemcpyAsync(fl, c->d_dirty, sizeof(fl), hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  c->ghost_dirty = 0;
+  bool tilde = false;
+  for (int f = 0; f < TV_NUM_FIELDS; ++f) {
+    if (fl[f] == 0.0 || !c->f[f].ptr || f == TV_F_T || f == TV_F_T_PREV) continue;
+    const int64_t stride = c->f[f].space == 0 ? c->nT : c->nS;  // the same vertex set (CG1 / CG1)
+    for (int k = 0; k < c->f[f].bs; ++k)
+      if (int e = halo_um(c, c->f[f].ptr + k * stride)) return e;
+    tilde = tilde || f == TV_F_S_TILDE || f == TV_F_S_TILDE_NEXT || f == TV_F_SIGMA_TILDE || f == TV_F_SIGMA_TILDE_NEXT;
+  }
+  if (tilde) {  // a neighbour's non-zero tilde values may now sit in this rank's ghosts
+    static const int one = 1;
+    HIPC(hipMemcpyAsync(c->tflag, &one, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  }
+  return TV_OK;
+}
+
+// RCCL peer of partition q: itself on a loopback communicator (one rank, peer 0)
+static inline int peer(const Ctx* c, int q) { return c->comm_self ? 0 : q; }
+
 // measurement stub (tv_comm_init_stub): the ghosts of the solver's vectors read
 // zero (each partition solves its own block: the operators stay SPD), the
 // temperature ghosts keep their initial value, reductions stay local.  Both
@@ -63,12 +101,12 @@ int halo_grid(Ctx* c, const CgGrid& g, double* v) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
   NCCLC(ncclGroupStart());
   if (g.g_lo) {  // neighbour rank-1: send first owned plane, receive ghost plane 0
-    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
-    NCCLC(ncclRecv(v, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
   }
   if (g.g_hi) {
-    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, c->rank + 1, c->comm, c->stream));
-    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
   }
   NCCLC(ncclGroupEnd());
   return TV_OK;
@@ -103,9 +141,9 @@ int halo_um(Ctx* c, double* v) {
   }
   NCCLC(ncclGroupStart());
   for (size_t k = 0; k < c->um_peer.size(); ++k) {
-    if (c->um_scnt[k]) NCCLC(ncclSend(c->um_sbuf + c->um_soff[k], c->um_scnt[k], ncclDouble, c->um_peer[k], c->comm, c->stream));
+    if (c->um_scnt[k]) NCCLC(ncclSend(c->um_sbuf + c->um_soff[k], c->um_scnt[k], ncclDouble, peer(c, c->um_peer[k]), c->comm, c->stream));
     if (c->um_rcnt[k])
-      NCCLC(ncclRecv(v + nown + c->um_roff[k], c->um_rcnt[k], ncclDouble, c->um_peer[k], c->comm, c->stream));
+      NCCLC(ncclRecv(v + nown + c->um_roff[k], c->um_rcnt[k], ncclDouble, peer(c, c->um_peer[k]), c->comm, c->stream));
   }
   NCCLC(ncclGroupEnd());
   return TV_OK;
@@ -131,12 +169,12 @@ int allreduce_halo(Ctx* c, double* sums, int n, double* v) {
   NCCLC(ncclGroupStart());
   NCCLC(ncclAllReduce(sums, sums, n, ncclDouble, ncclSum, c->comm, c->stream));
   if (g.g_lo) {
-    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
-    NCCLC(ncclRecv(v, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
   }
   if (g.g_hi) {
-    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, c->rank + 1, c->comm, c->stream));
-    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
   }
   NCCLC(ncclGroupEnd());
   return TV_OK;
@@ -215,6 +253,176 @@ __global__ __launch_bounds__(kBlock) void k_cgs_pack(CgGrid g, const double* __r
 
 int cgs_raxis(const Ctx* c) { return (c->cg.n2 >= c->cg.n1) ? 2 : 1; }  // = plan(g).raxis
 
+// ---- transport check (tv_comm_check) -----------------------------------------
+// owned nodes of a grid level <- their global index along the level (exact in
+// a double below 2^53), ghost planes <- -1
+__global__ __launch_bounds__(kBlock) void k_fill_ids(double* v, int64_t plane, int64_t n, int k_begin, int k_end,
+                                                     int64_t first_plane) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    const int k = (int)(t / plane);
+    v[t] = (k >= k_begin && k < k_end) ? (double)((first_plane + k) * plane + (t - (int64_t)k * plane)) : -1.0;
+  }
+}
+
+namespace {
+int fill_ids(Ctx* c, const CgGrid& g, double* v, int64_t first_plane) {
+  const int64_t plane = (int64_t)g.n0 * g.n1, n = plane * g.n2;
+  const int nb = (int)std::min<int64_t>(4096, (n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_fill_ids, dim3(nb), dim3(kBlock), 0, c->stream, v, plane, n, g.k_begin, g.k_end, first_plane);
+  HIPC(hipGetLastError());
+  return TV_OK;
+}
+
+// after an exchange of ids: the owned planes unchanged, each ghost plane holding
+// the ids its neighbour sent -- the ghost's own global ids, or on a loopback
+// communicator the ids of the boundary plane this rank sent itself
+void check_ids(const Ctx* c, const CgGrid& g, const std::vector<double>& h, int64_t first_plane, int64_t* n_chk,
+               int64_t* n_bad) {
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  for (int k = 0; k < g.n2; ++k) {
+    int64_t src = first_plane + k;                                  // global plane the values must come from
+    if (k < g.k_begin && c->comm_self) src = first_plane + g.k_begin;
+    if (k >= g.k_end && c->comm_self) src = first_plane + g.k_end - 1;
+    if ((k < g.k_begin && !g.g_lo) || (k >= g.k_end && !g.g_hi)) continue;
+    for (int64_t e = 0; e < plane; ++e) {
+      ++*n_chk;
+      if (h[(size_t)(k * plane + e)] != (double)(src * plane + e)) ++*n_bad;
+    }
+  }
+}
+}  // namespace
+
+// Every exchange pattern the solver issues, on id-valued vectors, checked on
+// the host: halo_grid (fine grid and every distributed multigrid level),
+// allreduce_halo (sums + ghosts in one group), cgs_exchange (single-reduction
+// form: 3 sums + packed planes), allreduce_vec (the replicated multigrid level),
+// halo_um (per-neighbour groups).  Collective: every rank calls it.
+int comm_check(Ctx* c, int64_t* n_chk, int64_t* n_bad) {
+  *n_chk = *n_bad = 0;
+  const double R = (double)c->nranks;
+  const double sum_ranks = c->comm_self ? (double)(c->rank + 1) : R * (R + 1) / 2;  // sum of (rank + 1)
+  const double n_contrib = c->comm_self ? 1.0 : R;
+  int64_t nmax = std::max<int64_t>(c->nT, 16);
+  for (const MgLevel& L : c->mg) nmax = std::max<int64_t>(nmax, L.n);
+  double* v = nullptr;
+  double* s = nullptr;
+  double* ff = nullptr;
+  HIPC(hipMalloc(&v, sizeof(double) * (size_t)nmax));
+  HIPC(hipMalloc(&s, sizeof(double) * 4));
+  std::vector<double> h((size_t)nmax);
+  auto sums_ok = [&](const double* d, int n, const double* want) -> int {
+    double hs[4];
+    HIPC(hipMemcpyAsync(hs, d, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) {
+      ++*n_chk;
+      if (hs[i] != want[i]) ++*n_bad;
+    }
+    return TV_OK;
+  };
+  auto run = [&]() -> int {
+    if (c->um) {
+      const int64_t nown = c->ownT_n;
+      std::vector<double> ids((size_t)c->nT, -1.0);
+      for (int64_t i = 0; i < nown; ++i) ids[(size_t)i] = (double)(c->globT_off + i);
+      HIPC(hipMemcpyAsync(v, ids.data(), sizeof(double) * ids.size(), hipMemcpyHostToDevice, c->stream));
+      if (int e = halo_um(c, v)) return e;
+      HIPC(hipMemcpyAsync(h.data(), v, sizeof(double) * (size_t)c->nT, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipStreamSynchronize(c->stream));
+      std::vector<int64_t> sidx(c->um_soff.empty() ? 0 : (size_t)(c->um_soff.back() + c->um_scnt.back()));
+      if (!sidx.empty())
+        HIPC(hipMemcpy(sidx.data(), c->um_sidx, sizeof(int64_t) * sidx.size(), hipMemcpyDeviceToHost));
+      for (int64_t i = 0; i < nown; ++i) {
+        ++*n_chk;
+        if (h[(size_t)i] != ids[(size_t)i]) ++*n_bad;
+      }
+      for (size_t k = 0; k < c->um_peer.size(); ++k)
+        for (int64_t j = 0; j < c->um_rcnt[k]; ++j) {
+          const double got = h[(size_t)(nown + c->um_roff[k] + j)];
+          ++*n_chk;
+          if (c->comm_self) {  // the owned values this rank packed for "neighbour" k, in send order
+            if (got != ids[(size_t)sidx[(size_t)(c->um_soff[k] + j)]]) ++*n_bad;
+          } else {  // ids of the neighbour's owned vertices: outside this part's range, ascending in send order
+            const bool own = got >= (double)c->globT_off && got < (double)(c->globT_off + nown);
+            const bool asc = j == 0 || got > h[(size_t)(nown + c->um_roff[k] + j - 1)];
+            if (got < 0 || own || !asc || got != std::floor(got)) ++*n_bad;
+          }
+        }
+      const double hs[2] = {(double)(c->rank + 1), 1.0};
+      HIPC(hipMemcpyAsync(s, hs, sizeof(hs), hipMemcpyHostToDevice, c->stream));
+      if (int e = allreduce_halo(c, s, 2, v)) return e;
+      const double want[2] = {sum_ranks, n_contrib};
+      return sums_ok(s, 2, want);
+    }
+    if (c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "tv_comm_check: CG temperature space");
+    const CgGrid& g = c->cg;
+    const int64_t first = c->plane_begin - g.k_begin;  // global plane of local plane 0
+    const int64_t nloc = (int64_t)g.n0 * g.n1 * g.n2;
+    auto fetch = [&](int64_t n) -> int {
+      HIPC(hipMemcpyAsync(h.data(), v, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipStreamSynchronize(c->stream));
+      return TV_OK;
+    };
+    // 1. halo_grid of the fine grid
+    if (int e = fill_ids(c, g, v, first)) return e;
+    if (int e = halo_grid(c, g, v)) return e;
+    if (int e = fetch(nloc)) return e;
+    check_ids(c, g, h, first, n_chk, n_bad);
+    // 2. allreduce_halo: the KSPCG iteration's closing group
+    if (int e = fill_ids(c, g, v, first)) return e;
+    {
+      const double hs[2] = {(double)(c->rank + 1), 1.0};
+      HIPC(hipMemcpyAsync(s, hs, sizeof(hs), hipMemcpyHostToDevice, c->stream));
+      if (int e = allreduce_halo(c, s, 2, v)) return e;
+      if (int e = fetch(nloc)) return e;
+      check_ids(c, g, h, first, n_chk, n_bad);
+      const double want[2] = {sum_ranks, n_contrib};
+      if (int e = sums_ok(s, 2, want)) return e;
+    }
+    // 3. cgs_exchange: the single-reduction iteration's group (facet terms zero)
+    if (c->cgs && c->wsend) {
+      HIPC(hipMalloc(&ff, sizeof(double) * (size_t)std::max<int64_t>(1, g.ffsize)));
+      HIPC(hipMemsetAsync(ff, 0, sizeof(double) * (size_t)std::max<int64_t>(1, g.ffsize), c->stream));
+      if (int e = fill_ids(c, g, v, first)) return e;
+      const double hs[3] = {(double)(c->rank + 1), 1.0, 2.0};
+      HIPC(hipMemcpyAsync(c->sums, hs, sizeof(hs), hipMemcpyHostToDevice, c->stream));
+      if (int e = cgs_exchange(c, v, ff)) return e;
+      if (int e = fetch(nloc)) return e;
+      check_ids(c, g, h, first, n_chk, n_bad);
+      const double want[3] = {sum_ranks, n_contrib, 2.0 * n_contrib};
+      if (int e = sums_ok(c->sums, 3, want)) return e;
+    }
+    // 4. the distributed multigrid levels' ghost planes, the replicated level's all-reduce
+    for (size_t l = 0; l < c->mg.size() && c->n_parts > 1; ++l) {
+      const MgLevel& L = c->mg[l];
+      const int64_t nl = (int64_t)L.g.n0 * L.g.n1 * L.g.n2;
+      if (L.dist) {
+        if (int e = fill_ids(c, L.g, v, L.first2)) return e;
+        if (int e = halo_grid(c, L.g, v)) return e;
+        if (int e = fetch(nl)) return e;
+        check_ids(c, L.g, h, L.first2, n_chk, n_bad);
+      } else if ((int)l + 1 == c->mg_A) {
+        std::vector<double> a((size_t)nl);
+        for (int64_t i = 0; i < nl; ++i) a[(size_t)i] = (double)(i % 1000) * (c->rank + 1);
+        HIPC(hipMemcpyAsync(v, a.data(), sizeof(double) * (size_t)nl, hipMemcpyHostToDevice, c->stream));
+        if (int e = allreduce_vec(c, v, nl)) return e;
+        if (int e = fetch(nl)) return e;
+        for (int64_t i = 0; i < nl; ++i) {
+          ++*n_chk;
+          if (h[(size_t)i] != (double)(i % 1000) * sum_ranks) ++*n_bad;
+        }
+      }
+    }
+    return TV_OK;
+  };
+  const int e = run();
+  hipStreamSynchronize(c->stream);
+  hipFree(v);
+  hipFree(s);
+  if (ff) hipFree(ff);
+  return e;
+}
+
 // ghost planes of w_i: neighbours' packed boundary planes (RCCL group with
 // the all-reduce of the iteration's sums, or the host-staged transport)
 int cgs_exchange(Ctx* c, double* wout, const double* fout) {
@@ -243,12 +451,12 @@ int cgs_exchange(Ctx* c, double* wout, const double* fout) {
   NCCLC(ncclGroupStart());
   NCCLC(ncclAllReduce(c->sums, c->sums, 3, ncclDouble, ncclSum, c->comm, c->stream));
   if (g.g_lo) {
-    NCCLC(ncclSend(c->wsend, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
-    NCCLC(ncclRecv(wout, plane, ncclDouble, c->rank - 1, c->comm, c->stream));
+    NCCLC(ncclSend(c->wsend, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+    NCCLC(ncclRecv(wout, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
   }
   if (g.g_hi) {
-    NCCLC(ncclSend(c->wsend + plane, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
-    NCCLC(ncclRecv(wout + plane * g.k_end, plane, ncclDouble, c->rank + 1, c->comm, c->stream));
+    NCCLC(ncclSend(c->wsend + plane, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+    NCCLC(ncclRecv(wout + plane * g.k_end, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
   }
   NCCLC(ncclGroupEnd());
   return TV_OK;
@@ -295,6 +503,38 @@ int tv_comm_init(void* ctx, const char* id, int n_ranks, int rank) {
 }
 
 
+int tv_comm_init_loopback(void* ctx, const char* id) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !id) return TV_ERR_ARG;
+  if (c->n_parts < 2) return c->fail(TV_ERR_ARG, "tv_comm_init_loopback: a partition of a partitioned mesh only");
+  if (c->comm || c->host_sendrecv || c->comm_stub) return c->fail(TV_ERR_STATE, "communicator already set");
+  for (size_t k = 0; k < c->um_peer.size(); ++k)  // a self send must match its receive
+    if (c->um_scnt[k] != c->um_rcnt[k])
+      return c->fail(TV_ERR_ARG, "tv_comm_init_loopback: a neighbour's send and receive counts differ");
+  hipSetDevice(c->device);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCLC(ncclCommInitRank(&c->comm, 1, uid, 0));
+  c->nranks = c->n_parts;
+  c->rank = c->part;
+  c->comm_self = true;
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
+  if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
+  HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+
+int tv_comm_check(void* ctx, int64_t* n_checked, int64_t* n_bad) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !n_checked || !n_bad) return TV_ERR_ARG;
+  if (!multi_rank(c) || c->comm_stub)
+    return c->fail(TV_ERR_STATE, "tv_comm_check: a partitioned context with a transport (not the stub)");
+  hipSetDevice(c->device);
+  return comm_check(c, n_checked, n_bad);
+}
+
+
 int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
                       tv_host_sendrecv_fn sendrecv_fn, void* user) {
   Ctx* c = static_cast<Ctx*>(ctx);
@@ -325,6 +565,8 @@ int tv_comm_init_stub(void* ctx) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c) return TV_ERR_ARG;
   if (c->n_parts < 2) return c->fail(TV_ERR_ARG, "tv_comm_init_stub: a partition of a partitioned mesh only");
+  if (c->O.ksp_fixed_its <= 0)  // measurement only: its decoupled solve is no solution
+    return c->fail(TV_ERR_ARG, "tv_comm_init_stub: measurement only, needs options.ksp_fixed_its > 0");
   hipSetDevice(c->device);
   c->nranks = c->n_parts;
   c->rank = c->part;

@@ -455,6 +455,7 @@ int transfer(Ctx* c, int field, double* host, size_t n, int dir) {
   }
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, ((int64_t)need + 255) / 256), 16384);
   if (dir == 0) {
+    if (c->um && c->n_parts > 1 && field != TV_F_T && field != TV_F_T_PREV) c->ghost_dirty |= 1u << field;
     const bool tilde = field == TV_F_S_TILDE || field == TV_F_S_TILDE_NEXT || field == TV_F_SIGMA_TILDE ||
                        field == TV_F_SIGMA_TILDE_NEXT;
     if (tilde) {  // values other than +0.0 end the all-zero tracking of the tilde fields
@@ -517,6 +518,7 @@ void tv_default_options(tv_options* o) {
   o->dg_tile_chunk = 0;
   o->mg_replicate_nodes = 0;
   o->ksp_fixed_its = 0;
+  o->mg_coupling = TV_MG_COUPLING_AUTO;
 }
 
 
@@ -830,6 +832,7 @@ int tv_destroy(void* ctx) {
   if (c->counters) hipFree(c->counters);
   if (c->h_st) hipHostFree(c->h_st);
   if (c->h_sums) hipHostFree(c->h_sums);
+  if (c->d_dirty) hipFree(c->d_dirty);
   if (c->h_halo) hipHostFree(c->h_halo);
   if (c->h_big) hipHostFree(c->h_big);
   if (c->mg_mask0) hipFree(c->mg_mask0);
@@ -930,6 +933,8 @@ int tv_set_field(void* ctx, int field, const double* host, size_t n) {
 int tv_get_field(void* ctx, int field, double* host, size_t n) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !host) return TV_ERR_ARG;
+  if (c->comm_stub)  // a stubbed share solves a decoupled block: timing only, no solution to read
+    return c->fail(TV_ERR_STATE, "tv_get_field: the context runs on the measurement stub (tv_comm_init_stub)");
   hipSetDevice(c->device);
   return transfer(c, field, host, n, 1);
 }
@@ -1035,6 +1040,7 @@ int tv_output_write(void* ctx, double t) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c) return TV_ERR_ARG;
   if (!c->out) return c->fail(TV_ERR_STATE, "output not open");
+  if (c->comm_stub) return c->fail(TV_ERR_STATE, "tv_output_write: the context runs on the measurement stub");
   hipSetDevice(c->device);
   int set = 0;
   double* d = output_acquire(c->out, &set);

@@ -129,6 +129,9 @@ struct Ctx {
   // partitioned GMG (tv_mgdist.cpp): levels 0 .. mg_A - 1 are distributed over
   // the partitions, mg_A .. the coarsest are replicated on every rank
   int mg_A = 0;
+  // options.mg_coupling LOCAL (block Jacobi): every level is this partition's
+  // own slab, the transfers stop at its owned planes, no exchange in the V-cycle
+  bool mg_local = false;
   double* mg_mask0 = nullptr;  // level 0 restriction mask when mg_A == 1 (1 owned / 0 ghost)
   double* h_big = nullptr;     // pinned staging of vector all-reduces (host-staged transport)
   size_t h_big_n = 0;
@@ -172,6 +175,15 @@ struct Ctx {
   tv_host_sendrecv_fn host_sendrecv = nullptr;
   void* host_user = nullptr;
   bool comm_stub = false;    // tv_comm_init_stub: measurement of one rank's share, no transport
+  // tv_comm_init_loopback: a ONE-rank RCCL communicator; every neighbour of the
+  // partition is this rank itself (peer 0), so the production RCCL groups run
+  // with self send/recv pairs and one-rank all-reduces (transport test)
+  bool comm_self = false;
+  // partitioned unstructured mesh: T-space / sigma-space fields written from
+  // the host since the last step (tv_set_field writes owned dofs only); their
+  // ghosts are refreshed collectively at the next step (refresh_dirty_ghosts)
+  uint32_t ghost_dirty = 0;
+  double* d_dirty = nullptr;
   double* h_halo = nullptr;  // pinned staging: 2 send + 2 recv planes
   size_t h_halo_n = 0;
   // in-solve kernel timing (tv_kernel_timing): the fused matvec and the PCG
@@ -246,12 +258,20 @@ bool multi_rank(const Ctx* c);
 int halo(Ctx* c, double* v);  // ghost planes of a T-space vector of the fine grid
 int halo_grid(Ctx* c, const CgGrid& g, double* v);  // ghost planes of a vector of grid g (a GMG level)
 int allreduce_vec(Ctx* c, double* v, int64_t n);
+int halo_um(Ctx* c, double* v);  // ghosts of a partitioned unstructured mesh's T-space vector
+int comm_check(Ctx* c, int64_t* n_checked, int64_t* n_bad);  // tv_comm_check
 int allreduce_halo(Ctx* c, double* sums, int n, double* v);
 int visco_timing_flush(Ctx* c);  // tv_solver.cpp  // one RCCL group: n-scalar sum + halo(v)  // sum over the ranks of a device vector, in place
 int allreduce(Ctx* c, double* v, int n);
 int reduce_logic(Ctx* c, int n, int W, int kind, int check_done);  // records -> (all-reduce) -> scalar logic
 int cgs_raxis(const Ctx* c);
 int cgs_exchange(Ctx* c, double* wout, const double* fout);
+// a partitioned context must have its transport before it solves (the solve
+// would otherwise run on stale ghosts with local-only norms)
+int require_comm(Ctx* c, const char* what);
+// partitioned unstructured mesh: the ghost values of every field some rank
+// wrote from the host since the last step, from their owners (collective)
+int refresh_dirty_ghosts(Ctx* c);
 
 // ---- tv_solver.cpp ----
 void op_residual(Ctx* c, const double* T, const double* Tp, double* F);

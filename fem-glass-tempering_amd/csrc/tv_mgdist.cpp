@@ -99,6 +99,11 @@ LevelRef level_ref(Ctx* c, size_t l, const double* T0) {
 int mg_setup_dist(Ctx* c) {
   if (c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "partitioned GMG: CG1 temperature space");
   const int P = c->n_parts, p = c->part;
+  // AUTO = GLOBAL: block Jacobi needs ~2.4x the Krylov iterations at C4's cell
+  // sizes (5 -> 10-12 per solve for 2-8 slabs, tools/mg_coupling_model.py),
+  // more than its saved exchanges are worth
+  const bool local = c->O.mg_coupling == TV_MG_COUPLING_LOCAL;
+  c->mg_local = local;
   std::vector<double> tmp, Xf[3];
   for (int s = 0; s < 3; ++s) Xf[s] = storage_coords(c, s, tmp);
   const double da = c->P.dt * c->P.alpha;
@@ -142,7 +147,10 @@ int mg_setup_dist(Ctx* c) {
       min_own = std::min(min_own, hi - lo);
     }
     const int64_t rep = c->O.mg_replicate_nodes > 0 ? c->O.mg_replicate_nodes : kMgReplicateNodes;
-    if (nodes <= rep || min_own < 2) {
+    if (min_own < 2 && local)  // a slab hierarchy needs >= 2 planes per level on every partition
+      return c->fail(TV_ERR_ARG, "partitioned GMG (local coupling): a level leaves a partition with < 2 planes; "
+                                 "fewer levels (mg_levels) or fewer partitions");
+    if (!local && (nodes <= rep || min_own < 2)) {
       A = l;
       break;
     }
@@ -209,10 +217,21 @@ int mg_setup_dist(Ctx* c) {
         nc = n2loc[l];
         std::vector<int> piL(2 * (size_t)nf), riL(3 * (size_t)nc);
         std::vector<double> pwL(2 * (size_t)nf), rwL(3 * (size_t)nc);
+        // LOCAL coupling (block Jacobi): a fine plane interpolates only from the
+        // coarse planes this partition owns and a coarse plane restricts only
+        // from owned fine planes (R = P^T of the slab); excluded entries keep
+        // weight 0 and point at an owned plane (finite data)
+        const int cown0 = own_lo[l] - c0, cown1 = own_hi[l] - c0;
+        const int fown0 = own_lo[l - 1] - f0, fown1 = own_hi[l - 1] - f0;
         for (int lf = 0; lf < nf; ++lf)
           for (int e = 0; e < 2; ++e) {
             const int cg = pi[2 * (size_t)(f0 + lf) + e] - c0;  // coarse local
-            const bool ok = cg >= 0 && cg < nc;
+            const bool ok = local ? (cg >= cown0 && cg < cown1 && lf >= fown0 && lf < fown1) : (cg >= 0 && cg < nc);
+            if (local && !ok) {
+              piL[2 * (size_t)lf + e] = std::min(std::max(cg, cown0), cown1 - 1);
+              pwL[2 * (size_t)lf + e] = 0.0;
+              continue;
+            }
             // every fine local plane interpolates from coarse local planes (nesting)
             if (!ok && pw[2 * (size_t)(f0 + lf) + e] != 0.0)
               return c->fail(TV_ERR_ARG, "partitioned GMG: prolongation leaves the local window (internal)");
@@ -222,7 +241,12 @@ int mg_setup_dist(Ctx* c) {
         for (int lc = 0; lc < nc; ++lc)
           for (int q = 0; q < 3; ++q) {
             const int fgl = ri[3 * (size_t)(c0 + lc) + q] - f0;  // fine local
-            const bool ok = fgl >= 0 && fgl < nf;
+            const bool ok = local ? (fgl >= fown0 && fgl < fown1 && lc >= cown0 && lc < cown1) : (fgl >= 0 && fgl < nf);
+            if (local && !ok) {
+              riL[3 * (size_t)lc + q] = std::min(std::max(fgl, fown0), fown1 - 1);
+              rwL[3 * (size_t)lc + q] = 0.0;
+              continue;
+            }
             // outside the fine window (a coarse ghost plane's far side, or a coarse
             // plane of the replicated level away from this slab): weight 0, and the
             // restriction never writes those planes from this rank's data
@@ -242,9 +266,10 @@ int mg_setup_dist(Ctx* c) {
       x.cn[s] = nc;
       x.coarse[s] = pl.coarse[s];
     }
-    // prolongation into every local fine plane (ghost planes included)
-    x.f_kb = 0;
-    x.f_ke = x.fn[2];
+    // prolongation into every local fine plane (ghost planes included; LOCAL:
+    // the owned ones, the ghost planes of a slab's V-cycle stay zero)
+    x.f_kb = local ? own_lo[l - 1] - first2[l - 1] : 0;
+    x.f_ke = local ? own_hi[l - 1] - first2[l - 1] : x.fn[2];
     if (Lv.dist) {  // restriction: the owned coarse planes
       x.c_kb = Lv.g.k_begin;
       x.c_ke = Lv.g.k_end;
@@ -310,17 +335,20 @@ int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
   const size_t A = (size_t)c->mg_A;
   const double* dmask = c->dir_on ? c->dinv : nullptr;  // Dirichlet: the free subspace (level 0)
   const size_t ldown = std::min(A, L);  // distributed levels
+  // the V-cycle's ghost exchanges (LOCAL coupling: none -- the slab's own cycle,
+  // whose ghost planes hold zeros)
+  auto vhalo = [&](const CgGrid& g, double* v) -> int { return c->mg_local ? TV_OK : halo_grid(c, g, v); };
   // ---- down: distributed levels 0 .. A - 1
   for (size_t l = 0; l < ldown; ++l) {
     const LevelRef r = level_ref(c, l, T);
-    if (int e = halo_grid(c, *r.g, r.x)) return e;  // ghosts of the pre-smoothed x_l
+    if (int e = vhalo(*r.g, r.x)) return e;  // ghosts of the pre-smoothed x_l
     if (l + 1 == L) break;                           // the coarsest level, distributed: x_l is its solve
     launch_cg_japply_partial(*r.g, r.T, r.x, r.w, c->st, s);
     FaceAdd fa = cg_face_add(*r.g, r.off);
     MgLevel& C = c->mg[l];
     if (l + 1 < A) {  // into a distributed level: exchange the residual, restrict on the owned coarse planes
       launch_mg_resid(r.n_own, c->st, r.b + r.off, r.w + r.off, &fa, l == 0 && dmask ? dmask + r.off : nullptr, s);
-      if (int e = halo_grid(c, *r.g, r.w)) return e;
+      if (int e = vhalo(*r.g, r.w)) return e;
       launch_mg_restrict(C.xf, c->st, r.w, nullptr, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
     } else {  // into the replicated level A: masked partial restriction, summed over the ranks
       const double* mask = (l == 0) ? c->mg_mask0 : c->mg[l - 1].mask;
@@ -346,7 +374,7 @@ int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
     const FaceAdd fa = cg_face_add(*r.g, r.off);
     if (l > 0) {
       launch_mg_jacobi(r.n_own, c->st, r.b + r.off, r.w + r.off, &fa, r.dinv + r.off, r.omega, r.x + r.off, 1, s);
-      if (int e = halo_grid(c, *r.g, r.x)) return e;
+      if (int e = vhalo(*r.g, r.x)) return e;
     } else {
       launch_mg_post(r.n_own, c->st, r.x + r.off, r.b + r.off, r.w + r.off, &fa, r.dinv + r.off, r.omega,
                      c->z + r.off, c->partials, tail, s);

@@ -478,14 +478,47 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
 
 using namespace tv;
 
+// tv_precond_apply on a partition (collective: every rank calls it): the
+// operator the partitioned Krylov solve applies, on this rank's owned dofs --
+// Jacobi, or the partitioned V-cycle (GLOBAL: the distributed cycle of the
+// whole box; LOCAL: this slab's own cycle)
+static int precond_apply_part(Ctx* c, const double* r_dev, double* z_dev) {
+  if (int e = require_comm(c, "tv_precond_apply")) return e;
+  if (c->um || c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "tv_precond_apply: partitioned CG1 box meshes");
+  const double* T = c->f[TV_F_T].ptr;
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  hipStream_t s = c->stream;
+  if (int e = halo(c, c->f[TV_F_T].ptr)) return e;  // the PC setup reads the ghost planes' T (side-face facets)
+  launch_cg_diag(c->cg, T, c->dinv, 1, s, c->dinv_interior);
+  c->dinv_interior = true;
+  if (c->dir_on) launch_bc_mask(c, c->dinv);
+  if (!c->mg_on) {
+    launch_mg_jacobi(n, nullptr, r_dev, nullptr, nullptr, c->dinv + off, 1.0, z_dev, 0, s);
+  } else {
+    PcgState h{};
+    HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, s));
+    if (int e = mg_prepare_dist(c, T)) return e;
+    if (c->dir_on)
+      if (int e = halo(c, c->dinv)) return e;
+    if (c->mg_mask0) launch_mg_ownmask(c->nT, off, off + n, c->dir_on ? c->dinv : nullptr, c->mg_mask0, s);
+    HIPC(hipMemcpyAsync(c->r + off, r_dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
+    launch_mg_jacobi(n, c->st, c->r + off, nullptr, nullptr, c->dinv + off, c->mg_omega0, c->mgx + off, 0, s);
+    if (int e = mg_apply0_dist(c, T, nullptr)) return e;
+    HIPC(hipMemcpyAsync(z_dev, c->z + off, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(s));
+  return TV_OK;
+}
+
 extern "C" {
 
 int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !r_dev || !z_dev) return TV_ERR_ARG;
-  if (c->n_parts > 1) return c->fail(TV_ERR_ARG, "tv_precond_apply: one partition only");
   hipSetDevice(c->device);
   HIPC(hipDeviceSynchronize());  // inputs written on other streams (header)
+  if (c->n_parts > 1) return precond_apply_part(c, r_dev, z_dev);
   const double* T = c->f[TV_F_T].ptr;
   const int64_t n = c->nT;
   hipStream_t s = c->stream;

@@ -319,6 +319,8 @@ int dirichlet_pre(Ctx* c, const double* T) {
 
 // dolfinx NewtonSolver::solve, convergence_criterion = "incremental"
 int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
+  if (int e = require_comm(c, "Newton solve")) return e;
+  if (int e = refresh_dirty_ghosts(c)) return e;
   double* T = c->f[TV_F_T].ptr;
   const double* Tp = c->f[TV_F_T_PREV].ptr;
   // NonlinearProblem.form: ghost update of the state before the first F

@@ -51,9 +51,10 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 4  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+#define TV_ABI_VERSION 5  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
                             3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its;
-                            4: tv_upart_desc / tv_create_unstructured_part */
+                            4: tv_upart_desc / tv_create_unstructured_part;
+                            5: tv_comm_init_loopback, tv_comm_check, tv_options.mg_coupling */
 
 /* status codes */
 #define TV_OK 0
@@ -170,7 +171,25 @@ typedef struct {
                              iterations, with no convergence test (PETSc
                              KSP_NORM_NONE + max_it; timing of partition shares
                              with the communication stubbed)                    */
+  int mg_coupling;        /* partitioned GMG: TV_MG_COUPLING_AUTO / _GLOBAL / _LOCAL */
 } tv_options;
+
+/* Coupling of the partitioned geometric multigrid (the Krylov iteration is
+ * always global: matvec over the ghost planes, all-reduced dot products):
+ *   GLOBAL  the V-cycle of the whole box, distributed (ghost planes of every
+ *           level exchanged, the small coarse levels replicated): the same
+ *           preconditioner as on one partition, ~5 exchanges per V-cycle;
+ *   LOCAL   block Jacobi over the partitions: each partition runs the V-cycle
+ *           of its own slab (the hierarchy of its owned planes, zero values
+ *           beyond them: the principal block of the operator) -- no exchange
+ *           inside the preconditioner, 2 exchange points per Krylov iteration.
+ *           The Krylov counts then depend on the partition count, as PCGAMG's
+ *           (its smoothers and coarse solve are process-local) do: ~2.4x the
+ *           GLOBAL count at C4's cell sizes (tools/mg_coupling_model.py);
+ *   AUTO    GLOBAL. */
+#define TV_MG_COUPLING_AUTO 0
+#define TV_MG_COUPLING_GLOBAL 1
+#define TV_MG_COUPLING_LOCAL 2
 
 /* 3D DG1 Jacobian kernel: AUTO = TILE, the marching tile kernel (production);
  * CELLS = one thread per cell, the straightforward SIPG evaluation the tile
@@ -262,7 +281,8 @@ int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, co
                            const tv_options* opts, int device, void** ctx_out);
 /* partition `part->part` of a distributed unstructured mesh (local mesh as
  * tv_upart_desc describes); the communicator (tv_comm_init / _host) must be
- * set before the first step.  Jacobi-PCG (KSPCG form), no Dirichlet mode. */
+ * set before the first step (a solve without one returns TV_ERR_STATE).
+ * Jacobi-PCG (KSPCG form); Dirichlet mode as on one partition. */
 int tv_create_unstructured_part(const tv_umesh_desc* local_mesh, const tv_upart_desc* part, const tv_fe_config* fe,
                                 const tv_params* params, const tv_options* opts, int device, void** ctx_out);
 int tv_destroy(void* ctx);
@@ -316,7 +336,10 @@ int tv_jacobian_diag(void* ctx, double* d_dev);                       /* diag J(
 /* z = B r with the context's preconditioner at the current T (tv_options.
  * preconditioner): Jacobi z = r / diag J(T), or one V-cycle of the geometric
  * multigrid -- exactly the operator the Krylov solve applies (the PC setup of
- * the current T included).  Single partition; uses the solver's work vectors. */
+ * the current T included).  Uses the solver's work vectors.  On a partition of
+ * a box mesh (owned dofs in and out) the call is collective: every rank calls
+ * it, through its communicator (the distributed or the per-slab V-cycle,
+ * tv_options.mg_coupling). */
 int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev);
 
 /* ---- solvers -------------------------------------------------------------- */
@@ -370,7 +393,25 @@ typedef int (*tv_host_sendrecv_fn)(const double* send, size_t n_send, int peer_s
  * every exchange fills the ghosts of the solver's vectors with zeros (the
  * partition solves its own block, so the operators stay SPD), the
  * temperature ghosts keep their values, every reduction stays local. */
-int tv_comm_init_stub(void* ctx);
+int tv_comm_init_stub(void* ctx);   /* needs options.ksp_fixed_its > 0; tv_get_field and
+                                       tv_output_write then refuse (TV_ERR_STATE) */
+/* Transport test on ONE GPU: a one-rank RCCL communicator (id from
+ * tv_comm_get_unique_id) on which every neighbour of this partition is the rank
+ * itself -- the production RCCL groups run unchanged with self send/recv pairs
+ * and one-rank all-reduces, so each ghost plane receives the boundary plane
+ * this partition sends (the plane next to it, not the neighbour's).  The
+ * host-staged transport with a callback that copies a send into its receive
+ * gives the same exchanges (tests/test_loopback.py compares the two). */
+int tv_comm_init_loopback(void* ctx, const char* id);
+/* Collective check of the transport (every rank calls it): the exchange
+ * patterns the solver issues -- ghost planes of the fine grid and of every
+ * distributed multigrid level, the sums + ghosts group of a KSPCG iteration,
+ * the single-reduction group, the replicated level's vector all-reduce, the
+ * per-neighbour unstructured halo -- run on vectors of global node ids and are
+ * compared on the host with what each ghost must receive.  n_bad = 0 when
+ * every one of the n_checked received values is right.  Replaces nothing in
+ * the reference (a pre-flight of :351's scatter_forward). */
+int tv_comm_check(void* ctx, int64_t* n_checked, int64_t* n_bad);
 int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
                       tv_host_sendrecv_fn sendrecv_fn, void* user);
 

@@ -13,10 +13,11 @@ tolerance, the preconditioner only changes the Krylov counts).
 Algorithm (each step as tv_amg.cpp states it):
   * A = the T-independent cell operator M + dt alpha K, exact zeros dropped;
   * greedy aggregation over every off-diagonal nonzero, three passes;
-  * P = (I - 4 / (3 lambda) D^-1 A) P0, lambda by 15 power iterations of
-    D^-1 A from the fixed xorshift start vector, rounded to float32 (the
-    device's storage of the transfers); R = P^T; A_c = R (A P) in double;
-  * coarse weights omega_l = 2 / (1.1 lambda_max(D^-1 A_l)) (20 iterations);
+  * P = (I - 4 / (3 lambda) D^-1 A) P0, lambda = lambda_max(D^-1 A) as the
+    largest Ritz value of 20 Lanczos steps from the fixed xorshift start
+    vector, rounded to float32 (the device's storage of the transfers);
+    R = P^T; A_c = R (A P) in double;
+  * coarse weights omega_l = 2 / (1.1 lambda_max(D^-1 A_l)) (20 Lanczos steps);
     level-0 weight 2 / (1.1 lambda_max(D^-1 J(T))) (30 iterations, the
     device's mg_dg_lambda);
   * cycle: z = omega0 D0^-1 r + P_0 V_1(R_0 r); V_l: x = omega D^-1 b,
@@ -41,16 +42,51 @@ def _xorshift_start(n, seed):
     return out
 
 
+def tridiag_max_eig(a, b):
+    """tv_amg.cpp tridiag_max_eig: bisection on the Sturm count."""
+    k = len(a)
+    r = [(abs(b[i - 1]) if i > 0 else 0.0) + (abs(b[i]) if i + 1 < k else 0.0) for i in range(k)]
+    lo = min(a[0], min(a[i] - r[i] for i in range(k)))
+    hi = max(a[0], max(a[i] + r[i] for i in range(k)))
+
+    def below(x):
+        cnt, d = 0, 1.0
+        for i in range(k):
+            d = a[i] - x - (b[i - 1] * b[i - 1] / d if i > 0 else 0.0)
+            if d == 0.0:
+                d = -1e-300
+            cnt += d < 0.0
+        return cnt
+    it = 0
+    while it < 200 and hi - lo > 1e-15 * max(abs(lo), abs(hi)):
+        mid = 0.5 * (lo + hi)
+        if below(mid) == k:
+            hi = mid
+        else:
+            lo = mid
+        it += 1
+    return hi
+
+
 def lam_max_host(A, dinv, its):
-    """tv_amg.cpp lam_max: normalise, w = D^-1 A v, lambda = |w|, v = w."""
-    v = _xorshift_start(A.shape[0], 0x2545F4914F6CDD1D)
-    lam = 1.0
-    for _ in range(its):
-        v = v / np.sqrt(np.dot(v, v))
-        w = dinv * (A @ v)
-        lam = np.sqrt(np.dot(w, w))
-        v = w
-    return lam
+    """tv_amg.cpp lam_max: the largest Ritz value of `its` Lanczos steps on
+    D^-1/2 A D^-1/2 from the fixed xorshift start vector."""
+    sd = np.sqrt(dinv)
+    q = _xorshift_start(A.shape[0], 0x2545F4914F6CDD1D)
+    q = q / np.sqrt(np.dot(q, q))
+    qp = np.zeros_like(q)
+    al, be, beta = [], [], 0.0
+    for j in range(its):
+        w = sd * (A @ (sd * q)) - beta * qp
+        alpha = float(np.dot(w, q))
+        w = w - alpha * q
+        al.append(alpha)
+        beta = float(np.sqrt(np.dot(w, w)))
+        if j + 1 == its or not beta > 0.0:
+            break
+        be.append(beta)
+        qp, q = q, w / beta
+    return tridiag_max_eig(al, be)
 
 
 def lam_max_device(J, dinv, its=30):
@@ -110,7 +146,7 @@ def build(V, max_levels=12):
         agg, na = aggregate(A)
         if na < 1 or na * 10 > A.shape[0] * 7:
             break
-        lam = lam_max_host(A, dinv, 15)
+        lam = lam_max_host(A, dinv, 20)
         P0 = sp.csr_matrix((np.ones(A.shape[0]), (np.arange(A.shape[0]), agg)), shape=(A.shape[0], na))
         P = sp.csr_matrix(P0 - (4.0 / (3.0 * lam)) * (sp.diags(dinv) @ (A @ P0)))
         P.data = P.data.astype(np.float32).astype(np.float64)  # the device stores the transfers in float32

@@ -195,84 +195,8 @@ def test_preconditioner_argument_checked():
 
 
 # ---- the V-cycle operator itself against a numpy restatement --------------------
-def _axis_mats(x):
-    """assembled 1D P1 mass / stiffness on nodes x (a single node: M = 1, K = 0)"""
-    import scipy.sparse as sp
-    n = len(x)
-    if n == 1:
-        return sp.csr_matrix(np.ones((1, 1))), sp.csr_matrix((1, 1))
-    h = np.diff(x)
-    M = np.zeros((n, n))
-    K = np.zeros((n, n))
-    for e in range(n - 1):
-        M[e:e + 2, e:e + 2] += h[e] * np.array([[1.0 / 3.0, 1.0 / 6.0], [1.0 / 6.0, 1.0 / 3.0]])
-        K[e:e + 2, e:e + 2] += np.array([[1.0, -1.0], [-1.0, 1.0]]) / h[e]
-    return sp.csr_matrix(M), sp.csr_matrix(K)
-
-
-def _kron3(z, y, x):
-    import scipy.sparse as sp
-    return sp.kron(z, sp.kron(y, x, format="csr"), format="csr")  # node i + n0 (j + n1 k)
-
-
-def _omega(axes, da):
-    """2 / (1.1 b), b = the Gershgorin bound of D^-1 (M + da K) (rows of the cell
-    operator, floor 2.25 for the Robin facet masses, x 1.05) -- mg_gershgorin"""
-    (Mx, Kx), (My, Ky), (Mz, Kz) = [_axis_mats(a) for a in axes]
-    A = _kron3(Mz, My, Mx) + da * (_kron3(Mz, My, Kx) + _kron3(Mz, Ky, Mx) + _kron3(Kz, My, Mx))
-    b = float(np.max(np.asarray(abs(A).sum(axis=1)).ravel() / A.diagonal()))
-    return 2.0 / (1.1 * (max(b, 2.25) * 1.05))
-
-
-def _vcycle_reference(axes, T, mp, dt, levels):
-    """The box hierarchy of tv_mgsolve.cpp mg_setup restated with the oracle's
-    assembled Jacobians: every other node plus the last one along each axis with
-    >= 2 cells, P = linear interpolation (kron of the per-axis maps), R = P^T,
-    coarse J(T) re-assembled with T injected, damped Jacobi before and after the
-    coarse correction, one Jacobi step on the coarsest level."""
-    import scipy.sparse as sp
-    da = dt * mp["alpha"]
-    prm = O.ThermalParams.from_dict(mp)
-    lev = []
-    Xp = [np.asarray(a, dtype=float) for a in axes]
-    Tp = T
-    while True:
-        mesh = O.rectilinear_mesh(Xp)
-        J = O.HeatForm(O.Space(mesh, "CG", 1), dt, prm).jacobian(Tp).tocsr()
-        lev.append({"J": J, "d": J.diagonal(), "omega": _omega(Xp, da)})
-        if len(lev) == levels:
-            break
-        keep, Ps = [], []
-        for a in Xp:
-            nf = len(a)
-            k = np.ones(nf, dtype=bool)
-            if nf - 1 >= 2:
-                k = (np.arange(nf) % 2 == 0) | (np.arange(nf) == nf - 1)
-            cpos = np.cumsum(k) - 1
-            P = np.zeros((nf, int(k.sum())))
-            for i in range(nf):
-                if k[i]:
-                    P[i, cpos[i]] = 1.0
-                else:
-                    wl = (a[i + 1] - a[i]) / (a[i + 1] - a[i - 1])
-                    P[i, cpos[i - 1]] = wl
-                    P[i, cpos[i + 1]] = 1.0 - wl
-            keep.append(k)
-            Ps.append(sp.csr_matrix(P))
-        lev[-1]["P_to_coarse"] = _kron3(Ps[2], Ps[1], Ps[0])
-        n = [len(a) for a in Xp]
-        Tp = Tp.reshape(n[2], n[1], n[0])[np.ix_(keep[2], keep[1], keep[0])].ravel()
-        Xp = [a[k] for a, k in zip(Xp, keep)]
-
-    def cycle(l, b):
-        L = lev[l]
-        x = L["omega"] * b / L["d"]  # the pre-smoothing step from 0
-        if l + 1 < len(lev):
-            P = L["P_to_coarse"]
-            x = x + P @ cycle(l + 1, P.T @ (b - L["J"] @ x))
-            x = x + L["omega"] * (b - L["J"] @ x) / L["d"]
-        return x
-    return lambda r: cycle(0, r)
+# (tests/gmg_reference.py: the box hierarchy restated on the oracle's assembled Jacobians)
+from gmg_reference import vcycle_reference as _vcycle_reference  # noqa: E402
 
 
 VCYCLE_CASES = {

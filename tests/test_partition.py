@@ -107,7 +107,7 @@ def test_gloo_two_rank_halo_exchange_cpu():
     assert all(ok for _, ok in res), res
 
 
-def _partition_check(world, comm, port, extra=()):
+def _partition_check(world, comm, port, extra=(), krylov_slack=1):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "partition_check.py"),
            "--comm", comm, *extra]
@@ -120,8 +120,9 @@ def _partition_check(world, comm, port, extra=()):
     assert res["xi"] < 1e-6, res
     assert res["sigma"] < 1e-6, res
     # the global reductions make the partitioned solve take the same iterations
+    # (krylov_slack None: a partition-dependent preconditioner, Newton counts only)
     for (n1, k1), (n2, k2) in zip(res["its_parts"], res["its_single"]):
-        assert n1 == n2 and abs(k1 - k2) <= n1, res
+        assert n1 == n2 and (krylov_slack is None or abs(k1 - k2) <= krylov_slack * n1), res
     return res
 
 
@@ -153,7 +154,7 @@ def test_partitioned_gmg_matches_single_partition(world, rep):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     _partition_check(world, "host", 29750 + 10 * world + (rep % 7), ("--pc", "gmg", "--mg-replicate", str(rep),
-                                                                       "--pcg", "kspcg"))
+                                                                       "--pcg", "kspcg", "--mg-coupling", "global"))
 
 
 @pytest.mark.gpu
@@ -165,6 +166,58 @@ def test_partitioned_output_series():
         pytest.skip("no GPU")
     res = _partition_check(2, "host", 29748, ("--steps", "2", "--output"))
     assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("coupling,world,rep", [("global", 2, 0), ("global", 3, 0), ("global", 3, 1),
+                                                ("local", 2, 0), ("local", 3, 0)])
+def test_partitioned_vcycle_operator_matches_restatement(coupling, world, rep):
+    """The partitioned V-cycle in isolation (tv_precond_apply on every rank,
+    host-staged transport): GLOBAL coupling -- its per-level ghost exchanges and
+    the replicated levels' all-reduce -- reproduces the single-partition V-cycle
+    of the whole box; LOCAL coupling (block Jacobi) each rank's block of the
+    numpy restatement (tests/gmg_reference.py).  1e-11, symmetric, positive."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(29770 + 3 * world + rep + (coupling == "local") * 20),
+           os.path.join(ROOT, "tests", "vcycle_part_check.py"), "--coupling", coupling, "--mg-replicate", str(rep)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("VCYCLE_CHECK ")]
+    assert line, out.stdout[-2000:] + out.stderr[-3000:]
+    res = json.loads(line[0].split(" ", 1)[1])
+    print("[vcycle-part]", json.dumps(res), flush=True)
+    assert res["err"] < 1e-11 and res["sym"] < 1e-12 and res["rBr"] > 0.0, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_local_gmg_solves(world):
+    """LOCAL coupling (block-Jacobi V-cycle, the partitioned default): the
+    Newton solution equals the single partition's (T <= 1e-12; the Krylov
+    tolerance is met either way), the Newton counts too; the Krylov counts may
+    differ (they depend on the partition count, as PCGAMG's do)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _partition_check(world, "host", 29790 + world, ("--pc", "gmg", "--pcg", "kspcg", "--mg-coupling", "local"),
+                           krylov_slack=None)
+    print("[local-gmg]", json.dumps(res), flush=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc", ["jacobi", "gmg"])
+def test_partitioned_dirichlet_matches_single_partition(pc):
+    """Paper mode with T = T_ambient on the exterior boundary on 2 slabs: the
+    lifting vector dB is exchanged before J dB, each slab masks its own
+    constrained rows; Jacobi and the distributed multigrid reproduce the
+    single partition."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _partition_check(2, "host", 29760 + (pc == "gmg"), ("--dirichlet", "--steps", "2", "--pc", pc, "--pcg", "kspcg",
+                                                        "--mg-coupling", "global"))
 
 
 @pytest.mark.gpu
@@ -218,7 +271,10 @@ def test_rccl_partitioned_run_matches_single_partition(world):
     if n < world:
         pytest.skip(f"{world} GPUs needed, {n} visible")
     _partition_check(world, "rccl", 29720 + world, ("--cells", "12,48,6"))
-    _partition_check(world, "rccl", 29730 + world, ("--cells", "12,48,6", "--pc", "gmg", "--pcg", "kspcg"))
+    _partition_check(world, "rccl", 29730 + world, ("--cells", "12,48,6", "--pc", "gmg", "--pcg", "kspcg",
+                                                     "--mg-coupling", "global"))
+    _partition_check(world, "rccl", 29740 + world, ("--cells", "12,48,6", "--pc", "gmg", "--pcg", "kspcg",
+                                                     "--mg-coupling", "local"), krylov_slack=None)
 
 
 @pytest.mark.gpu

@@ -156,6 +156,35 @@ def test_partitioned_unstructured_host_edit():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("field", ["Tf", "Tf_partial", "xi"])
+def test_partitioned_unstructured_host_edit_state_field(field):
+    """A host edit of a viscoelastic state field on the owning rank only: the
+    ghost copies of that field are refreshed from their owners at the next
+    step (one all-reduce of the per-field write flags, then the halo of the
+    written fields), so every part's ghost vertices keep evolving as their
+    owners do and the written series agree at shared vertices."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _partition_check(2, 29830, ("--cells", "10,30,5", "--edit", "--edit-field", field, "--steps", "2",
+                                      "--output"))
+    assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_unstructured_dirichlet(world):
+    """Paper mode with T = T_ambient on the exterior boundary on a distributed
+    distorted mesh: each part constrains its owned boundary vertices, the
+    lifting vector's ghosts come from their owners before J dB; the parts
+    reproduce the single partition."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _partition_check(world, 29833 + world, ("--cells", "10,30,5", "--dirichlet", "--steps", "2"))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_rccl_partitioned_unstructured(world):
     """The production transport for the unstructured partition: one rank per

@@ -1,0 +1,123 @@
+"""The production RCCL transport on ONE GPU: a partition of a partitioned mesh
+runs on a one-rank RCCL communicator whose every neighbour is the rank itself
+(tv_comm_init_loopback), so each RCCL group the solver issues -- the ghost
+planes of the fine grid and of the distributed multigrid levels, the sums +
+ghosts group closing a KSPCG iteration, the single-reduction group, the
+replicated multigrid level's vector all-reduce, the per-neighbour unstructured
+halo -- executes in real RCCL with self send/recv pairs.
+
+Per case:
+  1. tv_comm_check on the loopback communicator: every received value equals
+     the value sent (n_bad == 0);
+  2. the same partition with the host-staged transport and a callback that
+     copies each send into its receive (the loopback semantics through the
+     production host path): a few coupled steps on both must give bitwise
+     identical T / phi / xi / sigma and identical Newton / Krylov counts.
+
+    python tools/loopback_check.py [--case NAME ...]     (prints LOOPBACK <json> per case)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fem-glass-tempering_amd"))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")  # one process: the bootstrap needs no other interface
+
+from tvfem import box_mesh, distorted_box_mesh  # noqa: E402
+from tvfem import _native as N  # noqa: E402
+from tvfem.problem import ThermoViscoProblem  # noqa: E402
+
+MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 800.0, "alpha": 1.0, "htc": 280.1,
+      "rho": 2500.0, "cp": 1433.0, "k": 1.0, "H": 627.8e3, "Tb": 869.0, "Rg": 8.314, "alpha_solid": 9.1e-6,
+      "alpha_liquid": 25.1e-6}
+CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+
+# name: (mesh kind, cells, parts, part, Krylov form, preconditioner, replication bound)
+CASES = {
+    "box_single_mid": ("box", (10, 30, 5), 3, 1, "single", "jacobi", 0),
+    "box_kspcg_mid": ("box", (10, 30, 5), 3, 1, "kspcg", "jacobi", 0),
+    "box_kspcg_first": ("box", (10, 30, 5), 2, 0, "kspcg", "jacobi", 0),
+    "box_gmg_replicated": ("box", (10, 30, 5), 3, 1, "kspcg", "gmg", 0),
+    "box_gmg_distributed": ("box", (10, 30, 5), 3, 1, "kspcg", "gmg", 1),
+    "um_first": ("distorted", (6, 12, 3), 2, 0, "kspcg", "jacobi", 0),
+    "um_mid": ("distorted", (6, 12, 3), 3, 1, "kspcg", "jacobi", 0),
+}
+
+
+def _problem(kind, cells, parts, part, pcg, pc, rep):
+    mesh = (distorted_box_mesh if kind == "distorted" else box_mesh)([2.0, 6.0, 1.0], list(cells))
+    kw = {} if kind == "distorted" else {"part_axis": 1}
+    return ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, n_parts=parts, part=part, verbose=False,
+                              pcg_variant=pcg, preconditioner=pc, mg_replicate_nodes=rep, write_output=False, **kw)
+
+
+def _host_loopback(p):
+    """host-staged transport whose every exchange comes back to the sender"""
+    def allreduce(ptr, n, user):  # one contribution: the sum is the value itself
+        return 0
+
+    def sendrecv(sptr, ns, peer_s, rptr, nr, peer_r, user):
+        if ns != nr:
+            return 1
+        C.memmove(rptr, sptr, 8 * ns)
+        return 0
+    p._host_cbs = (N.HOST_ALLREDUCE_FN(allreduce), N.HOST_SENDRECV_FN(sendrecv))
+    N.check(p._lib.tv_comm_init_host(p._ctx, p._n_parts, p._part, p._host_cbs[0], p._host_cbs[1], None), p._ctx)
+
+
+def _steps(p, steps):
+    p.setup()
+    its, err = [], None
+    try:
+        for _ in range(steps):
+            p.solve_timestep()
+            its.append((p.last_newton_iterations, p.last_krylov_iterations))
+    except Exception as e:  # the same failure on both transports is still agreement
+        err = f"{type(e).__name__}: {e}"
+    out = {k: p.get_field(k) for k in ("T", "phi", "xi", "sigma")} if err is None else {}
+    return out, its, err
+
+
+def run_case(name, steps=3):
+    kind, cells, parts, part, pcg, pc, rep = CASES[name]
+    lib = N.load_library()
+    # RCCL loopback
+    a = _problem(kind, cells, parts, part, pcg, pc, rep)
+    uid = C.create_string_buffer(lib.tv_comm_unique_id_size())
+    N.check(lib.tv_comm_get_unique_id(uid))
+    N.check(lib.tv_comm_init_loopback(a._ctx, uid.raw), a._ctx)
+    nchk, nbad = C.c_int64(), C.c_int64()
+    N.check(lib.tv_comm_check(a._ctx, C.byref(nchk), C.byref(nbad)), a._ctx)
+    ra, ita, erra = _steps(a, steps)
+    variant = a.pcg_variant
+    a.close()
+    # host-staged loopback
+    b = _problem(kind, cells, parts, part, pcg, pc, rep)
+    _host_loopback(b)
+    rb, itb, errb = _steps(b, steps)
+    b.close()
+    res = {"case": name, "checked": nchk.value, "bad": nbad.value, "its_rccl": ita, "its_host": itb,
+           "err_rccl": erra, "err_host": errb, "krylov_form": variant, "pc": pc}
+    for k in ra:
+        res["maxdiff_" + k] = float(np.nanmax(np.abs(ra[k] - rb[k]))) if ra[k].size else 0.0
+        res["bitwise_" + k] = bool(np.array_equal(ra[k], rb[k], equal_nan=True))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--case", nargs="*", default=list(CASES))
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    for name in a.case:
+        print("LOOPBACK " + json.dumps(run_case(name, a.steps)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

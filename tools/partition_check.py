@@ -31,20 +31,35 @@ CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree":
 
 
 def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0,
-        outdir=None):
+        outdir=None, dirichlet=False, edit_field="T", mg_coupling="auto"):
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
                            verbose=False, pcg_variant=pcg, write_output=outdir is not None,
-                           output_dir=outdir or "output", preconditioner=pc, mg_replicate_nodes=mg_rep)
+                           output_dir=outdir or "output", preconditioner=pc, mg_replicate_nodes=mg_rep,
+                           model_mode="paper" if dirichlet else "reference", mg_coupling=mg_coupling)
     if comm is not None:
         comm(p)
-    p.setup()
+        if n_parts > 1:  # every exchange pattern on id-valued vectors first (collective)
+            import ctypes as C
+            nchk, nbad = C.c_int64(), C.c_int64()
+            rc = p._lib.tv_comm_check(p._ctx, C.byref(nchk), C.byref(nbad))
+            if rc != 0 or nbad.value or not nchk.value:
+                raise SystemExit(f"tv_comm_check: rc {rc}, {nbad.value} of {nchk.value} values wrong")
+    if dirichlet:  # paper mode with T = T_ambient on the boundary (tv_set_dirichlet)
+        p.setup(dirichlet_bc=True)
+    else:
+        p.setup()
     if edit:
         # a local hot spot written in place on the host by the ranks that own it
         # (rank 0 only when partitioned): the ghost planes must still follow
         X = p._dof_coordinates(0)
         m = (X[:, 0] < 0.6) & (X[:, 1] < 0.6)
         if m.any():
-            p.functions_current["T"].x.array[m] += 20.0
+            if edit_field == "T":
+                p.functions_current["T"].x.array[m] += 20.0
+            else:  # a T-space state field other than T: its ghost copies must follow too
+                arr = (p.functions_current if edit_field in p.functions_current else p.functions)[edit_field].x.array
+                bs = arr.size // m.size
+                arr.reshape(-1, bs)[m] += 20.0
     its = []
     for _ in range(steps):
         p.solve_timestep()
@@ -71,6 +86,10 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
     ap.add_argument("--edit", action="store_true", help="host edit of T on the owning rank only, after setup()")
+    ap.add_argument("--edit-field", default="T", help="--edit: the field edited (T, Tf, Tf_partial, phi, xi)")
+    ap.add_argument("--dirichlet", action="store_true", help="paper mode with the Dirichlet condition T = T_ambient")
+    ap.add_argument("--mg-coupling", choices=["auto", "global", "local"], default="auto",
+                    help="partitioned GMG: the distributed V-cycle of the whole box, or each slab's own (block Jacobi)")
     ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi")
     ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
                     help="distorted: the box as a general hexahedral mesh (tv_um.hip), RCB cell partition + ghost layer")
@@ -94,14 +113,16 @@ def main():
         if torch.cuda.device_count() < world:
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
-                       pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir)
+                       pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir,
+                       dirichlet=a.dirichlet, edit_field=a.edit_field, mg_coupling=a.mg_coupling)
     else:
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
-                       edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir)
+                       edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir, dirichlet=a.dirichlet,
+                       edit_field=a.edit_field, mg_coupling=a.mg_coupling)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
-        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc)
+        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc, dirichlet=a.dirichlet, edit_field=a.edit_field)
         res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "mesh": a.mesh, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             if "l2g" in gathered[0]:  # scatter every part's owned vertices to their global ids
