@@ -420,11 +420,14 @@ int fine_csr(Ctx* c, Csr& A) {
 
 }  // namespace
 
-// builds the hierarchy below the fine unstructured level (one partition)
-int amg_setup(Ctx* c) {
-  if (!c->um || c->n_parts > 1) return c->fail(TV_ERR_ARG, "AMG: unstructured meshes on one partition");
-  Csr A;
-  if (int e = fine_csr(c, A)) return e;
+// builds the hierarchy below the fine level from the fine operator A.  One
+// partition: A = the local operator.  Partitioned (amg_setup_part): A = the
+// GLOBAL operator in the partition-major numbering, identical on every rank,
+// and the level-0 transfer is cut to this rank's owned fine rows
+// [row0, row0 + nrow) -- P_0 (owned fine rows x all level-1 aggregates) and
+// R_0 = P_0^T; levels >= 1 are replicated on every rank (agglomerated).
+static int amg_build(Ctx* c, Csr A, int64_t row0, int64_t nrow) {
+  const bool part = c->n_parts > 1;
   const int max_levels = c->O.mg_levels > 0 ? c->O.mg_levels : 12;
   while ((int)c->amg.size() + 1 < max_levels && A.n > kAmgCoarseRows) {
     const std::vector<double> dinv = diag_inv(A);
@@ -443,6 +446,17 @@ int amg_setup(Ctx* c) {
       const Csr AP = spgemm(A, P);
       Ac = spgemm(R, AP);
     }
+    const bool cut = part && c->amg.empty();  // the level-0 transfer of a partition
+    Csr Pl, Rl;
+    if (cut) {  // the owned fine rows of P_0
+      Pl.n = nrow;
+      Pl.m = P.m;
+      Pl.ptr.assign((size_t)nrow + 1, 0);
+      for (int64_t i = 0; i < nrow; ++i) Pl.ptr[i + 1] = Pl.ptr[i] + (P.ptr[row0 + i + 1] - P.ptr[row0 + i]);
+      Pl.col.assign(P.col.begin() + P.ptr[row0], P.col.begin() + P.ptr[row0 + nrow]);
+      Pl.val.assign(P.val.begin() + P.ptr[row0], P.val.begin() + P.ptr[row0 + nrow]);
+      Rl = transpose(Pl);
+    }
     c->amg.emplace_back();
     AmgLevel& L = c->amg.back();
     L.n = na;
@@ -451,8 +465,8 @@ int amg_setup(Ctx* c) {
     // kAmgSortWindow rows, P's kept in order (its outputs are the fine vectors:
     // a sorted P would scatter three fine streams).  One row per lane in CSR
     // left the wave's loads uncoalesced (measured slower, 475 vs 411 us per V-cycle)
-    if (int e = upload_mat(c, P, L.P, false, true, 0, &L.p_nnz)) return e;
-    if (int e = upload_mat(c, R, L.R, false, true, kAmgSortWindow, &L.r_nnz)) return e;
+    if (int e = upload_mat(c, cut ? Pl : P, L.P, false, true, 0, &L.p_nnz)) return e;
+    if (int e = upload_mat(c, cut ? Rl : R, L.R, false, true, kAmgSortWindow, &L.r_nnz)) return e;
     if (int e = upload_mat(c, Ac, L.A, false, false, 0, &L.a_nnz)) return e;
     const std::vector<double> dc = diag_inv(Ac);
     for (double v : dc)
@@ -465,10 +479,105 @@ int amg_setup(Ctx* c) {
   }
   if (c->amg.empty()) return c->fail(TV_ERR_ARG, "AMG: the mesh is too small to coarsen");
   HIPC(hipMalloc(&c->mgx, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
+  HIPC(hipMemset(c->mgx, 0, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
   c->amg_on = true;
   c->mg_on = true;
   c->mg_omega0 = 0.0;  // the level-0 weight: lazily, at the temperature of the first solve (mg_dg_weight)
   return TV_OK;
+}
+
+int amg_setup(Ctx* c) {
+  if (!c->um || c->n_parts > 1) return c->fail(TV_ERR_ARG, "AMG: unstructured meshes on one partition");
+  Csr A;
+  if (int e = fine_csr(c, A)) return e;
+  const int64_t n = A.n;
+  return amg_build(c, std::move(A), 0, n);
+}
+
+// The hierarchy of a partition of a distributed unstructured mesh (collective,
+// at its first solve, once the communicator is set).  Every rank gathers the
+// GLOBAL fine operator in the partition-major numbering -- its owned rows with
+// global column ids (the ghosts' ids from their owners through the halo),
+// summed into zero-filled global arrays by vector all-reduces (each row comes
+// from one rank: the sums are exact) -- and builds the same hierarchy from it
+// (the host setup is deterministic), PCGAMG's agglomeration of the coarse
+// levels onto every process in the extreme: the V-cycle below level 0 runs
+// replicated, one all-reduce of the level-1 right-hand side per application.
+int amg_setup_part(Ctx* c) {
+  if (!c->um || c->n_parts < 2) return c->fail(TV_ERR_ARG, "AMG: partitioned unstructured meshes");
+  Csr Al;
+  if (int e = fine_csr(c, Al)) return e;  // owned rows, local columns
+  const int64_t nown = c->ownT_n, nloc = c->nT, off = c->globT_off;
+  hipStream_t s = c->stream;
+  double* dv = nullptr;
+  auto dev = [&](size_t n) -> int {
+    if (dv) HIPC(hipFree(dv));
+    dv = nullptr;
+    HIPC(hipMalloc(&dv, sizeof(double) * std::max<size_t>(1, n)));
+    return TV_OK;
+  };
+  auto run = [&]() -> int {
+    // global ids of the local vertices
+    std::vector<double> gid((size_t)nloc, -1.0);
+    for (int64_t i = 0; i < nown; ++i) gid[(size_t)i] = (double)(off + i);
+    if (int e = dev((size_t)nloc)) return e;
+    HIPC(hipMemcpyAsync(dv, gid.data(), sizeof(double) * (size_t)nloc, hipMemcpyHostToDevice, s));
+    if (int e = halo_um(c, dv)) return e;
+    HIPC(hipMemcpyAsync(gid.data(), dv, sizeof(double) * (size_t)nloc, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    for (double g : gid)
+      if (!(g >= 0.0)) return c->fail(TV_ERR_STATE, "AMG: a ghost vertex received no global id");
+    // global row count and row lengths
+    double nn = (double)nown;
+    if (int e = dev(1)) return e;
+    HIPC(hipMemcpyAsync(dv, &nn, sizeof(double), hipMemcpyHostToDevice, s));
+    if (int e = allreduce_vec(c, dv, 1)) return e;
+    HIPC(hipMemcpyAsync(&nn, dv, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    const int64_t N = (int64_t)nn;
+    if (N >= INT32_MAX) return c->fail(TV_ERR_ARG, "AMG: < 2^31 vertices");
+    std::vector<double> len((size_t)N, 0.0);
+    for (int64_t i = 0; i < nown; ++i) len[(size_t)(off + i)] = (double)(Al.ptr[i + 1] - Al.ptr[i]);
+    if (int e = dev((size_t)N)) return e;
+    HIPC(hipMemcpyAsync(dv, len.data(), sizeof(double) * (size_t)N, hipMemcpyHostToDevice, s));
+    if (int e = allreduce_vec(c, dv, N)) return e;
+    HIPC(hipMemcpyAsync(len.data(), dv, sizeof(double) * (size_t)N, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    Csr A;
+    A.n = A.m = N;
+    A.ptr.assign((size_t)N + 1, 0);
+    for (int64_t r = 0; r < N; ++r) A.ptr[r + 1] = A.ptr[r] + (int64_t)len[(size_t)r];
+    const int64_t nnz = A.ptr[N];
+    // columns (global ids, ascending per row) and values of the owned rows
+    std::vector<double> cv((size_t)nnz, 0.0), vv((size_t)nnz, 0.0);
+    std::vector<std::pair<int64_t, double>> row;
+    for (int64_t i = 0; i < nown; ++i) {
+      row.clear();
+      for (int64_t k = Al.ptr[i]; k < Al.ptr[i + 1]; ++k) row.emplace_back((int64_t)gid[(size_t)Al.col[k]], Al.val[k]);
+      std::sort(row.begin(), row.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+      const int64_t o = A.ptr[off + i];
+      for (size_t q = 0; q < row.size(); ++q) {
+        cv[(size_t)o + q] = (double)row[q].first;
+        vv[(size_t)o + q] = row[q].second;
+      }
+    }
+    if (int e = dev((size_t)nnz)) return e;
+    for (std::vector<double>* v : {&cv, &vv}) {
+      HIPC(hipMemcpyAsync(dv, v->data(), sizeof(double) * (size_t)nnz, hipMemcpyHostToDevice, s));
+      if (int e = allreduce_vec(c, dv, nnz)) return e;
+      HIPC(hipMemcpyAsync(v->data(), dv, sizeof(double) * (size_t)nnz, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+    }
+    A.col.resize((size_t)nnz);
+    A.val.swap(vv);
+    for (int64_t k = 0; k < nnz; ++k) A.col[(size_t)k] = (int)cv[(size_t)k];
+    if (dv) HIPC(hipFree(dv));
+    dv = nullptr;
+    return amg_build(c, std::move(A), off, nown);
+  };
+  const int e = run();
+  if (dv) hipFree(dv);
+  return e;
 }
 
 // the V-cycle on coarse level l >= 1 (c->amg[l - 1]); its pre-smoothing step
@@ -490,7 +599,13 @@ static const double* amg_level(Ctx* c, size_t l) {
 // with the (z.z, z.r) records and the KSPCG tail
 int amg_apply0(Ctx* c, const RedTail* tail) {
   AmgLevel& L1 = c->amg[0];
-  launch_amg_restrict(L1.R, c->st, c->r, nullptr, L1.dinv, L1.omega, L1.b, L1.x, c->stream);
+  if (c->n_parts > 1) {  // the partial restriction of the owned fine rows, summed over the ranks
+    launch_amg_restrict(L1.R, c->st, c->r, nullptr, nullptr, 0.0, L1.b, nullptr, c->stream);
+    if (int e = allreduce_vec(c, L1.b, L1.n)) return -e;
+    launch_mg_jacobi(L1.n, c->st, L1.b, nullptr, nullptr, L1.dinv, L1.omega, L1.x, 0, c->stream);
+  } else {
+    launch_amg_restrict(L1.R, c->st, c->r, nullptr, L1.dinv, L1.omega, L1.b, L1.x, c->stream);
+  }
   const double* x1 = amg_level(c, 1);
   return launch_amg_prolong0(L1.P, c->st, x1, c->mgx, c->r, c->z, c->partials, tail, c->stream);
 }

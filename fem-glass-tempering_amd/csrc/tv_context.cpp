@@ -716,13 +716,11 @@ static int create_unstructured(const tv_umesh_desc* mesh, const tv_upart_desc* p
                      "rectilinear mesh)");
     return TV_ERR_ARG;
   }
-  if (c->O.preconditioner == TV_PC_AMG && part && part->n_parts > 1) {
-    set_global_error("unstructured meshes: TV_PC_AMG on one partition (partitioned: TV_PC_JACOBI)");
-    return TV_ERR_ARG;
-  }
   int rc = setup_umesh(c.get(), mesh, part);
   if (rc == TV_OK) rc = setup_fields(c.get());
-  if (rc == TV_OK && c->O.preconditioner == TV_PC_AMG) rc = amg_setup(c.get());
+  // a partition builds its (agglomerated) hierarchy at its first solve: the
+  // setup gathers the global operator through the communicator set after creation
+  if (rc == TV_OK && c->O.preconditioner == TV_PC_AMG && c->n_parts < 2) rc = amg_setup(c.get());
   if (rc == TV_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = c->fail(TV_ERR_HIP, "sync failed");
   if (rc != TV_OK) {
     set_global_error(c->err);

@@ -240,6 +240,7 @@ constexpr int kTsCap = 1 << 15;                // timestamp slots of the in-solv
 
 // ---- tv_amg.cpp ----
 int amg_setup(Ctx* c);
+int amg_setup_part(Ctx* c);  // collective (partitioned unstructured mesh), at the first solve
 int amg_apply0(Ctx* c, const RedTail* tail);
 double amg_cycle_bytes(const Ctx* c);
 

@@ -330,6 +330,10 @@ int mg_prepare_dist(Ctx* c, const double* T) {
 // z.r) records reduced into c->sums by the tail (kind 0: the all-reduce and
 // the KSPCG logic follow).  Returns a status.
 int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
+  if (c->amg_on) {  // partitioned unstructured mesh: the agglomerated algebraic cycle (tv_amg.cpp)
+    const int r = amg_apply0(c, tail);
+    return r < 0 ? -r : TV_OK;
+  }
   hipStream_t s = c->stream;
   const size_t L = c->mg.size() + 1;  // levels incl. 0
   const size_t A = (size_t)c->mg_A;
@@ -404,7 +408,7 @@ int mg_iteration_dist(Ctx* c, const double* T, int it) {
     if (int e = allreduce(c, c->sums, 1)) return e;
     launch_logic(c->st, c->sums, 2, c->stream);  // alpha
   }
-  const FaceAdd fa = cg_face_add(c->cg, off);
+  const FaceAdd fa = c->um ? FaceAdd{} : cg_face_add(c->cg, off);  // unstructured: w is complete
   launch_mg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, &fa, c->dinv + off, c->mg_omega0, c->r + off,
                    c->f[TV_F_DX].ptr + off, c->mgx + off, it, 0, c->stream);
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};
@@ -418,7 +422,11 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
   const PcgState h = pcg_state_init(c);
   c->h_st[2] = h;
   HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
-  if (int e = mg_prepare_dist(c, T)) return e;
+  if (c->amg_on) {  // the algebraic hierarchy is T-independent; level 0's weight at the first solve
+    if (int e = mg_dg_weight(c, T)) return e;
+  } else if (int e = mg_prepare_dist(c, T)) {
+    return e;
+  }
   if (c->dir_on)  // the prolongation masks level 0's ghost planes with dinv too
     if (int e = halo(c, c->dinv)) return e;
   if (c->mg_mask0)  // level 0's restriction mask: owned nodes, Dirichlet rows out

@@ -63,30 +63,48 @@ int mg_add_cg_level(Ctx* c, const std::vector<double> (&X)[3], double da) {
 // SIPG rows have no closed-form
 // Gershgorin bound here.  The smoother takes it with a 21 % margin
 int mg_dg_lambda(Ctx* c, const double* T, double* lam) {
-  const int64_t n = c->nT;
+  // a partition of a distributed unstructured mesh (collective): its owned rows,
+  // the start vector's entries at their partition-major global indices, the
+  // ghosts refreshed before every product, the norms all-reduced
+  const bool part = c->n_parts > 1;
+  const int64_t n = part ? c->ownT_n : c->nT;
   std::vector<double> h((size_t)n);
   uint64_t st = 0x9E3779B97F4A7C15ull;
   double nrm = 0.0;
-  for (int64_t t = 0; t < n; ++t) {  // fixed-seed xorshift start vector in (0.5, 1.5)
+  const int64_t skip = part ? c->globT_off : 0;
+  for (int64_t t = 0; t < skip + n; ++t) {  // fixed-seed xorshift start vector in (0.5, 1.5)
     st ^= st << 13; st ^= st >> 7; st ^= st << 17;
-    h[(size_t)t] = 0.5 + (double)(st >> 11) * (1.0 / 9007199254740992.0);
-    nrm += h[(size_t)t] * h[(size_t)t];
+    if (t < skip) continue;
+    h[(size_t)(t - skip)] = 0.5 + (double)(st >> 11) * (1.0 / 9007199254740992.0);
+    nrm += h[(size_t)(t - skip)] * h[(size_t)(t - skip)];
   }
+  auto gsum = [&](double& v) -> int {  // sum over the ranks (partitioned)
+    if (!part) return TV_OK;
+    HIPC(hipMemcpyAsync(c->sums + 4, &v, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (int e = allreduce(c, c->sums + 4, 1)) return e;
+    HIPC(hipMemcpyAsync(&v, c->sums + 4, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return TV_OK;
+  };
+  if (int e = gsum(nrm)) return e;
   for (double& v : h) v /= std::sqrt(nrm);
   HIPC(hipMemcpyAsync(c->mgx, h.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice, c->stream));
   if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
   else if (!c->um) launch_dg_diag(c->dg, T, c->dinv, 1, c->stream);
-  std::vector<double> part(1024);
+  std::vector<double> prt(1024);
   double l = 0.0;
   if (c->um) op_diag(c, T, c->dinv, 1);  // the algebraic multigrid's level 0: point Jacobi of J(T)
   for (int it = 0; it < 30; ++it) {
+    if (part)
+      if (int e = halo(c, c->mgx)) return e;
     op_japply(c, T, c->mgx, c->w, nullptr, nullptr);
     if (c->dggface) launch_dg_bsmooth(c->dg, nullptr, c->w, nullptr, c->dggface, 1.0, c->w, 0, c->stream);  // in place, per cell
     const int nb = launch_mg_pow(n, c->dggface ? nullptr : c->dinv, c->w, c->partials, c->stream);
-    HIPC(hipMemcpyAsync(part.data(), c->partials, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipMemcpyAsync(prt.data(), c->partials, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, c->stream));
     HIPC(hipStreamSynchronize(c->stream));
     double s2 = 0.0;
-    for (int b = 0; b < nb; ++b) s2 += part[(size_t)b];
+    for (int b = 0; b < nb; ++b) s2 += prt[(size_t)b];
+    if (int e = gsum(s2)) return e;
     l = std::sqrt(s2);  // ||D^-1 J x|| with ||x|| = 1
     if (!(l > 0.0) || !std::isfinite(l)) return c->fail(TV_ERR_HIP, "GMG: DG eigenvalue estimate failed");
     launch_mg_scale(n, c->w, 1.0 / l, c->mgx, c->stream);

@@ -321,6 +321,8 @@ int dirichlet_pre(Ctx* c, const double* T) {
 int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
   if (int e = require_comm(c, "Newton solve")) return e;
   if (int e = refresh_dirty_ghosts(c)) return e;
+  if (c->um && c->n_parts > 1 && c->O.preconditioner == TV_PC_AMG && !c->amg_on)
+    if (int e = amg_setup_part(c)) return e;
   double* T = c->f[TV_F_T].ptr;
   const double* Tp = c->f[TV_F_T_PREV].ptr;
   // NonlinearProblem.form: ghost update of the state before the first F

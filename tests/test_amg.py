@@ -176,7 +176,3 @@ def test_amg_rejections():
     with pytest.raises(NativeError):  # box meshes take the geometric hierarchy
         ThermoViscoProblem(box_mesh([1.0, 1.0, 1.0], [4, 4, 4]), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS),
                            verbose=False, preconditioner="amg")
-    m = _mesh((16, 14, 12), (2.0, 2.0, 1.0))
-    with pytest.raises(NativeError):  # partitioned: Jacobi only
-        ThermoViscoProblem(m, (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), verbose=False, preconditioner="amg",
-                           n_parts=2, part=0)

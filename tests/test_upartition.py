@@ -99,7 +99,7 @@ def test_ghosted_partition_single_part_is_whole_mesh():
     assert np.array_equal(g["mesh"].cells, mesh.cells)
 
 
-def _partition_check(world, port, extra=()):
+def _partition_check(world, port, extra=(), krylov_slack=1):
     import json
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "partition_check.py"),
@@ -114,7 +114,7 @@ def _partition_check(world, port, extra=()):
     assert res["xi"] < 1e-6, res
     assert res["sigma"] < 1e-6, res
     for (n1, k1), (n2, k2) in zip(res["its_parts"], res["its_single"]):
-        assert n1 == n2 and abs(k1 - k2) <= n1, res
+        assert n1 == n2 and (krylov_slack is None or abs(k1 - k2) <= krylov_slack * n1), res
     return res
 
 
@@ -169,6 +169,27 @@ def test_partitioned_unstructured_host_edit_state_field(field):
     res = _partition_check(2, 29830, ("--cells", "10,30,5", "--edit", "--edit-field", field, "--steps", "2",
                                       "--output"))
     assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_unstructured_amg(world):
+    """The smoothed-aggregation AMG on a distributed distorted mesh: every rank
+    gathers the global fine operator (partition-major numbering) at its first
+    solve and builds the same hierarchy; level 0 restricts its owned rows, one
+    all-reduce forms the level-1 right-hand side, the coarse cycle runs
+    replicated.  T reproduces the single-partition AMG run (<= 1e-12, equal
+    Newton counts) and the Krylov counts stay within 1.5x of it (its aggregates
+    follow the input numbering, the partitioned ones the partition-major)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _partition_check(world, 29840 + world, ("--cells", "16,30,10", "--steps", "2", "--pc", "amg"),
+                           krylov_slack=None)
+    print("[upartition-amg]", res["its_parts"], res["its_single"], flush=True)
+    ka = sum(k for _, k in res["its_parts"])
+    ks = sum(k for _, k in res["its_single"])
+    assert ka <= 1.5 * ks, res
 
 
 @pytest.mark.gpu

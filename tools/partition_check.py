@@ -90,7 +90,7 @@ def main():
     ap.add_argument("--dirichlet", action="store_true", help="paper mode with the Dirichlet condition T = T_ambient")
     ap.add_argument("--mg-coupling", choices=["auto", "global", "local"], default="auto",
                     help="partitioned GMG: the distributed V-cycle of the whole box, or each slab's own (block Jacobi)")
-    ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi")
+    ap.add_argument("--pc", choices=["jacobi", "gmg", "amg"], default="jacobi")
     ap.add_argument("--mesh", choices=["box", "distorted"], default="box",
                     help="distorted: the box as a general hexahedral mesh (tv_um.hip), RCB cell partition + ghost layer")
     ap.add_argument("--output", action="store_true",
