@@ -36,6 +36,7 @@ namespace tv {
 
 struct FieldInfo {
   double* ptr = nullptr;
+  void* base = nullptr;  // the allocation (ptr = base + the field's stagger)
   int bs = 1;       // components
   int space = 0;    // 0 T space, 1 sigma space
   bool alloc = false;

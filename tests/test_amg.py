@@ -100,7 +100,7 @@ def test_amg_vcycle_matches_restatement(case):
     sym = abs(y @ z_r - r @ z_y) / abs(y @ z_r)
     print(f"[amg] V-cycle {case}: {len(levels) + 1} levels ({[lv[0].shape[0] for lv in levels]}), vs numpy {e:.2e}, "
           f"symmetry {sym:.1e}")
-    assert len(levels) + 1 == (2 if case == "two_levels" else 3)
+    assert len(levels) + 1 == {"two_levels": 2, "three_levels": 3, "stretched": 2}[case]
     assert e < 1e-10, e
     assert sym < 1e-12, sym
     assert r @ z_r > 0.0
