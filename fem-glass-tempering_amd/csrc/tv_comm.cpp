@@ -149,8 +149,69 @@ int halo_um(Ctx* c, double* v) {
   return TV_OK;
 }
 
+// ghost cell layers of a partitioned DG1 box (DgGrid layout): the first and
+// the last owned layer, all 2^d components, packed into one buffer each; the
+// neighbour's layer lands straight in the ghost region (one layer,
+// component-major, as the kernels address it)
+__global__ __launch_bounds__(kBlock) void k_dg_pack(const double* __restrict__ v, int64_t own, int64_t pc, int nl,
+                                                    int64_t last, double* __restrict__ out) {
+  const int64_t L = (int64_t)nl * pc;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < 2 * L; t += (int64_t)gridDim.x * kBlock) {
+    const int side = (int)(t / L);
+    const int64_t e = t - side * L;
+    const int l = (int)(e / pc);
+    const int64_t q = e - (int64_t)l * pc;
+    out[t] = v[(int64_t)l * own + (side ? last : 0) + q];
+  }
+}
+
+int halo_dg(Ctx* c, double* v) {
+  const DgGrid& g = c->dg;
+  const int nl = 1 << c->dim;
+  const int64_t pc = (int64_t)g.c0 * g.c1, L = (int64_t)nl * pc;
+  const bool lo = g.gofs[0] >= 0, hi = g.gofs[1] >= 0;
+  if (!lo && !hi) return TV_OK;
+  if (c->comm_stub) {  // see stub_ghosts: the solver's ghosts read zero, the temperature keeps its ghosts
+    if (v == c->f[TV_F_T].ptr || v == c->f[TV_F_T_PREV].ptr) return TV_OK;
+    if (lo) HIPC(hipMemsetAsync(v + g.gofs[0], 0, L * sizeof(double), c->stream));
+    if (hi) HIPC(hipMemsetAsync(v + g.gofs[1], 0, L * sizeof(double), c->stream));
+    return TV_OK;
+  }
+  if (!c->dg_sbuf) HIPC(hipMalloc(&c->dg_sbuf, sizeof(double) * 2 * (size_t)L));
+  const int nb = (int)std::min<int64_t>(1024, (2 * L + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_dg_pack, dim3(nb), dim3(kBlock), 0, c->stream, v, g.own, pc, nl,
+                     (int64_t)(g.k_end - g.k_begin - 1) * pc, c->dg_sbuf);
+  HIPC(hipGetLastError());
+  if (c->host_sendrecv) {
+    double* hs = c->h_halo;
+    double* hr = c->h_halo + 2 * L;
+    HIPC(hipMemcpyAsync(hs, c->dg_sbuf, 2 * L * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    if (lo && c->host_sendrecv(hs, (size_t)L, c->rank - 1, hr, (size_t)L, c->rank - 1, c->host_user))
+      return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (hi && c->host_sendrecv(hs + L, (size_t)L, c->rank + 1, hr + L, (size_t)L, c->rank + 1, c->host_user))
+      return c->fail(TV_ERR_COMM, "host sendrecv failed");
+    if (lo) HIPC(hipMemcpyAsync(v + g.gofs[0], hr, L * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (hi) HIPC(hipMemcpyAsync(v + g.gofs[1], hr + L, L * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return TV_OK;
+  }
+  NCCLC(ncclGroupStart());
+  if (lo) {
+    NCCLC(ncclSend(c->dg_sbuf, L, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v + g.gofs[0], L, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+  }
+  if (hi) {
+    NCCLC(ncclSend(c->dg_sbuf + L, L, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v + g.gofs[1], L, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  return TV_OK;
+}
+
 int halo(Ctx* c, double* v) {
-  if (!multi_rank(c) || c->fam_T != TV_CG) return TV_OK;
+  if (!multi_rank(c)) return TV_OK;
+  if (c->fam_T == TV_DG) return halo_dg(c, v);
   if (c->um) return halo_um(c, v);
   return halo_grid(c, c->cg, v);
 }
@@ -354,7 +415,41 @@ int comm_check(Ctx* c, int64_t* n_chk, int64_t* n_bad) {
       const double want[2] = {sum_ranks, n_contrib};
       return sums_ok(s, 2, want);
     }
-    if (c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "tv_comm_check: CG temperature space");
+    if (c->fam_T == TV_DG) {  // ghost cell layers: global dof ids (cell-major: cell * 2^d + l)
+      const DgGrid& g = c->dg;
+      const int nl = 1 << c->dim;
+      const int64_t pc = (int64_t)g.c0 * g.c1, L = (int64_t)nl * pc;
+      const int64_t b0 = c->plane_begin, b1 = c->plane_end, nk = b1 - b0;
+      std::vector<double> ids((size_t)c->nT, -1.0);
+      for (int l = 0; l < nl; ++l)
+        for (int64_t oc = 0; oc < g.own; ++oc) ids[(size_t)(l * g.own + oc)] = (double)((b0 * pc + oc) * nl + l);
+      HIPC(hipMemcpyAsync(v, ids.data(), sizeof(double) * ids.size(), hipMemcpyHostToDevice, c->stream));
+      const double hs[2] = {(double)(c->rank + 1), 1.0};
+      HIPC(hipMemcpyAsync(s, hs, sizeof(hs), hipMemcpyHostToDevice, c->stream));
+      if (int e = allreduce_halo(c, s, 2, v)) return e;
+      const double want[2] = {sum_ranks, n_contrib};
+      if (int e = sums_ok(s, 2, want)) return e;
+      HIPC(hipMemcpyAsync(h.data(), v, sizeof(double) * (size_t)c->nT, hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipStreamSynchronize(c->stream));
+      for (int64_t k = 0; k < nl * g.own; ++k) {
+        ++*n_chk;
+        if (h[(size_t)k] != ids[(size_t)k]) ++*n_bad;
+      }
+      for (int side = 0; side < 2; ++side) {
+        if (g.gofs[side] < 0) continue;
+        // the global layer the values must come from
+        const int64_t src = c->comm_self ? (side ? b1 - 1 : b0) : (side ? b1 : b0 - 1);
+        for (int l = 0; l < nl; ++l)
+          for (int64_t q = 0; q < pc; ++q) {
+            ++*n_chk;
+            if (h[(size_t)(g.gofs[side] + l * pc + q)] != (double)((src * pc + q) * nl + l)) ++*n_bad;
+          }
+      }
+      (void)nk;
+      (void)L;
+      return TV_OK;
+    }
+    if (c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "tv_comm_check: CG or DG temperature space");
     const CgGrid& g = c->cg;
     const int64_t first = c->plane_begin - g.k_begin;  // global plane of local plane 0
     const int64_t nloc = (int64_t)g.n0 * g.n1 * g.n2;
@@ -553,6 +648,9 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
   } else if (c->fam_T == TV_CG) {
     const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
     HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)plane));
+  } else {  // DG: 2 send + 2 receive cell layers of 2^d components
+    const int64_t L = ((int64_t)1 << c->dim) * c->dg.c0 * c->dg.c1;
+    HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)L));
   }
   if (int e = halo(c, c->f[TV_F_T].ptr)) return e;
   if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;

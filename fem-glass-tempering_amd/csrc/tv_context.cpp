@@ -189,8 +189,9 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   c->n_parts = std::max(1, m->n_parts);
   c->part = m->part;
   if (c->part < 0 || c->part >= c->n_parts) return c->fail(TV_ERR_ARG, "part out of range");
-  if (c->n_parts > 1 && (d == 1 || c->fam_T != TV_CG || c->fam_S != TV_CG))
-    return c->fail(TV_ERR_ARG, "partitioned meshes require dim >= 2 and CG temperature and stress spaces");
+  if (c->n_parts > 1 && (d == 1 || c->fam_T != c->fam_S))
+    return c->fail(TV_ERR_ARG, "partitioned meshes require dim >= 2 and the same family for temperature and stress "
+                               "(CG / CG or DG / DG)");
   for (int s = 0; s < 3; ++s) {
     c->Ncell_glob[s] = (c->perm[s] < 0) ? 0 : m->n_cells[c->perm[s]];
     c->Nnode_glob[s] = c->Ncell_glob[s] + 1;
@@ -223,20 +224,35 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     DgGrid& g = c->dg;
     g.c0 = c->Ncell_glob[0];
     g.c1 = std::max(1, c->Ncell_glob[1]);
-    g.c2 = std::max(1, c->Ncell_glob[2]);
-    g.k_begin = 0;
-    g.k_end = g.c2;
+    // partition: the owned cell layers [b0, b1) of storage axis 2 and one ghost
+    // layer towards each neighbour (the SIPG facets of the interface)
+    const int C2 = std::max(1, c->Ncell_glob[2]);
+    const int P = c->n_parts, p = c->part;
+    int b0 = 0, b1 = C2;
+    if (P > 1) part_planes(C2, P, p, &b0, &b1);
+    if (b1 - b0 < 1) return c->fail(TV_ERR_ARG, "too many partitions for the mesh");
+    const int g_lo = (P > 1 && p > 0) ? 1 : 0, g_hi = (P > 1 && p < P - 1) ? 1 : 0;
+    g.c2 = (b1 - b0) + g_lo + g_hi;
+    g.k_begin = g_lo;
+    g.k_end = g_lo + (b1 - b0);
     g.deg1 = (c->perm[1] < 0);
     g.deg2 = (c->perm[2] < 0);
     g.bnd[0][0] = g.bnd[0][1] = 1;
     g.bnd[1][0] = g.bnd[1][1] = g.deg1 ? 0 : 1;
-    g.bnd[2][0] = g.bnd[2][1] = g.deg2 ? 0 : 1;
+    g.bnd[2][0] = (g.deg2 || p > 0) ? 0 : 1;
+    g.bnd[2][1] = (g.deg2 || p < P - 1) ? 0 : 1;
+    const int64_t pc = (int64_t)g.c0 * g.c1;
+    const int nl0 = 1 << d;
+    g.own = pc * (b1 - b0);
+    g.gofs[0] = g_lo ? nl0 * g.own : -1;
+    g.gofs[1] = g_hi ? nl0 * g.own + (int64_t)nl0 * pc * g_lo : -1;
     g.tile = c->O.dg_kernel == TV_DG_KERNEL_CELLS ? 0 : 1;  // 1: k_dg_tile with halo-loading edge waves
     g.tile_chunk = c->O.dg_tile_chunk > 0 ? c->O.dg_tile_chunk : 5;  // 5 planes measured best (C5)
     for (int s = 0; s < 3; ++s) {
       const std::vector<double>& X = storage_coords(c, s, tmp);
       std::vector<double> h;
       if (X.size() == 1) h.assign(1, 1.0);
+      else if (s == 2) for (int k = b0 - g_lo; k < b1 + g_hi; ++k) h.push_back(X[k + 1] - X[k]);  // local layers
       else for (size_t i = 0; i + 1 < X.size(); ++i) h.push_back(X[i + 1] - X[i]);
       const size_t nh = h.size();
       for (size_t q = 0; q < nh; ++q) h.push_back(1.0 / h[q]);  // [h..., 1/h...]
@@ -247,11 +263,11 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     }
     const int nl = 1 << d;
     c->nT = (int64_t)g.c0 * g.c1 * g.c2 * nl;
-    c->ownT_off = 0;
-    c->ownT_n = c->nT;
-    c->globT_off = 0;
-    c->plane_begin = 0;
-    c->plane_end = g.c2;
+    c->ownT_off = 0;              // the owned layers' dofs come first (DgGrid)
+    c->ownT_n = g.own * nl;
+    c->globT_off = (int64_t)b0 * pc * nl;  // cell-major global numbering: the owned cells are contiguous
+    c->plane_begin = b0;
+    c->plane_end = b1;
   }
   // sigma space
   if (c->fam_S == c->fam_T) {
@@ -836,6 +852,7 @@ int tv_destroy(void* ctx) {
   if (c->h_st) hipHostFree(c->h_st);
   if (c->h_sums) hipHostFree(c->h_sums);
   if (c->d_dirty) hipFree(c->d_dirty);
+  if (c->dg_sbuf) hipFree(c->dg_sbuf);
   if (c->h_halo) hipHostFree(c->h_halo);
   if (c->h_big) hipHostFree(c->h_big);
   if (c->mg_mask0) hipFree(c->mg_mask0);
@@ -901,8 +918,9 @@ int tv_dof_coordinates(void* ctx, int space, double* xyz, size_t n_dofs) {
     const int nl = 1 << c->dim;
     const int C0 = std::max(1, c->Ncell_glob[0]), C1 = std::max(1, c->Ncell_glob[1]);
     const int act[3] = {1, c->perm[1] >= 0, c->perm[2] >= 0};
+    const int64_t cell0 = (space == 0 ? c->globT_off : c->globS_off) / nl;  // first owned cell (global)
     for (int64_t t = 0; t < nown; ++t) {
-      const int64_t cell = t / nl;
+      const int64_t cell = cell0 + t / nl;
       const int l = (int)(t % nl);
       const int ci[3] = {(int)(cell % C0), (int)((cell / C0) % C1), (int)(cell / ((int64_t)C0 * C1))};
       int bits[3] = {0, 0, 0}, k = 0;
@@ -989,8 +1007,9 @@ int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const
     Xs[sx] = storage_coords(c, sx, tmp);
     phys[sx] = c->perm[sx];
   }
-  if (c->fam_T == TV_CG && c->n_parts > 1 && !c->um)
-    Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin, Xs[2].begin() + c->plane_end);
+  if (c->n_parts > 1 && !c->um)  // CG: the owned node planes; DG: the nodes of the owned cell layers
+    Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin,
+                                Xs[2].begin() + c->plane_end + (c->fam_T == TV_DG ? 1 : 0));
   std::string err;
   // a partitioned unstructured mesh writes its own cells over all its local
   // vertices (the ghosts' values are kept current: visco runs on every local vertex)

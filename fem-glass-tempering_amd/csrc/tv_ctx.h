@@ -159,6 +159,7 @@ struct Ctx {
   std::vector<int> out_fields;
   double *cr[2] = {nullptr, nullptr}, *cs[2] = {nullptr, nullptr}, *cw1 = nullptr;
   double* wsend = nullptr;
+  double* dg_sbuf = nullptr;  // partitioned DG: the first and the last owned cell layer, packed for the halo
   double* partials = nullptr;
   int n_partials_cap = 0;
   double* sums = nullptr;

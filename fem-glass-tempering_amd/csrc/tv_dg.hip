@@ -36,6 +36,18 @@ struct Ax {
   __device__ static constexpr int axis(int k) { return DIM == 2 ? (k == 0 ? 0 : 2) : k; }
 };
 
+// dof addressing of a cell layer k (see DgGrid): dof of component l of the
+// cell at in-layer index ij (= i + c0 j) is base + l stride + ij
+struct DgAddr {
+  int64_t base, stride;
+};
+__device__ __forceinline__ DgAddr dg_layer(const DgGrid& g, int k) {
+  const int64_t pc = (int64_t)g.c0 * g.c1;
+  if (k < g.k_begin) return {g.gofs[0], pc};
+  if (k >= g.k_end) return {g.gofs[1], pc};
+  return {(int64_t)(k - g.k_begin) * pc, g.own};
+}
+
 __device__ __forceinline__ double gfun(const DgGrid& g, double T) {
   const double T2 = T * T;
   return g.a_rad * (T2 * T2 - g.T_amb4) + g.a_conv * (T - g.T_amb);
@@ -87,13 +99,14 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
   __shared__ double red[kBlock / kWave];
   if (FUSEP && st->done) return;
   const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
-  const int64_t cstride = ncell;  // component stride
   const int64_t cid = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool ok = cid < ncell;
   const int ci[3] = {ok ? (int)(cid % g.c0) : 0, ok ? (int)((cid / g.c0) % g.c1) : 0,
                      ok ? (int)(cid / ((int64_t)g.c0 * g.c1)) : 0};
   const int cn[3] = {g.c0, g.c1, g.c2};
   const int64_t cst[3] = {1, g.c0, (int64_t)g.c0 * g.c1};
+  const int64_t ij = (int64_t)ci[0] + (int64_t)g.c0 * ci[1];  // in-layer index
+  const DgAddr ac = dg_layer(g, ci[2]);
 
   double bcoef = 0.0;
   bool first = false;
@@ -104,8 +117,8 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
     bcoef = first ? 0.0 : st->beta / st->betaold;
     if (!(it & 1)) { pold = pout; pout = const_cast<double*>(in1); }
   }
-  auto ld = [&](int64_t c, int l) -> double {  // input value (p for FUSEP)
-    const int64_t o = (int64_t)l * cstride + c;
+  auto ld = [&](const DgAddr& a, int64_t q, int l) -> double {  // input value (p for FUSEP)
+    const int64_t o = a.base + (int64_t)l * a.stride + q;
     double v = in0[o];
     if (FUSEP && !first) v = v + bcoef * pold[o];
     return v;
@@ -120,9 +133,9 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
   double x[NL], m[NL], y[NL];
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
-    x[l] = ok ? ld(cid, l) : 0.0;
+    x[l] = ok ? ld(ac, ij, l) : 0.0;
     m[l] = 0.0;
-    if (MODE == MODE_RES && ok) m[l] = x[l] - in1[(int64_t)l * cstride + cid] - g.dt_f;
+    if (MODE == MODE_RES && ok) m[l] = x[l] - in1[ac.base + (int64_t)l * ac.stride + ij] - g.dt_f;
     y[l] = 0.0;
   }
   // ---- cell term: M m + dt alpha K x (tensor products of 2x2 blocks) ----
@@ -179,10 +192,12 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
       const int nbi = ci[ax] + (side ? 1 : -1);
       const bool interior = nbi >= 0 && nbi < cn[ax];
       if (interior) {
-        const int64_t nb = cid + (side ? cst[ax] : -cst[ax]);
+        // the neighbour: another layer along axis 2, else the same layer
+        const DgAddr an = (ax == 2) ? dg_layer(g, nbi) : ac;
+        const int64_t ijn = (ax == 2) ? ij : ij + (side ? cst[ax] : -cst[ax]);
         double xn[NL];
 #pragma unroll
-        for (int l = 0; l < NL; ++l) xn[l] = ok ? ld(nb, l) : 0.0;
+        for (int l = 0; l < NL; ++l) xn[l] = ok ? ld(an, ijn, l) : 0.0;
         // L = lower cell, R = upper cell along ax; '+' = L
         const double hL = side ? h[ax] : g.h[ax][ok ? nbi : 0];
         const double hR = side ? g.h[ax][ok ? nbi : 0] : h[ax];
@@ -217,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
 #pragma unroll
         for (int l = 0; l < NL; ++l) {
           if (MODE == MODE_RES) Tl[l] = x[l];
-          else Tl[l] = ok ? T[(int64_t)l * cstride + cid] : 0.0;
+          else Tl[l] = ok ? T[ac.base + (int64_t)l * ac.stride + ij] : 0.0;
         }
         constexpr int NT = A::NA - 1;  // tangential active axes
         constexpr int NQ = NT == 0 ? 1 : (NT == 1 ? 3 : 9);
@@ -264,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_cells(DgGrid g, const double* __r
   if (ok) {
 #pragma unroll
     for (int l = 0; l < NL; ++l) {
-      const int64_t o = (int64_t)l * cstride + cid;
+      const int64_t o = ac.base + (int64_t)l * ac.stride + ij;
       if (FUSEP) pout[o] = x[l];
       if (owned) {
         out[o] = y[l];
@@ -481,8 +496,6 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
   if (st != nullptr && st->done) return;  // uniform over the grid
   const int pa = 3 - ra;
   const int cn[3] = {g.c0, g.c1, g.c2};
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
-  const int64_t cst[3] = {1, g.c0, (int64_t)g.c0 * g.c1};
   const int npl = cn[pa];
   // chunk fastest: the chunks of one column of tiles share their boundary
   // planes and land on one XCD (contiguous range after the remap)
@@ -500,12 +513,16 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
   const bool valid = i >= 0 && i < g.c0 && r >= 0 && r < cn[ra];
   const bool compute = HL || (wave >= 1 && wave <= R);
   const bool writer = compute && valid && lane >= 1 && lane <= kSeg;
-  const int64_t cbase = (valid ? i : 0) + cst[ra] * (valid ? r : 0);  // cell of plane 0
+  // dof addressing (DgAddr) of the cell of row rr in plane L: the cell layer is
+  // the row (ra = 2) or the plane (ra = 1)
+  auto cell_addr = [&](int ii, int rr, int L, int64_t& q) -> DgAddr {
+    q = (int64_t)ii + (int64_t)g.c0 * (ra == 2 ? L : rr);
+    return dg_layer(g, ra == 2 ? rr : L);
+  };
   // HL: the halo row this wave loads (wave 0: the row below the tile, wave R - 1: above)
   const int rh = wave == 0 ? r - 1 : r + 1;
   const bool hvalid = HL && (wave == 0 || wave == R - 1) && i >= 0 && i < g.c0 && rh >= 0 && rh < cn[ra];
   const int hslot = wave == 0 ? 0 : R + 1;
-  const int64_t hbase = (hvalid ? i : 0) + cst[ra] * (hvalid ? rh : 0);
 
   double bcoef = 0.0;
   bool first = false;
@@ -520,10 +537,11 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
   // input values (p = z + b p_old for FUSEP)
   auto fetch = [&](int L, double (&rz)[8], double (&ro)[8]) {
     const bool ok = valid && L >= 0 && L < npl;
-    const int64_t c = cbase + cst[pa] * (ok ? L : 0);
+    int64_t q;
+    const DgAddr a = cell_addr(valid ? i : 0, valid ? r : 0, ok ? L : 0, q);
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-      const int64_t o = (int64_t)l * ncell + c;
+      const int64_t o = a.base + (int64_t)l * a.stride + q;
       rz[l] = ok ? in0[o] : 0.0;
       ro[l] = (FUSEP && !first && ok) ? pold[o] : 0.0;
     }
@@ -535,10 +553,11 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
   double hz[8], ho[8];  // HL: raw loads of the halo row of plane L + 1, in flight during step L
   auto hfetch = [&](int L) {
     const bool ok = hvalid && L >= 0 && L < npl;
-    const int64_t c = hbase + cst[pa] * (ok ? L : 0);
+    int64_t q;
+    const DgAddr a = cell_addr(hvalid ? i : 0, hvalid ? rh : 0, ok ? L : 0, q);
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-      const int64_t o = (int64_t)l * ncell + c;
+      const int64_t o = a.base + (int64_t)l * a.stride + q;
       hz[l] = ok ? in0[o] : 0.0;
       ho[l] = (FUSEP && !first && ok) ? pold[o] : 0.0;
     }
@@ -566,10 +585,11 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
       for (int l = 0; l < 8; ++l) sX[sb][hslot][l][lane] = FUSEP ? hz[l] + bcoef * ho[l] : hz[l];
       hfetch(L + 1);
     }
-    const int64_t cid = cbase + cst[pa] * L;
+    int64_t cq;
+    const DgAddr ca = cell_addr(valid ? i : 0, valid ? r : 0, L, cq);
     if (FUSEP && writer) {
 #pragma unroll
-      for (int l = 0; l < 8; ++l) pout[(int64_t)l * ncell + cid] = x[l];
+      for (int l = 0; l < 8; ++l) pout[ca.base + (int64_t)l * ca.stride + cq] = x[l];
     }
     __syncthreads();
     if (compute) {  // wave-uniform: every lane runs the DPP exchanges below; stores are masked
@@ -660,7 +680,7 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
 #pragma unroll
             for (int f = 0; f < 4; ++f) {
               const int l = (side << k) | ((f & 1) << e1) | ((f >> 1) << e2);
-              Tf[f] = T[(int64_t)l * ncell + cid];
+              Tf[f] = T[ca.base + (int64_t)l * ca.stride + cq];
               Xf[f] = x[l];
               acc[f] = 0.0;
             }
@@ -691,7 +711,7 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
       if (writer && ci[2] >= g.k_begin && ci[2] < g.k_end) {
 #pragma unroll
         for (int l = 0; l < 8; ++l) {
-          out[(int64_t)l * ncell + cid] = y[l];
+          out[ca.base + (int64_t)l * ca.stride + cq] = y[l];
           dot += x[l] * y[l];
         }
       }
@@ -752,9 +772,11 @@ __global__ __launch_bounds__(kBlock) void k_dg_diag(DgGrid g, const double* __re
   double hd2 = 0.0;
 #pragma unroll
   for (int k = 0; k < A::NA; ++k) hd2 += h[A::axis(k)] * h[A::axis(k)];
+  const DgAddr ac = dg_layer(g, ci[2]);
+  const int64_t ij = (int64_t)ci[0] + (int64_t)g.c0 * ci[1];
   double Tl[NL];
 #pragma unroll
-  for (int l = 0; l < NL; ++l) Tl[l] = T[(int64_t)l * ncell + cid];
+  for (int l = 0; l < NL; ++l) Tl[l] = T[ac.base + (int64_t)l * ac.stride + ij];
 #pragma unroll
   for (int l = 0; l < NL; ++l) {
     double mm = 1.0, kk = 0.0;
@@ -821,7 +843,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_diag(DgGrid g, const double* __re
         }
       }
     }
-    out[(int64_t)l * ncell + cid] = invert ? 1.0 / d : d;
+    out[ac.base + (int64_t)l * ac.stride + ij] = invert ? 1.0 / d : d;
   }
 }
 

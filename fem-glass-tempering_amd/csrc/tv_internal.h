@@ -77,6 +77,15 @@ struct DgGrid {
   // 0 = one thread per cell (k_dg_cells, the reference the tile kernel is
   // tested against); tv_options.dg_kernel / dg_tile_chunk
   int tile, tile_chunk;
+  // partitions along storage axis 2: local layers [0, c2) = k_begin ghost
+  // layers below the owned ones [k_begin, k_end) and c2 - k_end above.  The
+  // owned layers' dofs come first, component-major over the `own` owned cells
+  // ([l][owned cell], so the owned dofs are one contiguous range as the Krylov
+  // vector kernels need); each ghost layer's follow, component-major over its
+  // c0 c1 cells, from offset gofs[0] (below) / gofs[1] (above).  One partition:
+  // own = c0 c1 c2 -- the plain [l][cell] layout.
+  int64_t own;
+  int64_t gofs[2];
 };
 
 // two-level in-kernel reduction tails (tv_device.h fused_reduce_tail): kShards

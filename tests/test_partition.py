@@ -207,6 +207,50 @@ def test_partitioned_local_gmg_solves(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,kernel", [(2, "tile"), (3, "tile"), (3, "cells")])
+def test_partitioned_dg_matches_single_partition(world, kernel):
+    """DG1 temperature and stress on slabs of cell layers (the SIPG facets of
+    the interfaces read one ghost cell layer, exchanged with all 8 cell-local
+    dofs): Jacobi-PCG on 2 / 3 partitions reproduces the single partition --
+    T <= 1e-12, equal Newton counts -- with the marching tile kernel and the
+    one-thread-per-cell kernel (ThermoViscoProblem.py:308-325 under mpiexec)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _partition_check(world, "host", 29780 + world + (kernel == "cells") * 5,
+                     ("--family", "DG", "--dg-kernel", kernel, "--pcg", "kspcg", "--steps", "3"))
+
+
+@pytest.mark.gpu
+def test_partitioned_dg_output_series():
+    """The writers on a DG1 slab partition: each part writes the discontinuous
+    fields of its owned cell layers; concatenated they equal the gathered state."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _partition_check(2, "host", 29777, ("--family", "DG", "--steps", "2", "--output"))
+    assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
+def test_partitioned_mixed_families_refused():
+    """A partition needs the same family for T and sigma (DG T / CG sigma, the
+    main.py pairing, runs on one partition)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from tvfem import box_mesh
+    from tvfem._native import NativeError
+    from tvfem.problem import ThermoViscoProblem
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from partition_check import MP
+    with pytest.raises(NativeError):
+        ThermoViscoProblem(box_mesh([1.0, 2.0, 1.0], [4, 6, 2]), (0, 1), 0.1,
+                           {"T": {"element": "DG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}, MP,
+                           n_parts=2, part=0, part_axis=1, verbose=False)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pc", ["jacobi", "gmg"])
 def test_partitioned_dirichlet_matches_single_partition(pc):
     """Paper mode with T = T_ambient on the exterior boundary on 2 slabs: the

@@ -38,8 +38,9 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
       "alpha_liquid": 25.1e-6}
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
-# name: (mesh kind, cells, parts, part, Krylov form, preconditioner, replication bound)
+# name: (mesh kind, cells, parts, part, Krylov form, preconditioner, replication bound[, family])
 CASES = {
+    "dg_mid": ("box", (8, 12, 3), 3, 1, "kspcg", "jacobi", 0, "DG"),
     "box_single_mid": ("box", (10, 30, 5), 3, 1, "single", "jacobi", 0),
     "box_kspcg_mid": ("box", (10, 30, 5), 3, 1, "kspcg", "jacobi", 0),
     "box_kspcg_first": ("box", (10, 30, 5), 2, 0, "kspcg", "jacobi", 0),
@@ -50,10 +51,11 @@ CASES = {
 }
 
 
-def _problem(kind, cells, parts, part, pcg, pc, rep):
+def _problem(kind, cells, parts, part, pcg, pc, rep, family="CG"):
     mesh = (distorted_box_mesh if kind == "distorted" else box_mesh)([2.0, 6.0, 1.0], list(cells))
     kw = {} if kind == "distorted" else {"part_axis": 1}
-    return ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, n_parts=parts, part=part, verbose=False,
+    cfg = {"T": {"element": family, "degree": 1}, "sigma": {"element": family, "degree": 1}}
+    return ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, MP, n_parts=parts, part=part, verbose=False,
                               pcg_variant=pcg, preconditioner=pc, mg_replicate_nodes=rep, write_output=False, **kw)
 
 
@@ -85,10 +87,10 @@ def _steps(p, steps):
 
 
 def run_case(name, steps=3):
-    kind, cells, parts, part, pcg, pc, rep = CASES[name]
+    kind, cells, parts, part, pcg, pc, rep, *fam = CASES[name]
     lib = N.load_library()
     # RCCL loopback
-    a = _problem(kind, cells, parts, part, pcg, pc, rep)
+    a = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
     uid = C.create_string_buffer(lib.tv_comm_unique_id_size())
     N.check(lib.tv_comm_get_unique_id(uid))
     N.check(lib.tv_comm_init_loopback(a._ctx, uid.raw), a._ctx)
@@ -98,7 +100,7 @@ def run_case(name, steps=3):
     variant = a.pcg_variant
     a.close()
     # host-staged loopback
-    b = _problem(kind, cells, parts, part, pcg, pc, rep)
+    b = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
     _host_loopback(b)
     rb, itb, errb = _steps(b, steps)
     b.close()

@@ -31,8 +31,10 @@ CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree":
 
 
 def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0,
-        outdir=None, dirichlet=False, edit_field="T", mg_coupling="auto"):
-    p = ThermoViscoProblem(mesh, (0, 1), 0.1, CFG, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
+        outdir=None, dirichlet=False, edit_field="T", mg_coupling="auto", family="CG", dg_kernel="auto"):
+    cfg = {"T": {"element": family, "degree": 1}, "sigma": {"element": family, "degree": 1}}
+    p = ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
+                           dg_kernel=dg_kernel,
                            verbose=False, pcg_variant=pcg, write_output=outdir is not None,
                            output_dir=outdir or "output", preconditioner=pc, mg_replicate_nodes=mg_rep,
                            model_mode="paper" if dirichlet else "reference", mg_coupling=mg_coupling)
@@ -88,6 +90,8 @@ def main():
     ap.add_argument("--edit", action="store_true", help="host edit of T on the owning rank only, after setup()")
     ap.add_argument("--edit-field", default="T", help="--edit: the field edited (T, Tf, Tf_partial, phi, xi)")
     ap.add_argument("--dirichlet", action="store_true", help="paper mode with the Dirichlet condition T = T_ambient")
+    ap.add_argument("--family", choices=["CG", "DG"], default="CG", help="element family of T and sigma")
+    ap.add_argument("--dg-kernel", choices=["auto", "tile", "cells"], default="auto")
     ap.add_argument("--mg-coupling", choices=["auto", "global", "local"], default="auto",
                     help="partitioned GMG: the distributed V-cycle of the whole box, or each slab's own (block Jacobi)")
     ap.add_argument("--pc", choices=["jacobi", "gmg", "amg"], default="jacobi")
@@ -114,15 +118,17 @@ def main():
             raise SystemExit(f"--comm rccl needs {world} GPUs, {torch.cuda.device_count()} visible")
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
                        pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir,
-                       dirichlet=a.dirichlet, edit_field=a.edit_field, mg_coupling=a.mg_coupling)
+                       dirichlet=a.dirichlet, edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family,
+                       dg_kernel=a.dg_kernel)
     else:
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
                        edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir, dirichlet=a.dirichlet,
-                       edit_field=a.edit_field, mg_coupling=a.mg_coupling)
+                       edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family, dg_kernel=a.dg_kernel)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
-        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc, dirichlet=a.dirichlet, edit_field=a.edit_field)
+        ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc, dirichlet=a.dirichlet, edit_field=a.edit_field,
+                           family=a.family, dg_kernel=a.dg_kernel)
         res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "mesh": a.mesh, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             if "l2g" in gathered[0]:  # scatter every part's owned vertices to their global ids
