@@ -1009,380 +1009,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
 }
 
 // ---------------------------------------------------------------------------
-// The marching matvec with RPW rows per wave (round 4; the production shape,
-// RPW = 2): a workgroup of R waves owns a tile of R RPW ADJACENT rows, wave w
-// rows r0 + RPW w + j.  A row's neighbours inside the wave's own rows come from
-// registers, only the outer ones from the LDS slab -- per plane and barrier
-// the tile produces R RPW output rows for R RPW + 2 loaded rows (halo share
-// 1/(R RPW) instead of 1/R), and each wave keeps RPW rows of loads in flight
-// (tools/probe/march_probe.hip variant D: 35.3 vs 39.6 us for the bare C4
-// march, flushed).  Everything else as k_cg_march: the prefetch ring, the
-// march-axis Robin facets of the first / last chunk in the prologue, the face
-// workgroups appended to the launch (R waves, face_block), POST, the tails.
-// One LDS region serves the plane slab, the prologue's face-plane staging
-// (before the slab is first written) and the face workgroups.
-// ---------------------------------------------------------------------------
-constexpr int kRowsPerWave = 2;
-constexpr int cmax3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
-
-template <int MODE, bool FUSEP, int R, int RPW, int PF, bool POST = false>
-__global__ __launch_bounds__(R * kWave) void k_cg_march2(CgGrid g, const double* __restrict__ T,
-                                                         const double* __restrict__ in0, const double* in1,
-                                                         double* __restrict__ out, double* pout,
-                                                         const PcgState* __restrict__ st,
-                                                         double* __restrict__ partials, int nseg, int raxis,
-                                                         int qchunk, RedTail rt, int nrec, int nmarch,
-                                                         FaceOff fo, int it_host, PostArgs pa) {
-  static_assert(!POST || (MODE == MODE_JAC && !FUSEP), "POST: plain Jacobian march only");
-  constexpr int RT = R * RPW;                         // rows per tile
-  constexpr int NA = (MODE == MODE_RES) ? 2 : 1;      // slab arrays: stiffness input (+ mass input)
-  constexpr int kSlab = NA * 2 * (RT + 2) * kWave;    // double-buffered plane slab
-  constexpr int kPro = (MODE == MODE_JAC) ? (4 * RT + 4) * kWave : 0;  // face plane [T, p][RT + 2] + [c, d][RT]
-  constexpr int kFB = (MODE == MODE_JAC) ? (4 * R + 2) * kWave : 0;    // face_block: T, p of R + 1 rows, c, d of R
-  __shared__ double sm[cmax3(kSlab, kPro, kFB)];
-  __shared__ double red[R];
-  __shared__ double red2[R];
-  stamp_start(rt);
-  const int bid = (int)blockIdx.x;
-  const int fidx = (MODE == MODE_JAC && bid >= nmarch) ? bid - nmarch : -1;
-  if (fidx >= 0) {
-    if (st != nullptr && st->done) return;
-    face_block<FUSEP, R>(g, T, in0, in1, pout, st, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx, fo,
-                         sm, red, it_host);
-    return;
-  }
-  double (*lds)[2][RT + 2][kWave] = reinterpret_cast<double (*)[2][RT + 2][kWave]>(sm);
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int n0 = g.n0;
-  const int nR = (raxis == 1) ? g.n1 : g.n2;
-  const int nQ = (raxis == 1) ? g.n2 : g.n1;
-  const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
-  const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
-  const int qaxis = 3 - raxis;
-  const int nch = (nQ + qchunk - 1) / qchunk;
-  const int nrbk = (nR + RT - 1) / RT;
-  int seg, rb, chunk;
-  march_tile(bid, nmarch, nseg, nrbk, nch, seg, rb, chunk);
-  const int r0 = rb * RT;
-  const int w0 = RPW * wave;  // the wave's first row within the tile
-  const int q0 = chunk * qchunk;
-  const int q1 = min(q0 + qchunk, nQ);
-  const int i = seg * kSeg - 1 + lane;
-  const bool col_ok = (i >= 0) && (i < n0);
-  const bool writer = col_ok && lane >= 1 && lane <= kSeg;
-  double bcoef = 0.0;
-  bool first = false;
-  const double* pold = in1;
-  if (FUSEP) {
-    first = (it_host == 0);
-    if (!(it_host & 1)) { pold = pout; pout = const_cast<double*>(in1); }
-  }
-  const int kb = g.k_begin, ke = g.k_end;
-  int rj[RPW];
-  bool rok[RPW], rown[RPW];
-  double My0[RPW], My1[RPW], My2[RPW], Ky0[RPW], Ky1[RPW], Ky2[RPW], hq_own[RPW];
-#pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    rj[j] = r0 + w0 + j;
-    rok[j] = rj[j] < nR;
-    rown[j] = (raxis == 2) ? (rj[j] >= kb && rj[j] < ke) : true;
-    const double* cr = g.coef[raxis] + (int64_t)(rok[j] ? rj[j] : 0) * C_NCOEF;
-    My0[j] = uniform(cr[C_MLO]); My1[j] = uniform(cr[C_MDI]); My2[j] = uniform(cr[C_MUP]);
-    Ky0[j] = uniform(cr[C_KLO]); Ky1[j] = uniform(cr[C_KDI]); Ky2[j] = uniform(cr[C_KUP]);
-    hq_own[j] = uniform(cr[C_HHI]);
-  }
-  const double hq_low = uniform(g.coef[raxis][(int64_t)(r0 >= 1 ? r0 - 1 : 0) * C_NCOEF + C_HHI]);
-  const double da = g.dt_alpha;
-  const bool fq0 = (MODE == MODE_JAC) && q0 == 0 && g.bnd[qaxis][0];
-  const bool fq1 = (MODE == MODE_JAC) && q1 == nQ && g.bnd[qaxis][1];
-  const double* second = (MODE == MODE_RES) ? in1 : pold;
-  constexpr bool TWO = (MODE == MODE_RES) || FUSEP;
-  const uint32_t nbytes = (uint32_t)g.n0 * (uint32_t)g.n1 * (uint32_t)g.n2 * 8u;
-  const buf_t rs0 = mk_rsrc(in0, nbytes);
-  const buf_t rs1 = mk_rsrc(TWO ? second : in0, (FUSEP && first) ? 0u : nbytes);
-  const buf_t rso = mk_rsrc(out, nbytes);
-  const buf_t rsp = mk_rsrc(FUSEP ? pout : out, FUSEP ? nbytes : 0u);
-  const buf_t rsT = mk_rsrc(T, (fq0 || fq1) ? nbytes : 0u);
-  const buf_t rsZ = mk_rsrc(in0, (fq0 || fq1) ? nbytes : 0u);
-  const buf_t rsO = mk_rsrc(TWO ? second : in0, ((fq0 || fq1) && FUSEP && !first) ? nbytes : 0u);
-  const bool halo = (wave == 0) || (wave == R - 1);
-  const int hrow = (wave == 0) ? r0 - 1 : r0 + RT;
-  const int hslot = (wave == 0) ? 0 : RT + 1;
-  auto lane_off = [&](int rr) -> uint32_t {
-    return (col_ok && rr >= 0 && rr < nR) ? (uint32_t)(i + sR * rr) * 8u : kBadOff;
-  };
-  uint32_t vo_own[RPW], vo_wr[RPW];
-#pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    vo_own[j] = lane_off(rj[j]);
-    vo_wr[j] = writer ? vo_own[j] : kBadOff;
-  }
-  const uint32_t vo_halo = halo ? lane_off(hrow) : kBadOff;
-  auto plane_off = [&](int L) -> uint32_t { return (L >= 0 && L < nQ) ? (uint32_t)(sQ * L) * 8u : kBadOff; };
-  auto fetch = [&](uint32_t vo, int L, double& a0, double& a1) {
-    const uint32_t o = vo + plane_off(L);
-    a0 = bload(rs0, o);
-    a1 = TWO ? bload(rs1, o) : 0.0;
-  };
-  const buf_t rsr = mk_rsrc(pa.r, POST ? nbytes : 0u);
-  const buf_t rsd = mk_rsrc(pa.dinv, POST ? nbytes : 0u);
-  auto fetch_post = [&](uint32_t vw, int L, double& a_r, double& a_d) {
-    if (!POST) return;
-    const uint32_t o = vw + plane_off(L - 1);
-    a_r = bload(rsr, o);
-    a_d = bload(rsd, o);
-  };
-  auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
-    v = a0;
-    vm = 0.0;
-    if (MODE == MODE_RES) vm = (vo != kBadOff && L >= 0 && L < nQ) ? a0 - a1 - g.dt_f : 0.0;
-    if (FUSEP) v = a0 + bcoef * a1;
-  };
-  // prefetch ring: PF + 1 register sets, RPW own rows + the halo row each
-  double ra0[PF + 1][RPW], ra1[PF + 1][RPW], rh0[PF + 1], rh1[PF + 1];
-  double rr[PF + 1][RPW], rd[PF + 1][RPW];
-#pragma unroll
-  for (int s = 0; s < PF; ++s) {
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      fetch(vo_own[j], q0 - 1 + s, ra0[s][j], ra1[s][j]);
-      fetch_post(vo_wr[j], q0 - 1 + s, rr[s][j], rd[s][j]);
-    }
-    fetch(vo_halo, q0 - 1 + s, rh0[s], rh1[s]);
-  }
-  if (FUSEP) {
-    if (st->done) return;
-    bcoef = first ? 0.0 : st->beta / st->betaold;
-  } else if (st != nullptr && st->done) {
-    return;
-  }
-  // face planes (T, z, p_old of the own rows and the halo row), loads first
-  double fT[2][RPW + 1], fZ[2][RPW + 1], fO[2][RPW + 1];
-  if (fq0 || fq1) {
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const uint32_t po = plane_off(f == 0 ? (fq0 ? 0 : -1) : (fq1 ? nQ - 1 : -1));
-#pragma unroll
-      for (int j = 0; j <= RPW; ++j) {
-        const uint32_t vo = (j < RPW) ? vo_own[j] : vo_halo;
-        fT[f][j] = bload(rsT, vo + po);
-        fZ[f][j] = bload(rsZ, vo + po);
-        fO[f][j] = FUSEP ? bload(rsO, vo + po) : 0.0;
-      }
-    }
-  }
-  __shared__ double2 cql[kFaceChunk + 2][5];
-  __shared__ double2 cxl[4][kWave];
-  const int nqs = q1 - q0 + 2;
-  const bool st_q = (int)threadIdx.x < nqs * 6;
-  const bool st_x = (int)threadIdx.x < 8 * kWave;
-  double cqv, cxv;
-  {
-    const int e = threadIdx.x;
-    const int qq = q0 - 1 + e / 6;
-    const bool okq = st_q && qq >= 0 && qq < nQ;
-    cqv = g.coef[qaxis][okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
-    cqv = okq ? cqv : 0.0;
-    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
-    const bool okx = st_x && ii >= 0 && ii < n0;
-    const int k = e >> 6;
-    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
-    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
-    cxv = (okx && k < 7) ? cxv : 0.0;
-  }
-  if (st_q) {
-    const int qs = threadIdx.x / 6, c = threadIdx.x % 6;
-    double* row = reinterpret_cast<double*>(cql[qs]);
-    if (c < 3) {
-      row[c] = cqv;
-      row[6 + c] = da * cqv;
-    } else {
-      row[c] = da * cqv;
-    }
-    if (c == 0) row[9] = 0.0;
-  }
-  if (st_x) reinterpret_cast<double*>(cxl[(threadIdx.x >> 6) >> 1])[2 * (threadIdx.x & (kWave - 1)) + ((threadIdx.x >> 6) & 1)] = cxv;
-  double yq[2][RPW];
-#pragma unroll
-  for (int f = 0; f < 2; ++f)
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) yq[f][j] = 0.0;
-  __syncthreads();  // cql / cxl
-  if (fq0 || fq1) {
-    // one face plane at a time through the staging area (both only when the
-    // march axis is a single chunk); facet rows rj of the wave's rows, wave 0
-    // also r0 - 1; corners c, d exchanged through LDS
-    double (*sF)[RT + 2][kWave] = reinterpret_cast<double (*)[RT + 2][kWave]>(sm);                  // [T, p]
-    double (*sC)[RT][kWave] = reinterpret_cast<double (*)[RT][kWave]>(sm + 2 * (RT + 2) * kWave);  // [c, d]
-    const bool cok = i >= 0 && i < n0 - 1;
-    const double h1 = cxl[3][lane].x;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      if (!(f == 0 ? fq0 : fq1)) continue;  // block-uniform
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        sF[0][w0 + j + 1][lane] = fT[f][j];
-        sF[1][w0 + j + 1][lane] = FUSEP ? fZ[f][j] + bcoef * fO[f][j] : fZ[f][j];
-      }
-      if (halo) {
-        sF[0][hslot][lane] = fT[f][RPW];
-        sF[1][hslot][lane] = FUSEP ? fZ[f][RPW] + bcoef * fO[f][RPW] : fZ[f][RPW];
-      }
-      __syncthreads();
-      double ylow = 0.0;
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        double ya, yb, yc, yd;
-        facet_corners(g, cok && rj[j] < nR - 1, h1, hq_own[j], sF[0][w0 + j + 1][lane], sF[0][w0 + j + 2][lane],
-                      sF[1][w0 + j + 1][lane], sF[1][w0 + j + 2][lane], ya, yb, yc, yd);
-        yq[f][j] = ya + shr1(yb);
-        sC[0][w0 + j][lane] = yc;
-        sC[1][w0 + j][lane] = yd;
-      }
-      if (wave == 0) {  // the facet row below the tile
-        double ya, yb, yc, yd;
-        facet_corners(g, cok && r0 >= 1 && r0 - 1 < nR - 1, h1, hq_low, sF[0][0][lane], sF[0][1][lane],
-                      sF[1][0][lane], sF[1][1][lane], ya, yb, yc, yd);
-        ylow = yc + shr1(yd);
-      }
-      __syncthreads();
-      const int lm = lane >= 1 ? lane - 1 : 0;
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        const int idx = w0 + j;
-        if (idx >= 1) yq[f][j] += sC[0][idx - 1][lane] + sC[1][idx - 1][lm];
-      }
-      if (wave == 0) yq[f][0] += ylow;
-      __syncthreads();  // the staging area is the slab (or the next face plane) next
-    }
-  }
-  // sliding windows per row over three planes
-  double us_m[RPW], us_c[RPW], t_m[RPW], t_c[RPW], xc[RPW];
-#pragma unroll
-  for (int j = 0; j < RPW; ++j) us_m[j] = us_c[j] = t_m[j] = t_c[j] = xc[j] = 0.0;
-  double dot = 0.0, zz = 0.0, zr = 0.0;
-  auto step = [&](int L, const double (&c0)[RPW], const double (&c1)[RPW], double h0, double h1v,
-                  const double (&pr)[RPW], const double (&pd)[RPW]) {
-    const int buf = L & 1;
-    double v[RPW], vm[RPW];
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      combine(vo_own[j], L, c0[j], c1[j], v[j], vm[j]);
-      if (FUSEP) bstore(rsp, vo_wr[j] + ((L >= q0 && L < q1) ? plane_off(L) : kBadOff), v[j]);
-      lds[0][buf][w0 + j + 1][lane] = v[j];
-      if (MODE == MODE_RES) lds[NA - 1][buf][w0 + j + 1][lane] = vm[j];
-    }
-    if (halo) {
-      double hv, hvm;
-      combine(vo_halo, L, h0, h1v, hv, hvm);
-      lds[0][buf][hslot][lane] = hv;
-      if (MODE == MODE_RES) lds[NA - 1][buf][hslot][lane] = hvm;
-    }
-    __syncthreads();
-    const double xlo = lds[0][buf][w0][lane], xhi = lds[0][buf][w0 + RPW + 1][lane];
-    double mlo = 0.0, mhi = 0.0;
-    if (MODE == MODE_RES) {
-      mlo = lds[NA - 1][buf][w0][lane];
-      mhi = lds[NA - 1][buf][w0 + RPW + 1][lane];
-    }
-    const bool outp = L >= q0 + 1 && L <= q1;
-    const int q = L - 1;
-    double S1c = 0.0, S2c = 0.0;
-    double2 c01{}, c23{}, c45{}, c67{}, c89{}, xlo2{}, xdi{}, xup{};
-    if (outp) {
-      const double2* cq = cql[q - q0 + 1];
-      c01 = cq[0]; c23 = cq[1]; c45 = cq[2]; c67 = cq[3]; c89 = cq[4];
-      xlo2 = cxl[0][lane]; xdi = cxl[1][lane]; xup = cxl[2][lane];
-    }
-    (void)S1c; (void)S2c;
-    const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      const double x0 = (j == 0) ? xlo : v[j - 1];
-      const double x2 = (j == RPW - 1) ? xhi : v[j + 1];
-      const double us_p = My0[j] * x0 + My1[j] * v[j] + My2[j] * x2;
-      const double vs_p = Ky0[j] * x0 + Ky1[j] * v[j] + Ky2[j] * x2;
-      double um_p = us_p;
-      if (MODE == MODE_RES) {
-        const double m0 = (j == 0) ? mlo : vm[j - 1];
-        const double m2 = (j == RPW - 1) ? mhi : vm[j + 1];
-        um_p = My0[j] * m0 + My1[j] * vm[j] + My2[j] * m2;
-      }
-      const double t_p = um_p + da * vs_p;
-      if (outp) {
-        const double S1 = c01.x * t_m[j] + c01.y * t_c[j] + c23.x * t_p + (c23.y * us_m[j] + c45.x * us_c[j] + c45.y * us_p);
-        const double S2 = c67.x * us_m[j] + c67.y * us_c[j] + c89.x * us_p;
-        const double Lt = xup.x * S1 + xup.y * S2;
-        const double Rt = xlo2.x * S1 + xlo2.y * S2;
-        const double y = (xdi.x * S1 + xdi.y * S2) + (shr1(Lt) + shl1(Rt));
-        const bool wr = writer && rok[j] && rown[j] && q_owned;
-        double yb = y;
-        if (fq0 && q == 0) yb += yq[0][j];
-        if (fq1 && q == nQ - 1) yb += yq[1][j];
-        if (POST) {
-          const double zq = xc[j] + pa.omega * pd[j] * (pr[j] - yb);
-          bstore(rso, (rown[j] && q_owned) ? vo_wr[j] + plane_off(q) : kBadOff, zq);
-          zz += wr ? zq * zq : 0.0;
-          zr += wr ? zq * pr[j] : 0.0;
-        } else {
-          bstore(rso, (rown[j] && q_owned) ? vo_wr[j] + plane_off(q) : kBadOff, yb);
-        }
-        if (MODE == MODE_JAC && !POST) dot += wr ? xc[j] * yb : 0.0;
-      }
-      xc[j] = v[j];
-      us_m[j] = us_c[j]; us_c[j] = us_p;
-      t_m[j] = t_c[j]; t_c[j] = t_p;
-    }
-  };
-  for (int L = q0 - 1; L <= q1; L += PF + 1) {
-#pragma unroll
-    for (int s = 0; s <= PF; ++s) {
-      const int sf = (s + PF) % (PF + 1);
-#pragma unroll
-      for (int j = 0; j < RPW; ++j) {
-        fetch(vo_own[j], L + s + PF, ra0[sf][j], ra1[sf][j]);
-        fetch_post(vo_wr[j], L + s + PF, rr[sf][j], rd[sf][j]);
-      }
-      fetch(vo_halo, L + s + PF, rh0[sf], rh1[sf]);
-      step(L + s, ra0[s], ra1[s], rh0[s], rh1[s], rr[s], rd[s]);
-    }
-  }
-  if (POST) {
-    zz = wave_sum(zz);
-    zr = wave_sum(zr);
-    if (lane == 0) {
-      red[wave] = zz;
-      red2[wave] = zr;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double a = 0.0, c = 0.0;
-#pragma unroll
-      for (int w = 0; w < R; ++w) {
-        a += red[w];
-        c += red2[w];
-      }
-      store_partial(&partials[2 * (int64_t)bid], a);
-      store_partial(&partials[2 * (int64_t)bid + 1], c);
-    }
-    return;
-  }
-  if (MODE == MODE_JAC && partials != nullptr) {
-    dot = wave_sum(dot);
-    if (lane == 0) red[wave] = dot;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double sacc = 0.0;
-#pragma unroll
-      for (int w = 0; w < R; ++w) sacc += red[w];
-      store_partial(&partials[blockIdx.x], sacc);
-    }
-    fused_reduce_tail<1>(rt, nrec);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Single-reduction Jacobi-PCG iteration fused with the marching Jacobian: the
 // Chronopoulos-Gear form of CG, ONE launch and ONE reduction per iteration
 // (PETSc KSPCG, which the reference runs at ThermoViscoProblem.py:339-346,
@@ -1938,12 +1564,7 @@ int bnd_blocks(const CgGrid& g) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 1024));
 }
 
-// rows of the production march tiles (kRows waves x kMarchRPW rows each; 1:
-// the one-row-per-wave k_cg_march).  The single-reduction march (k_cgs_march)
-// keeps 8-row tiles (plan(g, ghosts) with the default `rows`).
-constexpr int kMarchRPW = kRowsPerWave;
-
-Launch plan(const CgGrid& g, bool ghosts, int rows = kRows) {
+Launch plan(const CgGrid& g, bool ghosts) {
   Launch L{};
   L.nseg = (g.n0 + kSeg - 1) / kSeg;
   L.march = use_march(g);
@@ -1952,7 +1573,7 @@ Launch plan(const CgGrid& g, bool ghosts, int rows = kRows) {
     // the kernel covers every local node (ghost planes included) so the fused
     // PCG matvec refreshes p everywhere; outputs go to owned nodes only.
     L.raxis = (g.n2 >= g.n1) ? 2 : 1;
-    L.rows = rows;
+    L.rows = kRows;
     const int nR = (L.raxis == 1) ? g.n1 : g.n2;
     const int nQ = (L.raxis == 1) ? g.n2 : g.n1;
     const int nrb = (nR + L.rows - 1) / L.rows;
@@ -1967,8 +1588,8 @@ Launch plan(const CgGrid& g, bool ghosts, int rows = kRows) {
     L.qchunk = (nQ + nchunks - 1) / nchunks;
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
     L.blocks = L.nseg * nrb * nchunks;
-    // Jacobian partial records: one per marching tile and face workgroup (kRows waves)
-    L.nparts = L.blocks + face_offsets(g, kRows, 3 - L.raxis).off[6];
+    // Jacobian partial records: one per marching tile and face workgroup
+    L.nparts = L.blocks + face_offsets(g, L.rows, 3 - L.raxis).off[6];
     return L;
   }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
@@ -1988,7 +1609,7 @@ template <int MODE, bool FUSEP>
 bool launch_rows(const CgGrid& g, const double* T, const double* in0, const double* in1, double* out,
                  double* pout, const PcgState* st, double* partials, bool ghosts, hipStream_t s,
                  const RedTail* tail = nullptr, int it_host = 0, bool addfaces = true, double* dinv_bnd = nullptr) {
-  const Launch L = plan(g, ghosts, kRows * kMarchRPW);
+  const Launch L = plan(g, ghosts);
   if (L.blocks <= 0) return false;
   if (L.march) {
     // Jacobian: the Robin facet terms come from k_cg_faces (launched first)
@@ -1997,18 +1618,13 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     const bool folded = MODE == MODE_JAC;
     RedTail rt{};
     if (folded && tail && partials) rt = *tail;
-    const FaceOff fo = folded ? face_offsets(g, kRows, 3 - L.raxis) : FaceOff{};
+    const FaceOff fo = folded ? face_offsets(g, L.rows, 3 - L.raxis) : FaceOff{};
     const int grid = L.blocks + fo.off[6];
-    // R = 8 waves, prefetch depth 2 (measured best, round 1-2: R = 16, PF 3 / 4,
-    // 8 waves per SIMD and an LDS-DMA plane ring were all slower); kMarchRPW rows per wave
-    if constexpr (kMarchRPW == 1)
-      hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, kRows, 1, 2>), dim3(grid), dim3(kRows * kWave), 0, s, g, T, in0,
-                         in1, out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, it_host,
-                         PostArgs{});
-    else
-      hipLaunchKernelGGL((k_cg_march2<MODE, FUSEP, kRows, kMarchRPW, 2>), dim3(grid), dim3(kRows * kWave), 0, s, g, T,
-                         in0, in1, out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo,
-                         it_host, PostArgs{});
+    // R = 8 rows, prefetch depth 2 (measured best, round 1-2: R = 16, PF 3 / 4,
+    // 8 waves per SIMD and an LDS-DMA plane ring were all slower)
+    hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, kRows, 1, 2>), dim3(grid), dim3(kRows * kWave), 0, s, g, T, in0, in1,
+                       out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, it_host,
+                       PostArgs{});
     if (folded && !FUSEP && addfaces && fo.off[6] > 0) {  // complete J x (else the consumer adds them)
       const int64_t nodes = 2 * ((int64_t)g.n1 * (g.k_end - g.k_begin) + (int64_t)g.n0 * std::max(g.n1, g.n2));
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, 1024));
@@ -2148,22 +1764,17 @@ __global__ __launch_bounds__(kBlock) void k_mg_prep_diag(MgPrep p) {
 int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
                           double omega, double* z, const PcgState* st, double* partials, const RedTail* tail,
                           hipStream_t s) {
-  const Launch L = plan(g, false, kRows * kMarchRPW);
+  const Launch L = plan(g, false);
   // the production march configuration only; a partition's slab too (the march
   // writes z and its records on the owned planes only, the side-face pass skips
   // the ghost planes)
   if (!L.march || g.n0 < 3) return -1;
-  const FaceOff fo = face_offsets(g, kRows, 3 - L.raxis);
+  const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
   const int grid = L.blocks + fo.off[6];
   const PostArgs pa{r, dinv, omega};
-  if constexpr (kMarchRPW == 1)
-    hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, kRows, 1, 2, true>), dim3(grid), dim3(kRows * kWave), 0, s, g, T,
-                       x, nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks,
-                       fo, 0, pa);
-  else
-    hipLaunchKernelGGL((k_cg_march2<MODE_JAC, false, kRows, kMarchRPW, 2, true>), dim3(grid), dim3(kRows * kWave), 0,
-                       s, g, T, x, nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts,
-                       L.blocks, fo, 0, pa);
+  hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, 1, 2, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T, x,
+                     nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks, fo,
+                     0, pa);
   const FaceAdd fa = cg_face_add(g, 0);
   const int nO = (L.raxis == 2) ? g.n1 : g.n2;
   const int64_t nodes = 2 * (int64_t)g.n1 * g.n2 + 2 * (int64_t)(g.n0 - 2) * nO;
@@ -2185,9 +1796,7 @@ void launch_mg_prepare(const MgPrep& p, hipStream_t s) {
   if (nb > 0) hipLaunchKernelGGL(k_mg_prep_diag, dim3((unsigned)((nb + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p);
 }
 
-int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) {
-  return std::max(plan(g, with_ghost_planes).nparts, plan(g, with_ghost_planes, kRows * kMarchRPW).nparts);
-}
+int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }
 
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off) {
   FaceAdd fa{};
@@ -2218,7 +1827,7 @@ bool launch_cg_residual_diag(const CgGrid& g, const double* T, const double* Tp,
 void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double* y, double* partials,
                       int* n_partials, hipStream_t s, const PcgState* st) {
   launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, st, partials, false, s);
-  if (n_partials) *n_partials = plan(g, false, kRows * kMarchRPW).nparts;
+  if (n_partials) *n_partials = plan(g, false).nparts;
 }
 
 void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
@@ -2232,7 +1841,7 @@ bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, d
   // neighbour values of p_new are recomputed from z and p_old; p_new goes to the
   // other buffer of the pair (selected on device from st->it).
   const bool fused = launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s, tail, it_host);
-  if (n_partials) *n_partials = plan(g, true, kRows * kMarchRPW).nparts;
+  if (n_partials) *n_partials = plan(g, true).nparts;
   return fused;
 }
 

@@ -19,7 +19,9 @@ int require_comm(Ctx* c, const char* what) {
 }
 
 int refresh_dirty_ghosts(Ctx* c) {
-  if (!(c->um && c->n_parts > 1) || !multi_rank(c) || c->comm_stub) return TV_OK;
+  // partitioned unstructured meshes and mixed-family slabs run the visco T pass
+  // on their ghost dofs too (their sigma pass / writers read them)
+  if (!((c->um && c->n_parts > 1) || c->mixed_part) || !multi_rank(c) || c->comm_stub) return TV_OK;
   // T and T_prev are exchanged every step anyway (newton); the other fields
   // only when a rank wrote them.  Every rank learns the union of the writes
   // through one all-reduce of a flag per field.
@@ -34,9 +36,10 @@ int refresh_dirty_ghosts(Ctx* c) {
   bool tilde = false;
   for (int f = 0; f < TV_NUM_FIELDS; ++f) {
     if (fl[f] == 0.0 || !c->f[f].ptr || f == TV_F_T || f == TV_F_T_PREV) continue;
-    const int64_t stride = c->f[f].space == 0 ? c->nT : c->nS;  // the same vertex set (CG1 / CG1)
+    if (c->mixed_part && c->f[f].space != 0) continue;  // the sigma space of a mixed slab has no ghosts
+    const int64_t stride = c->f[f].space == 0 ? c->nT : c->nS;  // unstructured: the same vertex set (CG1 / CG1)
     for (int k = 0; k < c->f[f].bs; ++k)
-      if (int e = halo_um(c, c->f[f].ptr + k * stride)) return e;
+      if (int e = halo(c, c->f[f].ptr + k * stride)) return e;
     tilde = tilde || f == TV_F_S_TILDE || f == TV_F_S_TILDE_NEXT || f == TV_F_SIGMA_TILDE || f == TV_F_SIGMA_TILDE_NEXT;
   }
   if (tilde) {  // a neighbour's non-zero tilde values may now sit in this rank's ghosts

@@ -172,6 +172,101 @@ int build_cg_grid(Ctx* c, int d, const std::vector<double> (&X)[3], int first2, 
   return TV_OK;
 }
 
+// Mixed families on a slab partition (the reference's main.py pairing DG T /
+// CG sigma, ThermoViscoProblem.py:61-103 under mpiexec, and CG T / DG sigma).
+// The T space is partitioned as on its own (CG: node planes [b0, b1) + one
+// ghost plane per interface; DG: cell layers [b0, b1) + one ghost cell layer),
+// the sigma space follows without ghosts of its own:
+//  1 (DG T, CG sigma): sigma nodes on planes [b0, b1] are local -- [b0, b1)
+//    owned, plane b1 too on the last part -- and node (i, j, k) reads the T dof
+//    of the LAST cell fem::interpolate writes it from (the highest global cell
+//    index around it: (min(i, C0-1), min(j, C1-1), min(k, C2-1))), which is an
+//    owned cell, or for plane b1 of an inner part the ghost layer above;
+//  2 (CG T, DG sigma): sigma owns the cell layers [b0, min(b1, C2)); every
+//    corner node of those cells is local (plane b1 = the ghost plane above).
+// The visco T pass runs over every local T dof (ghosts included: their T is
+// exchanged after each Newton update, so they evolve as on their owners).
+int setup_mixed_part(Ctx* c) {
+  const int d = c->dim, nl = 1 << d;
+  const int P = c->n_parts, p = c->part;
+  const bool last = (p == P - 1);
+  const int b0 = c->plane_begin, b1 = c->plane_end;
+  const int C[3] = {std::max(1, c->Ncell_glob[0]), std::max(1, c->Ncell_glob[1]), std::max(1, c->Ncell_glob[2])};
+  const int N0 = c->Nnode_glob[0], N1 = c->Nnode_glob[1];
+  const bool act[3] = {true, c->perm[1] >= 0, c->perm[2] >= 0};
+  const int64_t npl = (int64_t)N0 * N1;   // nodes per plane
+  const int64_t pc = (int64_t)C[0] * C[1];  // cells per layer
+  // local corner index l of a cell from the corner offsets (active axes only)
+  auto corner = [&](const int bits[3]) {
+    int l = 0, k = 0;
+    for (int s = 0; s < 3; ++s) {
+      if (!act[s]) continue;
+      l |= bits[s] << k;
+      ++k;
+    }
+    return l;
+  };
+  std::vector<int> map;
+  if (c->fam_T == TV_DG) {  // 1: CG sigma on the nodes of planes [b0, b1]
+    c->mixed_part = 1;
+    const int nq = b1 - b0 + 1;
+    c->nS = npl * nq;
+    c->ownS_off = 0;
+    c->ownS_n = npl * (last ? nq : nq - 1);
+    c->globS_off = npl * b0;
+    c->outS_n = c->nS;
+    c->outT_n = c->ownT_n;
+    const DgGrid& g = c->dg;
+    map.assign((size_t)c->nS, -1);
+    for (int k = b0; k <= b1; ++k)
+      for (int j = 0; j < N1; ++j)
+        for (int i = 0; i < N0; ++i) {
+          const int ci[3] = {std::min(i, C[0] - 1), act[1] ? std::min(j, C[1] - 1) : 0,
+                             act[2] ? std::min(k, C[2] - 1) : 0};
+          const int bits[3] = {i - ci[0], j - ci[1], k - ci[2]};
+          const int l = corner(bits);
+          const int kl = ci[2] - b0 + g.k_begin;  // local cell layer
+          int64_t base, stride;
+          if (kl < g.k_begin) base = g.gofs[0], stride = pc;
+          else if (kl >= g.k_end) base = g.gofs[1], stride = pc;
+          else base = (int64_t)(kl - g.k_begin) * pc, stride = g.own;
+          if (base < 0) return c->fail(TV_ERR_ARG, "mixed partition: a sigma node outside the local cells (internal)");
+          const int64_t dof = base + (int64_t)l * stride + ci[0] + (int64_t)C[0] * ci[1];
+          map[(size_t)(i + N0 * (j + (int64_t)N1 * (k - b0)))] = (int)dof;
+        }
+  } else {  // 2: DG sigma on the cell layers [b0, L1)
+    c->mixed_part = 2;
+    const int L1 = std::min(b1, C[2]);
+    const int64_t ncl = pc * (L1 - b0);
+    c->nS = ncl * nl;
+    c->ownS_off = 0;
+    c->ownS_n = c->nS;
+    c->globS_off = pc * nl * b0;
+    c->outS_n = c->nS;
+    const CgGrid& g = c->cg;
+    c->outT_n = c->ownT_n + (g.g_hi ? npl : 0);  // the plane above: the owned cells' upper corners
+    map.assign((size_t)c->nS, -1);
+    for (int64_t cl = 0; cl < ncl; ++cl) {
+      const int ci[3] = {(int)(cl % C[0]), (int)((cl / C[0]) % C[1]), b0 + (int)(cl / pc)};
+      for (int l = 0; l < nl; ++l) {
+        int bits[3] = {0, 0, 0}, k = 0;
+        for (int s = 0; s < 3; ++s) {
+          if (!act[s]) continue;
+          bits[s] = (l >> k) & 1;
+          ++k;
+        }
+        const int kl = ci[2] + bits[2] - (b0 - g.g_lo);  // local node plane
+        if (kl < 0 || kl >= g.n2) return c->fail(TV_ERR_ARG, "mixed partition: a corner outside the local planes (internal)");
+        map[(size_t)((int64_t)l * ncl + cl)] =
+            (int)((ci[0] + bits[0]) + (int64_t)g.n0 * ((ci[1] + bits[1]) + (int64_t)g.n1 * kl));
+      }
+    }
+  }
+  HIPC(hipMalloc(&c->map, sizeof(int) * (size_t)std::max<int64_t>(1, c->nS)));
+  HIPC(hipMemcpy(c->map, map.data(), sizeof(int) * (size_t)c->nS, hipMemcpyHostToDevice));
+  return TV_OK;
+}
+
 int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   const int d = m->dim;
   if (d < 1 || d > 3) return c->fail(TV_ERR_ARG, "mesh dim must be 1..3");
@@ -189,9 +284,7 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
   c->n_parts = std::max(1, m->n_parts);
   c->part = m->part;
   if (c->part < 0 || c->part >= c->n_parts) return c->fail(TV_ERR_ARG, "part out of range");
-  if (c->n_parts > 1 && (d == 1 || c->fam_T != c->fam_S))
-    return c->fail(TV_ERR_ARG, "partitioned meshes require dim >= 2 and the same family for temperature and stress "
-                               "(CG / CG or DG / DG)");
+  if (c->n_parts > 1 && d == 1) return c->fail(TV_ERR_ARG, "partitioned meshes require dim >= 2");
   for (int s = 0; s < 3; ++s) {
     c->Ncell_glob[s] = (c->perm[s] < 0) ? 0 : m->n_cells[c->perm[s]];
     c->Nnode_glob[s] = c->Ncell_glob[s] + 1;
@@ -275,6 +368,8 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     c->ownS_off = c->ownT_off;
     c->ownS_n = c->ownT_n;
     c->globS_off = c->globT_off;
+  } else if (c->n_parts > 1) {
+    if (int e = setup_mixed_part(c)) return e;
   } else {
     const int nl = 1 << d;
     const int64_t ncell = (int64_t)std::max(1, c->Ncell_glob[0]) * std::max(1, c->Ncell_glob[1]) *
@@ -476,7 +571,8 @@ int transfer(Ctx* c, int field, double* host, size_t n, int dir) {
   }
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>(1, ((int64_t)need + 255) / 256), 16384);
   if (dir == 0) {
-    if (c->um && c->n_parts > 1 && field != TV_F_T && field != TV_F_T_PREV) c->ghost_dirty |= 1u << field;
+    if (((c->um && c->n_parts > 1) || (c->mixed_part && fi.space == 0)) && field != TV_F_T && field != TV_F_T_PREV)
+      c->ghost_dirty |= 1u << field;
     const bool tilde = field == TV_F_S_TILDE || field == TV_F_S_TILDE_NEXT || field == TV_F_SIGMA_TILDE ||
                        field == TV_F_SIGMA_TILDE_NEXT;
     if (tilde) {  // values other than +0.0 end the all-zero tracking of the tilde fields
@@ -1007,9 +1103,13 @@ int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const
     Xs[sx] = storage_coords(c, sx, tmp);
     phys[sx] = c->perm[sx];
   }
-  if (c->n_parts > 1 && !c->um)  // CG: the owned node planes; DG: the nodes of the owned cell layers
-    Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin,
-                                Xs[2].begin() + c->plane_end + (c->fam_T == TV_DG ? 1 : 0));
+  // CG: the owned node planes; DG: the nodes of the owned cell layers; mixed
+  // families: the nodes of the owned cell layers of the DG space
+  if (c->n_parts > 1 && !c->um) {
+    const int end = c->mixed_part == 2 ? std::min(c->plane_end + 1, c->Nnode_glob[2])
+                                       : c->plane_end + (c->fam_T == TV_DG ? 1 : 0);
+    Xs[2] = std::vector<double>(Xs[2].begin() + c->plane_begin, Xs[2].begin() + end);
+  }
   std::string err;
   // a partitioned unstructured mesh writes its own cells over all its local
   // vertices (the ghosts' values are kept current: visco runs on every local vertex)
@@ -1033,7 +1133,9 @@ int tv_output_open_named(void* ctx, const char* dir, const int* field_ids, const
     }
     const FieldInfo& fi = c->f[id];
     const bool dg = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
-    const int64_t n = (c->um && c->n_parts > 1) ? c->nT : (fi.space == 0) ? c->ownT_n : c->ownS_n;
+    const int64_t n = (c->um && c->n_parts > 1) ? c->nT
+                      : c->mixed_part ? (fi.space == 0 ? c->outT_n : c->outS_n)
+                                      : (fi.space == 0) ? c->ownT_n : c->ownS_n;
     const char* nm = (series_names && series_names[k] && series_names[k][0]) ? series_names[k] : names[id];
     for (const char* q = nm; *q; ++q)
       if (*q == '/' || *q == '\\') {
@@ -1069,7 +1171,10 @@ int tv_output_write(void* ctx, double t) {
   for (size_t k = 0; k < c->out_fields.size(); ++k) {
     const FieldInfo& fi = c->f[c->out_fields[k]];
     const bool local_all = c->um && c->n_parts > 1;  // see tv_output_open_named
-    const int64_t ndof = local_all ? c->nT : (fi.space == 0) ? c->ownT_n : c->ownS_n;
+    // a mixed-family slab: the dofs of its output mesh (setup_mixed_part)
+    const int64_t ndof = local_all ? c->nT
+                         : c->mixed_part ? (fi.space == 0 ? c->outT_n : c->outS_n)
+                                         : (fi.space == 0) ? c->ownT_n : c->ownS_n;
     const int64_t off = local_all ? 0 : (fi.space == 0) ? c->ownT_off : c->ownS_off;
     const int64_t stride = (fi.space == 0) ? c->nT : c->nS;
     const bool dgsp = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;

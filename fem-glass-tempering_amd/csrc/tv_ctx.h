@@ -101,6 +101,11 @@ struct Ctx {
   int64_t ownT_off = 0, ownT_n = 0;
   int64_t ownS_off = 0, ownS_n = 0;
   int64_t globT_off = 0, globS_off = 0;
+  // mixed families on a slab partition (setup_mixed_part): 1 = DG T / CG sigma
+  // (main.py), 2 = CG T / DG sigma; outT_n / outS_n: dofs each space writes to
+  // the part's output mesh (the nodes of its owned cell layers)
+  int mixed_part = 0;
+  int64_t outT_n = 0, outS_n = 0;
   std::vector<std::vector<double>> coords;  // physical axes
   FieldInfo f[TV_NUM_FIELDS];
   double* coef[3] = {nullptr, nullptr, nullptr};

@@ -480,11 +480,14 @@ int visco(Ctx* c, bool copy_Tprev) {
       launch_copy(v.Tp + o, v.T + o, c->nT - o, c->stream);
     }
   } else {
-    v.n = c->ownT_n;
-    v.off_T = c->ownT_off;
+    // mixed families; on a slab partition (setup_mixed_part) the T pass covers
+    // the ghost dofs too (the sigma pass reads them at the slab's upper plane)
+    // and the sigma pass every local sigma dof
+    v.n = c->mixed_part ? c->nT : c->ownT_n;
+    v.off_T = c->mixed_part ? 0 : c->ownT_off;
     launch_visco_Tpass(c->dim, all, k, v, c->stream);
-    v.n = c->ownS_n;
-    v.off_S = c->ownS_off;
+    v.n = c->mixed_part ? c->nS : c->ownS_n;
+    v.off_S = c->mixed_part ? 0 : c->ownS_off;
     v.map = c->map;
     launch_visco_Spass(c->dim, all, k, v, c->stream);
     if (copy_Tprev) launch_copy(v.Tp, v.T, c->nT, c->stream);

@@ -77,7 +77,12 @@ extern "C" {
  *   coords[a]       n_cells[a]+1 increasing node coordinates along axis a
  *   part_axis       physical axis along which the mesh is sliced into
  *                   partitions (-1: automatic = longest of the axes >= 1)
- *   n_parts, part   number of partitions / this context's partition      */
+ *   n_parts, part   number of partitions / this context's partition
+ * A partition (dim >= 2) is a slab: CG T owns node planes with one ghost plane
+ * per interface, DG T owns cell layers with one ghost cell layer; mixed
+ * families (DG T / CG sigma as main.py, or CG T / DG sigma) partition the T
+ * space so and give sigma the owned nodes / cells it reads from it
+ * (tv_num_dofs returns each space's owned count and global offset). */
 typedef struct {
   int dim;
   int n_cells[3];

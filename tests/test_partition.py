@@ -115,14 +115,19 @@ def _partition_check(world, comm, port, extra=(), krylov_slack=1):
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("PARTITION_CHECK ")]
     assert line, out.stdout[-2000:] + out.stderr[-2000:]
     res = json.loads(line[0].split(" ", 1)[1])
+    print("[partition] " + json.dumps(res))
     assert res["T"] < 1e-12, res
     assert res["phi"] < 1e-11, res
     assert res["xi"] < 1e-6, res
     assert res["sigma"] < 1e-6, res
     # the global reductions make the partitioned solve take the same iterations
-    # (krylov_slack None: a partition-dependent preconditioner, Newton counts only)
+    # up to the summation order of the dot products: within max(krylov_slack per
+    # Newton solve, 5 %) -- the rule the oracle comparisons use (check_counts);
+    # DG Jacobi-PCG runs ~50 iterations per solve, where rounding moves the
+    # threshold crossing by a few (krylov_slack None: a partition-dependent
+    # preconditioner, Newton counts only)
     for (n1, k1), (n2, k2) in zip(res["its_parts"], res["its_single"]):
-        assert n1 == n2 and (krylov_slack is None or abs(k1 - k2) <= krylov_slack * n1), res
+        assert n1 == n2 and (krylov_slack is None or abs(k1 - k2) <= max(krylov_slack * n1, 0.05 * k2)), res
     return res
 
 
@@ -233,21 +238,36 @@ def test_partitioned_dg_output_series():
 
 
 @pytest.mark.gpu
-def test_partitioned_mixed_families_refused():
-    """A partition needs the same family for T and sigma (DG T / CG sigma, the
-    main.py pairing, runs on one partition)."""
+@pytest.mark.parametrize("family", ["DG-CG", "CG-DG"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_mixed_families_match_single_partition(world, family):
+    """Mixed element families on slabs: DG1 T / CG1 sigma -- the reference's own
+    main.py pairing (main.py:24-27) under mpiexec -- and CG1 T / DG1 sigma.  The
+    T space is partitioned as on its own, the sigma space follows without ghosts
+    (setup_mixed_part): each sigma dof reads the T-space state of the dof that
+    fem::interpolate's last-writer rule picks, an owned dof or one of the ghost
+    layer above.  2 / 3 partitions reproduce the single partition (T <= 1e-12,
+    sigma <= 1e-6, equal Newton counts), and every part's written series equals
+    the gathered state over its output mesh (the nodes of its owned cell layers)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from tvfem import box_mesh
-    from tvfem._native import NativeError
-    from tvfem.problem import ThermoViscoProblem
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from partition_check import MP
-    with pytest.raises(NativeError):
-        ThermoViscoProblem(box_mesh([1.0, 2.0, 1.0], [4, 6, 2]), (0, 1), 0.1,
-                           {"T": {"element": "DG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}, MP,
-                           n_parts=2, part=0, part_axis=1, verbose=False)
+    res = _partition_check(world, "host", 29790 + world + (family == "CG-DG") * 7,
+                           ("--family", family, "--pcg", "kspcg", "--steps", "3", "--output"))
+    assert res["output_T"] == 0.0 and res["output_sigma"] == 0.0, res
+
+
+@pytest.mark.gpu
+def test_partitioned_mixed_families_host_edit():
+    """A host edit of a T-space state field (Tf) on one rank of a CG T / DG sigma
+    slab pair: the sigma pass reads that field at the ghost plane above, so the
+    edited values must reach the neighbour's ghost copy before the next update."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    # nodes on both sides of the interface planes (y = 3.0 / 3.2 of the 10 x 30 x 5 slab pair) are edited
+    _partition_check(2, "host", 29805, ("--family", "CG-DG", "--pcg", "kspcg", "--steps", "2", "--edit",
+                                        "--edit-field", "Tf", "--edit-box", "0,0.6,2.5,3.5"))
 
 
 @pytest.mark.gpu

@@ -31,8 +31,10 @@ CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree":
 
 
 def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0,
-        outdir=None, dirichlet=False, edit_field="T", mg_coupling="auto", family="CG", dg_kernel="auto"):
-    cfg = {"T": {"element": family, "degree": 1}, "sigma": {"element": family, "degree": 1}}
+        outdir=None, dirichlet=False, edit_field="T", mg_coupling="auto", family="CG", dg_kernel="auto",
+        edit_box=(0.0, 0.6, 0.0, 0.6)):
+    fam_T, fam_S = family.split("-") if "-" in family else (family, family)  # "DG-CG": DG T, CG sigma (main.py)
+    cfg = {"T": {"element": fam_T, "degree": 1}, "sigma": {"element": fam_S, "degree": 1}}
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
                            dg_kernel=dg_kernel,
                            verbose=False, pcg_variant=pcg, write_output=outdir is not None,
@@ -54,7 +56,8 @@ def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False,
         # a local hot spot written in place on the host by the ranks that own it
         # (rank 0 only when partitioned): the ghost planes must still follow
         X = p._dof_coordinates(0)
-        m = (X[:, 0] < 0.6) & (X[:, 1] < 0.6)
+        x0, x1, y0, y1 = edit_box
+        m = (X[:, 0] >= x0) & (X[:, 0] < x1) & (X[:, 1] >= y0) & (X[:, 1] < y1)
         if m.any():
             if edit_field == "T":
                 p.functions_current["T"].x.array[m] += 20.0
@@ -67,6 +70,11 @@ def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False,
         p.solve_timestep()
         its.append((p.last_newton_iterations, p.last_krylov_iterations))
     out = {k: p.get_field(k) for k in ("T", "phi", "xi", "sigma")}
+    import ctypes as C
+    for sp in (0, 1):  # global offset of the part's first owned dof per space (its written series start there)
+        no, go = C.c_int64(), C.c_int64()
+        p._lib.tv_num_dofs(p._ctx, sp, C.byref(no), C.byref(go))
+        out["goff%d" % sp] = np.array([go.value])
     up = getattr(p, "_upart", None)
     if up is not None:  # unstructured partition: owned vertices -> global ids
         out["l2g"] = up["l2g"][:up["n_owned"]]
@@ -89,8 +97,11 @@ def main():
     ap.add_argument("--pcg", choices=["auto", "kspcg", "single"], default="auto")
     ap.add_argument("--edit", action="store_true", help="host edit of T on the owning rank only, after setup()")
     ap.add_argument("--edit-field", default="T", help="--edit: the field edited (T, Tf, Tf_partial, phi, xi)")
+    ap.add_argument("--edit-box", default="0,0.6,0,0.6",
+                    help="--edit: x0,x1,y0,y1 of the edited nodes (an interface plane inside: the ghost copies follow)")
     ap.add_argument("--dirichlet", action="store_true", help="paper mode with the Dirichlet condition T = T_ambient")
-    ap.add_argument("--family", choices=["CG", "DG"], default="CG", help="element family of T and sigma")
+    ap.add_argument("--family", choices=["CG", "DG", "DG-CG", "CG-DG"], default="CG",
+                    help="element family of T and sigma (one name: both; DG-CG: DG T and CG sigma, main.py's pairing)")
     ap.add_argument("--dg-kernel", choices=["auto", "tile", "cells"], default="auto")
     ap.add_argument("--mg-coupling", choices=["auto", "global", "local"], default="auto",
                     help="partitioned GMG: the distributed V-cycle of the whole box, or each slab's own (block Jacobi)")
@@ -106,6 +117,7 @@ def main():
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     dist.init_process_group("gloo")
+    eb = tuple(float(v) for v in a.edit_box.split(","))
     nc = [int(v) for v in a.cells.split(",")]
     mesh = (distorted_box_mesh if a.mesh == "distorted" else box_mesh)([2.0, 6.0, 1.0], nc)
     steps = a.steps
@@ -119,16 +131,17 @@ def main():
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
                        pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir,
                        dirichlet=a.dirichlet, edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family,
-                       dg_kernel=a.dg_kernel)
+                       dg_kernel=a.dg_kernel, edit_box=eb)
     else:
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
                        edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir, dirichlet=a.dirichlet,
-                       edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family, dg_kernel=a.dg_kernel)
+                       edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family, dg_kernel=a.dg_kernel,
+                       edit_box=eb)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
         ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc, dirichlet=a.dirichlet, edit_field=a.edit_field,
-                           family=a.family, dg_kernel=a.dg_kernel)
+                           family=a.family, dg_kernel=a.dg_kernel, edit_box=eb)
         res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "mesh": a.mesh, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             if "l2g" in gathered[0]:  # scatter every part's owned vertices to their global ids
@@ -146,8 +159,14 @@ def main():
                     fr = full.reshape(mesh.num_vertices, -1)
                     errs = [np.abs(np.asarray(g[key]) - fr[np.asarray(g["l2g_local"], dtype=np.int64)].ravel()).max()
                             for g in gathered]
-                else:  # box: the owned planes, in partition order
-                    errs = [np.abs(np.concatenate([np.asarray(g[key]) for g in gathered]) - full).max()]
+                else:  # box: each part's series is the global range from its first owned dof (owned planes or
+                    # cell layers, plus the shared plane above of a mixed-family slab)
+                    bs = 1 if k == "T" else mesh.dim * mesh.dim
+                    errs = []
+                    for g in gathered:
+                        wv = np.asarray(g[key])
+                        o0 = int(g["goff0" if k == "T" else "goff1"][0]) * bs
+                        errs.append(np.abs(wv - full[o0:o0 + wv.size]).max() if wv.size else 0.0)
                 res["output_" + k] = float(max(errs) / np.abs(full).max())
         print("PARTITION_CHECK " + json.dumps(res), flush=True)
     dist.barrier()
