@@ -259,15 +259,18 @@ def test_partitioned_mixed_families_match_single_partition(world, family):
 
 @pytest.mark.gpu
 def test_partitioned_mixed_families_host_edit():
-    """A host edit of a T-space state field (Tf) on one rank of a CG T / DG sigma
+    """A host edit of a T-space state field (Tf_partial: Tf itself is recomputed
+    from it every step) on one rank of a CG T / DG sigma
     slab pair: the sigma pass reads that field at the ghost plane above, so the
     edited values must reach the neighbour's ghost copy before the next update."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    # nodes on both sides of the interface planes (y = 3.0 / 3.2 of the 10 x 30 x 5 slab pair) are edited
-    _partition_check(2, "host", 29805, ("--family", "CG-DG", "--pcg", "kspcg", "--steps", "2", "--edit",
-                                        "--edit-field", "Tf", "--edit-box", "0,0.6,2.5,3.5"))
+    # nodes on both sides of the interface planes (y = 3.0 / 3.2 of the 10 x 30 x 5 slab pair) are edited;
+    # paper mode, where Tf (from Tf_partial) enters the thermal strain -- the
+    # reference mode's stress reads T alone (Q2), which is exchanged every step
+    _partition_check(2, "host", 29805, ("--family", "CG-DG", "--pcg", "kspcg", "--steps", "2", "--edit", "--paper",
+                                        "--edit-field", "Tf_partial", "--edit-box", "0,0.6,2.5,3.5"))
 
 
 @pytest.mark.gpu

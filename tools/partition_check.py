@@ -32,14 +32,14 @@ CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree":
 
 def run(mesh, n_parts, part, steps, comm=None, device=0, pcg="auto", edit=False, pc="jacobi", mg_rep=0,
         outdir=None, dirichlet=False, edit_field="T", mg_coupling="auto", family="CG", dg_kernel="auto",
-        edit_box=(0.0, 0.6, 0.0, 0.6)):
+        edit_box=(0.0, 0.6, 0.0, 0.6), paper=False):
     fam_T, fam_S = family.split("-") if "-" in family else (family, family)  # "DG-CG": DG T, CG sigma (main.py)
     cfg = {"T": {"element": fam_T, "degree": 1}, "sigma": {"element": fam_S, "degree": 1}}
     p = ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, MP, device=device, n_parts=n_parts, part=part, part_axis=1,
                            dg_kernel=dg_kernel,
                            verbose=False, pcg_variant=pcg, write_output=outdir is not None,
                            output_dir=outdir or "output", preconditioner=pc, mg_replicate_nodes=mg_rep,
-                           model_mode="paper" if dirichlet else "reference", mg_coupling=mg_coupling)
+                           model_mode="paper" if (dirichlet or paper) else "reference", mg_coupling=mg_coupling)
     if comm is not None:
         comm(p)
         if n_parts > 1:  # every exchange pattern on id-valued vectors first (collective)
@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--edit-field", default="T", help="--edit: the field edited (T, Tf, Tf_partial, phi, xi)")
     ap.add_argument("--edit-box", default="0,0.6,0,0.6",
                     help="--edit: x0,x1,y0,y1 of the edited nodes (an interface plane inside: the ghost copies follow)")
+    ap.add_argument("--paper", action="store_true",
+                    help="paper model mode (Tf_partial / Tf feed the stress; the reference mode's stress reads T only)")
     ap.add_argument("--dirichlet", action="store_true", help="paper mode with the Dirichlet condition T = T_ambient")
     ap.add_argument("--family", choices=["CG", "DG", "DG-CG", "CG-DG"], default="CG",
                     help="element family of T and sigma (one name: both; DG-CG: DG T and CG sigma, main.py's pairing)")
@@ -131,17 +133,17 @@ def main():
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_rccl(p, rank, world, dist), device=local,
                        pcg=a.pcg, edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir,
                        dirichlet=a.dirichlet, edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family,
-                       dg_kernel=a.dg_kernel, edit_box=eb)
+                       dg_kernel=a.dg_kernel, edit_box=eb, paper=a.paper)
     else:
         loc, its = run(mesh, world, rank, steps, comm=lambda p: init_host_comm(p, rank, world), pcg=a.pcg,
                        edit=a.edit, pc=a.pc, mg_rep=a.mg_replicate, outdir=outdir, dirichlet=a.dirichlet,
                        edit_field=a.edit_field, mg_coupling=a.mg_coupling, family=a.family, dg_kernel=a.dg_kernel,
-                       edit_box=eb)
+                       edit_box=eb, paper=a.paper)
     gathered = [None] * world
     dist.all_gather_object(gathered, {k: v.tolist() for k, v in loc.items()})
     if rank == 0:
         ref, its_ref = run(mesh, 1, 0, steps, edit=a.edit, pc=a.pc, dirichlet=a.dirichlet, edit_field=a.edit_field,
-                           family=a.family, dg_kernel=a.dg_kernel, edit_box=eb)
+                           family=a.family, dg_kernel=a.dg_kernel, edit_box=eb, paper=a.paper)
         res = {"comm": a.comm, "pcg": a.pcg, "pc": a.pc, "mesh": a.mesh, "its_parts": its, "its_single": its_ref}
         for k in ("T", "phi", "xi", "sigma"):
             if "l2g" in gathered[0]:  # scatter every part's owned vertices to their global ids
