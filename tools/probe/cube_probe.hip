@@ -219,6 +219,156 @@ __global__ __launch_bounds__(R * W) void kR(Grid g, const double* __restrict__ i
   if (col_ok && r < g.nR) out[(long)i + g.sR * r] = acc;
 }
 
+// ---------------- R-BAL: the same reads, halo rows spread over every wave -----
+// planes in groups of G = R / 2: per group each wave loads its own row on the
+// G planes and ONE of the 2 G halo row-planes, so no wave carries twice the loads
+template <int R>
+__global__ __launch_bounds__(R * W) void kRB(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                             int nseg, int qchunk) {
+  constexpr int G = R / 2;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int b = remap(blockIdx.x, gridDim.x);
+  const int seg = b % nseg, t = b / nseg, rb = t % nrb, chunk = t / nrb;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const int hr = (wave & 1) ? r0 + R : r0 - 1, hq = wave >> 1;
+  double acc = 0.0;
+  for (int P = q0 - 1; P <= q1; P += G) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int L = P + k;
+      const bool ok = col_ok && r < g.nR && L >= 0 && L < g.nQ && L <= q1;
+      acc += in[ok ? (long)i + g.sR * r + g.sQ * L : 0];
+    }
+    const int L = P + hq;
+    const bool okh = col_ok && hr >= 0 && hr < g.nR && L >= 0 && L < g.nQ && L <= q1;
+    acc += in[okh ? (long)i + g.sR * hr + g.sQ * L : 0];
+  }
+  if (col_ok && r < g.nR) out[(long)i + g.sR * r] = acc;
+}
+
+// ---------------- AB: the march with balanced halo loads ---------------------
+// G = R / 2 planes per barrier step; per step every wave loads its own row on
+// the G planes and one of the 2 G halo row-planes (loads of the next step in
+// flight while this one is computed); LDS [2][G][R + 2][64]
+template <int R>
+__global__ __launch_bounds__(R * W) void kAB(Grid g, const double* __restrict__ in, double* __restrict__ out,
+                                             int nseg, int qchunk) {
+  constexpr int G = R / 2;
+  __shared__ double lds[2][G][R + 2][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int b = remap(blockIdx.x, gridDim.x);
+  const int seg = b % nseg, t = b / nseg, rb = t % nrb, chunk = t / nrb;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool writer = col_ok && lane >= 1 && lane <= SEG && r < g.nR;
+  const int hr = (wave & 1) ? r0 + R : r0 - 1, hq = wave >> 1, hslot = (wave & 1) ? R + 1 : 0;
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ && L <= q1; };
+  auto fetch = [&](int rr, int L) { return in[okf(rr, L) ? (long)i + g.sR * rr + g.sQ * L : 0]; };
+  double own[2][G], hv[2];
+  auto load = [&](int s, int P) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) own[s][k] = fetch(r, P + k);
+    hv[s] = fetch(hr, P + hq);
+  };
+  Win win;
+  auto step = [&](const int s, int P) {  // s: a literal 0 / 1 (static register indices after inlining)
+    if (P + G <= q1) load(s ^ 1, P + G);
+#pragma unroll
+    for (int k = 0; k < G; ++k) lds[s][k][wave + 1][lane] = okf(r, P + k) ? own[s][k] : 0.0;
+    lds[s][hq][hslot][lane] = okf(hr, P + hq) ? hv[s] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int L = P + k;
+      const bool emit = L >= q0 + 1 && L <= q1;
+      const double y = win.push(lds[s][k][wave][lane], lds[s][k][wave + 1][lane], lds[s][k][wave + 2][lane], emit);
+      if (emit && writer) out[(long)i + g.sR * r + g.sQ * (L - 1)] = y;
+    }
+  };
+  int P = q0 - 1;
+  load(0, P);
+  for (; P <= q1; P += 2 * G) {
+    step(0, P);
+    if (P + G > q1) break;
+    step(1, P + G);
+  }
+}
+
+// ---------------- A2 / AB2: the fused-PCG shape (two inputs z, p_old; p = z + b p_old stored)
+template <int R, bool BAL>
+__global__ __launch_bounds__(R * W) void kF2(Grid g, const double* __restrict__ z, const double* __restrict__ po,
+                                             double* __restrict__ pn, double* __restrict__ out, int nseg, int qchunk) {
+  constexpr int G = BAL ? R / 2 : 1;
+  __shared__ double lds[2][G][R + 2][W];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nrb = (g.nR + R - 1) / R;
+  const int b = remap(blockIdx.x, gridDim.x);
+  const int seg = b % nseg, t = b / nseg, rb = t % nrb, chunk = t / nrb;
+  const int r0 = rb * R, r = r0 + wave;
+  const int q0 = chunk * qchunk, q1 = min(q0 + qchunk, g.nQ);
+  const int i = seg * SEG - 1 + lane;
+  const bool col_ok = i >= 0 && i < g.n0;
+  const bool writer = col_ok && lane >= 1 && lane <= SEG && r < g.nR;
+  const double beta = 0.37;
+  // halo row-planes: BAL -> one per wave per group; else waves 0 / R-1 on every plane
+  const int hr = BAL ? ((wave & 1) ? r0 + R : r0 - 1) : (wave == 0 ? r0 - 1 : r0 + R);
+  const int hq = BAL ? (wave >> 1) : 0, hslot = BAL ? ((wave & 1) ? R + 1 : 0) : (wave == 0 ? 0 : R + 1);
+  const bool hload = BAL || wave == 0 || wave == R - 1;
+  auto okf = [&](int rr, int L) { return col_ok && rr >= 0 && rr < g.nR && L >= 0 && L < g.nQ && L <= q1; };
+  auto off = [&](int rr, int L) { return okf(rr, L) ? (long)i + g.sR * rr + g.sQ * L : 0L; };
+  double oz[2][G], op[2][G], hz[2], hp[2];
+  auto load = [&](int s, int P) {
+#pragma unroll
+    for (int k = 0; k < G; ++k) { const long o = off(r, P + k); oz[s][k] = z[o]; op[s][k] = po[o]; }
+    if (hload) { const long o = off(hr, P + hq); hz[s] = z[o]; hp[s] = po[o]; }
+  };
+  Win win;
+  auto step = [&](const int s, int P) {
+    if (P + G <= q1) load(s ^ 1, P + G);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int L = P + k;
+      const double pv = oz[s][k] + beta * op[s][k];
+      if (writer && L >= q0 && L < q1) pn[(long)i + g.sR * r + g.sQ * L] = pv;
+      lds[s][k][wave + 1][lane] = okf(r, L) ? pv : 0.0;
+    }
+    if (hload) lds[s][hq][hslot][lane] = okf(hr, P + hq) ? hz[s] + beta * hp[s] : 0.0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int L = P + k;
+      const bool emit = L >= q0 + 1 && L <= q1;
+      const double y = win.push(lds[s][k][wave][lane], lds[s][k][wave + 1][lane], lds[s][k][wave + 2][lane], emit);
+      if (emit && writer) out[(long)i + g.sR * r + g.sQ * (L - 1)] = y;
+    }
+  };
+  int P = q0 - 1;
+  load(0, P);
+  if (BAL) {
+    for (; P <= q1; P += 2 * G) {
+      step(0, P);
+      if (P + G > q1) break;
+      step(1, P + G);
+    }
+  } else {  // one plane per step, prefetch one step ahead (the library's PF 2 is one more)
+    for (; P <= q1; P += 2) {
+      step(0, P);
+      if (P + 1 > q1) break;
+      step(1, P + 1);
+    }
+  }
+}
+
 __global__ void copy1(const double* __restrict__ a, double* __restrict__ b, long n) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
 }
@@ -347,6 +497,45 @@ int main(int argc, char** argv) {
     rep("R reads 62-seg, no halos", timeit([&] { kR<8, false, false><<<nseg * nrb * nch, 8 * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nseg * nrb * nch);
     rep("R reads aligned 64-seg, halos", timeit([&] { kR<8, true, true><<<nsegA * nrb * nch, 8 * W>>>(g, x, y, nsegA, qc); }, reps, e0, e1), nsegA * nrb * nch);
     rep("R reads aligned 64-seg, no halos", timeit([&] { kR<8, true, false><<<nsegA * nrb * nch, 8 * W>>>(g, x, y, nsegA, qc); }, reps, e0, e1), nsegA * nrb * nch);
+    rep("R-BAL reads, halos spread R=8", timeit([&] { kRB<8><<<nseg * nrb * nch, 8 * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nseg * nrb * nch);
+    rep("R-BAL reads, halos spread R=4", timeit([&] { kRB<4><<<nseg * ((g.nR + 3) / 4) * nch, 4 * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nseg * ((g.nR + 3) / 4) * nch);
+    for (int qcb : {13, 16, 26}) {
+      const int nchb = (g.nQ + qcb - 1) / qcb;
+      char nm[64];
+      snprintf(nm, sizeof nm, "AB march balanced R=8 qchunk=%d", qcb);
+      rep(nm, timeit([&] { kAB<8><<<nseg * nrb * nchb, 8 * W>>>(g, x, y, nseg, qcb); }, reps, e0, e1), nseg * nrb * nchb);
+      CK(hipMemset(y, 0, N * 8));
+      kAB<8><<<nseg * nrb * nchb, 8 * W>>>(g, x, y, nseg, qcb);
+      check(nm);
+    }
+    {
+      const int nrb4 = (g.nR + 3) / 4;
+      rep("AB march balanced R=4 qchunk=13", timeit([&] { kAB<4><<<nseg * nrb4 * nch, 4 * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nseg * nrb4 * nch);
+      CK(hipMemset(y, 0, N * 8));
+      kAB<4><<<nseg * nrb4 * nch, 4 * W>>>(g, x, y, nseg, qc);
+      check("AB R=4");
+      const int nrb16 = (g.nR + 15) / 16;
+      rep("AB march balanced R=16 qchunk=13", timeit([&] { kAB<16><<<nseg * nrb16 * nch, 16 * W>>>(g, x, y, nseg, qc); }, reps, e0, e1), nseg * nrb16 * nch);
+    }
+    {  // fused-PCG shape: reads z and p_old, writes p and w (32 B per node)
+      double *z2, *pn;
+      CK(hipMalloc(&z2, N * 8));
+      CK(hipMalloc(&pn, N * 8));
+      CK(hipMemcpy(z2, x, N * 8, hipMemcpyDeviceToDevice));
+      auto rep2 = [&](const char* name, float us, int blocks) {
+        printf("%-36s %8.2f us  %7.1f GB/s (32 B/node)  blocks %d\n", name, us, 32.0 * N / (us * 1e-6) / 1e9, blocks);
+      };
+      for (int qcb : {13, 26}) {
+        const int nchb = (g.nQ + qcb - 1) / qcb;
+        char nm[64];
+        snprintf(nm, sizeof nm, "F2 fused shape, halos on 2 waves q=%d", qcb);
+        rep2(nm, timeit([&] { kF2<8, false><<<nseg * nrb * nchb, 8 * W>>>(g, z2, x, pn, y, nseg, qcb); }, reps, e0, e1), nseg * nrb * nchb);
+        snprintf(nm, sizeof nm, "F2 fused shape, balanced q=%d", qcb);
+        rep2(nm, timeit([&] { kF2<8, true><<<nseg * nrb * nchb, 8 * W>>>(g, z2, x, pn, y, nseg, qcb); }, reps, e0, e1), nseg * nrb * nchb);
+      }
+      CK(hipFree(z2));
+      CK(hipFree(pn));
+    }
     rep("R reads aligned, 1 chunk (51 planes)", timeit([&] { kR<8, true, false><<<nsegA * nrb, 8 * W>>>(g, x, y, nsegA, 51); }, reps, e0, e1), nsegA * nrb);
   }
   RUN_E(4, 13)
