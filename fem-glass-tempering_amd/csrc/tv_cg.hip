@@ -461,7 +461,7 @@ __device__ __forceinline__ void facet_corners(const CgGrid& g, bool ok, double h
 // p.(facet terms) record, then the tile takes part in the reduction tail.
 template <bool FUSEP, int R>
 __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const double* __restrict__ in0,
-                           const double* pA, const double* pB, const PcgState* __restrict__ st,
+                           const double* pA, const double* pB, double beta_ratio,
                            double* __restrict__ partials, const RedTail& rt, int nrec, int fb,
                            const FaceOff& fo, double* sm, double* redf, int it_host) {
   // LDS carved from the kernel's shared buffer (the marching tiles use it for
@@ -490,7 +490,7 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
   const double* pold = pA;
   if (FUSEP) {  // iteration parity from the host (no dependent load before the staging loads)
     first = (it_host == 0);
-    bcoef = first ? 0.0 : st->beta / st->betaold;
+    bcoef = first ? 0.0 : beta_ratio;
     pold = (it_host & 1) ? pA : pB;
   }
   auto node_of = [&](int cc1, int cc2) {
@@ -677,9 +677,32 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   // (placed before the tiles or interleaved with them: measured no better)
   const int bid = (int)blockIdx.x;
   const int fidx = (MODE == MODE_JAC && bid >= nmarch) ? bid - nmarch : -1;
+  // lagged logic (multi-rank fused matvec): the state after the previous
+  // all-reduce is formed here and committed by the tail (lagged_state)
+  const bool lagged = FUSEP && rt.lag != nullptr;
+  if (lagged && bid == 0 && threadIdx.x == 0) {
+    // a lagged state that ends the solve is committed here, by workgroup 0
+    // before it has anything in flight (every workgroup then exits; formed
+    // here rather than at the exit test below, where the full logic would
+    // raise the kernel's register count); otherwise the tail commits it
+    // (written through rt.st: st itself stays read-only, so the compiler keeps
+    // its reads scalar and ahead of nothing)
+    const PcgState s = lagged_state(st, rt.lag, rt.lag_kind);
+    if (s.done) *rt.st = s;
+  }
   if (fidx >= 0) {
-    if (st != nullptr && st->done) return;
-    face_block<FUSEP, R>(g, T, in0, in1, pout, st, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx, fo,
+    double ratio = 0.0;
+    if (lagged) {
+      int ldone;
+      double lbeta;
+      lag_update_lean(st, rt.lag, ldone, lbeta);
+      if (ldone) return;
+      ratio = lbeta / st->betaold;
+    } else if (st != nullptr) {
+      if (st->done) return;
+      if (FUSEP) ratio = st->beta / st->betaold;
+    }
+    face_block<FUSEP, R>(g, T, in0, in1, pout, ratio, POST ? nullptr : partials, POST ? RedTail{} : rt, nrec, fidx, fo,
                          fsm, red, it_host);
     return;
   }
@@ -690,7 +713,6 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   const int nQ = (raxis == 1) ? g.n2 : g.n1;
   const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
   const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
-  const int qaxis = 3 - raxis;
   // tile order (march_tile): x segment fastest, then row block, then chunk;
   // each XCD takes a contiguous run of tiles, i.e. whole x-rows of a band of row
   // blocks in one chunk -- the concurrent tiles of an XCD read long contiguous
@@ -717,28 +739,43 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     first = (it_host == 0);
     if (!(it_host & 1)) { pold = pout; pout = const_cast<double*>(in1); }
   }
+  // the solver state (scalar loads, issued first; read after the block's
+  // loads are all in flight)
+  int st_done = 0;
+  double st_beta = 0.0, st_betaold = 1.0;
+  if (lagged) {  // the multi-rank solves lag logic_update (kind 3) into this launch
+    lag_update_lean(st, rt.lag, st_done, st_beta);
+    st_done = __builtin_amdgcn_readfirstlane(st_done);  // wave-uniform: keep them in SGPRs
+    st_beta = uniform(st_beta);
+    st_betaold = st->betaold;
+  } else if (st != nullptr) {
+    st_done = st->done;
+    if (FUSEP) {
+      st_beta = st->beta;
+      st_betaold = st->betaold;
+    }
+  }
   // ownership along storage axis 2 (partition axis)
   const int kb = g.k_begin, ke = g.k_end;
   const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
+  // per-axis data of the row / march axes by selects, not by indexing the
+  // kernel arguments with a runtime axis (each such index is a dependent
+  // scalar load of the argument segment ahead of the first memory request)
+  const double* coefR = (raxis == 1) ? g.coef[1] : g.coef[2];
+  const double* coefQ = (raxis == 1) ? g.coef[2] : g.coef[1];
+  const int bq_lo = (raxis == 1) ? g.bnd[2][0] : g.bnd[1][0];
+  const int bq_hi = (raxis == 1) ? g.bnd[2][1] : g.bnd[1][1];
 
   // Robin facet terms of the faces normal to the march axis (Jacobian): the
   // tile's first / last chunk holds that face's plane.  They are integrated in
   // the tile's prologue -- T and p of the face plane's R + 2 rows staged in
   // LDS, one facet row per wave (wave 0 also the row below the tile), corner
   // exchange through LDS -- and added to that plane's output in the march.
-  const bool fq0 = (MODE == MODE_JAC) && q0 == 0 && g.bnd[qaxis][0];
-  const bool fq1 = (MODE == MODE_JAC) && q1 == nQ && g.bnd[qaxis][1];
+  const bool fq0 = (MODE == MODE_JAC) && q0 == 0 && bq_lo;
+  const bool fq1 = (MODE == MODE_JAC) && q1 == nQ && bq_hi;
   double (*sFq)[2][R + 2][kWave] = reinterpret_cast<double (*)[2][R + 2][kWave]>(fsm);  // [face][T, p]
   double (*sCD)[2][R][kWave] = reinterpret_cast<double (*)[2][R][kWave]>(fsm + 4 * (R + 2) * kWave);
   double yq0 = 0.0, yq1 = 0.0;
-  // facet-row cell lengths along the row axis (own facet row r; r0 - 1 for wave 0)
-  const double hq_own = uniform(g.coef[raxis][(int64_t)(row_ok ? r : 0) * C_NCOEF + C_HHI]);
-  const double hq_low = uniform(g.coef[raxis][(int64_t)(r0 >= 1 ? r0 - 1 : 0) * C_NCOEF + C_HHI]);
-
-  // row coefficients are wave-uniform: keep them in SGPRs
-  const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
-  const double My0 = uniform(cr[C_MLO]), My1 = uniform(cr[C_MDI]), My2 = uniform(cr[C_MUP]);
-  const double Ky0 = uniform(cr[C_KLO]), Ky1 = uniform(cr[C_KDI]), Ky2 = uniform(cr[C_KUP]);
   const double da = g.dt_alpha;
 
   // raw loads of one (row, plane) value (+ second array); the combination
@@ -794,8 +831,11 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   };
   // Block start: ONE memory round trip for everything the march needs before
   // its first plane -- the first two planes (prefetch), the coefficient
-  // stages and the Robin facet terms of the tile's boundary nodes -- issued
-  // back to back, prefetch first.
+  // stages (march axis, x axis, the tile's rows) and the face planes of the
+  // Robin facets -- issued back to back, prefetch first, all before the
+  // solver state is tested.  (Round 4: the row coefficients used to be read
+  // per wave ahead of the prefetch, and the stages only after the state test,
+  // so a tile waited for three memory round trips before its first plane.)
   // prefetch ring: PF + 1 register sets rotate through a fully unrolled loop,
   // so PF planes of loads are in flight while a plane is combined, exchanged
   // and computed
@@ -807,13 +847,37 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     fetch(vo_halo, q0 - 1 + s, rh0[s], rh1[s]);
     fetch_post(q0 - 1 + s, rr[s], rd[s]);
   }
-  // the solver state is read only now, so its latency overlaps the prefetch;
-  // once the PCG has converged every launch of the batch exits here
-  if (FUSEP) {
-    if (st->done) return;
-    bcoef = first ? 0.0 : st->beta / st->betaold;
-  } else if (st != nullptr && st->done) {
-    return;  // plain J x inside a converged solve's queued V-cycle
+  // march-axis coefficients of the chunk, pre-scaled per plane q into
+  // (Mz0, Mz1, Mz2, da Kz0, da Kz1, da Kz2, da Mz0, da Mz1, da Mz2, 0): read
+  // as 5 uniform 16-byte LDS loads per plane; x-axis coefficients of the
+  // block's 64 columns as (Mlo, Klo), (Mdi, Kdi), (Mup, Kup), (Hhi, -) pairs
+  // per lane: 3 conflict-free 16-byte LDS loads per plane; the coefficients
+  // of the tile's rows r0 - 1 .. r0 + R - 1 (row slot + 1), read per wave
+  // into SGPRs after the barrier
+  __shared__ double2 cql[kFaceChunk + 2][5];
+  __shared__ double2 cxl[4][kWave];
+  __shared__ double crl[R + 1][C_NCOEF];
+  const int nqs = q1 - q0 + 2;
+  const bool st_q = (int)threadIdx.x < nqs * 6;
+  const bool st_x = (int)threadIdx.x < 8 * kWave;
+  const bool st_r = (int)threadIdx.x < (R + 1) * C_NCOEF;
+  double cqv, cxv, crv;
+  {
+    const int e = threadIdx.x;
+    const int qq = q0 - 1 + e / 6;
+    const bool okq = st_q && qq >= 0 && qq < nQ;
+    cqv = coefQ[okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
+    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
+    const bool okx = st_x && ii >= 0 && ii < n0;
+    const int k = e >> 6;  // slot: pair k >> 1, half k & 1
+    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
+    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
+    const int rrow = r0 - 1 + e / C_NCOEF;
+    const bool okr = st_r && rrow >= 0 && rrow < nR;
+    crv = coefR[okr ? (int64_t)rrow * C_NCOEF + e % C_NCOEF : 0];
+    cqv = okq ? cqv : 0.0;
+    cxv = (okx && k < 7) ? cxv : 0.0;
+    crv = okr ? crv : 0.0;
   }
   // face planes: T, z (, p_old) of the own and halo rows
   double fT[2][2], fZ[2][2], fO[2][2];  // [face][own, halo]
@@ -827,30 +891,10 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       fO[f][1] = FUSEP ? bload(rsO, vo_halo + po) : 0.0;
     }
   }
-  // march-axis coefficients of the chunk, pre-scaled per plane q into
-  // (Mz0, Mz1, Mz2, da Kz0, da Kz1, da Kz2, da Mz0, da Mz1, da Mz2, 0): read
-  // as 5 uniform 16-byte LDS loads per plane; x-axis coefficients of the
-  // block's 64 columns as (Mlo, Klo), (Mdi, Kdi), (Mup, Kup), (Hhi, -) pairs
-  // per lane: 3 conflict-free 16-byte LDS loads per plane
-  __shared__ double2 cql[kFaceChunk + 2][5];
-  __shared__ double2 cxl[4][kWave];
-  const int nqs = q1 - q0 + 2;
-  const bool st_q = (int)threadIdx.x < nqs * 6;
-  const bool st_x = (int)threadIdx.x < 8 * kWave;
-  double cqv, cxv;
-  {
-    const int e = threadIdx.x;
-    const int qq = q0 - 1 + e / 6;
-    const bool okq = st_q && qq >= 0 && qq < nQ;
-    cqv = g.coef[qaxis][okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
-    cqv = okq ? cqv : 0.0;
-    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
-    const bool okx = st_x && ii >= 0 && ii < n0;
-    const int k = e >> 6;  // slot: pair k >> 1, half k & 1
-    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
-    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
-    cxv = (okx && k < 7) ? cxv : 0.0;
-  }
+  // once the PCG has converged every launch of the batch exits here (a plain
+  // J x inside a converged solve's queued V-cycle too)
+  if (st_done) return;
+  if (FUSEP) bcoef = first ? 0.0 : st_beta / st_betaold;
   if (st_q) {
     const int qs = threadIdx.x / 6, c = threadIdx.x % 6;
     double* row = reinterpret_cast<double*>(cql[qs]);
@@ -863,6 +907,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     if (c == 0) row[9] = 0.0;
   }
   if (st_x) reinterpret_cast<double*>(cxl[(threadIdx.x >> 6) >> 1])[2 * (threadIdx.x & (kWave - 1)) + ((threadIdx.x >> 6) & 1)] = cxv;
+  if (st_r) crl[threadIdx.x / C_NCOEF][threadIdx.x % C_NCOEF] = crv;
   if (fq0 || fq1) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -875,6 +920,14 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     }
   }
   __syncthreads();
+  // row coefficients are wave-uniform: keep them in SGPRs (row slot wave + 1;
+  // zeros past the last row, as before)
+  const double* crw = crl[wave + 1];
+  const double My0 = uniform(crw[C_MLO]), My1 = uniform(crw[C_MDI]), My2 = uniform(crw[C_MUP]);
+  const double Ky0 = uniform(crw[C_KLO]), Ky1 = uniform(crw[C_KDI]), Ky2 = uniform(crw[C_KUP]);
+  // facet-row cell lengths along the row axis (own facet row r; r0 - 1 for wave 0)
+  const double hq_own = uniform(crw[C_HHI]);
+  const double hq_low = uniform(crl[0][C_HHI]);
   if (fq0 || fq1) {  // facet row r (rows r, r + 1) of each face plane; wave 0 also row r0 - 1
     const bool cok = i >= 0 && i < n0 - 1;
     const double h1 = cxl[3][lane].x;
@@ -1004,7 +1057,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       for (int w = 0; w < R; ++w) s += red[w];
       store_partial(&partials[blockIdx.x], s);
     }
-    fused_reduce_tail<1>(rt, nrec);  // p.w over all tiles (+ KSPCG logic)
+    fused_reduce_tail<1>(rt, nrec);  // p.w over all tiles (+ KSPCG logic, or the lagged state)
   }
 }
 
@@ -1175,6 +1228,7 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
   __shared__ PcgState sst;  // lagged mode: this launch's view of the state
   // ---- scalars: alpha_{i-1}, beta_{i-1} ----------------------------------------
   CgsScal ks{0.0, 0.0, it_host == 1};
+  int st_done = 0;
   if (lag_sums != nullptr) {
     // multi-rank: the state after the previous iteration is formed here from
     // the all-reduced sums (identically in every workgroup); committed by WG 0
@@ -1191,12 +1245,15 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
     ks.a = sst.a;
     ks.b = sst.beta;
   } else if (!INIT) {
-    if (st->done) return;  // converged: every launch queued behind exits here
+    // converged: every launch queued behind exits -- tested once the block's
+    // first loads are in flight (scalar loads, issued here)
+    st_done = st->done;
     ks.a = st->a;
     ks.b = st->beta;
   }
   const int nface = (int)gridDim.x - nmarch;
   if ((int)blockIdx.x >= nmarch && nface > 0) {
+    if (st_done) return;
     face_block_cgs<INIT, R>(g, v, ks, raxis, partials, (int)blockIdx.x - nmarch, fo, fsm, red);
     cgs_tail(rt, nrec, st, lag_sums != nullptr ? &sst : nullptr);
     return;
@@ -1208,7 +1265,6 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
   const int nQ = (raxis == 1) ? g.n2 : g.n1;
   const int64_t sR = (raxis == 1) ? (int64_t)n0 : (int64_t)n0 * g.n1;
   const int64_t sQ = (raxis == 1) ? (int64_t)n0 * g.n1 : (int64_t)n0;
-  const int qaxis = 3 - raxis;
   // tile order as k_cg_march: x segment fastest, then row block, then chunk
   const int nrbk = (nR + R - 1) / R;
   int seg, rb, chunk;  // face-chunk tiles spread over the XCDs, first (march_tile)
@@ -1224,16 +1280,16 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
   const int kb = g.k_begin, ke = g.k_end;
   const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
 
-  const bool fq0 = q0 == 0 && g.bnd[qaxis][0];
-  const bool fq1 = q1 == nQ && g.bnd[qaxis][1];
+  // per-axis data by selects (as k_cg_march)
+  const double* coefR = (raxis == 1) ? g.coef[1] : g.coef[2];
+  const double* coefQ = (raxis == 1) ? g.coef[2] : g.coef[1];
+  const int bq_lo = (raxis == 1) ? g.bnd[2][0] : g.bnd[1][0];
+  const int bq_hi = (raxis == 1) ? g.bnd[2][1] : g.bnd[1][1];
+  const bool fq0 = q0 == 0 && bq_lo;
+  const bool fq1 = q1 == nQ && bq_hi;
   double (*sFq)[2][R + 2][kWave] = reinterpret_cast<double (*)[2][R + 2][kWave]>(fsm);
   double (*sCD)[2][R][kWave] = reinterpret_cast<double (*)[2][R][kWave]>(fsm + 4 * (R + 2) * kWave);
   double yq0 = 0.0, yq1 = 0.0;
-  const double hq_own = uniform(g.coef[raxis][(int64_t)(row_ok ? r : 0) * C_NCOEF + C_HHI]);
-  const double hq_low = uniform(g.coef[raxis][(int64_t)(r0 >= 1 ? r0 - 1 : 0) * C_NCOEF + C_HHI]);
-  const double* cr = g.coef[raxis] + (int64_t)(row_ok ? r : 0) * C_NCOEF;
-  const double My0 = uniform(cr[C_MLO]), My1 = uniform(cr[C_MDI]), My2 = uniform(cr[C_MUP]);
-  const double Ky0 = uniform(cr[C_KLO]), Ky1 = uniform(cr[C_KDI]), Ky2 = uniform(cr[C_KUP]);
   const double da = g.dt_alpha;
 
   // ---- buffer descriptors (out-of-range offsets read 0 / drop the store) -----
@@ -1309,6 +1365,34 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
     fetch(vo_own, xb_own, rb_own, r, q0 - 1 + sI, ra[sI], true);
     if (halo) fetch(vo_halo, xb_hal, rb_hal, hrow, q0 - 1 + sI, rh[sI], false);
   }
+  // coefficient stages (march axis, x axis, the tile's rows; as k_cg_march),
+  // issued with the prefetch
+  __shared__ double2 cql[kFaceChunk + 2][5];
+  __shared__ double2 cxl[4][kWave];
+  __shared__ double crl[R + 1][C_NCOEF];
+  const int nqs = q1 - q0 + 2;
+  const bool st_q = (int)threadIdx.x < nqs * 6;
+  const bool st_x = (int)threadIdx.x < 8 * kWave;
+  const bool st_r = (int)threadIdx.x < (R + 1) * C_NCOEF;
+  double cqv, cxv, crv;
+  {
+    const int e = threadIdx.x;
+    const int qq = q0 - 1 + e / 6;
+    const bool okq = st_q && qq >= 0 && qq < nQ;
+    cqv = coefQ[okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
+    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
+    const bool okx = st_x && ii >= 0 && ii < n0;
+    const int k = e >> 6;
+    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
+    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
+    const int rrow = r0 - 1 + e / C_NCOEF;
+    const bool okr = st_r && rrow >= 0 && rrow < nR;
+    crv = coefR[okr ? (int64_t)rrow * C_NCOEF + e % C_NCOEF : 0];
+    cqv = okq ? cqv : 0.0;
+    cxv = (okx && k < 7) ? cxv : 0.0;
+    crv = okr ? crv : 0.0;
+  }
+  if (st_done) return;
   // face planes normal to the march axis: T and z of the own and halo rows
   double fT[2][2], fU[2][2];
   if (fq0 || fq1) {
@@ -1326,26 +1410,6 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
       cgs_node<INIT>(ks, a1.Rv, a1.Sv, a1.Wv, a1.Dv, a1.FX + a1.FR, s_, r_, fU[f][1]);
     }
   }
-  // march-axis coefficients of the chunk and x coefficients (as k_cg_march)
-  __shared__ double2 cql[kFaceChunk + 2][5];
-  __shared__ double2 cxl[4][kWave];
-  const int nqs = q1 - q0 + 2;
-  const bool st_q = (int)threadIdx.x < nqs * 6;
-  const bool st_x = (int)threadIdx.x < 8 * kWave;
-  double cqv, cxv;
-  {
-    const int e = threadIdx.x;
-    const int qq = q0 - 1 + e / 6;
-    const bool okq = st_q && qq >= 0 && qq < nQ;
-    cqv = g.coef[qaxis][okq ? (int64_t)qq * C_NCOEF + e % 6 : 0];
-    cqv = okq ? cqv : 0.0;
-    const int ii = seg * kSeg - 1 + (e & (kWave - 1));
-    const bool okx = st_x && ii >= 0 && ii < n0;
-    const int k = e >> 6;
-    const int cc = k == 0 ? C_MLO : k == 1 ? C_KLO : k == 2 ? C_MDI : k == 3 ? C_KDI : k == 4 ? C_MUP : k == 5 ? C_KUP : C_HHI;
-    cxv = g.coef[0][okx ? (int64_t)ii * C_NCOEF + cc : 0];
-    cxv = (okx && k < 7) ? cxv : 0.0;
-  }
   if (st_q) {
     const int qs = threadIdx.x / 6, c = threadIdx.x % 6;
     double* row = reinterpret_cast<double*>(cql[qs]);
@@ -1358,6 +1422,7 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
     if (c == 0) row[9] = 0.0;
   }
   if (st_x) reinterpret_cast<double*>(cxl[(threadIdx.x >> 6) >> 1])[2 * (threadIdx.x & (kWave - 1)) + ((threadIdx.x >> 6) & 1)] = cxv;
+  if (st_r) crl[threadIdx.x / C_NCOEF][threadIdx.x % C_NCOEF] = crv;
   if (fq0 || fq1) {
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -1370,6 +1435,12 @@ __global__ __launch_bounds__(R * kWave) void k_cgs_march(CgGrid g, CgsBuffers v,
     }
   }
   __syncthreads();
+  // row coefficients, wave-uniform in SGPRs (row slot wave + 1)
+  const double* crw = crl[wave + 1];
+  const double My0 = uniform(crw[C_MLO]), My1 = uniform(crw[C_MDI]), My2 = uniform(crw[C_MUP]);
+  const double Ky0 = uniform(crw[C_KLO]), Ky1 = uniform(crw[C_KDI]), Ky2 = uniform(crw[C_KUP]);
+  const double hq_own = uniform(crw[C_HHI]);
+  const double hq_low = uniform(crl[0][C_HHI]);
   if (fq0 || fq1) {
     const bool cok = i >= 0 && i < n0 - 1;
     const double h1 = cxl[3][lane].x;

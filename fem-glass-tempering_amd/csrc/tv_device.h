@@ -213,6 +213,34 @@ __device__ __forceinline__ void apply_logic(PcgState* st, const double* sums, in
   else if (kind == 5) logic_cgs(st, sums);
 }
 
+// Lagged scalar logic (multi-rank): the state after the previous all-reduce,
+// formed identically in every workgroup from *st and the all-reduced sums
+// (lag != nullptr; logic `kind`).  The launch's tail workgroup forms it once
+// more and commits it -- every workgroup has read *st by then, and nothing
+// else writes *st or the sums before -- or, when it ends the solve, workgroup
+// 0 commits it (commit_done) and every workgroup exits: a workgroup that reads
+// the committed state concludes `done` as well.  (Forming it again in the tail
+// keeps the ~30-dword state out of the kernel's registers.)
+__device__ __forceinline__ PcgState lagged_state(const PcgState* st, const double* lag, int kind) {
+  PcgState s = *st;
+  if (lag != nullptr) apply_logic(&s, lag, kind);
+  return s;
+}
+// logic_update's outcome on lagged sums as the fused matvec needs it (done,
+// beta; betaold is unchanged by it), branch-free so that the march's first
+// loads are not held behind the state: the same decisions as logic_update
+__device__ __forceinline__ void lag_update_lean(const PcgState* st, const double* lag, int& done, double& beta) {
+  const double dp = sqrt(lag[0]);
+  const double b = lag[1];
+  const bool stop = (st->done != 0) | !isfinite(dp) | (dp <= st->ttol) | (dp >= st->dtol * st->rnorm0) |
+                    (st->it + 1 >= st->max_it) | (b == 0.0) | (b * st->betaold < 0.0);
+  done = stop ? 1 : 0;
+  beta = stop ? st->beta : b;
+}
+__device__ __forceinline__ void commit_done(PcgState* st, const PcgState& s) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !st->done) *st = s;
+}
+
 // Tail of a kernel that produced one partial record (width W) per workgroup:
 // the last workgroup to arrive reduces all n records in a fixed order into
 // rt.out and (kind > 0) runs the PCG logic on the sums.  Measured alternative,
@@ -221,6 +249,13 @@ __device__ __forceinline__ void apply_logic(PcgState* st, const double* sums, in
 // (MI355X_MICROARCH.md price list "fanin"): 1-2 us SLOWER per launch at 0.1M,
 // 1M and 8M nodes (the arrivals are spread out by the march's own skew; the
 // extra hop is not).  Counters: rt.counter[0].
+// rt.lag != nullptr: the launch's lagged state (lagged_state, formed from the
+// sums before they are overwritten) is committed instead of running logic
+// rt.kind on this launch's sums.
+__device__ __forceinline__ void commit_lagged(const RedTail& rt) {
+  const PcgState s = lagged_state(rt.st, rt.lag, rt.lag_kind);
+  *rt.st = s;
+}
 template <int W>
 __device__ __forceinline__ void fused_reduce_tail(const RedTail& rt, int n) {
   if (rt.counter == nullptr) return;
@@ -228,8 +263,9 @@ __device__ __forceinline__ void fused_reduce_tail(const RedTail& rt, int n) {
   double sums[3] = {0.0, 0.0, 0.0};
   block_reduce_records<W>(rt.partials, 0, 1, n, sums);
   if (threadIdx.x == 0) {
+    if (rt.lag != nullptr) commit_lagged(rt);  // reads rt.lag (== rt.out) first
     for (int w = 0; w < W; ++w) rt.out[w] = sums[w];
-    apply_logic(rt.st, sums, rt.kind);
+    if (rt.lag == nullptr) apply_logic(rt.st, sums, rt.kind);
     if (rt.ts) rt.ts[1] = __builtin_amdgcn_s_memrealtime();
   }
 }

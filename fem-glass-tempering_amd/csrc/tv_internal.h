@@ -94,6 +94,8 @@ struct DgGrid {
 constexpr int kShards = 8;
 constexpr int kTailCounters = kShards + 1;
 constexpr int kCounterWords = 32;
+constexpr int kUpdateCounter = 2 * kTailCounters;  // the multigrid update's commit ticket (lagged logic)
+static_assert(kUpdateCounter < kCounterWords, "counter words");
 
 // Device-resident scalars of one PCG solve (PETSc KSPCG restated, preconditioned norm).
 struct PcgState {
@@ -118,6 +120,12 @@ struct RedTail {
   // in-solve kernel timing (tv_kernel_timing), or nullptr: ts[0] = REALTIME
   // clock when workgroup 0 starts, ts[1] = when the tail workgroup finishes
   uint64_t* ts;
+  // lagged scalar logic (multi-rank, tv_device.h lagged_state): the launch
+  // forms the state from *st and the all-reduced sums `lag` (logic lag_kind)
+  // at its start and its tail commits it -- the one-thread logic launch after
+  // the previous all-reduce is folded into this launch
+  const double* lag = nullptr;
+  int lag_kind = 0;
 };
 
 enum PcgReason {
@@ -433,7 +441,8 @@ void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x,
 // assigned by iteration 1 / launch_mg_dx_finish)
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
-                      int it_host, int init, hipStream_t s);
+                      int it_host, int init, hipStream_t s, const double* lag = nullptr,
+                      unsigned* counter = nullptr);
 // the same post-smoothing fused into the level-0 J x march (k_cg_march POST)
 // plus a pass over the side-face nodes for the face-workgroup facet terms
 // (k_mg_post_faces, which runs the reduction tail); z <- x + omega dinv (r - J x),

@@ -396,21 +396,34 @@ int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
 
 namespace {
 
-int mg_iteration_dist(Ctx* c, const double* T, int it) {
+// fold: the box march path -- the scalar logic after each all-reduce runs
+// lagged inside the next launch (lagged_state) instead of as a one-thread
+// launch: the beta / convergence logic of the previous iteration's closing
+// group inside this iteration's fused matvec (lag3), the alpha logic inside
+// the update.  Every rank forms the same state from the same all-reduced sums.
+int mg_iteration_dist(Ctx* c, const double* T, int it, bool fold, bool lag3) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
   const int slot = c->ts_next + it;
   uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
   RedTail t1{c->counters, c->partials, c->sums, c->st, 0, ts};
+  if (lag3) {
+    t1.lag = c->sums;
+    t1.lag_kind = 3;
+  }
   int np = 0;
+  bool lag2 = false;
   if (!op_japply_fused(c, T, &np, &t1, it)) {  // p <- z + b p ; w <- J p ; p.w
+    if (lag3) return c->fail(TV_ERR_STATE, "lagged PCG logic without the fused march");
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;
   } else {
     if (int e = allreduce(c, c->sums, 1)) return e;
-    launch_logic(c->st, c->sums, 2, c->stream);  // alpha
+    if (fold) lag2 = true;
+    else launch_logic(c->st, c->sums, 2, c->stream);  // alpha
   }
   const FaceAdd fa = c->um ? FaceAdd{} : cg_face_add(c->cg, off);  // unstructured: w is complete
   launch_mg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, &fa, c->dinv + off, c->mg_omega0, c->r + off,
-                   c->f[TV_F_DX].ptr + off, c->mgx + off, it, 0, c->stream);
+                   c->f[TV_F_DX].ptr + off, c->mgx + off, it, 0, c->stream, lag2 ? c->sums : nullptr,
+                   lag2 ? c->counters + kUpdateCounter : nullptr);
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};
   return mg_apply0_dist(c, T, &t2);
 }
@@ -435,15 +448,24 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
                    c->f[TV_F_DX].ptr + off, c->mgx + off, 0, 1, c->stream);  // x0 <- omega dinv r
   // the three collectives of an iteration close it: the (z.z, z.r) all-reduce
   // + KSPCG logic, and the ghost planes of z for the next fused matvec
-  auto close = [&](int kind) -> int {  // one RCCL group: the sums and the ghosts of z
+  // the lagged logic needs the box march's fused matvec (not the unstructured
+  // or DG kernels)
+  const bool fold = !c->um && c->fam_T == TV_CG && cg_cgs_supported(c->cg);
+  bool lag3 = false;  // the last closing group's logic is still to run (inside the next fused matvec)
+  auto close = [&](int kind, bool defer) -> int {  // one RCCL group: the sums and the ghosts of z
     if (int e = allreduce_halo(c, c->sums, 2, c->z)) return e;
-    launch_logic(c->st, c->sums, kind, c->stream);
+    if (defer) {
+      lag3 = true;
+    } else {
+      launch_logic(c->st, c->sums, kind, c->stream);
+      lag3 = false;
+    }
     return TV_OK;
   };
   {
     RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};
     if (int e = mg_apply0_dist(c, T, &t0)) return e;
-    if (int e = close(1)) return e;  // dp, beta (KSPCG init)
+    if (int e = close(1, false)) return e;  // dp, beta (KSPCG init)
   }
   if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
     if (int e = ts_flush(c)) return e;
@@ -453,8 +475,10 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
   int launched = 0;
   auto enqueue = [&](int nb) -> int {
     for (int b = 0; b < nb; ++b) {
-      if (int e = mg_iteration_dist(c, T, launched + b)) return e;
-      if (int e = close(3)) return e;  // z.z, z.r -> beta, convergence
+      if (int e = mg_iteration_dist(c, T, launched + b, fold, lag3)) return e;
+      // z.z, z.r -> beta, convergence: lagged into the next iteration's fused
+      // matvec, except after the batch's last iteration (the host polls the state)
+      if (int e = close(3, fold && b + 1 < nb)) return e;
     }
     launched += nb;
     HIPC(hipGetLastError());

@@ -72,6 +72,8 @@ __device__ __forceinline__ void stc(double* p, double v) {
 // DXU: odd iteration, applies the dx steps of this and the previous iteration.
 // Streams: w, dinv (+ p_prev, p, dx) read, z read and written (+ dx written):
 // 32 B per node on even iterations, 64 B on odd ones.
+// rt.lag (multi-rank): the alpha logic on the all-reduced p.w runs lagged
+// here (lagged_state) and the tail commits it.
 template <bool FACES, int NT, bool DXU>
 __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState* __restrict__ st,
                                                        const double* __restrict__ pA,
@@ -81,9 +83,17 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
                                                        double* __restrict__ z, double* __restrict__ partials,
                                                        RedTail rt, FaceAdd fa, int it_host) {
   stamp_start(rt);
-  if (st->done) return;
-  const double a = st->a;
-  const double ap = DXU ? st->a_prev : 0.0;
+  double a, ap;
+  if (rt.lag != nullptr) {
+    const PcgState ls = lagged_state(st, rt.lag, rt.lag_kind);
+    if (ls.done) { commit_done(rt.st, ls); return; }  // (rt.st == st; st stays read-only)
+    a = ls.a;
+    ap = DXU ? ls.a_prev : 0.0;
+  } else {
+    if (st->done) return;
+    a = st->a;
+    ap = DXU ? st->a_prev : 0.0;
+  }
   const double* __restrict__ p = (it_host & 1) ? pB : pA;   // this iteration's p (== st->it parity)
   const double* __restrict__ pp = (it_host & 1) ? pA : pB;  // the previous iteration's
   constexpr bool NT1 = (NT & 1) != 0, NT2 = (NT & 2) != 0, NT4 = (NT & 4) != 0;
@@ -143,16 +153,29 @@ __global__ __launch_bounds__(kBlock) void k_pcg_update(int64_t n, const PcgState
 // FIRST (iteration 1, the first DXU one): dx is assigned, not accumulated, so
 // the init pass does not have to zero it (mg_dx_finish covers solves of 0 / 1
 // iterations)
+// lag != nullptr (multi-rank): the alpha logic (kind 2) on the all-reduced
+// p.w is formed here (lagged_state) and committed by the last workgroup to
+// arrive at `counter` -- no one-thread logic launch between the all-reduce
+// and this update.
 template <bool FACES, bool INIT, bool DXU, bool FIRST = false>
 __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState* __restrict__ st,
                                                       const double* __restrict__ pA, const double* __restrict__ pB,
                                                       const double* __restrict__ w, FaceAdd fa,
                                                       const double* __restrict__ dinv, double omega,
                                                       double* __restrict__ r, double* __restrict__ dx,
-                                                      double* __restrict__ x0, int it_host) {
-  if (st->done) return;
-  const double a = INIT ? 0.0 : st->a;
-  const double ap = DXU ? st->a_prev : 0.0;
+                                                      double* __restrict__ x0, int it_host, const double* lag,
+                                                      unsigned* counter, PcgState* st_w) {
+  double a = 0.0, ap = 0.0;
+  if (!INIT && lag != nullptr) {
+    const PcgState ls = lagged_state(st, lag, 2);
+    if (ls.done) { commit_done(st_w, ls); return; }  // st_w == st (writes only through it)
+    a = ls.a;
+    ap = DXU ? ls.a_prev : 0.0;
+  } else {
+    if (st->done) return;
+    a = INIT ? 0.0 : st->a;
+    ap = DXU ? st->a_prev : 0.0;
+  }
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
   const double* __restrict__ pp = (it_host & 1) ? pA : pB;
   // v = {r, w, dinv, dx, p_prev, p}
@@ -193,6 +216,10 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
     double v[6];
     load(t, v);
     node(t, v);
+  }
+  if (!INIT && lag != nullptr && last_block_arrived(counter, gridDim.x) && threadIdx.x == 0) {
+    const PcgState ls = lagged_state(st, lag, 2);  // formed again (see lagged_state)
+    *st_w = ls;
   }
 }
 
@@ -306,13 +333,14 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
-                      int it_host, int init, hipStream_t s) {
+                      int it_host, int init, hipStream_t s, const double* lag, unsigned* counter) {
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
   const dim3 g(vec_blocks(n)), b(kBlock);
   const bool odd = (it_host & 1) != 0;
   const bool first = it_host == 1;
 #define TV_MGU(F, I, D, FI) \
-  hipLaunchKernelGGL((k_mg_update<F, I, D, FI>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host)
+  hipLaunchKernelGGL((k_mg_update<F, I, D, FI>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host, \
+                     lag, counter, const_cast<PcgState*>(st))
   if (init) TV_MGU(false, true, false, false);
   else if (f.on) {
     if (first) TV_MGU(true, false, true, true);

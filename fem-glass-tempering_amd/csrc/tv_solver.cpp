@@ -82,7 +82,11 @@ int ts_flush(Ctx* c) {
   return TV_OK;
 }
 
-int pcg_iteration(Ctx* c, const double* T, int it) {
+// lag3: the beta / convergence logic of the previous closing group runs lagged
+// inside this iteration's fused matvec (box march only); defer3: this
+// iteration's closing logic is left to the next one the same way.  The alpha
+// logic of a multi-rank iteration runs lagged inside the update.
+int pcg_iteration(Ctx* c, const double* T, int it, bool lag3, bool defer3) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
   // timestamp slot of this iteration (see ts_flush); the matvec launchers
   // without a reduction tail (DG, 1D/2D CG) leave theirs at 0
@@ -93,21 +97,27 @@ int pcg_iteration(Ctx* c, const double* T, int it) {
   // records and runs the KSPCG scalar logic in-kernel (no separate reduce
   // launch); multi-GPU: it only reduces, RCCL all-reduces, then the logic runs.
   RedTail t1{c->counters, c->partials, c->sums, c->st, multi ? 0 : 2, ts};
+  if (lag3) {
+    t1.lag = c->sums;
+    t1.lag_kind = 3;
+  }
   int np = 0;
   const bool fused1 = op_japply_fused(c, T, &np, &t1, it);  // p <- z + b p ; w <- J p ; p.w
+  RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
   if (!fused1) {
+    if (lag3) return c->fail(TV_ERR_STATE, "lagged PCG logic without the fused march");
     if (int e = reduce_logic(c, np, 1, 2, 1)) return e;  // dpi, a
   } else if (multi) {
     if (int e = allreduce(c, c->sums, 1)) return e;
-    launch_logic(c->st, c->sums, 2, c->stream);
+    t2.lag = c->sums;  // alpha, inside the update
+    t2.lag_kind = 2;
   }
-  RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, multi ? 0 : 3, ts ? ts + 2 : nullptr};
   const FaceAdd fa = (c->fam_T == TV_CG && !c->um) ? cg_face_add(c->cg, off) : FaceAdd{};
   launch_pcg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, c->dinv + off, c->f[TV_F_DX].ptr + off,
                     c->z + off, c->partials, c->stream, &t2, &fa, it);
   if (multi) {  // dp, beta, convergence; the ghosts of z in the same RCCL group
     if (int e = allreduce_halo(c, c->sums, 2, c->z)) return e;
-    launch_logic(c->st, c->sums, 3, c->stream);
+    if (!defer3) launch_logic(c->st, c->sums, 3, c->stream);
   }
   return TV_OK;
 }
@@ -130,9 +140,12 @@ int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   // already in the stream, so the GPU never idles on the host's turnaround.
   // After convergence the queued launches exit at their first instruction.
   int launched = 0, slot = 0;
+  // multi-rank box march: the closing logic of an iteration runs lagged in the
+  // next one's fused matvec, except after a batch's last iteration (polled)
+  const bool fold = multi_rank(c) && !c->um && c->fam_T == TV_CG && cg_cgs_supported(c->cg);
   auto enqueue = [&](int nb, int k) -> int {
     for (int b = 0; b < nb; ++b)
-      if (int e = pcg_iteration(c, T, launched + b)) return e;
+      if (int e = pcg_iteration(c, T, launched + b, fold && b > 0, fold && b + 1 < nb)) return e;
     launched += nb;
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
