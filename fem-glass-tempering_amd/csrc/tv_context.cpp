@@ -488,6 +488,7 @@ int setup_fields(Ctx* c) {
   HIPC(hipMemsetAsync(c->tflag, 0, sizeof(int), c->stream));  // the tilde fields start at +0.0
   HIPC(hipHostMalloc(&c->h_st, 3 * sizeof(PcgState)));
   for (int k = 0; k < 2; ++k) HIPC(hipEventCreateWithFlags(&c->evp[k], hipEventDisableTiming));
+  HIPC(hipEventCreateWithFlags(&c->evn, hipEventDisableTiming));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
   const int var = c->O.pcg_variant;
   const bool can = c->fam_T == TV_CG && !c->um && cg_cgs_supported(c->cg);
@@ -959,6 +960,7 @@ int tv_destroy(void* ctx) {
     if (c->evp[k]) hipEventDestroy(c->evp[k]);
     if (c->vev[k]) hipEventDestroy(c->vev[k]);
   }
+  if (c->evn) hipEventDestroy(c->evn);
   if (c->d_ts) hipFree(c->d_ts);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;

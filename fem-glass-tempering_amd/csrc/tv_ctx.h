@@ -84,6 +84,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evp[2] = {nullptr, nullptr};  // PCG convergence polls (double-buffered)
+  hipEvent_t evn = nullptr;                 // Newton: ||dx|| copied to the host
   tv_params P{};
   tv_options O{};
   int dim = 1;

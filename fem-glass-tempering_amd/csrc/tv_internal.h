@@ -473,6 +473,7 @@ void launch_mg_dx_finish(int64_t n, const PcgState* st, const double* pA, const 
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
                          int check_done, hipStream_t s);
 void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s);
+void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s);
 // T <- T - dx, ||dx||^2 partials; with `tail` the last workgroup reduces them into tail->out
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s,
                           const RedTail* tail = nullptr);

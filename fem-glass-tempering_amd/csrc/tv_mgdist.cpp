@@ -434,7 +434,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
   const PcgState h = pcg_state_init(c);
   c->h_st[2] = h;
-  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  launch_set_state(c->st, h, c->stream);
   if (c->amg_on) {  // the algebraic hierarchy is T-independent; level 0's weight at the first solve
     if (int e = mg_dg_weight(c, T)) return e;
   } else if (int e = mg_prepare_dist(c, T)) {

@@ -440,7 +440,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
-  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  launch_set_state(c->st, h, c->stream);
   mg_prepare(c, T);
   if (int e = mg_dg_weight(c, T)) return e;
   if (c->dggface)

@@ -299,6 +299,7 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
 }
 
 __global__ void k_logic(PcgState* st, const double* sums, int kind) { apply_logic(st, sums, kind); }
+__global__ void k_set_state(PcgState* st, PcgState h) { *st = h; }
 
 __global__ __launch_bounds__(kBlock) void k_fill(double* x, int64_t n, double v) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = v;
@@ -421,6 +422,14 @@ void launch_newton_update(int64_t n, double* T, const double* dx, double* partia
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
                          int check_done, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, partials, n, W, out, st, kind, check_done);
+}
+
+// the solver state at a solve's start, by a one-thread launch rather than a
+// host-to-device copy: the copy of a pinned 160-byte struct was followed by a
+// ~45 us gap before the next kernel in the C4 trace (the runtime's copy path),
+// a launch is queued like every other kernel
+void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_state, dim3(1), dim3(1), 0, s, st, h);
 }
 
 void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s) {

@@ -129,7 +129,7 @@ int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
-  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  launch_set_state(c->st, h, c->stream);
   launch_pcg_init(n, c->r + off, c->dinv + off, c->z + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
   if (int e = reduce_logic(c, pcg_vec_blocks(n), 2, 1, 0)) return e;
   if (int e = halo(c, c->z)) return e;
@@ -216,7 +216,7 @@ int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
-  HIPC(hipMemcpyAsync(c->st, &c->h_st[2], sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+  launch_set_state(c->st, h, c->stream);
   // ghost planes of r_0 and diag^-1 (the halo rows recompute z there)
   if (int e = halo(c, c->r)) return e;
   if (int e = halo(c, c->dinv)) return e;
@@ -385,6 +385,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     launch_newton_update(n, T + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
     if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
     HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evn, c->stream));
     if (int e = halo(c, T)) return e;
     // the next F queued before the host reads ||dx|| when the previous step
     // took more Newton iterations than this one has so far (the counts repeat
@@ -392,7 +393,10 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     // A wrong guess costs one residual, whose result is simply not used.
     const bool spec = its + 1 < c->newton_pred && its + 1 < c->O.newton_max_it;
     if (spec) dinv_fresh = residual();
-    HIPC(hipStreamSynchronize(c->stream));
+    // the host waits for ||dx|| only, not for the queued residual: it decides
+    // and queues the next Newton iteration while the GPU computes F (the C4
+    // trace showed the GPU idle ~27 us per Newton iteration behind a stream sync)
+    HIPC(hipEventSynchronize(c->evn));
     rn = std::sqrt(c->h_sums[0]);
     ++its;
     if (its == 1) {
