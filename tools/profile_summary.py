@@ -48,5 +48,28 @@ for name, pat in pats.items():
         "bench_launches_timed": kb.get("launches_timed"),
         "bench_over_rocprof": bus / wm if wm else None,
     }
+# the flushed J x of bench.py's hbm_flushed record under the same trace: the
+# kernels between each Infinity-Cache sweep (k_read_sweep) and the next one
+# (the march + k_cg_addfaces), their durations summed -- the rocprof
+# counterpart of bench.py's HIP-event median, which includes the dispatch
+sweeps = [i for i, r in enumerate(rows) if "k_read_sweep" in r["Kernel_Name"]]
+fl = []
+for i in sweeps:
+    ks = []
+    j = i + 1
+    while j < len(rows) and len(ks) < 3 and "k_read_sweep" not in rows[j]["Kernel_Name"] \
+            and "fillBuffer" not in rows[j]["Kernel_Name"]:
+        ks.append(rows[j])
+        j += 1
+    if ks:
+        fl.append(sum(int(k["End_Timestamp"]) - int(k["Start_Timestamp"]) for k in ks) / 1e3)
+hf = bench.get("roofline", {}).get("hbm_flushed")
+if fl and hf:
+    med = statistics.median(fl)
+    res["hbm_flushed"] = {"launches": len(fl), "rocprof_median_us": round(med, 2),
+                          "bench_hip_event_median_us": round(hf["ms_per_launch"] * 1e3, 2),
+                          "bytes_per_launch": hf["bytes_per_launch"],
+                          "rocprof_frac": round(hf["bytes_per_launch"] / (med * 1e-6) / 8e12, 4),
+                          "bench_frac": round(hf["frac"], 4)}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
