@@ -299,7 +299,9 @@ int mg_setup(Ctx* c);
 void mg_prepare(Ctx* c, const double* T);
 int mg_dg_weight(Ctx* c, const double* T);
 int mg_apply0(Ctx* c, const double* T, const RedTail* tail);
-int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason);
+// post: queue the Newton iteration's post-solve group (launch_post_group, ||dx||
+// copied to h_sums, evn recorded) behind every batch, gated on the device state
+int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post = false);
 bool mg_next_level(const std::vector<double> (&Xp)[3], double da, bool automatic, std::vector<double> (&Xc)[3],
                    std::vector<char> (&is_c)[3], int coarse[3]);
 void mg_axis_tables(const std::vector<double>& Xf, const std::vector<char>& is_c, std::vector<int>& pi,

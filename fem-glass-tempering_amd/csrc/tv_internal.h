@@ -102,6 +102,7 @@ struct PcgState {
   double beta, betaold, dpi, dpiold, a, dp, rnorm0, ttol;
   double rtol, atol, dtol;
   int it, done, reason, max_it;
+  int post;                   // the post-solve group queued behind the batches has run (pcg_solve_mg)
   double dx_norm2;            // ||dx||^2 of the last Newton update
   double a_prev;              // step length of the previous iteration (dx is updated every 2nd)
   // single-reduction form (k_cgs_march): gamma = (r, z) and eta = (p, A p) of
@@ -477,6 +478,11 @@ void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s);
 // T <- T - dx, ||dx||^2 partials; with `tail` the last workgroup reduces them into tail->out
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s,
                           const RedTail* tail = nullptr);
+// the post-solve group of a Newton iteration, gated on the solver state (runs
+// once, behind the batch that ends the solve): dx finish, T <- T - dx, ||dx||^2
+// into sums[0] (single partition)
+void launch_post_group(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, double* T,
+                       double* partials, double* sums, hipStream_t s);
 int pcg_vec_blocks(int64_t n);
 void launch_fill(double* x, int64_t n, double v, hipStream_t s);
 

@@ -434,7 +434,7 @@ int mg_iteration(Ctx* c, const double* T, int it) {
   return TV_OK;
 }
 
-int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
+int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
   const int64_t n = c->nT;
   const PcgState h = pcg_state_init(c);
   // from pinned memory (an asynchronous upload; a pageable source is staged by
@@ -467,6 +467,11 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPC(hipEventRecord(c->evp[0], c->stream));
+    if (post) {  // the Newton iteration's next work, queued before the host's poll (it runs once)
+      launch_post_group(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, c->f[TV_F_T].ptr, c->partials, c->sums, c->stream);
+      HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipEventRecord(c->evn, c->stream));
+    }
     return TV_OK;
   };
   const int hk = std::min(c->newton_k, 15);
@@ -481,7 +486,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason) {
   *reason = c->h_st[0].reason;
   // level 0 updates dx in pairs of iterations from iteration 1 on (k_mg_update /
   // k_dg_bupdate DXU): solves of 0 / 1 iterations and the last step of an odd-length one
-  launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
+  if (!post) launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
   c->pcg_hint = std::max(1, c->h_st[0].it);
   c->mg_hint[hk] = c->pcg_hint;
   if (c->ktime) {

@@ -254,9 +254,32 @@ __global__ __launch_bounds__(kBlock) void k_dx_tail(int64_t n, const PcgState* _
     dx[t] += a * p[t];
 }
 
+// the post-solve group of a Newton iteration queued behind every batch of a
+// multigrid solve (pcg_solve_mg): it runs once, behind the batch that ends
+// the solve, so the host's convergence poll overlaps it
+__device__ __forceinline__ bool post_gate(const PcgState* st) { return st->done && !st->post; }
+
+// dx after the solve, from the device's iteration count (launch_mg_dx_finish)
+__global__ __launch_bounds__(kBlock) void k_dx_finish_gated(int64_t n, const PcgState* __restrict__ st,
+                                                            const double* __restrict__ pA,
+                                                            const double* __restrict__ pB, double* __restrict__ dx) {
+  if (!post_gate(st)) return;
+  const int its = st->it;
+  const double a = st->a;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  if (its <= 1) {
+    for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] = its == 0 ? 0.0 : a * pA[t];
+  } else if (its & 1) {
+    const double* __restrict__ p = ((its - 1) & 1) ? pB : pA;
+    for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] += a * p[t];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __restrict__ T,
                                                           const double* __restrict__ dx,
-                                                          double* __restrict__ partials, RedTail rt) {
+                                                          double* __restrict__ partials, RedTail rt,
+                                                          const PcgState* __restrict__ gate) {
+  if (gate != nullptr && !post_gate(gate)) return;
   double acc[1] = {0.0};
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     const double d = dx[t];
@@ -272,7 +295,8 @@ __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __r
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ partials, int n, int W,
                                                  double* __restrict__ out, PcgState* st, int kind,
                                                  int check_done) {
-  if (check_done && st->done) return;
+  // check_done 2: the post-solve group's norm (post_gate), which marks the group as run
+  if (check_done == 2 ? !post_gate(st) : (check_done && st->done)) return;
   __shared__ double red[2][16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc[2] = {0.0, 0.0};
@@ -295,6 +319,7 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
       out[w] = s;
     }
     apply_logic(st, sums, kind);
+    if (check_done == 2) st->post = 1;
   }
 }
 
@@ -416,7 +441,16 @@ void launch_pcg_dx_tail(int64_t n, const PcgState* st, const double* pA, const d
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s,
                           const RedTail* tail) {
   const RedTail rt = tail ? *tail : RedTail{};
-  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials, rt);
+  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials, rt,
+                     static_cast<const PcgState*>(nullptr));
+}
+
+void launch_post_group(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, double* T,
+                       double* partials, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(k_dx_finish_gated, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, dx);
+  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials, RedTail{}, st);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, partials, vec_blocks(n), 1, sums, const_cast<PcgState*>(st), 0,
+                     2);
 }
 
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,

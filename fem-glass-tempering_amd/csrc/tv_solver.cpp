@@ -371,7 +371,11 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
       if (int e = dirichlet_pre(c, T)) return e;
     int k = 0, reason = 0;
     c->newton_k = its;  // the multigrid solves queue the count this Newton index took last step
-    if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason) : pcg_solve_mg(c, T, &k, &reason))
+    // single-partition multigrid: the post-solve group (dx, u <- u - dx, ||dx||)
+    // is queued behind every batch and runs behind the one that ends the solve
+    const bool post_in_solve = c->mg_on && c->n_parts == 1 && !dir;
+    if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason)
+                                            : pcg_solve_mg(c, T, &k, &reason, post_in_solve))
                           : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
       return e;
     kits += k;
@@ -382,10 +386,12 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
                          c->stream, c->f[TV_F_DX].ptr, c->dB, c->nT);
     // u <- u - dx; ||dx||^2 by a separate one-block reduce (a reduction tail on
     // the update's 1024 workgroups measured 7 us slower: 1024 serialised arrivals)
-    launch_newton_update(n, T + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
-    if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
-    HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPC(hipEventRecord(c->evn, c->stream));
+    if (!post_in_solve) {
+      launch_newton_update(n, T + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
+      if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
+      HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipEventRecord(c->evn, c->stream));
+    }
     if (int e = halo(c, T)) return e;
     // the next F queued before the host reads ||dx|| when the previous step
     // took more Newton iterations than this one has so far (the counts repeat
