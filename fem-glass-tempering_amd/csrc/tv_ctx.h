@@ -322,7 +322,7 @@ int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
 
 // ---- tv_mgdist.cpp (GMG on a slab-partitioned box) ----
 int mg_setup_dist(Ctx* c);
-int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason);
+int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post = false);
 int mg_prepare_dist(Ctx* c, const double* T);
 int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail);
 

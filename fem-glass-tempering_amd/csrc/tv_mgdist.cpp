@@ -430,7 +430,7 @@ int mg_iteration_dist(Ctx* c, const double* T, int it, bool fold, bool lag3) {
 
 }  // namespace
 
-int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
+int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
   const PcgState h = pcg_state_init(c);
   c->h_st[2] = h;
@@ -484,6 +484,14 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
     HIPC(hipEventRecord(c->evp[0], c->stream));
+    if (post) {  // the Newton iteration's next work, gated on the (all-reduced, rank-identical) state
+      double* nrm = c->sums + 6;  // not c->sums: the lagged logic reads those across the batch boundary
+      launch_post_group(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, c->f[TV_F_T].ptr + off,
+                        c->partials, nrm, c->stream);
+      if (int e = allreduce(c, nrm, 1)) return e;  // collective on every rank, run or gated off
+      HIPC(hipMemcpyAsync(c->h_sums, nrm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipEventRecord(c->evn, c->stream));
+    }
     return TV_OK;
   };
   const int hk = std::min(c->newton_k, 15);  // every rank polls the same all-reduced state: same decisions
@@ -496,7 +504,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason) {
   }
   *its = c->h_st[0].it;
   *reason = c->h_st[0].reason;
-  launch_mg_dx_finish(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
+  if (!post) launch_mg_dx_finish(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
   c->pcg_hint = std::max(1, c->h_st[0].it);
   c->mg_hint[hk] = c->pcg_hint;
   if (c->ktime) {

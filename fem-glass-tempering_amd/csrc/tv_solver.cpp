@@ -373,8 +373,8 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     c->newton_k = its;  // the multigrid solves queue the count this Newton index took last step
     // single-partition multigrid: the post-solve group (dx, u <- u - dx, ||dx||)
     // is queued behind every batch and runs behind the one that ends the solve
-    const bool post_in_solve = c->mg_on && c->n_parts == 1 && !dir;
-    if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason)
+    const bool post_in_solve = c->mg_on && !dir;
+    if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason, post_in_solve)
                                             : pcg_solve_mg(c, T, &k, &reason, post_in_solve))
                           : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
       return e;
