@@ -1911,6 +1911,9 @@ bool launch_cg_japply_fused(const CgGrid& g, const double* T, const double* z, d
                             hipStream_t s, const RedTail* tail, int it_host) {
   // neighbour values of p_new are recomputed from z and p_old; p_new goes to the
   // other buffer of the pair (selected on device from st->it).
+  // The march forms a lagged state with logic_update only (lag_update_lean):
+  // any other lagged kind is refused (the callers then fail loudly)
+  if (tail && tail->lag && tail->lag_kind != 3) return false;
   const bool fused = launch_rows<MODE_JAC, true>(g, T, z, pA, w, pB, st, partials, true, s, tail, it_host);
   if (n_partials) *n_partials = plan(g, true).nparts;
   return fused;
