@@ -535,7 +535,12 @@ int amg_setup_part(Ctx* c) {
     HIPC(hipMemcpyAsync(&nn, dv, sizeof(double), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     const int64_t N = (int64_t)nn;
-    if (N >= INT32_MAX) return c->fail(TV_ERR_ARG, "AMG: < 2^31 vertices");
+    // every rank holds the global CSR on the host (~27 entries x 16 B per row,
+    // plus the hierarchy): 20M rows ~ 9 GB per rank before setup temporaries
+    constexpr int64_t kAmgPartMaxRows = 20000000;
+    if (N > kAmgPartMaxRows)
+      return c->fail(TV_ERR_ARG, "AMG on a partitioned mesh gathers the global operator on every rank: at most 20M "
+                                 "global vertices (use Jacobi beyond)");
     std::vector<double> len((size_t)N, 0.0);
     for (int64_t i = 0; i < nown; ++i) len[(size_t)(off + i)] = (double)(Al.ptr[i + 1] - Al.ptr[i]);
     if (int e = dev((size_t)N)) return e;

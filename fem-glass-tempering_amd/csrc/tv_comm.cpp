@@ -679,6 +679,50 @@ int tv_comm_init_stub(void* ctx) {
 }
 
 
+int tv_comm_time(void* ctx, int pattern, int reps, double* us_per_call) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !us_per_call || reps < 1 || pattern < 0 || pattern >= TV_XCHG_COUNT) return TV_ERR_ARG;
+  if (!multi_rank(c)) return c->fail(TV_ERR_STATE, "tv_comm_time: a partitioned context with a transport");
+  if (c->um || c->fam_T != TV_CG) return c->fail(TV_ERR_ARG, "tv_comm_time: partitioned CG1 box meshes");
+  hipSetDevice(c->device);
+  // the multigrid level a pattern needs (distributed level 1 / 2, the replicated level mg_A)
+  MgLevel* lev = nullptr;
+  if (pattern == TV_XCHG_VEC) {
+    if (!c->mg_on || c->mg_A < 1 || (size_t)c->mg_A > c->mg.size()) return TV_ERR_ARG;
+    lev = &c->mg[(size_t)c->mg_A - 1];
+  } else if (pattern == TV_XCHG_HALO_L1 || pattern == TV_XCHG_HALO_L2) {
+    const size_t l = pattern == TV_XCHG_HALO_L1 ? 1 : 2;
+    if (!c->mg_on || c->mg.size() < l || !c->mg[l - 1].dist) return TV_ERR_ARG;
+    lev = &c->mg[l - 1];
+  }
+  auto once = [&]() -> int {
+    switch (pattern) {
+      case TV_XCHG_HALO: return halo_grid(c, c->cg, c->w);
+      case TV_XCHG_ALLREDUCE1: return allreduce(c, c->sums + 4, 1);
+      case TV_XCHG_CLOSE: return allreduce_halo(c, c->sums + 4, 2, c->w);
+      case TV_XCHG_VEC: return allreduce_vec(c, lev->b, lev->n);
+      default: return halo_grid(c, lev->g, lev->x);
+    }
+  };
+  if (int e = once()) return e;  // warm-up (RCCL connects its peers at the first use)
+  hipEvent_t e0, e1;
+  HIPC(hipEventCreate(&e0));
+  HIPC(hipEventCreate(&e1));
+  HIPC(hipStreamSynchronize(c->stream));
+  HIPC(hipEventRecord(e0, c->stream));
+  for (int r = 0; r < reps; ++r)
+    if (int e = once()) return e;
+  HIPC(hipEventRecord(e1, c->stream));
+  HIPC(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPC(hipEventElapsedTime(&ms, e0, e1));
+  HIPC(hipEventDestroy(e0));
+  HIPC(hipEventDestroy(e1));
+  *us_per_call = 1e3 * (double)ms / reps;
+  return TV_OK;
+}
+
+
 int tv_halo_exchange(void* ctx, int field) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || field < 0 || field >= TV_NUM_FIELDS || !c->f[field].ptr) return TV_ERR_ARG;

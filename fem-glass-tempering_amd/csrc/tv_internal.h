@@ -103,6 +103,7 @@ struct PcgState {
   double rtol, atol, dtol;
   int it, done, reason, max_it;
   int post;                   // the post-solve group queued behind the batches has run (pcg_solve_mg)
+  int accept_its;             // ksp_fixed_its > 0: a solve ending at max_it (DIVERGED_ITS) is a good outcome
   double dx_norm2;            // ||dx||^2 of the last Newton update
   double a_prev;              // step length of the previous iteration (dx is updated every 2nd)
   // single-reduction form (k_cgs_march): gamma = (r, z) and eta = (p, A p) of

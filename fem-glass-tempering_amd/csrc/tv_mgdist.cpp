@@ -130,6 +130,24 @@ int mg_setup_dist(Ctx* c) {
       if (nl.is_c[2][k]) nl.owner.push_back(fl.owner[k]);  // a coarse plane belongs to its fine centre's owner
     plan.push_back(std::move(nl));
   }
+  // LOCAL coupling with automatic depth: each partition runs its own slab
+  // hierarchy, which needs >= 2 planes per level on every partition -- end the
+  // hierarchy at the last level where that holds (an explicit mg_levels that
+  // goes deeper is refused below)
+  if (local && automatic) {
+    for (size_t l = 1; l < plan.size(); ++l) {
+      int min_own = 1 << 30;
+      for (int q = 0; q < P; ++q) {
+        int lo, hi;
+        owned_range(plan[l].owner, q, &lo, &hi);
+        min_own = std::min(min_own, hi - lo);
+      }
+      if (min_own < 2) {
+        plan.resize(l);
+        break;
+      }
+    }
+  }
   const int L = (int)plan.size();
   // the transfers of a partitioned level are the row kernels with table-driven
   // y / z maps (k_mg_restrict_pairs, k_mg_prolong_pairs): x must coarsen

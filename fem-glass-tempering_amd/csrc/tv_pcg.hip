@@ -256,8 +256,14 @@ __global__ __launch_bounds__(kBlock) void k_dx_tail(int64_t n, const PcgState* _
 
 // the post-solve group of a Newton iteration queued behind every batch of a
 // multigrid solve (pcg_solve_mg): it runs once, behind the batch that ends
-// the solve, so the host's convergence poll overlaps it
-__device__ __forceinline__ bool post_gate(const PcgState* st) { return st->done && !st->post; }
+// the solve, so the host's convergence poll overlaps it -- and only when the
+// solve ended well (converged, or the fixed iteration count of ksp_fixed_its):
+// a diverged solve (NaN / Inf, DTOL, indefinite, DIVERGED_ITS) leaves T and dx
+// untouched, and newton() then returns TV_ERR_KSP with the state as it was
+__device__ __forceinline__ bool post_gate(const PcgState* st) {
+  const bool good = st->reason > 0 || (st->reason == R_DIV_ITS && st->accept_its);
+  return st->done && !st->post && good;
+}
 
 // dx after the solve, from the device's iteration count (launch_mg_dx_finish)
 __global__ __launch_bounds__(kBlock) void k_dx_finish_gated(int64_t n, const PcgState* __restrict__ st,

@@ -57,6 +57,7 @@ PcgState pcg_state_init(const Ctx* c) {
     h.atol = 0.0;
     h.dtol = 1e300;
     h.max_it = c->O.ksp_fixed_its;
+    h.accept_its = 1;
   }
   return h;
 }
@@ -371,8 +372,9 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
       if (int e = dirichlet_pre(c, T)) return e;
     int k = 0, reason = 0;
     c->newton_k = its;  // the multigrid solves queue the count this Newton index took last step
-    // single-partition multigrid: the post-solve group (dx, u <- u - dx, ||dx||)
-    // is queued behind every batch and runs behind the one that ends the solve
+    // multigrid (one partition or distributed): the post-solve group (dx,
+    // u <- u - dx, ||dx||) is queued behind every batch and runs behind the
+    // one that ends the solve, and only if it ended well (post_gate)
     const bool post_in_solve = c->mg_on && !dir;
     if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason, post_in_solve)
                                             : pcg_solve_mg(c, T, &k, &reason, post_in_solve))

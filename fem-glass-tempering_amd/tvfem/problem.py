@@ -112,7 +112,7 @@ class ThermoViscoProblem:
                  write_output: bool | None = None, output_dir: str = "output", preconditioner: str = "jacobi",
                  mg_levels: int = 0, dg_kernel: str = "auto", dg_tile_chunk: int = 0,
                  mg_replicate_nodes: int = 0, ksp_fixed_its: int = 0, newton_fixed_its: int = 0,
-                 cell_parts=None, mg_coupling: str = "auto") -> None:
+                 cell_parts=None, mg_coupling: str = "auto", ksp_max_it: int = 10000) -> None:
         if isinstance(mesh_path, (RectilinearMesh, UnstructuredMesh)):
             self.mesh = mesh_path
         elif isinstance(mesh_path, str):
@@ -157,6 +157,7 @@ class ThermoViscoProblem:
         self._mg_coupling = {"auto": N.TV_MG_COUPLING_AUTO, "global": N.TV_MG_COUPLING_GLOBAL,
                              "local": N.TV_MG_COUPLING_LOCAL}[mg_coupling]
         self._ksp_fixed_its = int(ksp_fixed_its)
+        self._ksp_max_it = int(ksp_max_it)  # PETSc KSP max_it (default 10000)
         self._newton_fixed_its = int(newton_fixed_its)
         # partitioned unstructured mesh: cell -> part ids (default: tv_partition_rcb)
         self._cell_parts = None if cell_parts is None else np.asarray(cell_parts)
@@ -244,6 +245,7 @@ class ThermoViscoProblem:
         opts.dg_tile_chunk = self._dg_tile_chunk
         opts.mg_replicate_nodes = self._mg_replicate_nodes
         opts.ksp_fixed_its = self._ksp_fixed_its
+        opts.ksp_max_it = self._ksp_max_it
         opts.mg_coupling = self._mg_coupling
         if self._newton_fixed_its > 0:  # timing runs only: exactly this many Newton iterations per step
             opts.newton_rtol = 0.0

@@ -51,10 +51,11 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 5  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+#define TV_ABI_VERSION 6  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
                             3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its;
                             4: tv_upart_desc / tv_create_unstructured_part;
-                            5: tv_comm_init_loopback, tv_comm_check, tv_options.mg_coupling */
+                            5: tv_comm_init_loopback, tv_comm_check, tv_options.mg_coupling;
+                            6: tv_comm_time */
 
 /* status codes */
 #define TV_OK 0
@@ -287,7 +288,11 @@ int tv_create_unstructured(const tv_umesh_desc* mesh, const tv_fe_config* fe, co
 /* partition `part->part` of a distributed unstructured mesh (local mesh as
  * tv_upart_desc describes); the communicator (tv_comm_init / _host) must be
  * set before the first step (a solve without one returns TV_ERR_STATE).
- * Jacobi-PCG (KSPCG form); Dirichlet mode as on one partition. */
+ * KSPCG form with Jacobi (TV_PC_JACOBI) or the agglomerated algebraic multigrid
+ * (TV_PC_AMG: at the first solve every rank gathers the GLOBAL T-independent
+ * cell operator and builds the whole hierarchy -- host memory and setup time
+ * per rank grow with the global nnz, O(27 x 12 B) per global vertex; refused
+ * above 20M global rows, TV_ERR_ARG); Dirichlet mode as on one partition. */
 int tv_create_unstructured_part(const tv_umesh_desc* local_mesh, const tv_upart_desc* part, const tv_fe_config* fe,
                                 const tv_params* params, const tv_options* opts, int device, void** ctx_out);
 int tv_destroy(void* ctx);
@@ -419,6 +424,19 @@ int tv_comm_init_loopback(void* ctx, const char* id);
 int tv_comm_check(void* ctx, int64_t* n_checked, int64_t* n_bad);
 int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn allreduce_fn,
                       tv_host_sendrecv_fn sendrecv_fn, void* user);
+/* Cost of one exchange pattern of the partitioned solve on the transport in
+ * place (collective; measurement only -- it overwrites solver scratch): `reps`
+ * back-to-back calls on the context stream between two HIP events, the mean
+ * stream time per call in microseconds.  Patterns (TV_XCHG_*): the fine-grid
+ * ghost planes, a one-scalar all-reduce, the closing group of a KSPCG
+ * iteration (2 sums + the ghost planes of z), the replicated multigrid level's
+ * vector all-reduce, the ghost planes of distributed multigrid level 1 / 2.
+ * TV_ERR_ARG when the pattern does not occur on this context.  On a loopback
+ * communicator (tv_comm_init_loopback) this is the fixed cost of each RCCL
+ * group on one GPU -- a lower bound of the same group across xGMI. */
+enum { TV_XCHG_HALO = 0, TV_XCHG_ALLREDUCE1 = 1, TV_XCHG_CLOSE = 2, TV_XCHG_VEC = 3, TV_XCHG_HALO_L1 = 4,
+       TV_XCHG_HALO_L2 = 5, TV_XCHG_COUNT = 6 };
+int tv_comm_time(void* ctx, int pattern, int reps, double* us_per_call);
 
 /* ---- measurement ------------------------------------------------------------ */
 /* time `reps` launches of one hot kernel on the context stream with HIP events;

@@ -186,6 +186,23 @@ def test_gmg_rejects_unsupported_meshes():
                            preconditioner="gmg")
 
 
+@pytest.mark.gpu
+def test_gmg_failed_krylov_solve_leaves_state_untouched():
+    """A Krylov solve that ends badly (here DIVERGED_ITS at ksp_max_it = 1)
+    raises, and the post-solve group queued behind the multigrid batches
+    (dx finish, T <- T - dx, ||dx||) must not have run: T bitwise as before."""
+    _torch()
+    from tvfem._native import NativeError
+    dev, _ = _pair(CASES["plate"], preconditioner="gmg", ksp_max_it=1)
+    dev.setup()
+    T0 = dev.functions_current["T"].x.array.copy()
+    with pytest.raises(NativeError, match="DIVERGED_ITS"):
+        dev.solve_timestep()
+    T1 = dev.functions_current["T"].x.array
+    assert np.array_equal(T0.view(np.uint64), T1.view(np.uint64))
+    dev.close()
+
+
 def test_preconditioner_argument_checked():
     from tvfem import RectilinearMesh
     from tvfem.problem import ThermoViscoProblem

@@ -199,7 +199,7 @@ def test_partitioned_vcycle_operator_matches_restatement(coupling, world, rep):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
 def test_partitioned_local_gmg_solves(world):
-    """LOCAL coupling (block-Jacobi V-cycle, the partitioned default): the
+    """LOCAL coupling (block-Jacobi V-cycle, opt-in; AUTO = GLOBAL): the
     Newton solution equals the single partition's (T <= 1e-12; the Krylov
     tolerance is met either way), the Newton counts too; the Krylov counts may
     differ (they depend on the partition count, as PCGAMG's do)."""
