@@ -122,8 +122,6 @@ def main():
         # the same solver at every rank count: partitioned boxes run the distributed
         # V-cycle (tv_mgdist.cpp), so N = 1 and N > 1 lines compare like with like
         pc = "gmg" if (not um and a.pcg != "single" and big) else "jacobi"
-        if a.family == "DG" and (world > 1 or a.share > 1):
-            pc = "jacobi"  # DG1 slabs: Jacobi-PCG (no partitioned DG1 V-cycle)
         if um and world == 1:  # general hexahedra: the smoothed-aggregation AMG (distorted C4: 71.9 vs 127.0 ms)
             pc = "amg"
     # unstructured: RCB cell partition + ghost layer (tvfem.parallel.ghosted_partition)

@@ -250,12 +250,13 @@ __global__ __launch_bounds__(kBlock) void k_cg_rows(CgGrid g, const double* __re
   }
 
   // ---- outputs --------------------------------------------------------------------
-  const bool owned = (k >= g.k_begin) && (k < g.k_end);
+  const bool owned = (k >= g.k_begin) && (k < g.k_end);   // records
+  const bool inwin = (k >= g.w_begin) && (k < g.w_end);   // writes (CgGrid: write window)
   const bool writer = col_ok && lane >= 1 && lane <= kSeg;
   const int64_t me = (int64_t)i + (int64_t)n0 * j + plane * k;
   if (writer) {
     if (FUSEP) pout[me] = X[1][1];
-    if (owned) out[me] = y;
+    if (inwin) out[me] = y;
   }
   if (MODE == MODE_JAC && partials != nullptr) {
     double d = (writer && owned) ? X[1][1] * y : 0.0;
@@ -319,8 +320,8 @@ template <int DIM, bool FACETS>
 __global__ __launch_bounds__(kBlock) void k_cg_diag(CgGrid g, const double* __restrict__ T,
                                                     double* __restrict__ out, int invert) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
-  const int64_t nown = plane * (g.k_end - g.k_begin);
-  const int64_t base = plane * g.k_begin;
+  const int64_t nown = plane * (g.w_end - g.w_begin);  // the write window
+  const int64_t base = plane * g.w_begin;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < nown;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t n = base + t;
@@ -535,7 +536,7 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
     c[t2] = c2;
     c[a] = side ? n[a] - 1 : 0;
     const bool owned = c[2] >= g.k_begin && c[2] < g.k_end;
-    g.fface[f][c1 + n1 * c2] = owned ? acc : 0.0;
+    g.fface[f][c1 + n1 * c2] = (c[2] >= g.w_begin && c[2] < g.w_end) ? acc : 0.0;
     dot = owned ? Pa * acc : 0.0;
   }
   if (partials != nullptr) {
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, double* __rest
                                                         const PcgState* __restrict__ st) {
   if (st != nullptr && st->done) return;  // queued behind a converged solve (multigrid V-cycle)
   const int n[3] = {g.n0, g.n1, g.n2};
-  const int kb = g.k_begin, nk = g.k_end - g.k_begin;
+  const int kb = g.w_begin, nk = g.w_end - g.w_begin;  // the write window
   const int sx = n[0] > 1 ? 2 : 1;
   const int64_t nA = (int64_t)sx * n[1] * nk;
   // row-axis faces: raxis 1 -> j in {0, n1 - 1} x owned k; raxis 2 -> the owned ones of k in {0, n2 - 1} x j
@@ -592,7 +593,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, double* __rest
       } else {
         c[1] = o;
         c[2] = side ? n[2] - 1 : 0;
-        if (c[2] < kb || c[2] >= g.k_end) continue;  // that plane is not owned here
+        if (c[2] < kb || c[2] >= g.w_end) continue;  // that plane is not in the write window
       }
     }
     double add = 0.0;
@@ -755,9 +756,11 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       st_betaold = st->betaold;
     }
   }
-  // ownership along storage axis 2 (partition axis)
-  const int kb = g.k_begin, ke = g.k_end;
+  // ownership along storage axis 2 (partition axis): outputs on the write
+  // window, the records (p.w, z.z, z.r) over the owned planes
+  const int kb = g.k_begin, ke = g.k_end, wb = g.w_begin, we = g.w_end;
   const bool row_owned = (raxis == 2) ? (r >= kb && r < ke) : true;
+  const bool row_inwin = (raxis == 2) ? (r >= wb && r < we) : true;
   // per-axis data of the row / march axes by selects, not by indexing the
   // kernel arguments with a runtime axis (each such index is a dependent
   // scalar load of the argument segment ahead of the first memory request)
@@ -995,7 +998,9 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       const double Rt = xlo.x * S1 + xlo.y * S2;
       const double y = (xdi.x * S1 + xdi.y * S2) + (shr1(Lt) + shl1(Rt));
       const bool q_owned = (raxis == 2) ? true : (q >= kb && q < ke);
-      const bool wr = writer && row_ok && row_owned && q_owned;
+      const bool q_inwin = (raxis == 2) ? true : (q >= wb && q < we);
+      const bool wr = writer && row_ok && row_owned && q_owned;  // records
+      const bool inwin = row_inwin && q_inwin;                   // stores
       // Robin facet terms: in-tile face planes (above), face workgroups
       // (other faces, added by the consumer) / k_cg_boundary (residual)
       double yb = y;
@@ -1003,11 +1008,11 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       if (fq1 && q == nQ - 1) yb += yq1;
       if (POST) {  // z = x + omega dinv (r - J x): the post-smoothing step (facet terms of the side faces later)
         const double zq = xc + pa.omega * pd * (pr - yb);
-        bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, zq);
+        bstore(rso, inwin ? vo_wr + plane_off(q) : kBadOff, zq);
         zz += wr ? zq * zq : 0.0;
         zr += wr ? zq * pr : 0.0;
       } else {
-        bstore(rso, (row_owned && q_owned) ? vo_wr + plane_off(q) : kBadOff, yb);
+        bstore(rso, inwin ? vo_wr + plane_off(q) : kBadOff, yb);
       }
       if (MODE == MODE_JAC && !POST) dot += wr ? xc * yb : 0.0;
     }
@@ -1697,7 +1702,7 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
                        out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, it_host,
                        PostArgs{});
     if (folded && !FUSEP && addfaces && fo.off[6] > 0) {  // complete J x (else the consumer adds them)
-      const int64_t nodes = 2 * ((int64_t)g.n1 * (g.k_end - g.k_begin) + (int64_t)g.n0 * std::max(g.n1, g.n2));
+      const int64_t nodes = 2 * ((int64_t)g.n1 * (g.w_end - g.w_begin) + (int64_t)g.n0 * std::max(g.n1, g.n2));
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, 1024));
       hipLaunchKernelGGL(k_cg_addfaces, dim3(nb), dim3(kBlock), 0, s, g, out, L.raxis, st);
     }
@@ -1731,13 +1736,15 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
 // tiles wrote records 0 .. rec0 - 1); the last block reduces all of them and
 // runs the KSPCG logic.  Nodes on both face families are visited once (the
 // row-axis faces skip i = 0 and i = n0 - 1; face_at sums every face of a node).
-// [kb, ke): the owned planes of storage axis 2 (a partition's ghost planes are
-// neither rewritten nor counted)
+// [kb, ke): the owned planes of storage axis 2, the only ones counted; z is
+// rewritten on the write window [wb, we) (the owned planes, or on a deep-ghost
+// slab every ghost plane but the outermost, where the single-reduction form
+// needs z one plane out)
 __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis, const double* __restrict__ r,
                                                          const double* __restrict__ dinv, double omega,
                                                          double* __restrict__ z, double* __restrict__ partials,
                                                          int rec0, RedTail rt, const PcgState* __restrict__ st, int kb,
-                                                         int ke) {
+                                                         int ke, int wb, int we) {
   if (st->done) return;  // uniform: a converged solve's queued launch
   const int n0 = fa.n0, n1 = fa.n1, n2 = fa.n2;
   const int64_t nA = 2 * (int64_t)n1 * n2;
@@ -1767,13 +1774,14 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
         j = side ? n1 - 1 : 0;
       }
     }
-    if (k < kb || k >= ke) continue;  // a ghost plane
+    if (k < wb || k >= we) continue;  // outside the write window
     const int64_t q = i + (int64_t)n0 * (j + (int64_t)n1 * k);
     // the node's three loads first, independent of the face lookups (one round trip)
     const double zo = z[q], dq = dinv[q], rq = r[q];
     const double add = face_at(fa, i, j, k);
     const double zn = zo - omega * dq * add;
     z[q] = zn;
+    if (k < kb || k >= ke) continue;  // a ghost plane: rewritten, not counted
     a0 += zn * zn - zo * zo;
     a1 += (zn - zo) * rq;
   }
@@ -1855,7 +1863,7 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, cap));
   const RedTail rt = tail ? *tail : RedTail{};
   hipLaunchKernelGGL(k_mg_post_faces, dim3(nb), dim3(kBlock), 0, s, fa, L.raxis, r, dinv, omega, z, partials,
-                     L.blocks, rt, st, g.k_begin, g.k_end);
+                     L.blocks, rt, st, g.k_begin, g.k_end, g.w_begin, g.w_end);
   return L.blocks + nb;
 }
 
@@ -1868,6 +1876,23 @@ void launch_mg_prepare(const MgPrep& p, hipStream_t s) {
 }
 
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }
+
+DiagFly cg_diag_fly(const CgGrid& g, int64_t t_off) {
+  DiagFly df{};
+  if (!use_march(g)) return df;  // 3D box levels only
+  df.on = 1;
+  df.n0 = g.n0;
+  df.n1 = g.n1;
+  df.n2 = g.n2;
+  df.t_off = t_off;
+  df.inv_n0 = 1.0 / g.n0;
+  df.inv_plane = 1.0 / ((double)g.n0 * g.n1);
+  for (int s = 0; s < 3; ++s) df.coef[s] = g.coef[s];
+  df.dt_alpha = g.dt_alpha;
+  for (int a = 0; a < 3; ++a)
+    for (int sd = 0; sd < 2; ++sd) df.bnd[a][sd] = g.bnd[a][sd];
+  return df;
+}
 
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off) {
   FaceAdd fa{};
@@ -1899,6 +1924,14 @@ void launch_cg_japply(const CgGrid& g, const double* T, const double* x, double*
                       int* n_partials, hipStream_t s, const PcgState* st) {
   launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, st, partials, false, s);
   if (n_partials) *n_partials = plan(g, false).nparts;
+}
+
+bool launch_cg_japply_tail(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
+                           double* partials, const RedTail* tail, hipStream_t s) {
+  // complete J x (the face-workgroup terms added by k_cg_addfaces behind the
+  // march) with the x.(J x) records of the march tiles and face workgroups
+  // reduced by the tail into tail->out[0]
+  return launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, st, partials, false, s, tail, 0, true);
 }
 
 void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
@@ -1944,7 +1977,7 @@ int cg_cgs_records(const CgGrid& g) {
 bool cg_cgs_supported(const CgGrid& g) { return use_march(g); }
 
 void launch_cg_diag(const CgGrid& g, const double* T, double* dinv, int invert, hipStream_t s, bool bnd_only) {
-  const int64_t nown = (int64_t)g.n0 * g.n1 * (g.k_end - g.k_begin);
+  const int64_t nown = (int64_t)g.n0 * g.n1 * (g.w_end - g.w_begin);  // the write window
   int blocks = (int)std::min<int64_t>((nown + kBlock - 1) / kBlock, 4096);
   if (blocks <= 0) return;
   switch (dim_of(g)) {

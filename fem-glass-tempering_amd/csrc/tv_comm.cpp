@@ -57,10 +57,10 @@ static inline int peer(const Ctx* c, int q) { return c->comm_self ? 0 : q; }
 // temperature ghosts keep their initial value, reductions stay local.  Both
 // ghost planes in ONE small launch (two hipMemsetAsync fills cost ~5 us each:
 // ~2 ms of a C4 / 8 share step went into the stand-ins for its exchanges)
-__global__ __launch_bounds__(kBlock) void k_zero_ghosts(double* lo, double* hi, int64_t plane) {
-  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < 2 * plane; t += (int64_t)gridDim.x * kBlock) {
-    double* p = (t < plane) ? lo : hi;
-    if (p != nullptr) p[t < plane ? t : t - plane] = 0.0;
+__global__ __launch_bounds__(kBlock) void k_zero_ghosts(double* lo, double* hi, int64_t nlo, int64_t nhi) {
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nlo + nhi; t += (int64_t)gridDim.x * kBlock) {
+    if (t < nlo) lo[t] = 0.0;
+    else hi[t - nlo] = 0.0;
   }
 }
 
@@ -68,32 +68,49 @@ static int stub_ghosts(Ctx* c, const CgGrid& g, double* v) {
   if (v == c->f[TV_F_T].ptr || v == c->f[TV_F_T_PREV].ptr) return TV_OK;
   const int64_t plane = (int64_t)g.n0 * g.n1;
   if (!g.g_lo && !g.g_hi) return TV_OK;
-  const int nb = (int)std::min<int64_t>(1024, (2 * plane + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_zero_ghosts, dim3(nb), dim3(kBlock), 0, c->stream, g.g_lo ? v + plane * (g.k_begin - 1) : nullptr,
-                     g.g_hi ? v + plane * g.k_end : nullptr, plane);
+  const int64_t nlo = plane * g.g_lo, nhi = plane * g.g_hi;
+  const int nb = (int)std::min<int64_t>(1024, (nlo + nhi + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_zero_ghosts, dim3(nb), dim3(kBlock), 0, c->stream, v, v + plane * g.k_end, nlo, nhi);
   HIPC(hipGetLastError());
   return TV_OK;
 }
 
-// ghost planes of v on grid g (the fine grid or a distributed multigrid level:
-// one plane per interface, storage axis 2): send the first / last owned plane,
-// receive into ghost plane 0 / n2 - 1
+// ghost planes of v on grid g (the fine grid or a distributed multigrid level,
+// storage axis 2): g_lo / g_hi planes per interface (1, or kDeepGhosts on a
+// deep-ghost fine slab) -- send the first / last g owned planes (one
+// contiguous block each), receive into the ghost planes below / above
 int halo_host(Ctx* c, const CgGrid& g, double* v) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
+  const int64_t nlo = plane * g.g_lo, nhi = plane * g.g_hi;
   double* s_lo = c->h_halo;
-  double* s_hi = c->h_halo + plane;
-  double* r_lo = c->h_halo + 2 * plane;
-  double* r_hi = c->h_halo + 3 * plane;
-  if (g.g_lo) HIPC(hipMemcpyAsync(s_lo, v + plane * g.k_begin, plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  if (g.g_hi) HIPC(hipMemcpyAsync(s_hi, v + plane * (g.k_end - 1), plane * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  double* s_hi = c->h_halo + nlo;
+  double* r_lo = c->h_halo + nlo + nhi;
+  double* r_hi = c->h_halo + 2 * nlo + nhi;
+  if (nlo) HIPC(hipMemcpyAsync(s_lo, v + plane * g.k_begin, nlo * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (nhi) HIPC(hipMemcpyAsync(s_hi, v + plane * (g.k_end - g.g_hi), nhi * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
-  if (g.g_lo && c->host_sendrecv(s_lo, (size_t)plane, c->rank - 1, r_lo, (size_t)plane, c->rank - 1, c->host_user))
+  if (nlo && c->host_sendrecv(s_lo, (size_t)nlo, c->rank - 1, r_lo, (size_t)nlo, c->rank - 1, c->host_user))
     return c->fail(TV_ERR_COMM, "host sendrecv failed");
-  if (g.g_hi && c->host_sendrecv(s_hi, (size_t)plane, c->rank + 1, r_hi, (size_t)plane, c->rank + 1, c->host_user))
+  if (nhi && c->host_sendrecv(s_hi, (size_t)nhi, c->rank + 1, r_hi, (size_t)nhi, c->rank + 1, c->host_user))
     return c->fail(TV_ERR_COMM, "host sendrecv failed");
-  if (g.g_lo) HIPC(hipMemcpyAsync(v, r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  if (g.g_hi) HIPC(hipMemcpyAsync(v + plane * g.k_end, r_hi, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (nlo) HIPC(hipMemcpyAsync(v, r_lo, nlo * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (nhi) HIPC(hipMemcpyAsync(v + plane * g.k_end, r_hi, nhi * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
+  return TV_OK;
+}
+
+// the plane sends / receives of halo_grid inside an open RCCL group
+static int group_planes(Ctx* c, const CgGrid& g, double* v) {
+  const int64_t plane = (int64_t)g.n0 * g.n1;
+  const size_t nlo = (size_t)(plane * g.g_lo), nhi = (size_t)(plane * g.g_hi);
+  if (nlo) {  // neighbour rank - 1: send the first g_lo owned planes, receive the ghost planes below
+    NCCLC(ncclSend(v + plane * g.k_begin, nlo, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v, nlo, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+  }
+  if (nhi) {
+    NCCLC(ncclSend(v + plane * (g.k_end - g.g_hi), nhi, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, nhi, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+  }
   return TV_OK;
 }
 
@@ -101,16 +118,8 @@ int halo_grid(Ctx* c, const CgGrid& g, double* v) {
   if (!multi_rank(c)) return TV_OK;
   if (c->comm_stub) return stub_ghosts(c, g, v);
   if (c->host_sendrecv) return halo_host(c, g, v);
-  const int64_t plane = (int64_t)g.n0 * g.n1;
   NCCLC(ncclGroupStart());
-  if (g.g_lo) {  // neighbour rank-1: send first owned plane, receive ghost plane 0
-    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
-    NCCLC(ncclRecv(v, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
-  }
-  if (g.g_hi) {
-    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
-    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
-  }
+  if (int e = group_planes(c, g, v)) return e;
   NCCLC(ncclGroupEnd());
   return TV_OK;
 }
@@ -228,18 +237,9 @@ int allreduce_halo(Ctx* c, double* sums, int n, double* v) {
     if (int e = allreduce(c, sums, n)) return e;
     return halo(c, v);
   }
-  const CgGrid& g = c->cg;
-  const int64_t plane = (int64_t)g.n0 * g.n1;
   NCCLC(ncclGroupStart());
   NCCLC(ncclAllReduce(sums, sums, n, ncclDouble, ncclSum, c->comm, c->stream));
-  if (g.g_lo) {
-    NCCLC(ncclSend(v + plane * g.k_begin, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
-    NCCLC(ncclRecv(v, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
-  }
-  if (g.g_hi) {
-    NCCLC(ncclSend(v + plane * (g.k_end - 1), plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
-    NCCLC(ncclRecv(v + plane * g.k_end, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
-  }
+  if (int e = group_planes(c, c->cg, v)) return e;
   NCCLC(ncclGroupEnd());
   return TV_OK;
 }
@@ -345,8 +345,8 @@ void check_ids(const Ctx* c, const CgGrid& g, const std::vector<double>& h, int6
   const int64_t plane = (int64_t)g.n0 * g.n1;
   for (int k = 0; k < g.n2; ++k) {
     int64_t src = first_plane + k;                                  // global plane the values must come from
-    if (k < g.k_begin && c->comm_self) src = first_plane + g.k_begin;
-    if (k >= g.k_end && c->comm_self) src = first_plane + g.k_end - 1;
+    if (k < g.k_begin && c->comm_self) src = first_plane + g.k_begin + k;  // this rank's first g_lo planes
+    if (k >= g.k_end && c->comm_self) src = first_plane + g.k_end - g.g_hi + (k - g.k_end);
     if ((k < g.k_begin && !g.g_lo) || (k >= g.k_end && !g.g_hi)) continue;
     for (int64_t e = 0; e < plane; ++e) {
       ++*n_chk;
@@ -648,9 +648,9 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
   if (c->um) {  // the packed sends, then the ghosts
     const int64_t stot = c->um_soff.empty() ? 0 : c->um_soff.back() + c->um_scnt.back();
     HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * (size_t)std::max<int64_t>(1, stot + c->nT - c->ownT_n)));
-  } else if (c->fam_T == TV_CG) {
+  } else if (c->fam_T == TV_CG) {  // send + receive blocks of g_lo + g_hi planes
     const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
-    HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)plane));
+    HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 2 * (size_t)plane * std::max(2, c->cg.g_lo + c->cg.g_hi)));
   } else {  // DG: 2 send + 2 receive cell layers of 2^d components
     const int64_t L = ((int64_t)1 << c->dim) * c->dg.c0 * c->dg.c1;
     HIPC(hipHostMalloc(&c->h_halo, sizeof(double) * 4 * (size_t)L));

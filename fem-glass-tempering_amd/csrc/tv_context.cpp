@@ -112,6 +112,8 @@ int build_cg_grid(Ctx* c, int d, const std::vector<double> (&X)[3], int first2, 
   g.n2 = n2;
   g.k_begin = g_lo;
   g.k_end = n2 - g_hi;
+  g.w_begin = g.k_begin - std::max(0, g_lo - 1);
+  g.w_end = g.k_end + std::max(0, g_hi - 1);
   g.deg1 = X[1].size() == 1;
   g.deg2 = X[2].size() == 1;
   g.bnd[0][0] = g.bnd[0][1] = 1;
@@ -129,9 +131,9 @@ int build_cg_grid(Ctx* c, int d, const std::vector<double> (&X)[3], int first2, 
   }
   const int64_t plane = (int64_t)g.n0 * g.n1;
   for (int f = 0; f < 6; ++f) g.ffoff[f] = -1;
-  if (d == 3) {  // owned nodes on physical boundary faces (Robin facets, marching kernel path)
+  if (d == 3) {  // write-window nodes on physical boundary faces (Robin facets, marching kernel path)
     std::vector<int64_t> bn;
-    for (int k = g.k_begin; k < g.k_end; ++k)
+    for (int k = g.w_begin; k < g.w_end; ++k)
       for (int j = 0; j < g.n1; ++j)
         for (int i = 0; i < g.n0; ++i) {
           const bool on = (i == 0 && g.bnd[0][0]) || (i == g.n0 - 1 && g.bnd[0][1]) ||
@@ -301,7 +303,15 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     CgGrid& g = c->cg;
     std::vector<double> X[3];
     for (int s = 0; s < 3; ++s) X[s] = storage_coords(c, s, tmp);
-    const int g_lo = (p > 0) ? 1 : 0, g_hi = (p < P - 1) ? 1 : 0;
+    // deep ghosts (three planes per interface) for the distributed multigrid
+    // with global coupling: the level-0 vectors of a V-cycle are then computed
+    // on the ghost planes too and need no exchange of their own (tv_mgdist.cpp)
+    const bool deep = P > 1 && d == 3 && c->O.preconditioner == TV_PC_GMG && c->O.mg_coupling != TV_MG_COUPLING_LOCAL &&
+                      c->O.pcg_variant != TV_PCG_SINGLE_REDUCTION;
+    c->ghost_depth = deep ? kDeepGhosts : 1;
+    const int G = c->ghost_depth;
+    if (deep && b1 - b0 < G) return c->fail(TV_ERR_ARG, "partitioned GMG: fewer owned planes than the ghost depth (3)");
+    const int g_lo = (p > 0) ? G : 0, g_hi = (p < P - 1) ? G : 0;
     if (int e = build_cg_grid(c, d, X, b0 - g_lo, (b1 - b0) + g_lo + g_hi, g_lo, g_hi, p == 0, p == P - 1, g, c->coef,
                               &c->bnodes, c->ffbuf))
       return e;
@@ -932,6 +942,7 @@ int tv_destroy(void* ctx) {
     if (L.mask) hipFree(L.mask);
   }
   if (c->mgx) hipFree(c->mgx);
+  if (c->mg_s) hipFree(c->mg_s);
   if (c->dggface) hipFree(c->dggface);
   for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
     if (p) hipFree(p);

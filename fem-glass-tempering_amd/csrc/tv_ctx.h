@@ -94,6 +94,7 @@ struct Ctx {
   // global / local sizes
   int Nnode_glob[3] = {1, 1, 1};  // per storage axis
   int Ncell_glob[3] = {0, 0, 0};
+  int ghost_depth = 1;  // ghost planes per interface of the fine CG slab (3: deep ghosts, tv_mgdist.cpp)
   int plane_begin = 0, plane_end = 0;  // owned global planes (CG) / cell layers (DG) along storage axis 2
   CgGrid cg{};
   bool dinv_interior = false;  // dinv holds the T-independent interior diagonal (CG march path)
@@ -132,6 +133,10 @@ struct Ctx {
   std::vector<MgLevel> mg;
   double mg_omega0 = 0.0;
   double* mgx = nullptr;    // level-0 V-cycle iterate
+  // the single-reduction (Chronopoulos-Gear) form of the distributed GMG-PCG
+  // on a deep-ghost slab (tv_mgdist.cpp): s = A p by recurrence
+  bool mg_cgs = false;
+  double* mg_s = nullptr;
   double* dggface = nullptr; // DG level 0: facet means of dg(T) for the cell-block Jacobi smoother
   // partitioned GMG (tv_mgdist.cpp): levels 0 .. mg_A - 1 are distributed over
   // the partitions, mg_A .. the coarsest are replicated on every rank
@@ -296,7 +301,7 @@ void launch_bc_mask(Ctx* c, double* dinv);  // dinv = 0 on the Dirichlet-constra
 
 // ---- tv_mgsolve.cpp ----
 int mg_setup(Ctx* c);
-void mg_prepare(Ctx* c, const double* T);
+int mg_prepare(Ctx* c, const double* T);
 int mg_dg_weight(Ctx* c, const double* T);
 int mg_apply0(Ctx* c, const double* T, const RedTail* tail);
 // post: queue the Newton iteration's post-solve group (launch_post_group, ||dx||
@@ -324,6 +329,7 @@ int mg_upload(Ctx* c, MgLevel& L, const std::vector<T>& h, const T** out) {
 int mg_setup_dist(Ctx* c);
 int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post = false);
 int mg_prepare_dist(Ctx* c, const double* T);
+void fine_window(const Ctx* c, int64_t* off, int64_t* n);
 int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail);
 
 }  // namespace tv

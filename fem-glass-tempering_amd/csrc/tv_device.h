@@ -205,12 +205,20 @@ __device__ __forceinline__ void logic_cgs(PcgState* st, const double* s) {
   st->a = gamma / eta;
 }
 
+// kinds 6 / 7: the single-reduction logic (5 / 4) on sums laid out as the
+// multigrid form writes them -- (z.z, z.r) by the V-cycle's post-smoothing
+// tail, then (z, A z) by the matvec's: (nu, gamma, delta)
 __device__ __forceinline__ void apply_logic(PcgState* st, const double* sums, int kind) {
   if (kind == 1) logic_init(st, sums);
   else if (kind == 2) logic_dpi(st, sums);
   else if (kind == 3) logic_update(st, sums);
   else if (kind == 4) logic_cgs_init(st, sums);
   else if (kind == 5) logic_cgs(st, sums);
+  else if (kind >= 6) {
+    const double s[3] = {sums[1], sums[2], sums[0]};
+    if (kind == 7) logic_cgs_init(st, s);
+    else logic_cgs(st, s);
+  }
 }
 
 // Lagged scalar logic (multi-rank): the state after the previous all-reduce,
@@ -309,6 +317,31 @@ __device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
   if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
   if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
   return add;
+}
+
+// D^-1 at local node t + df.t_off (DiagFly): stored on the physical boundary,
+// 1 / diag(M + dt alpha K) from the axis tables elsewhere
+__device__ __forceinline__ double dinv_fly(const DiagFly& df, const double* __restrict__ dinv, int64_t t) {
+  const int nd = (int)(t + df.t_off);
+  const int plane = df.n0 * df.n1;
+  int k = (int)((double)nd * df.inv_plane);
+  k -= (k * plane > nd) ? 1 : 0;
+  k += ((k + 1) * plane <= nd) ? 1 : 0;
+  const int rem = nd - k * plane;
+  int j = (int)((double)rem * df.inv_n0);
+  j -= (j * df.n0 > rem) ? 1 : 0;
+  j += ((j + 1) * df.n0 <= rem) ? 1 : 0;
+  const int i = rem - j * df.n0;
+  const bool bnd = (i == 0 && df.bnd[0][0]) || (i == df.n0 - 1 && df.bnd[0][1]) || (j == 0 && df.bnd[1][0]) ||
+                   (j == df.n1 - 1 && df.bnd[1][1]) || (k == 0 && df.bnd[2][0]) || (k == df.n2 - 1 && df.bnd[2][1]);
+  if (bnd) return __builtin_nontemporal_load(&dinv[t]);
+  const double* cx = df.coef[0] + (int64_t)i * C_NCOEF;
+  const double* cy = df.coef[1] + (int64_t)j * C_NCOEF;
+  const double* cz = df.coef[2] + (int64_t)k * C_NCOEF;
+  const double d = cx[C_MDI] * cy[C_MDI] * cz[C_MDI] +
+                   df.dt_alpha * (cx[C_KDI] * cy[C_MDI] * cz[C_MDI] + cx[C_MDI] * cy[C_KDI] * cz[C_MDI] +
+                                  cx[C_MDI] * cy[C_MDI] * cz[C_KDI]);
+  return 1.0 / d;
 }
 
 // the same at local node (i, j, k) (coordinates known)

@@ -335,12 +335,12 @@ __global__ __launch_bounds__(kBlock) void k_dg_gface(DgGrid g, const double* __r
   ci[k] = side ? cn[k] - 1 : 0;
   ci[ea] = ia;
   ci[eb] = ib;
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
-  const int64_t cid = ci[0] + (int64_t)g.c0 * (ci[1] + (int64_t)g.c1 * ci[2]);
+  const DgAddr a = dg_layer(g, ci[2]);  // a slab's layers (DgGrid)
+  const int64_t ij = ci[0] + (int64_t)g.c0 * ci[1];
   double acc = 0.0;
 #pragma unroll
   for (int l = 0; l < 8; ++l)
-    if (((l >> k) & 1) == side) acc += dgfun(g, T[(int64_t)l * ncell + cid]);
+    if (((l >> k) & 1) == side) acc += dgfun(g, T[a.base + (int64_t)l * a.stride + ij]);
   gface[t] = 0.25 * acc;
 }
 
@@ -855,18 +855,21 @@ __global__ __launch_bounds__(kBlock) void k_dg_diag(DgGrid g, const double* __re
 }
 
 // level >= 1 style smoothing step on DG: MODE 0 x = omega B^-1 b ; MODE 1 x += omega B^-1 (b - w)
+// The block-smoother kernels run over the OWNED cells: dof (l, c) at l own + c
+// (DgGrid: one partition owns every cell, a slab its own layers, which come
+// first); fdm_mul takes the local cell index c + k_begin c0 c1.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_dg_bsmooth(DgGrid g, const PcgState* __restrict__ st,
                                                        const double* __restrict__ b, const double* __restrict__ w,
                                                        const double* __restrict__ gface, double omega,
                                                        double* __restrict__ x) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int64_t ncell = g.own, c_loc = (int64_t)g.k_begin * g.c0 * g.c1;
   if (st != nullptr && st->done) return;
   for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
     double v[8], y[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) v[l] = MODE ? b[l * ncell + c] - w[l * ncell + c] : b[l * ncell + c];
-    fdm_mul(g, gface, c, v, y);
+    fdm_mul(g, gface, c + c_loc, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) x[l * ncell + c] = MODE ? x[l * ncell + c] + omega * y[l] : omega * y[l];
   }
@@ -883,7 +886,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_bupdate(DgGrid g, const PcgState*
                                                        const double* __restrict__ w, const double* __restrict__ gface,
                                                        double omega, double* __restrict__ r, double* __restrict__ dx,
                                                        double* __restrict__ x0, int it_host) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int64_t ncell = g.own, c_loc = (int64_t)g.k_begin * g.c0 * g.c1;  // owned cells
   if (st->done) return;
   const double a = INIT ? 0.0 : st->a;
   const double ap = DXU ? st->a_prev : 0.0;
@@ -906,7 +909,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_bupdate(DgGrid g, const PcgState*
       }
       v[l] = rr;
     }
-    fdm_mul(g, gface, c, v, y);
+    fdm_mul(g, gface, c + c_loc, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) x0[l * ncell + c] = omega * y[l];
   }
@@ -919,7 +922,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_bpost(DgGrid g, const PcgState* _
                                                      const double* __restrict__ w, const double* __restrict__ gface,
                                                      double omega, double* __restrict__ z,
                                                      double* __restrict__ partials, RedTail rt) {
-  const int64_t ncell = (int64_t)g.c0 * g.c1 * g.c2;
+  const int64_t ncell = g.own, c_loc = (int64_t)g.k_begin * g.c0 * g.c1;  // owned cells
   __shared__ double red[2][kBlock / kWave];
   if (st->done) return;
   double acc[2] = {0.0, 0.0};
@@ -930,7 +933,7 @@ __global__ __launch_bounds__(kBlock) void k_dg_bpost(DgGrid g, const PcgState* _
       rr[l] = r[l * ncell + c];
       v[l] = rr[l] - w[l * ncell + c];
     }
-    fdm_mul(g, gface, c, v, y);
+    fdm_mul(g, gface, c + c_loc, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       const double zz = x0[l * ncell + c] + omega * y[l];
@@ -1051,7 +1054,7 @@ void launch_dg_gface(const DgGrid& g, const double* T, double* gface, hipStream_
 
 void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, const double* w, const double* gface,
                        double omega, double* x, int mode, hipStream_t s) {
-  const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
+  const int nb = dg_vblocks(g.own);
   if (mode == 0) hipLaunchKernelGGL(k_dg_bsmooth<0>, dim3(nb), dim3(kBlock), 0, s, g, st, b, w, gface, omega, x);
   else hipLaunchKernelGGL(k_dg_bsmooth<1>, dim3(nb), dim3(kBlock), 0, s, g, st, b, w, gface, omega, x);
 }
@@ -1059,7 +1062,7 @@ void launch_dg_bsmooth(const DgGrid& g, const PcgState* st, const double* b, con
 void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, const double* pB, const double* w,
                        const double* gface, double omega, double* r, double* dx, double* x0, int it_host, int init,
                        hipStream_t s) {
-  const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
+  const int nb = dg_vblocks(g.own);
 #define TV_DGU(I, D, F) \
   hipLaunchKernelGGL((k_dg_bupdate<I, D, F>), dim3(nb), dim3(kBlock), 0, s, g, st, pA, pB, w, gface, omega, r, dx, x0, \
                      it_host)
@@ -1073,7 +1076,7 @@ void launch_dg_bupdate(const DgGrid& g, const PcgState* st, const double* pA, co
 int launch_dg_bpost(const DgGrid& g, const PcgState* st, const double* x0, const double* r, const double* w,
                     const double* gface, double omega, double* z, double* partials, const RedTail* tail, hipStream_t s) {
   const RedTail rt = tail ? *tail : RedTail{};
-  const int nb = dg_vblocks((int64_t)g.c0 * g.c1 * g.c2);
+  const int nb = dg_vblocks(g.own);
   hipLaunchKernelGGL(k_dg_bpost, dim3(nb), dim3(kBlock), 0, s, g, st, x0, r, w, gface, omega, z, partials, rt);
   return nb;
 }

@@ -23,7 +23,11 @@ enum { C_MLO = 0, C_MDI, C_MUP, C_KLO, C_KDI, C_KUP, C_HLO, C_HHI, C_NCOEF };
 // Grid of the CG1 (Q1 / P1) temperature space on one partition.  Storage axis
 // 0 is physical x (fastest), storage axis 2 is the partition axis (slowest);
 // local node index = i + n0*(j + n1*k).  Along axis 2 the local array holds the
-// owned planes plus one ghost plane towards each neighbouring partition.
+// owned planes plus g_lo / g_hi ghost planes towards the neighbouring
+// partitions: one, or three on the fine grid of a distributed multigrid solve
+// (deep ghosts, tv_mgdist.cpp), whose kernels then write every plane of the
+// write window [w_begin, w_end) -- all local planes but the outermost ghost
+// plane on each side -- and reduce over the owned planes only.
 // Operands of the multigrid post-smoothing fused into the Jacobian march
 // (k_cg_march POST): z = x + omega dinv (r - J x)
 struct PostArgs {
@@ -32,10 +36,13 @@ struct PostArgs {
   double omega;
 };
 
+constexpr int kDeepGhosts = 3;  // ghost planes of a deep-ghost fine slab
+
 struct CgGrid {
   int n0, n1, n2;             // local node counts per storage axis (n2 incl. ghosts)
   int k_begin, k_end;         // owned planes along axis 2, local indexing
   int g_lo, g_hi;             // ghost planes present below / above
+  int w_begin, w_end;         // write window (= [k_begin, k_end) with one ghost plane)
   int deg1, deg2;             // storage axis 1 / 2 degenerate (single node)
   int bnd[3][2];              // face of storage axis a at side s is a physical boundary here
   const double* coef[3];      // device, C_NCOEF doubles per local node per axis
@@ -182,6 +189,13 @@ struct UmGrid {
   const double* K;       // dt alpha K      (residual)
   const double* bvec;    // int phi_i       (f term of the residual)
   const double* vdiag;   // diag V
+  // topologically structured hexahedra (vertex i + s1 j + s2 k, the box's cells,
+  // any coordinates -- a jittered / warped plate, an extruded or transfinite
+  // gmsh mesh): V as 27 stencil slots per row, V27[slot nv + r] for column
+  // r + di + s1 dj + s2 dk, slot = (di + 1) + 3 (dj + 1) + 9 (dk + 1); no column
+  // indices (216 instead of ~330 B per row); nullptr: SELL only
+  const double* V27;
+  int64_t s1, s2;
   // Robin terms
   const int* fv;         // [m][facet] facet vertex ids, facet-local tensor order
   const double* fw;      // [q][facet] w_q |J_s|(q), 3^(d-1) points
@@ -348,6 +362,23 @@ struct FaceAdd {
 };
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off);
 
+// The Jacobi diagonal of a box level formed on the fly by a pointwise kernel
+// (instead of streaming the stored dinv): off the physical boundary diag J =
+// diag(M + dt alpha K) is the per-axis product of diag_value<3, false>
+// (tv_cg.hip), the same expression; the boundary nodes (Robin facet terms,
+// T-dependent, rewritten every Newton iteration; 0 on Dirichlet rows) read the
+// stored value.  on = 0: the stored dinv everywhere (unstructured levels).
+struct DiagFly {
+  int on;
+  int n0, n1, n2;
+  int64_t t_off;             // local index of the kernel's first node
+  double inv_n0, inv_plane;
+  const double* coef[3];
+  double dt_alpha;
+  int bnd[3][2];
+};
+DiagFly cg_diag_fly(const CgGrid& g, int64_t t_off);
+
 // ---- geometric multigrid on the box hierarchy (tv_mg.hip, tv_pcg.hip) ----
 // Transfer between a level and the next coarser one (nested rectilinear grids:
 // along a coarsened axis fine node 2I is coarse node I, odd fine nodes
@@ -421,19 +452,26 @@ struct MgPrep {
 };
 void launch_mg_prepare(const MgPrep& p, hipStream_t s);
 bool cg_uses_march(const CgGrid& g);  // the 3D marching kernels (not the x-row kernel) serve this grid
-// DG1 level 0 -> CG1 level 1 of the same box (3D; cells c0 x c1 x c2, DG dof
-// (l, cell) at l * ncell + cell, l = a + 2b + 4c over the storage axes):
-// restriction = sum of the cell-local copies at each vertex (P = injection of
-// the vertex value into every copy), with the CG level's pre-smoothing fused
-void launch_mg_dg_restrict(int c0, int c1, int c2, const PcgState* st, const double* bf, const double* wf,
-                           const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
-                           hipStream_t s);
-void launch_mg_dg_prolong(int c0, int c1, int c2, const PcgState* st, double* xf, const double* xc, const double* mask,
-                          hipStream_t s);
-void launch_mg_dg_T(int c0, int c1, int c2, const double* Tdg, double* Tcg, hipStream_t s);  // vertex mean
+// DG1 level 0 -> CG1 level 1 of the same box (3D; DG dofs as DgGrid lays them
+// out, l = a + 2b + 4c over the storage axes): restriction = sum of the
+// cell-local copies at each vertex (P = injection of the vertex value into
+// every copy), with the CG level's pre-smoothing fused when xc is given (one
+// partition).  A slab writes its vertex planes of the global CG vector (kg0 =
+// global layer of its local layer 0): the restriction from its owned cells,
+// the prolongation into every local cell (ghost layers included), the vertex
+// mean of T on its owned vertex planes
+void launch_mg_dg_restrict(const DgGrid& g, const PcgState* st, const double* bf, const double* wf, const double* mask,
+                           double* bc, const double* dinv_c, double omega_c, double* xc, int kg0, hipStream_t s);
+void launch_mg_dg_prolong(const DgGrid& g, const PcgState* st, double* xf, const double* xc, const double* mask,
+                          int kg0, hipStream_t s);
+void launch_mg_dg_T(const DgGrid& g, const double* Tdg, double* Tcg, int kg0, hipStream_t s);  // vertex mean
 // power-iteration step for lambda_max(D^-1 J): y <- dinv .* y, per-block sums of y^2 (returns the count)
 int launch_mg_pow(int64_t n, const double* dinv, double* y, double* partials, hipStream_t s);
 void launch_mg_scale(int64_t n, const double* y, double a, double* x, hipStream_t s);  // x <- a y
+// complete J x with x.(J x) reduced by the tail (kind 0: into tail->out[0]);
+// false where the marching kernel does not serve the grid (no tail ran)
+bool launch_cg_japply_tail(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
+                           double* partials, const RedTail* tail, hipStream_t s);
 // J x without the facet terms of the faces along the march (the FaceAdd the
 // consumer adds, cg_face_add); the whole J x where the row kernel runs
 void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,
@@ -444,7 +482,14 @@ void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x,
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
                       int it_host, int init, hipStream_t s, const double* lag = nullptr,
-                      unsigned* counter = nullptr);
+                      unsigned* counter = nullptr, const DiagFly* df = nullptr);
+// the single-reduction form's update (k_mg_update_cgs, tv_pcg.hip): s <- u + beta s,
+// p <- z + beta p, dx <- dx + a p, r <- r - a s, x0 <- omega dinv r (first: s = u,
+// p = z, dx = a p); lag: the all-reduced sums whose logic (lag_kind 6 / 7) this
+// launch forms and its last workgroup (counter) commits
+void launch_mg_update_cgs(int64_t n, const PcgState* st, const double* u, double* s, const double* z, double* p,
+                          double* dx, double* r, const double* dinv, double omega, double* x0, bool first,
+                          const double* lag, int lag_kind, unsigned* counter, hipStream_t stream);
 // the same post-smoothing fused into the level-0 J x march (k_cg_march POST)
 // plus a pass over the side-face nodes for the face-workgroup facet terms
 // (k_mg_post_faces, which runs the reduction tail); z <- x + omega dinv (r - J x),
@@ -481,7 +526,7 @@ void launch_newton_update(int64_t n, double* T, const double* dx, double* partia
                           const RedTail* tail = nullptr);
 // the post-solve group of a Newton iteration, gated on the solver state (runs
 // once, behind the batch that ends the solve): dx finish, T <- T - dx, ||dx||^2
-// into sums[0] (single partition)
+// into sums[0] (single partition); pA == nullptr: the single-reduction form (dx complete)
 void launch_post_group(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, double* T,
                        double* partials, double* sums, hipStream_t s);
 int pcg_vec_blocks(int64_t n);

@@ -106,7 +106,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     if (c->n_parts > 1) {
       if (int e = mg_prepare_dist(c, c->f[TV_F_T].ptr)) return e;
     } else {
-      mg_prepare(c, c->f[TV_F_T].ptr);
+      if (int e = mg_prepare(c, c->f[TV_F_T].ptr)) return e;
     }
     if (int e = mg_dg_weight(c, c->f[TV_F_T].ptr)) return e;
   }

@@ -478,67 +478,93 @@ __global__ __launch_bounds__(kBlock) void k_mg_ownmask(int64_t n, int64_t own0, 
 }
 
 // ---- DG1 level 0 <-> CG1 level 1 ------------------------------------------------------
-// vertex (i, j, k) of the box: the cell-local copies (a, b, c) of the cells
-// (i - a, j - b, k - c) that exist
-__global__ __launch_bounds__(kBlock) void k_mg_dg_restrict(int c0, int c1, int c2, const PcgState* __restrict__ st,
+// DG dof addressing of local cell layer k (DgGrid: a slab's owned layers
+// first, [l][owned cell]; its ghost layers after them, [l][cell of the layer])
+struct DgL {
+  int64_t base, stride;
+};
+__device__ __forceinline__ DgL dg_lay(const DgGrid& g, int k) {
+  const int64_t pc = (int64_t)g.c0 * g.c1;
+  if (k < g.k_begin) return {g.gofs[0], pc};
+  if (k >= g.k_end) return {g.gofs[1], pc};
+  return {(int64_t)(k - g.k_begin) * pc, g.own};
+}
+
+// vertex (i, j, K) of local vertex plane K in [v0, v1): the sum of the
+// cell-local copies (a, b, c) of the cells (i - a, j - b, K - c) whose layer
+// lies in [ck0, ck1) (a slab: its owned layers; the ranks' partial sums on the
+// shared vertex planes add up in the all-reduce of the replicated level), into
+// the CG vector at global vertex plane K + kg0; with xc the CG level's
+// pre-smoothing x = omega D^-1 b (one partition only: a partial sum is not b)
+__global__ __launch_bounds__(kBlock) void k_mg_dg_restrict(DgGrid g, const PcgState* __restrict__ st,
                                                            const double* __restrict__ bf,
                                                            const double* __restrict__ wf,
                                                            const double* __restrict__ mask, double* __restrict__ bc,
                                                            const double* __restrict__ dinv_c, double omega_c,
-                                                           double* __restrict__ xc) {
+                                                           double* __restrict__ xc, int v0, int v1, int ck0, int ck1,
+                                                           int kg0) {
   if (st != nullptr && st->done) return;
-  const int n0 = c0 + 1, n1 = c1 + 1, n2 = c2 + 1;
-  const int64_t nv = (int64_t)n0 * n1 * n2, ncell = (int64_t)c0 * c1 * c2;
+  const int c0 = g.c0, c1 = g.c1, n0 = c0 + 1, n1 = c1 + 1;
+  const int64_t nv = (int64_t)n0 * n1 * (v1 - v0);
   for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
-    const int i = (int)(v % n0), j = (int)((v / n0) % n1), k = (int)(v / ((int64_t)n0 * n1));
+    const int i = (int)(v % n0), j = (int)((v / n0) % n1), K = v0 + (int)(v / ((int64_t)n0 * n1));
     double acc = 0.0;
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = k - (l >> 2);
-      if (ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < 0 || ck >= c2) continue;
-      const int64_t f = (int64_t)l * ncell + ci + (int64_t)c0 * (cj + (int64_t)c1 * ck);
+      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = K - (l >> 2);
+      if (ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < ck0 || ck >= ck1) continue;
+      const DgL a = dg_lay(g, ck);
+      const int64_t f = a.base + (int64_t)l * a.stride + ci + (int64_t)c0 * cj;
       if (mask != nullptr && mask[f] == 0.0) continue;
       acc += bf[f] - wf[f];
     }
-    bc[v] = acc;
-    if (xc != nullptr) xc[v] = omega_c * dinv_c[v] * acc;
+    const int64_t o = i + (int64_t)n0 * (j + (int64_t)n1 * (K + kg0));
+    bc[o] = acc;
+    if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;
   }
 }
 
-// every cell-local copy takes its vertex value: x_dg(l, cell) += x_cg(vertex)
-__global__ __launch_bounds__(kBlock) void k_mg_dg_prolong(int c0, int c1, int c2, const PcgState* __restrict__ st,
+// every cell-local copy of the cells of local layers [ck0, ck1) takes its
+// vertex value: x_dg(l, cell) += x_cg(vertex), the CG vector at global planes
+// (a slab: its ghost layers too -- the replicated level holds every vertex)
+__global__ __launch_bounds__(kBlock) void k_mg_dg_prolong(DgGrid g, const PcgState* __restrict__ st,
                                                           double* __restrict__ xf, const double* __restrict__ xc,
-                                                          const double* __restrict__ mask) {
+                                                          const double* __restrict__ mask, int ck0, int ck1, int kg0) {
   if (st != nullptr && st->done) return;
-  const int n0 = c0 + 1, n1 = c1 + 1;
-  const int64_t ncell = (int64_t)c0 * c1 * c2;
+  const int c0 = g.c0, c1 = g.c1, n0 = c0 + 1, n1 = c1 + 1;
+  const int64_t pc = (int64_t)c0 * c1, ncell = pc * (ck1 - ck0);
   for (int64_t cell = blockIdx.x * (int64_t)kBlock + threadIdx.x; cell < ncell; cell += (int64_t)gridDim.x * kBlock) {
-    const int i = (int)(cell % c0), j = (int)((cell / c0) % c1), k = (int)(cell / ((int64_t)c0 * c1));
+    const int i = (int)(cell % c0), j = (int)((cell / c0) % c1), k = ck0 + (int)(cell / pc);
+    const DgL a = dg_lay(g, k);
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-      const int64_t v = (i + (l & 1)) + (int64_t)n0 * ((j + ((l >> 1) & 1)) + (int64_t)n1 * (k + (l >> 2)));
-      const int64_t f = (int64_t)l * ncell + cell;
+      const int64_t v = (i + (l & 1)) + (int64_t)n0 * ((j + ((l >> 1) & 1)) + (int64_t)n1 * (k + kg0 + (l >> 2)));
+      const int64_t f = a.base + (int64_t)l * a.stride + i + (int64_t)c0 * j;
       xf[f] = (mask != nullptr && mask[f] == 0.0) ? 0.0 : xf[f] + xc[v];
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_mg_dg_T(int c0, int c1, int c2, const double* __restrict__ Tdg,
-                                                    double* __restrict__ Tcg) {
-  const int n0 = c0 + 1, n1 = c1 + 1, n2 = c2 + 1;
-  const int64_t nv = (int64_t)n0 * n1 * n2, ncell = (int64_t)c0 * c1 * c2;
+// T of the CG level: the mean of the cell-local copies at each vertex of local
+// vertex planes [v0, v1) (over every local layer: a slab's ghost layers hold
+// the neighbours' T), at global vertex plane K + kg0
+__global__ __launch_bounds__(kBlock) void k_mg_dg_T(DgGrid g, const double* __restrict__ Tdg, double* __restrict__ Tcg,
+                                                    int v0, int v1, int kg0) {
+  const int c0 = g.c0, c1 = g.c1, c2 = g.c2, n0 = c0 + 1, n1 = c1 + 1;
+  const int64_t nv = (int64_t)n0 * n1 * (v1 - v0);
   for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
-    const int i = (int)(v % n0), j = (int)((v / n0) % n1), k = (int)(v / ((int64_t)n0 * n1));
+    const int i = (int)(v % n0), j = (int)((v / n0) % n1), K = v0 + (int)(v / ((int64_t)n0 * n1));
     double s = 0.0;
     int cnt = 0;
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = k - (l >> 2);
+      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = K - (l >> 2);
       if (ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < 0 || ck >= c2) continue;
-      s += Tdg[(int64_t)l * ncell + ci + (int64_t)c0 * (cj + (int64_t)c1 * ck)];
+      const DgL a = dg_lay(g, ck);
+      s += Tdg[a.base + (int64_t)l * a.stride + ci + (int64_t)c0 * cj];
       ++cnt;
     }
-    Tcg[v] = s / cnt;
+    Tcg[i + (int64_t)n0 * (j + (int64_t)n1 * (K + kg0))] = s / cnt;
   }
 }
 
@@ -677,23 +703,27 @@ void launch_mg_ownmask(int64_t n, int64_t own0, int64_t own1, const double* dinv
   hipLaunchKernelGGL(k_mg_ownmask, dim3(blocks_for(n)), dim3(kBlock), 0, s, n, own0, own1, dinv, mask);
 }
 
-void launch_mg_dg_restrict(int c0, int c1, int c2, const PcgState* st, const double* bf, const double* wf,
-                           const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
-                           hipStream_t s) {
-  const int64_t nv = (int64_t)(c0 + 1) * (c1 + 1) * (c2 + 1);
-  hipLaunchKernelGGL(k_mg_dg_restrict, dim3(blocks_for(nv)), dim3(kBlock), 0, s, c0, c1, c2, st, bf, wf, mask, bc,
-                     dinv_c, omega_c, xc);
+// the vertex planes of the CG level a DG slab writes (DgRange): one
+// partition -- every plane; a slab -- the planes of its owned layers (their
+// restriction, the shared planes as partial sums) or its owned vertex planes
+// (vertex plane K belongs to the owner of layer K, the last one to the last slab)
+void launch_mg_dg_restrict(const DgGrid& g, const PcgState* st, const double* bf, const double* wf, const double* mask,
+                           double* bc, const double* dinv_c, double omega_c, double* xc, int kg0, hipStream_t s) {
+  const int64_t nv = (int64_t)(g.c0 + 1) * (g.c1 + 1) * (g.k_end - g.k_begin + 1);
+  hipLaunchKernelGGL(k_mg_dg_restrict, dim3(blocks_for(nv)), dim3(kBlock), 0, s, g, st, bf, wf, mask, bc, dinv_c,
+                     omega_c, xc, g.k_begin, g.k_end + 1, g.k_begin, g.k_end, kg0);
 }
 
-void launch_mg_dg_prolong(int c0, int c1, int c2, const PcgState* st, double* xf, const double* xc, const double* mask,
-                          hipStream_t s) {
-  const int64_t nc = (int64_t)c0 * c1 * c2;
-  hipLaunchKernelGGL(k_mg_dg_prolong, dim3(blocks_for(nc)), dim3(kBlock), 0, s, c0, c1, c2, st, xf, xc, mask);
+void launch_mg_dg_prolong(const DgGrid& g, const PcgState* st, double* xf, const double* xc, const double* mask,
+                          int kg0, hipStream_t s) {
+  const int64_t nc = (int64_t)g.c0 * g.c1 * g.c2;
+  hipLaunchKernelGGL(k_mg_dg_prolong, dim3(blocks_for(nc)), dim3(kBlock), 0, s, g, st, xf, xc, mask, 0, g.c2, kg0);
 }
 
-void launch_mg_dg_T(int c0, int c1, int c2, const double* Tdg, double* Tcg, hipStream_t s) {
-  const int64_t nv = (int64_t)(c0 + 1) * (c1 + 1) * (c2 + 1);
-  hipLaunchKernelGGL(k_mg_dg_T, dim3(blocks_for(nv)), dim3(kBlock), 0, s, c0, c1, c2, Tdg, Tcg);
+void launch_mg_dg_T(const DgGrid& g, const double* Tdg, double* Tcg, int kg0, hipStream_t s) {
+  const int v1 = g.k_end + (g.gofs[1] < 0 ? 1 : 0);  // the top vertex plane: the last slab's
+  const int64_t nv = (int64_t)(g.c0 + 1) * (g.c1 + 1) * (v1 - g.k_begin);
+  hipLaunchKernelGGL(k_mg_dg_T, dim3(blocks_for(nv)), dim3(kBlock), 0, s, g, Tdg, Tcg, g.k_begin, v1, kg0);
 }
 
 int launch_mg_pow(int64_t n, const double* dinv, double* y, double* partials, hipStream_t s) {

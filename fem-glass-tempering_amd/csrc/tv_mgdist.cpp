@@ -66,6 +66,7 @@ struct LevelRef {
   const double* dinv;
   double omega;
   int64_t off, n_own;  // first owned local node, owned node count
+  int64_t woff, n_win;  // the write window (= owned, but on a deep-ghost fine slab)
 };
 
 LevelRef level_ref(Ctx* c, size_t l, const double* T0) {
@@ -91,6 +92,8 @@ LevelRef level_ref(Ctx* c, size_t l, const double* T0) {
   const int64_t plane = (int64_t)r.g->n0 * r.g->n1;
   r.off = plane * r.g->k_begin;
   r.n_own = plane * (r.g->k_end - r.g->k_begin);
+  r.woff = plane * r.g->w_begin;
+  r.n_win = plane * (r.g->w_end - r.g->w_begin);
   return r;
 }
 
@@ -176,10 +179,22 @@ int mg_setup_dist(Ctx* c) {
   c->mg_A = A;
   // local window of each level: [first2, first2 + n2) global planes of axis 2
   std::vector<int> first2(L), n2loc(L), own_lo(L), own_hi(L);
+  const int G0 = c->ghost_depth;  // level 0: kDeepGhosts planes per interface (deep ghosts), else 1
+  if (G0 > 1 && local) return c->fail(TV_ERR_ARG, "partitioned GMG: deep ghosts with LOCAL coupling (internal)");
+  // the single-reduction (Chronopoulos-Gear) form on a deep-ghost slab (pcg_variant
+  // AUTO): its matvec u = A z right after the V-cycle needs z one plane beyond
+  // the owned ones, so level 0's post-smoothing reads x two planes out and the
+  // prolongation into them reads level 1 two ghost planes deep
+  c->mg_cgs = G0 > 1 && c->O.pcg_variant == TV_PCG_AUTO;
+  auto gdep = [&](int l) { return l == 0 ? G0 : (l == 1 && c->mg_cgs) ? 2 : 1; };  // ghost planes of level l
+  // fine planes the prolongation into level l fills: within `need` planes of
+  // the owned ones (every local plane where the level has one ghost plane)
+  auto need = [&](int l) { return (l == 0 && c->mg_cgs) ? 2 : 1; };
   for (int l = 0; l < L; ++l) {
     owned_range(plan[l].owner, p, &own_lo[l], &own_hi[l]);
     if (l < A) {
-      const int glo = p > 0 ? 1 : 0, ghi = p < P - 1 ? 1 : 0;
+      const int gd = gdep(l);
+      const int glo = p > 0 ? gd : 0, ghi = p < P - 1 ? gd : 0;
       first2[l] = own_lo[l] - glo;
       n2loc[l] = own_hi[l] - own_lo[l] + glo + ghi;
     } else {
@@ -197,7 +212,7 @@ int mg_setup_dist(Ctx* c) {
     Lv.dist = l < A;
     Lv.first2 = first2[l];
     if (Lv.dist) {
-      const int glo = p > 0 ? 1 : 0, ghi = p < P - 1 ? 1 : 0;
+      const int glo = p > 0 ? gdep(l) : 0, ghi = p < P - 1 ? gdep(l) : 0;
       if (int e = build_cg_grid(c, 3, Lv.X, first2[l], n2loc[l], glo, ghi, p == 0, p == P - 1, Lv.g, Lv.coef,
                                 &Lv.bnodes, Lv.ffbuf))
         return e;
@@ -241,9 +256,19 @@ int mg_setup_dist(Ctx* c) {
         // weight 0 and point at an owned plane (finite data)
         const int cown0 = own_lo[l] - c0, cown1 = own_hi[l] - c0;
         const int fown0 = own_lo[l - 1] - f0, fown1 = own_hi[l - 1] - f0;
+        // deep ghosts: the prolongation fills the fine planes within need(l - 1)
+        // of the owned ones -- all the post-smoothing J x reads; the outer
+        // ghost planes keep x0 and take no weight
+        const int skip = (l - 1 < A) ? std::max(0, gdep(l - 1) - need(l - 1)) : 0;
+        const int fin0 = p > 0 ? skip : 0, fin1 = p < P - 1 ? nf - skip : nf;
         for (int lf = 0; lf < nf; ++lf)
           for (int e = 0; e < 2; ++e) {
             const int cg = pi[2 * (size_t)(f0 + lf) + e] - c0;  // coarse local
+            if (!local && (lf < fin0 || lf >= fin1)) {
+              piL[2 * (size_t)lf + e] = std::min(std::max(cg, 0), nc - 1);
+              pwL[2 * (size_t)lf + e] = 0.0;
+              continue;
+            }
             const bool ok = local ? (cg >= cown0 && cg < cown1 && lf >= fown0 && lf < fown1) : (cg >= 0 && cg < nc);
             if (local && !ok) {
               piL[2 * (size_t)lf + e] = std::min(std::max(cg, cown0), cown1 - 1);
@@ -288,15 +313,25 @@ int mg_setup_dist(Ctx* c) {
     // the owned ones, the ghost planes of a slab's V-cycle stay zero)
     x.f_kb = local ? own_lo[l - 1] - first2[l - 1] : 0;
     x.f_ke = local ? own_hi[l - 1] - first2[l - 1] : x.fn[2];
+    if (!local && l - 1 < A) {  // deep ghosts: within need(l - 1) planes of the owned fine planes
+      const int skip = std::max(0, gdep(l - 1) - need(l - 1));
+      x.f_kb = p > 0 ? skip : 0;
+      x.f_ke = p < P - 1 ? x.fn[2] - skip : x.fn[2];
+    }
     if (Lv.dist) {  // restriction: the owned coarse planes
       x.c_kb = Lv.g.k_begin;
       x.c_ke = Lv.g.k_end;
       x.aligned = 0;
     } else if (l == A) {
-      // restriction into the replicated level: every coarse plane this rank's
-      // owned fine planes reach (the masked partial sums of the ranks add up)
-      x.c_kb = reach_lo < reach_hi ? reach_lo : 0;
-      x.c_ke = reach_lo < reach_hi ? reach_hi : 0;
+      // restriction into the replicated level: every coarse plane -- the ones
+      // this rank's owned fine planes reach get its masked partial sums (which
+      // add up over the ranks), the others exact zeros (weight-0 entries), so
+      // the level vector needs no zero fill before it (a 4.7 us launch per
+      // V-cycle at the C4 / 8 share)
+      (void)reach_lo;
+      (void)reach_hi;
+      x.c_kb = 0;
+      x.c_ke = x.cn[2];
       x.aligned = 0;
     } else {
       x.c_kb = 0;
@@ -313,6 +348,10 @@ int mg_setup_dist(Ctx* c) {
     launch_mg_ownmask(nloc, r.off, r.off + r.n_own, nullptr, *m, c->stream);
     HIPC(hipGetLastError());
   }
+  if (c->mg_cgs) {  // s = A p of the single-reduction form
+    HIPC(hipMalloc(&c->mg_s, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT)));
+    HIPC(hipMemsetAsync(c->mg_s, 0, sizeof(double) * (size_t)std::max<int64_t>(1, c->nT), c->stream));
+  }
   c->mg_on = true;
   return TV_OK;
 }
@@ -322,6 +361,7 @@ int mg_setup_dist(Ctx* c) {
 // level: each rank injects its own planes into a zeroed vector, summed over
 // the ranks; below it, injected locally) and the Jacobi diagonals
 int mg_prepare_dist(Ctx* c, const double* T) {
+  if (c->mg_dg) return mg_prepare(c, T);  // a DG1 slab: level 1 onwards replicated (mg_setup)
   const double* Tf = T;
   for (size_t l = 1; l <= c->mg.size(); ++l) {
     MgLevel& L = c->mg[l - 1];
@@ -348,8 +388,8 @@ int mg_prepare_dist(Ctx* c, const double* T) {
 // z.r) records reduced into c->sums by the tail (kind 0: the all-reduce and
 // the KSPCG logic follow).  Returns a status.
 int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
-  if (c->amg_on) {  // partitioned unstructured mesh: the agglomerated algebraic cycle (tv_amg.cpp)
-    const int r = amg_apply0(c, tail);
+  if (c->amg_on || c->mg_dg) {  // the agglomerated algebraic cycle (tv_amg.cpp); a DG1 slab (tv_mgsolve.cpp)
+    const int r = c->amg_on ? amg_apply0(c, tail) : mg_apply0(c, T, tail);
     return r < 0 ? -r : TV_OK;
   }
   hipStream_t s = c->stream;
@@ -360,21 +400,27 @@ int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
   // the V-cycle's ghost exchanges (LOCAL coupling: none -- the slab's own cycle,
   // whose ghost planes hold zeros)
   auto vhalo = [&](const CgGrid& g, double* v) -> int { return c->mg_local ? TV_OK : halo_grid(c, g, v); };
+  // deep ghosts: level 0's x0 (the KSPCG update) and residual d0 are computed
+  // on the write window -- every ghost plane but the outermost -- from
+  // vectors that are valid there, so neither needs an exchange (two exchange
+  // points fewer per V-cycle); the closing group refreshes z's kDeepGhosts planes
+  const bool deep = c->ghost_depth > 1;
   // ---- down: distributed levels 0 .. A - 1
   for (size_t l = 0; l < ldown; ++l) {
     const LevelRef r = level_ref(c, l, T);
-    if (int e = vhalo(*r.g, r.x)) return e;  // ghosts of the pre-smoothed x_l
+    if (!(deep && l == 0))
+      if (int e = vhalo(*r.g, r.x)) return e;  // ghosts of the pre-smoothed x_l
     if (l + 1 == L) break;                           // the coarsest level, distributed: x_l is its solve
     launch_cg_japply_partial(*r.g, r.T, r.x, r.w, c->st, s);
-    FaceAdd fa = cg_face_add(*r.g, r.off);
+    FaceAdd fa = cg_face_add(*r.g, r.woff);
     MgLevel& C = c->mg[l];
     if (l + 1 < A) {  // into a distributed level: exchange the residual, restrict on the owned coarse planes
-      launch_mg_resid(r.n_own, c->st, r.b + r.off, r.w + r.off, &fa, l == 0 && dmask ? dmask + r.off : nullptr, s);
-      if (int e = vhalo(*r.g, r.w)) return e;
+      launch_mg_resid(r.n_win, c->st, r.b + r.woff, r.w + r.woff, &fa, l == 0 && dmask ? dmask + r.woff : nullptr, s);
+      if (!(deep && l == 0))
+        if (int e = vhalo(*r.g, r.w)) return e;
       launch_mg_restrict(C.xf, c->st, r.w, nullptr, nullptr, nullptr, C.b, C.dinv, C.omega, C.x, s);
     } else {  // into the replicated level A: masked partial restriction, summed over the ranks
       const double* mask = (l == 0) ? c->mg_mask0 : c->mg[l - 1].mask;
-      HIPC(hipMemsetAsync(C.b, 0, sizeof(double) * (size_t)C.n, s));
       const FaceAdd fa0 = cg_face_add(*r.g, 0);
       launch_mg_restrict(C.xf, c->st, r.b, r.w, &fa0, mask, C.b, nullptr, 0.0, nullptr, s);
       if (int e = allreduce_vec(c, C.b, C.n)) return e;
@@ -419,8 +465,27 @@ namespace {
 // launch: the beta / convergence logic of the previous iteration's closing
 // group inside this iteration's fused matvec (lag3), the alpha logic inside
 // the update.  Every rank forms the same state from the same all-reduced sums.
+}  // namespace
+
+// the level-0 nodes a partition's pointwise V-cycle kernels cover: the owned
+// ones, or on a deep-ghost slab the write window (every ghost plane but the
+// outermost: x0 = omega D^-1 r is needed there, so J x0 is right one plane out)
+void fine_window(const Ctx* c, int64_t* off, int64_t* n) {
+  if (c->um || c->fam_T != TV_CG) {
+    *off = c->ownT_off;
+    *n = c->ownT_n;
+    return;
+  }
+  const int64_t plane = (int64_t)c->cg.n0 * c->cg.n1;
+  *off = plane * c->cg.w_begin;
+  *n = plane * (c->cg.w_end - c->cg.w_begin);
+}
+
+namespace {
+
 int mg_iteration_dist(Ctx* c, const double* T, int it, bool fold, bool lag3) {
-  const int64_t off = c->ownT_off, n = c->ownT_n;
+  int64_t off, n;
+  fine_window(c, &off, &n);
   const int slot = c->ts_next + it;
   uint64_t* ts = (c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
   RedTail t1{c->counters, c->partials, c->sums, c->st, 0, ts};
@@ -438,18 +503,116 @@ int mg_iteration_dist(Ctx* c, const double* T, int it, bool fold, bool lag3) {
     if (fold) lag2 = true;
     else launch_logic(c->st, c->sums, 2, c->stream);  // alpha
   }
-  const FaceAdd fa = c->um ? FaceAdd{} : cg_face_add(c->cg, off);  // unstructured: w is complete
-  launch_mg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, &fa, c->dinv + off, c->mg_omega0, c->r + off,
-                   c->f[TV_F_DX].ptr + off, c->mgx + off, it, 0, c->stream, lag2 ? c->sums : nullptr,
-                   lag2 ? c->counters + kUpdateCounter : nullptr);
+  if (c->dggface) {  // a DG1 slab: the cell-block update (the alpha logic ran above: no fold on DG)
+    launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it,
+                      0, c->stream);
+  } else {
+    const FaceAdd fa = c->um ? FaceAdd{} : cg_face_add(c->cg, off);  // unstructured: w is complete
+    const DiagFly df = c->um ? DiagFly{} : cg_diag_fly(c->cg, off);
+    launch_mg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, &fa, c->dinv + off, c->mg_omega0, c->r + off,
+                     c->f[TV_F_DX].ptr + off, c->mgx + off, it, 0, c->stream, lag2 ? c->sums : nullptr,
+                     lag2 ? c->counters + kUpdateCounter : nullptr, &df);
+  }
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};
   return mg_apply0_dist(c, T, &t2);
 }
 
 }  // namespace
 
-int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post) {
+// The single-reduction (Chronopoulos-Gear) form of the GMG-preconditioned CG
+// on deep-ghost slabs (c->mg_cgs): per iteration the update (k_mg_update_cgs:
+// the scalars from the lagged all-reduced sums, s, p, dx, r, x0), the V-cycle
+// (z = M r with z.z, z.r), the matvec u = A z (with z.u) and ONE RCCL group --
+// the all-reduce of the three sums and the ghost planes of u.  Exchange points
+// per iteration: that group and the V-cycle's level-1 ghosts (pre / post) and
+// the replicated level's all-reduce: 4, against 7 for KSPCG with one ghost
+// plane.  Same iterates as KSPCG in exact arithmetic
+// (PETSc KSPCG's tests on ||z|| and (z, r), iteration counts alike).
+static int pcg_solve_mg_dist_cgs(Ctx* c, const double* T, int* its, int* reason, bool post) {
   const int64_t off = c->ownT_off, n = c->ownT_n;
+  int64_t woff, nwin;
+  fine_window(c, &woff, &nwin);
+  const PcgState h = pcg_state_init(c);
+  c->h_st[2] = h;
+  launch_set_state(c->st, h, c->stream);
+  if (int e = mg_prepare_dist(c, T)) return e;
+  if (c->dir_on)
+    if (int e = halo(c, c->dinv)) return e;
+  if (c->mg_mask0) launch_mg_ownmask(c->nT, off, off + n, c->dir_on ? c->dinv : nullptr, c->mg_mask0, c->stream);
+  launch_mg_update(nwin, c->st, c->pA + woff, c->pB + woff, c->w + woff, nullptr, c->dinv + woff, c->mg_omega0,
+                   c->r + woff, c->f[TV_F_DX].ptr + woff, c->mgx + woff, 0, 1, c->stream);  // x0 <- omega dinv r
+  double* u = c->w;  // A z, completed on the ghost planes by the closing group
+  int pending = 0;   // logic kind of the last closing group still to run (inside the next update)
+  // V-cycle (z, z.z, z.r -> sums[0..1]), u = A z (z.u -> sums[2]), the closing group
+  auto half = [&](int it) -> int {
+    RedTail tz{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};
+    if (int e = mg_apply0_dist(c, T, &tz)) return e;
+    const int slot = c->ts_next + it;
+    uint64_t* ts = (it >= 0 && c->ktime && (it % c->kstride) == 0 && slot < kTsCap) ? c->d_ts + 4 * slot : nullptr;
+    RedTail tu{c->counters, c->partials, c->sums + 2, c->st, 0, ts};
+    if (!launch_cg_japply_tail(c->cg, T, c->z, u, c->st, c->partials, &tu, c->stream))
+      return c->fail(TV_ERR_STATE, "single-reduction GMG needs the marching matvec (internal)");
+    if (int e = allreduce_halo(c, c->sums, 3, u)) return e;
+    pending = it < 0 ? 7 : 6;
+    return TV_OK;
+  };
+  if (int e = half(-1)) return e;  // iteration 0's z, u and sums
+  if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
+    if (int e = ts_flush(c)) return e;
+  int launched = 0;
+  auto enqueue = [&](int nb) -> int {
+    for (int b = 0; b < nb; ++b) {
+      const int it = launched + b;
+      launch_mg_update_cgs(nwin, c->st, u + woff, c->mg_s + woff, c->z + woff, c->pA + woff, c->f[TV_F_DX].ptr + woff,
+                           c->r + woff, c->dinv + woff, c->mg_omega0, c->mgx + woff, it == 0,
+                           pending ? c->sums : nullptr, pending, c->counters + kUpdateCounter, c->stream);
+      pending = 0;
+      if (int e = half(it)) return e;
+    }
+    launched += nb;
+    if (pending) {  // the host polls the state: the last group's logic as a launch of its own
+      launch_logic(c->st, c->sums, pending, c->stream);
+      pending = 0;
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    HIPC(hipEventRecord(c->evp[0], c->stream));
+    if (post) {  // dx is complete (the updates apply it); the group zeroes it after a 0-iteration solve
+      double* nrm = c->sums + 6;
+      launch_post_group(n, c->st, nullptr, nullptr, c->f[TV_F_DX].ptr + off, c->f[TV_F_T].ptr + off, c->partials, nrm,
+                        c->stream);
+      if (int e = allreduce(c, nrm, 1)) return e;
+      HIPC(hipMemcpyAsync(c->h_sums, nrm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPC(hipEventRecord(c->evn, c->stream));
+    }
+    return TV_OK;
+  };
+  const int hk = std::min(c->newton_k, 15);
+  if (int e = enqueue(std::max(1, c->mg_hint[hk] > 0 ? c->mg_hint[hk] : c->pcg_hint))) return e;
+  for (;;) {
+    HIPC(hipEventSynchronize(c->evp[0]));
+    if (c->h_st[0].done) break;
+    if (launched > c->O.ksp_max_it + 2) return c->fail(TV_ERR_KSP, "PCG: iteration guard exceeded");
+    if (int e = enqueue(1)) return e;
+  }
+  *its = c->h_st[0].it;
+  *reason = c->h_st[0].reason;
+  if (!post && *its == 0) launch_fill(c->f[TV_F_DX].ptr + off, n, 0.0, c->stream);
+  c->pcg_hint = std::max(1, c->h_st[0].it);
+  c->mg_hint[hk] = c->pcg_hint;
+  if (c->ktime) {
+    for (int it = 0; it < *its; it += c->kstride)
+      if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
+    c->ts_next = std::min(kTsCap, c->ts_next + launched);
+  }
+  return TV_OK;
+}
+
+int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post) {
+  if (c->mg_cgs) return pcg_solve_mg_dist_cgs(c, T, its, reason, post);
+  const int64_t off = c->ownT_off, n = c->ownT_n;
+  int64_t woff, nwin;
+  fine_window(c, &woff, &nwin);
   const PcgState h = pcg_state_init(c);
   c->h_st[2] = h;
   launch_set_state(c->st, h, c->stream);
@@ -462,8 +625,14 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post)
     if (int e = halo(c, c->dinv)) return e;
   if (c->mg_mask0)  // level 0's restriction mask: owned nodes, Dirichlet rows out
     launch_mg_ownmask(c->nT, off, off + n, c->dir_on ? c->dinv : nullptr, c->mg_mask0, c->stream);
-  launch_mg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, nullptr, c->dinv + off, c->mg_omega0, c->r + off,
-                   c->f[TV_F_DX].ptr + off, c->mgx + off, 0, 1, c->stream);  // x0 <- omega dinv r
+  if (c->dggface) {  // a DG1 slab: x0 <- omega B^-1 r over the owned cells
+    if (int e = mg_dg_weight(c, T)) return e;
+    launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
+                      c->stream);
+  } else {
+    launch_mg_update(nwin, c->st, c->pA + woff, c->pB + woff, c->w + woff, nullptr, c->dinv + woff, c->mg_omega0,
+                     c->r + woff, c->f[TV_F_DX].ptr + woff, c->mgx + woff, 0, 1, c->stream);  // x0 <- omega dinv r
+  }
   // the three collectives of an iteration close it: the (z.z, z.r) all-reduce
   // + KSPCG logic, and the ghost planes of z for the next fused matvec
   // the lagged logic needs the box march's fused matvec (not the unstructured

@@ -223,7 +223,14 @@ int mg_setup(Ctx* c) {
   if (c->dim != 3 || c->um || (!dg && !cg_cgs_supported(c->cg)) || (dg && (c->dg.deg1 || c->dg.deg2)))
     return c->fail(TV_ERR_ARG, "preconditioner GMG: 3D CG1 or DG1 temperature space on a rectilinear mesh only");
   if (c->cgs) return c->fail(TV_ERR_ARG, "preconditioner GMG runs in the KSPCG form (pcg_variant KSPCG or AUTO)");
-  if (c->n_parts > 1) return mg_setup_dist(c);  // slab-partitioned box (tv_mgdist.cpp)
+  if (c->n_parts > 1 && !dg) return mg_setup_dist(c);  // slab-partitioned CG1 box (tv_mgdist.cpp)
+  // a DG1 box, one partition or slab-partitioned: level 1 is the CG1 space of
+  // the WHOLE box (the global coordinates), and it and every coarser level are
+  // replicated on every slab (mg_A = 1): a slab restricts its owned cells into
+  // the vertex planes they touch, one all-reduce of the level-1 vector sums the
+  // shared planes, every slab runs the CG cycle below and prolongs into all its
+  // local cells (ghost layers included: the level holds every vertex)
+  if (c->n_parts > 1) c->mg_A = 1;
   std::vector<double> tmp, Xf[3];
   for (int s = 0; s < 3; ++s) Xf[s] = storage_coords(c, s, tmp);
   const double da = c->P.dt * c->P.alpha;
@@ -281,8 +288,20 @@ int mg_setup(Ctx* c) {
 // per Newton iteration: T injected down the hierarchy (DG: the vertex mean of
 // the cell-local values onto the CG level), coarse Jacobi diagonals
 
-void mg_prepare(Ctx* c, const double* T) {
-  if (c->amg_on) return;  // the algebraic hierarchy is T-independent (tv_amg.cpp)
+int mg_prepare(Ctx* c, const double* T) {
+  if (c->amg_on) return TV_OK;  // the algebraic hierarchy is T-independent (tv_amg.cpp)
+  // a DG1 slab: level 1's T = the vertex means on its owned vertex planes,
+  // summed over the slabs into the replicated vector (each plane from one slab)
+  const bool dgpart = c->mg_dg && c->n_parts > 1;
+  auto dg_T = [&](MgLevel& L) -> int {
+    if (!dgpart) {
+      launch_mg_dg_T(c->dg, T, L.T, 0, c->stream);
+      return TV_OK;
+    }
+    HIPC(hipMemsetAsync(L.T, 0, sizeof(double) * (size_t)L.n, c->stream));
+    launch_mg_dg_T(c->dg, T, L.T, c->plane_begin - c->dg.k_begin, c->stream);
+    return allreduce_vec(c, L.T, L.n);
+  };
   // after the first call (dinv interiors in place): the CG levels below the
   // base in two launches (launch_mg_prepare)
   const size_t base = c->mg_dg ? 1 : 0;  // DG: level 1 is the vertex mean of the DG field
@@ -293,7 +312,7 @@ void mg_prepare(Ctx* c, const double* T) {
   if (ready) {
     if (base == 1) {
       MgLevel& L = c->mg[0];
-      launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+      if (int e = dg_T(L)) return e;
       if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
       launch_cg_diag(L.g, L.T, L.dinv, 1, c->stream, true);
     }
@@ -310,13 +329,13 @@ void mg_prepare(Ctx* c, const double* T) {
       p.off_b[i + 1] = p.off_b[i] + (L.g.n_bnodes + 63) / 64 * 64;
     }
     launch_mg_prepare(p, c->stream);
-    return;
+    return TV_OK;
   }
   const double* Tf = T;
   for (size_t l = 0; l < c->mg.size(); ++l) {
     MgLevel& L = c->mg[l];
     if (l == 0 && c->mg_dg) {
-      launch_mg_dg_T(c->dg.c0, c->dg.c1, c->dg.c2, T, L.T, c->stream);
+      if (int e = dg_T(L)) return e;
       if (c->dggface) launch_dg_gface(c->dg, T, c->dggface, c->stream);
     }
     else launch_mg_inject(L.xf, Tf, L.T, c->stream);
@@ -324,6 +343,7 @@ void mg_prepare(Ctx* c, const double* T) {
     L.dinv_interior = true;
     Tf = L.T;
   }
+  return TV_OK;
 }
 
 // V-cycle on coarse level l >= 1 (index l - 1 in c->mg): rhs b -> x; the
@@ -379,10 +399,23 @@ int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
   if (c->mg_dg) {  // DG1 level 0: complete DG J x (Robin facets inline), vertex sums / injection to CG1
     const DgGrid& d = c->dg;
     MgLevel& C = c->mg[0];
-    launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
-    launch_mg_dg_restrict(d.c0, d.c1, d.c2, c->st, c->r, c->w, mask, C.b, C.dinv, C.omega, C.x, s);
-    mg_level(c, 1);
-    launch_mg_dg_prolong(d.c0, d.c1, d.c2, c->st, c->mgx, C.x, mask, s);
+    if (c->n_parts > 1) {  // a slab (mg_setup): the replicated level 1, see there
+      const int kg0 = c->plane_begin - d.k_begin;
+      if (int e = halo(c, c->mgx)) return -e;  // x0 of the ghost layers (J x0, the prolongation into them)
+      launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+      if (hipMemsetAsync(C.b, 0, sizeof(double) * (size_t)C.n, s) != hipSuccess)
+        return -c->fail(TV_ERR_HIP, "GMG: level-1 memset");
+      launch_mg_dg_restrict(d, c->st, c->r, c->w, mask, C.b, nullptr, 0.0, nullptr, kg0, s);
+      if (int e = allreduce_vec(c, C.b, C.n)) return -e;
+      launch_mg_jacobi(C.n, c->st, C.b, nullptr, nullptr, C.dinv, C.omega, C.x, 0, s);  // pre-smoothing from 0
+      mg_level(c, 1);
+      launch_mg_dg_prolong(d, c->st, c->mgx, C.x, mask, kg0, s);
+    } else {
+      launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
+      launch_mg_dg_restrict(d, c->st, c->r, c->w, mask, C.b, C.dinv, C.omega, C.x, 0, s);
+      mg_level(c, 1);
+      launch_mg_dg_prolong(d, c->st, c->mgx, C.x, mask, 0, s);
+    }
     launch_dg_japply(d, T, c->mgx, c->w, nullptr, nullptr, s, c->st);
     if (c->dggface)
       return launch_dg_bpost(d, c->st, c->mgx, c->r, c->w, c->dggface, c->mg_omega0, c->z, c->partials, tail, s);
@@ -426,9 +459,11 @@ int mg_iteration(Ctx* c, const double* T, int it) {
   if (c->dggface)
     launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
                       c->stream);
-  else
+  else {
+    const DiagFly df = c->um ? DiagFly{} : cg_diag_fly(c->cg, 0);  // D^-1 off the boundary from the axis tables
     launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
-                     c->stream);
+                     c->stream, nullptr, nullptr, &df);
+  }
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 3, nullptr};
   mg_apply0(c, T, &t2);  // z <- V(r); z.z, z.r; beta, convergence
   return TV_OK;
@@ -441,14 +476,16 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
   launch_set_state(c->st, h, c->stream);
-  mg_prepare(c, T);
+  if (int e = mg_prepare(c, T)) return e;
   if (int e = mg_dg_weight(c, T)) return e;
   if (c->dggface)
     launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
                       c->stream);  // dx <- 0, x0 <- omega B^-1 r
-  else
+  else {
+    const DiagFly df = c->um ? DiagFly{} : cg_diag_fly(c->cg, 0);
     launch_mg_update(n, c->st, c->pA, c->pB, c->w, nullptr, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
-                     c->stream);  // dx <- 0, x0 <- omega dinv r
+                     c->stream, nullptr, nullptr, &df);  // x0 <- omega dinv r
+  }
   RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 1, nullptr};
   mg_apply0(c, T, &t0);  // z <- V(r); dp, beta (KSPCG init)
   if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)
@@ -525,7 +562,11 @@ static int precond_apply_part(Ctx* c, const double* r_dev, double* z_dev) {
       if (int e = halo(c, c->dinv)) return e;
     if (c->mg_mask0) launch_mg_ownmask(c->nT, off, off + n, c->dir_on ? c->dinv : nullptr, c->mg_mask0, s);
     HIPC(hipMemcpyAsync(c->r + off, r_dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
-    launch_mg_jacobi(n, c->st, c->r + off, nullptr, nullptr, c->dinv + off, c->mg_omega0, c->mgx + off, 0, s);
+    int64_t woff, nwin;  // deep ghosts: r on the ghost planes, x0 on the write window
+    fine_window(c, &woff, &nwin);
+    if (c->ghost_depth > 1)
+      if (int e = halo(c, c->r)) return e;
+    launch_mg_jacobi(nwin, c->st, c->r + woff, nullptr, nullptr, c->dinv + woff, c->mg_omega0, c->mgx + woff, 0, s);
     if (int e = mg_apply0_dist(c, T, nullptr)) return e;
     HIPC(hipMemcpyAsync(z_dev, c->z + off, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
   }
@@ -565,7 +606,7 @@ int tv_precond_apply(void* ctx, const double* r_dev, double* z_dev) {
   } else {
     PcgState h{};  // running state: the V-cycle's kernels skip work once a solve is done
     HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, s));
-    mg_prepare(c, T);
+    if (int e = mg_prepare(c, T)) return e;
     HIPC(hipMemcpyAsync(c->r, r_dev, sizeof(double) * (size_t)n, hipMemcpyDeviceToDevice, s));
     if (c->dggface)  // x0 = omega0 B^-1 r (cell blocks)
       launch_dg_bsmooth(c->dg, c->st, c->r, nullptr, c->dggface, c->mg_omega0, c->mgx, 0, s);

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
                                                       const double* __restrict__ dinv, double omega,
                                                       double* __restrict__ r, double* __restrict__ dx,
                                                       double* __restrict__ x0, int it_host, const double* lag,
-                                                      unsigned* counter, PcgState* st_w) {
+                                                      unsigned* counter, PcgState* st_w, DiagFly df) {
   double a = 0.0, ap = 0.0;
   if (!INIT && lag != nullptr) {
     const PcgState ls = lagged_state(st, lag, 2);
@@ -178,10 +178,11 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
   }
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
   const double* __restrict__ pp = (it_host & 1) ? pA : pB;
-  // v = {r, w, dinv, dx, p_prev, p}
+  // v = {r, w, dinv, dx, p_prev, p}; D^-1 formed on the fly off the physical
+  // boundary (DiagFly: 8 B per node fewer, 40 -> 32 / 72 -> 64 B)
   auto load = [&](int64_t q, double (&v)[6]) {
     v[0] = r[q];
-    v[2] = ldc<true>(&dinv[q]);
+    v[2] = df.on ? dinv_fly(df, dinv, q) : ldc<true>(&dinv[q]);
     if (!INIT) v[1] = ldc<true>(&w[q]);
     if (DXU) {
       v[3] = FIRST ? 0.0 : ldc<true>(&dx[q]);
@@ -221,6 +222,72 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
     const PcgState ls = lagged_state(st, lag, 2);  // formed again (see lagged_state)
     *st_w = ls;
   }
+}
+
+// The single-reduction (Chronopoulos-Gear) form of the multigrid-preconditioned
+// CG on a deep-ghost slab (tv_mgdist.cpp): after the V-cycle (z = M r, z.z and
+// z.r) and the matvec (u = A z complete, z.u) ONE all-reduce of the three sums
+// closes an iteration, and this launch forms the scalars from them (lagged
+// kind 6, or 7 at iteration 0) and applies
+//   s <- u + beta s,  p <- z + beta p,  dx <- dx + a p,  r <- r - a s,
+//   x0 <- omega dinv r  (the next V-cycle's pre-smoothing from 0)
+// FIRST (iteration 0): s = u, p = z, dx = a p.  96 B per node.  Runs over the
+// write window (r, s and x0 are needed on the ghost planes; p and dx are only
+// read on the owned ones).
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_mg_update_cgs(int64_t n, const PcgState* __restrict__ st,
+                                                          const double* __restrict__ u, double* __restrict__ s,
+                                                          const double* __restrict__ z, double* __restrict__ p,
+                                                          double* __restrict__ dx, double* __restrict__ r,
+                                                          const double* __restrict__ dinv, double omega,
+                                                          double* __restrict__ x0, const double* lag, int lag_kind,
+                                                          unsigned* counter, PcgState* st_w) {
+  double a, beta;
+  if (lag != nullptr) {
+    const PcgState ls = lagged_state(st, lag, lag_kind);
+    if (ls.done) { commit_done(st_w, ls); return; }
+    a = ls.a;
+    beta = ls.beta;
+  } else {
+    if (st->done) return;
+    a = st->a;
+    beta = st->beta;
+  }
+  constexpr int U = 2;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x;
+  auto node = [&](int64_t q, const double (&v)[7]) {  // v = {u, s, z, p, dx, r, dinv}
+    const double sn = FIRST ? v[0] : v[0] + beta * v[1];
+    const double pn = FIRST ? v[2] : v[2] + beta * v[3];
+    const double rn = v[5] - a * sn;
+    s[q] = sn;
+    p[q] = pn;
+    __builtin_nontemporal_store(FIRST ? a * pn : v[4] + a * pn, &dx[q]);
+    r[q] = rn;
+    x0[q] = omega * v[6] * rn;
+  };
+  auto load = [&](int64_t q, double (&v)[7]) {
+    v[0] = __builtin_nontemporal_load(&u[q]);
+    v[1] = FIRST ? 0.0 : s[q];
+    v[2] = __builtin_nontemporal_load(&z[q]);
+    v[3] = FIRST ? 0.0 : p[q];
+    v[4] = FIRST ? 0.0 : __builtin_nontemporal_load(&dx[q]);
+    v[5] = r[q];
+    v[6] = __builtin_nontemporal_load(&dinv[q]);
+  };
+  for (; t + (U - 1) * stride < n; t += U * stride) {
+    double v[U][7];
+#pragma unroll
+    for (int k = 0; k < U; ++k) load(t + k * stride, v[k]);
+#pragma unroll
+    for (int k = 0; k < U; ++k) node(t + k * stride, v[k]);
+  }
+  for (; t < n; t += stride) {
+    double v[7];
+    load(t, v);
+    node(t, v);
+  }
+  if (lag != nullptr && last_block_arrived(counter, gridDim.x) && threadIdx.x == 0) *st_w = lagged_state(st, lag, lag_kind);
 }
 
 // post-smoothing of level 0: z <- x0 + omega dinv (r - w), w = J x0; (z.z,
@@ -265,7 +332,9 @@ __device__ __forceinline__ bool post_gate(const PcgState* st) {
   return st->done && !st->post && good;
 }
 
-// dx after the solve, from the device's iteration count (launch_mg_dx_finish)
+// dx after the solve, from the device's iteration count (launch_mg_dx_finish);
+// pA == nullptr: the single-reduction form, whose updates keep dx complete --
+// only a solve that converged at its start (0 iterations) leaves dx to zero
 __global__ __launch_bounds__(kBlock) void k_dx_finish_gated(int64_t n, const PcgState* __restrict__ st,
                                                             const double* __restrict__ pA,
                                                             const double* __restrict__ pB, double* __restrict__ dx) {
@@ -273,7 +342,10 @@ __global__ __launch_bounds__(kBlock) void k_dx_finish_gated(int64_t n, const Pcg
   const int its = st->it;
   const double a = st->a;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  if (its <= 1) {
+  if (pA == nullptr) {
+    if (its == 0)
+      for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] = 0.0;
+  } else if (its <= 1) {
     for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] = its == 0 ? 0.0 : a * pA[t];
   } else if (its & 1) {
     const double* __restrict__ p = ((its - 1) & 1) ? pB : pA;
@@ -365,14 +437,16 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
-                      int it_host, int init, hipStream_t s, const double* lag, unsigned* counter) {
+                      int it_host, int init, hipStream_t s, const double* lag, unsigned* counter,
+                      const DiagFly* dfp) {
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
+  const DiagFly df = dfp ? *dfp : DiagFly{};
   const dim3 g(vec_blocks(n)), b(kBlock);
   const bool odd = (it_host & 1) != 0;
   const bool first = it_host == 1;
 #define TV_MGU(F, I, D, FI) \
   hipLaunchKernelGGL((k_mg_update<F, I, D, FI>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host, \
-                     lag, counter, const_cast<PcgState*>(st))
+                     lag, counter, const_cast<PcgState*>(st), df)
   if (init) TV_MGU(false, true, false, false);
   else if (f.on) {
     if (first) TV_MGU(true, false, true, true);
@@ -397,6 +471,19 @@ int launch_mg_post(int64_t n, const PcgState* st, const double* x0, const double
   else
     hipLaunchKernelGGL(k_mg_post<false>, dim3(nb), dim3(kBlock), 0, s, n, st, x0, r, w, f, dinv, omega, z, partials, rt);
   return nb;
+}
+
+void launch_mg_update_cgs(int64_t n, const PcgState* st, const double* u, double* s, const double* z, double* p,
+                          double* dx, double* r, const double* dinv, double omega, double* x0, bool first,
+                          const double* lag, int lag_kind, unsigned* counter, hipStream_t stream) {
+  const dim3 g(vec_blocks(n)), b(kBlock);
+  PcgState* stw = const_cast<PcgState*>(st);
+  if (first)
+    hipLaunchKernelGGL(k_mg_update_cgs<true>, g, b, 0, stream, n, st, u, s, z, p, dx, r, dinv, omega, x0, lag, lag_kind,
+                       counter, stw);
+  else
+    hipLaunchKernelGGL(k_mg_update_cgs<false>, g, b, 0, stream, n, st, u, s, z, p, dx, r, dinv, omega, x0, lag, lag_kind,
+                       counter, stw);
 }
 
 void launch_pcg_update(int64_t n, PcgState* st, const double* pA, const double* pB, const double* w,

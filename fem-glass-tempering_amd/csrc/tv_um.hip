@@ -390,6 +390,18 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
         acc += __builtin_nontemporal_load(&ms[64 * k]) * (xc - up[c]);
         acc2 += __builtin_nontemporal_load(&ks[64 * k]) * xc;
       }
+    } else if (MODE != UM_DIAG && g.V27 != nullptr) {
+      // structured topology: the 27 slots in column order (the SELL row's sorted
+      // columns, absent neighbours as zeros: the same sum, term by term)
+      if (r < g.nv) {
+        const double* __restrict__ vs = g.V27 + r;
+#pragma unroll
+        for (int q = 0; q < 27; ++q) {
+          const int64_t o = (int64_t)(q % 3 - 1) + g.s1 * ((q / 3) % 3 - 1) + g.s2 * (q / 9 - 1);
+          const int64_t c = r + o < 0 ? 0 : (r + o >= g.nv ? g.nv - 1 : r + o);
+          acc += __builtin_nontemporal_load(&vs[(int64_t)q * g.nv]) * u[c];
+        }
+      }
     } else if (MODE != UM_DIAG) {
       const double* __restrict__ vs = g.V + so + lane;
       // U entries in flight per lane and round, the last round masked (27
@@ -514,6 +526,52 @@ int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, do
   const double* p = (it_host & 1) ? pB : pA;
   launch_rows<UM_FUSED>(g, T, p, nullptr, w, st, partials, rt, 0, s);
   return row_blocks(g);
+}
+
+// SELL rows -> the 27 stencil slots of a structured-topology mesh (V27 zeroed
+// first; a row's padding entries -- column r, value 0 -- add 0 to its centre)
+__global__ __launch_bounds__(kBlock) void k_um_to_stencil(int64_t nrow, const int64_t* __restrict__ soff,
+                                                          const int* __restrict__ cols, const double* __restrict__ V,
+                                                          int64_t s1, int64_t s2, int64_t nv, double* __restrict__ V27) {
+  for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < nrow; r += (int64_t)gridDim.x * kBlock) {
+    const int64_t sl = r >> 6, lane = r & 63, so = soff[sl];
+    const int wdt = (int)((soff[sl + 1] - so) >> 6);
+    for (int k = 0; k < wdt; ++k) {
+      const int64_t e = so + 64 * k + lane;
+      const int64_t off = (int64_t)cols[e] - r;
+      const int64_t dk = (off + s2 / 2 + s2) / s2 - 1;  // |di + s1 dj| < s2 / 2
+      const int64_t rem = off - dk * s2;
+      const int64_t dj = (rem + s1 / 2 + s1) / s1 - 1;  // |di| < s1 / 2
+      const int64_t di = rem - dj * s1;
+      const int q = (int)((di + 1) + 3 * (dj + 1) + 9 * (dk + 1));
+      V27[(int64_t)q * nv + r] += V[e];
+    }
+  }
+}
+
+// A hexahedral mesh whose vertex and cell numbering is a box's: vertex v = i +
+// N0 (j + N1 k), every cell the box cell of its first vertex in the tensor
+// order l = a + 2b + 4c (from_rectilinear, a jittered / warped plate, an
+// extruded gmsh mesh).  The coordinates can be anything.
+static bool structured_topology(int dim, int64_t nv, int64_t nc, const int64_t* cells, int64_t* s1, int64_t* s2) {
+  if (dim != 3 || nc < 1) return false;
+  const int64_t N0 = cells[2] - cells[0], P = cells[4] - cells[0];
+  if (cells[1] - cells[0] != 1 || N0 < 3 || P < 3 * N0 || P % N0 != 0 || nv % P != 0) return false;
+  const int64_t N1 = P / N0, N2 = nv / P;
+  if (N2 < 2 || nc != (N0 - 1) * (N1 - 1) * (N2 - 1)) return false;
+  std::vector<char> seen((size_t)nv, 0);
+  for (int64_t e = 0; e < nc; ++e) {
+    const int64_t b = cells[e * 8];
+    if (b < 0 || b >= nv) return false;
+    const int64_t i = b % N0, j = (b / N0) % N1, k = b / P;
+    if (i >= N0 - 1 || j >= N1 - 1 || k >= N2 - 1 || seen[(size_t)b]) return false;
+    seen[(size_t)b] = 1;
+    for (int l = 1; l < 8; ++l)
+      if (cells[e * 8 + l] != b + (l & 1) + N0 * ((l >> 1) & 1) + P * (l >> 2)) return false;
+  }
+  *s1 = N0;
+  *s2 = P;
+  return true;
 }
 
 // ---- host: mesh analysis and device setup ----------------------------------------
@@ -776,6 +834,15 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
                                Xd[2], fv_d, fw);
   }
   UMC(hipGetLastError());
+  // structured topology on one partition: J x from the 27 stencil slots
+  int64_t ss1 = 0, ss2 = 0;
+  double* V27 = nullptr;
+  if (nrow == nv && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
+    if (um_alloc(d, (size_t)27 * nv, &V27, err)) return 1;
+    UMC(hipMemsetAsync(V27, 0, sizeof(double) * 27 * (size_t)nv, s));
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V27);
+    UMC(hipGetLastError());
+  }
   UMC(hipStreamSynchronize(s));
   // setup-only arrays
   for (void* p : {(void*)Xd[0], (void*)Xd[1], (void*)Xd[2], (void*)cell_d, (void*)rnnz_d, (void*)inc_off_d,
@@ -794,6 +861,9 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   g.K = K;
   g.bvec = bvec;
   g.vdiag = vdiag;
+  g.V27 = V27;
+  g.s1 = ss1;
+  g.s2 = ss2;
   g.fv = fv_d;
   g.fw = fw;
   g.boff = boff_d;

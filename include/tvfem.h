@@ -297,7 +297,9 @@ int tv_create_unstructured_part(const tv_umesh_desc* local_mesh, const tv_upart_
                                 const tv_params* params, const tv_options* opts, int device, void** ctx_out);
 int tv_destroy(void* ctx);
 
-/* Host-only (no GPU needed): layout of partition `part` of a CG1 mesh —
+/* Host-only (no GPU needed): layout of partition `part` of a CG1 mesh with one
+ * ghost plane per interface (a context with the distributed GMG keeps three on
+ * its fine slab internally; the owned range is the same) —
  * out[0..2] storage axis -> physical axis (-1 degenerate), out[3..5] global
  * nodes per storage axis, out[6..7] owned node planes [b0, b1) along storage
  * axis 2, out[8] global offset of the first owned dof, out[9] owned dofs,

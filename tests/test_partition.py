@@ -145,8 +145,9 @@ def test_partitioned_run_matches_single_partition(world, pcg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pcg", ["kspcg", "auto"])
 @pytest.mark.parametrize("world,rep", [(2, 0), (3, 0), (2, 200), (3, 200), (3, 1)])
-def test_partitioned_gmg_matches_single_partition(world, rep):
+def test_partitioned_gmg_matches_single_partition(world, rep, pcg):
     """The geometric-multigrid preconditioner on a partitioned box (the solver
     of the single-GPU line, distributed: tv_mgdist.cpp) reproduces the
     single-partition GMG run: T <= 1e-12, equal Newton counts, Krylov counts
@@ -154,12 +155,16 @@ def test_partitioned_gmg_matches_single_partition(world, rep):
     hierarchy has three levels (31 -> 16 -> 9 planes along the partition axis);
     `rep` is the replication bound: 0 (default) keeps only level 0
     distributed, 200 levels 0-1 (level 2 replicated, 108 nodes), 1 all three
-    (the coarsest level's solve distributed too)."""
+    (the coarsest level's solve distributed too).  Both Krylov forms run on
+    deep-ghost slabs (three ghost planes: the V-cycle's level-0 vectors are
+    computed on them and need no exchange of their own): KSPCG as written, and
+    AUTO -- the single-reduction form, one all-reduce + ghost group per
+    iteration (tv_mgdist.cpp pcg_solve_mg_dist_cgs)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    _partition_check(world, "host", 29750 + 10 * world + (rep % 7), ("--pc", "gmg", "--mg-replicate", str(rep),
-                                                                       "--pcg", "kspcg", "--mg-coupling", "global"))
+    _partition_check(world, "host", 29750 + 10 * world + (rep % 7) + (pcg == "auto") * 100,
+                     ("--pc", "gmg", "--mg-replicate", str(rep), "--pcg", pcg, "--mg-coupling", "global"))
 
 
 @pytest.mark.gpu
@@ -224,6 +229,25 @@ def test_partitioned_dg_matches_single_partition(world, kernel):
         pytest.skip("no GPU")
     _partition_check(world, "host", 29780 + world + (kernel == "cells") * 5,
                      ("--family", "DG", "--dg-kernel", kernel, "--pcg", "kspcg", "--steps", "3"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,family", [(2, "DG"), (3, "DG"), (2, "DG-CG"), (3, "DG-CG")])
+def test_partitioned_dg_gmg_matches_single_partition(world, family):
+    """The DG1 -> CG1 multigrid on slabs of cell layers (tv_mgsolve.cpp
+    mg_setup: the CG levels replicated, the owned cells restricted into the
+    vertex planes they touch and summed by one all-reduce, the prolongation
+    into every local cell): DG/DG and the reference's main.py pairing DG T /
+    CG sigma reproduce the single-partition DG multigrid run (T <= 1e-12,
+    equal Newton counts, Krylov within one per Newton solve -- the level-1
+    sums add in another order, and the smoother weight's power iteration starts
+    from the partition-major vector); the reference runs this under mpiexec
+    with PCGAMG (ThermoViscoProblem.py:343-346, main.py:24-27)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    _partition_check(world, "host", 29810 + world + (family == "DG-CG") * 5,
+                     ("--family", family, "--pc", "gmg", "--pcg", "kspcg", "--steps", "3"))
 
 
 @pytest.mark.gpu

@@ -60,20 +60,26 @@ def measure(world, reps, transport):
     return us
 
 
-def exchanges_per_step(us, newton=4, krylov=20):
-    """Exchange points of one C4 step of the distributed GMG-PCG (KSPCG form),
-    as tv_mgdist.cpp / tv_solver.cpp issue them; each entry (pattern, count)"""
+def exchanges_per_step(us, newton=4, krylov=20, form="cgs"):
+    """Exchange points of one C4 step of the distributed GMG-PCG as tv_mgdist.cpp
+    / tv_solver.cpp issue them (each entry: pattern -> calls per step).
+    form "kspcg1": KSPCG with one ghost plane (rounds 3-4); "kspcg": KSPCG on
+    deep-ghost slabs; "cgs": the single-reduction form on deep-ghost slabs."""
     dist_l1 = us["halo_l1"] is not None
     dist_l2 = us["halo_l2"] is not None
     rep = us["vec"] is not None
-    vcyc = [("halo", 1)]                       # pre-smoothed x0
+    vcyc = [] if form != "kspcg1" else [("halo", 1)]   # pre-smoothed x0 (deep ghosts: computed on the ghosts)
     if dist_l1:
-        vcyc += [("halo", 1), ("halo_l1", 2)]  # d0; x1 pre and post
+        vcyc += [] if form != "kspcg1" else [("halo", 1)]  # the residual d0
+        vcyc += [("halo_l1", 2)]                             # x1 pre- and post-smoothed
         if dist_l2:
             vcyc += [("halo_l1", 1), ("halo_l2", 2)]
     if rep:
         vcyc += [("vec", 1)]
-    per_it = [("allreduce1", 1), ("close", 1)] + vcyc   # p.w; (z.z, z.r) + z ghosts; the V-cycle
+    if form == "cgs":
+        per_it = [("close", 1)] + vcyc          # (z.z, z.r, z.u) + u ghosts; the V-cycle
+    else:
+        per_it = [("allreduce1", 1), ("close", 1)] + vcyc  # p.w; (z.z, z.r) + z ghosts; the V-cycle
     per_newton = [("close", 1)] + vcyc + [("allreduce1", 1), ("halo", 1)]  # the solve's init; ||dx||; T ghosts
     cnt = {}
     for name, n in per_it:
@@ -89,6 +95,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--worlds", type=str, default="2,4,8")
+    ap.add_argument("--form", choices=["cgs", "kspcg", "kspcg1"], default="cgs",
+                    help="the Krylov form whose exchange points are counted (the contexts measured are this "
+                         "library's: deep ghosts on the fine grid)")
     ap.add_argument("--floors", type=str, default=os.path.join(ROOT, "profiles", "r05_bench_n{N}.json"))
     a = ap.parse_args()
     out = {"transport": "RCCL one-rank loopback on one MI355X (self send/recv, one-rank all-reduce)",
@@ -96,7 +105,7 @@ def main():
     for w in (int(v) for v in a.worlds.split(",")):
         rc = measure(w, a.reps, "rccl")
         st = measure(w, a.reps, "stub")
-        cnt, pts = exchanges_per_step(rc)
+        cnt, pts = exchanges_per_step(rc, form=a.form)
         comm_ms = sum(cnt[k] * rc[k] for k in cnt) * 1e-3
         stub_ms = sum(cnt[k] * (st[k] or 0.0) for k in cnt) * 1e-3
         rec = {"us_rccl_loopback": rc, "us_stub": st, "exchanges_per_step": cnt, "points_per_krylov_it": pts,

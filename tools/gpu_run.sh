@@ -47,7 +47,7 @@ for MODE in "$@"; do
         ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/tests.log 2>&1
       rc=$?; tail -3 $OUT/tests.log
       grep -h "^\[parity\]\|^\[c3\|^\[fullsize\]\|^\[amg\]\|upartition\]" $OUT/tests.log > $OUT/parity_lines.txt
-      [ $rc -ne 0 ] && { grep -E "FAILED|ERROR|Error" $OUT/tests.log | head -20; exit $rc; }
+      if [ $rc -ne 0 ]; then grep -E "FAILED|ERROR|Error" $OUT/tests.log | head -20; exit $rc; fi
       ;;
     bench)
       IFS=';' read -r -a CFGS <<< "${BENCHES:-c4|--steps 20 --warmup 2}"
@@ -98,7 +98,7 @@ for MODE in "$@"; do
     ab)
       IFS=';' read -r -a CFGS <<< "${BENCHES:?BENCHES}"
       for v in ${LIBS:?LIBS}; do
-        [ "$v" = base ] && continue
+        if [ "$v" = base ]; then continue; fi
         step "parity subset on libtvfem$v.so"
         TVFEM_LIB=$PWD/fem-glass-tempering_amd/tvfem/libtvfem$v.so timeout -k 10 600 python -u -m pytest tests -m gpu -x -q \
           --timeout 200 --timeout-method thread -k "${PYTEST_AB:-steps or partition or vcycle or fullsize}" \
@@ -107,7 +107,7 @@ for MODE in "$@"; do
       done
       for rep in 1 2; do
         for v in $LIBS; do
-          [ "$v" = base ] && v=""
+          if [ "$v" = base ]; then v=""; fi
           for cfg in "${CFGS[@]}"; do
             tag=${cfg%%|*}; IFS=' ' read -r -a argv <<< "${cfg#*|}"
             run_bench ${tag}_$rep "$v" --no-cpu-baseline "${argv[@]}" || exit 1

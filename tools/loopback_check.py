@@ -12,7 +12,14 @@ Per case:
   2. the same partition with the host-staged transport and a callback that
      copies each send into its receive (the loopback semantics through the
      production host path): a few coupled steps on both must give bitwise
-     identical T / phi / xi / sigma and identical Newton / Krylov counts.
+     identical T / phi / xi / sigma and identical Newton / Krylov counts;
+  3. multigrid cases: the partitioned V-cycle (tv_precond_apply, every
+     exchange of the distributed cycle) applied to the same vector on both
+     transports gives bitwise identical results.
+A deep-ghost slab (the distributed multigrid keeps three ghost planes on its
+fine grid) receives under self-loopback a SHIFTED copy of its boundary planes,
+not a mirror: the reflected operator is not symmetric, and its Krylov solves
+may stop as indefinite -- on both transports alike, which is what is compared.
 
     python tools/loopback_check.py [--case NAME ...]     (prints LOOPBACK <json> per case)
 """
@@ -46,6 +53,7 @@ CASES = {
     "box_kspcg_first": ("box", (10, 30, 5), 2, 0, "kspcg", "jacobi", 0),
     "box_gmg_replicated": ("box", (10, 30, 5), 3, 1, "kspcg", "gmg", 0),
     "box_gmg_distributed": ("box", (10, 30, 5), 3, 1, "kspcg", "gmg", 1),
+    "box_gmg_single_reduction": ("box", (10, 30, 5), 3, 1, "auto", "gmg", 1),
     "um_first": ("distorted", (6, 12, 3), 2, 0, "kspcg", "jacobi", 0),
     "um_mid": ("distorted", (6, 12, 3), 3, 1, "kspcg", "jacobi", 0),
 }
@@ -82,30 +90,57 @@ def _steps(p, steps):
             its.append((p.last_newton_iterations, p.last_krylov_iterations))
     except Exception as e:  # the same failure on both transports is still agreement
         err = f"{type(e).__name__}: {e}"
-    out = {k: p.get_field(k) for k in ("T", "phi", "xi", "sigma")} if err is None else {}
+    out = {k: p.get_field(k) for k in ("T", "phi", "xi", "sigma")}  # (after an error: the state it left)
     return out, its, err
+
+
+def _vcycle(p):
+    """the partitioned V-cycle applied to a fixed vector (multigrid cases)"""
+    import torch
+    p.setup()
+    n, _ = p.num_dofs(0)
+    r = torch.tensor(np.random.default_rng(7).standard_normal(n), dtype=torch.float64, device="cuda")
+    z = torch.empty_like(r)
+    N.check(p._lib.tv_precond_apply(p._ctx, r.data_ptr(), z.data_ptr()), p._ctx)
+    return z.cpu().numpy()
 
 
 def run_case(name, steps=3):
     kind, cells, parts, part, pcg, pc, rep, *fam = CASES[name]
     lib = N.load_library()
+    box_gmg = pc == "gmg" and kind == "box" and not fam
+
+    def rccl():
+        q = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
+        uid = C.create_string_buffer(lib.tv_comm_unique_id_size())
+        N.check(lib.tv_comm_get_unique_id(uid))
+        N.check(lib.tv_comm_init_loopback(q._ctx, uid.raw), q._ctx)
+        return q
+
+    def host():
+        q = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
+        _host_loopback(q)
+        return q
     # RCCL loopback
-    a = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
-    uid = C.create_string_buffer(lib.tv_comm_unique_id_size())
-    N.check(lib.tv_comm_get_unique_id(uid))
-    N.check(lib.tv_comm_init_loopback(a._ctx, uid.raw), a._ctx)
+    a = rccl()
     nchk, nbad = C.c_int64(), C.c_int64()
     N.check(lib.tv_comm_check(a._ctx, C.byref(nchk), C.byref(nbad)), a._ctx)
     ra, ita, erra = _steps(a, steps)
     variant = a.pcg_variant
     a.close()
     # host-staged loopback
-    b = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
-    _host_loopback(b)
+    b = host()
     rb, itb, errb = _steps(b, steps)
     b.close()
     res = {"case": name, "checked": nchk.value, "bad": nbad.value, "its_rccl": ita, "its_host": itb,
            "err_rccl": erra, "err_host": errb, "krylov_form": variant, "pc": pc}
+    if box_gmg:  # the V-cycle operator through both transports
+        a, b = rccl(), host()
+        za, zb = _vcycle(a), _vcycle(b)
+        a.close()
+        b.close()
+        res["vcycle_bitwise"] = bool(np.array_equal(za, zb))
+        res["vcycle_norm"] = float(np.linalg.norm(za))
     for k in ra:
         res["maxdiff_" + k] = float(np.nanmax(np.abs(ra[k] - rb[k]))) if ra[k].size else 0.0
         res["bitwise_" + k] = bool(np.array_equal(ra[k], rb[k], equal_nan=True))
