@@ -816,14 +816,21 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
     a0 = bload(rs0, o);
     a1 = TWO ? bload(rs1, o) : 0.0;
   };
-  // POST: r and dinv of the own row at plane L - 1 (the output plane of step L)
+  // POST: r and dinv of the own row at plane L - 1 (the output plane of step L).
+  // D^-1 is loaded on the physical-boundary nodes only (their Robin facet
+  // terms, rewritten every Newton iteration; Dirichlet zeros): everywhere else
+  // step() forms 1 / diag(M + dt alpha K) from the staged axis coefficients
+  // (8 B per node fewer; the other lanes' loads carry an out-of-range offset)
   const buf_t rsr = mk_rsrc(pa.r, POST ? nbytes : 0u);
   const buf_t rsd = mk_rsrc(pa.dinv, POST ? nbytes : 0u);
+  const int bR_lo = (raxis == 1) ? g.bnd[1][0] : g.bnd[2][0], bR_hi = (raxis == 1) ? g.bnd[1][1] : g.bnd[2][1];
+  const bool bnd_lr = (i == 0) || (i == n0 - 1) || (r == 0 && bR_lo) || (r == nR - 1 && bR_hi);  // x face, row face
+  auto bnd_q = [&](int q) { return (q == 0 && bq_lo) || (q == nQ - 1 && bq_hi); };    // march-axis face
   auto fetch_post = [&](int L, double& a_r, double& a_d) {
     if (!POST) return;
     const uint32_t o = vo_wr + plane_off(L - 1);
     a_r = bload(rsr, o);
-    a_d = bload(rsd, o);
+    a_d = bload(rsd, (bnd_lr || bnd_q(L - 1)) ? o : kBadOff);
   };
 
   auto combine = [&](uint32_t vo, int L, double a0, double a1, double& v, double& vm) {
@@ -1007,7 +1014,11 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
       if (fq0 && q == 0) yb += yq0;
       if (fq1 && q == nQ - 1) yb += yq1;
       if (POST) {  // z = x + omega dinv (r - J x): the post-smoothing step (facet terms of the side faces later)
-        const double zq = xc + pa.omega * pd * (pr - yb);
+        // interior D^-1 from the staged coefficients (x pair, row SGPRs, plane slots 1 / 4 / 7 = Mz, da Kz, da Mz)
+        const double xm = xdi.x, xk = xdi.y;
+        const double dI = xm * My1 * c01.y + ((xk * My1 * c67.y + xm * Ky1 * c67.y) + xm * My1 * c45.x);
+        const double dq = (bnd_lr || bnd_q(q)) ? pd : 1.0 / dI;
+        const double zq = xc + pa.omega * dq * (pr - yb);
         bstore(rso, inwin ? vo_wr + plane_off(q) : kBadOff, zq);
         zz += wr ? zq * zq : 0.0;
         zr += wr ? zq * pr : 0.0;
@@ -1876,23 +1887,6 @@ void launch_mg_prepare(const MgPrep& p, hipStream_t s) {
 }
 
 int cg_num_blocks(const CgGrid& g, bool with_ghost_planes) { return plan(g, with_ghost_planes).nparts; }
-
-DiagFly cg_diag_fly(const CgGrid& g, int64_t t_off) {
-  DiagFly df{};
-  if (!use_march(g)) return df;  // 3D box levels only
-  df.on = 1;
-  df.n0 = g.n0;
-  df.n1 = g.n1;
-  df.n2 = g.n2;
-  df.t_off = t_off;
-  df.inv_n0 = 1.0 / g.n0;
-  df.inv_plane = 1.0 / ((double)g.n0 * g.n1);
-  for (int s = 0; s < 3; ++s) df.coef[s] = g.coef[s];
-  df.dt_alpha = g.dt_alpha;
-  for (int a = 0; a < 3; ++a)
-    for (int sd = 0; sd < 2; ++sd) df.bnd[a][sd] = g.bnd[a][sd];
-  return df;
-}
 
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off) {
   FaceAdd fa{};

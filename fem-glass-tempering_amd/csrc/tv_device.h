@@ -130,7 +130,7 @@ __device__ __forceinline__ void logic_dpi(PcgState* st, const double* sums) {
   if (!isfinite(dpi)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
   const double dpiold = st->dpiold;
   st->betaold = st->beta;
-  if (dpi == 0.0 || (st->it > 0 && ((dpi > 0.0) != (dpiold > 0.0)))) {
+  if (dpi == 0.0 || (!st->relaxed && st->it > 0 && ((dpi > 0.0) != (dpiold > 0.0)))) {
     st->done = 1; st->reason = R_DIV_INDEF_MAT; return;
   }
   st->dpi = dpi;
@@ -150,7 +150,7 @@ __device__ __forceinline__ void logic_update(PcgState* st, const double* sums) {
   if (st->it >= st->max_it) { st->done = 1; st->reason = R_DIV_ITS; return; }
   const double beta = sums[1];
   if (beta == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
-  if (beta * st->betaold < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
+  if (!st->relaxed && beta * st->betaold < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
   st->beta = beta;
 }
 
@@ -194,11 +194,15 @@ __device__ __forceinline__ void logic_cgs(PcgState* st, const double* s) {
   if (st->it >= st->max_it) { st->done = 1; st->reason = R_DIV_ITS; return; }
   const double gamma = s[0];
   if (gamma == 0.0) { st->done = 1; st->reason = R_CONV_ATOL; return; }
-  if (gamma * st->gamma < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
+  if (!st->relaxed && gamma * st->gamma < 0.0) { st->done = 1; st->reason = R_DIV_INDEF_PC; return; }
   const double beta = gamma / st->gamma;
   const double eta = s[1] - beta * gamma / st->a;
   if (!isfinite(eta)) { st->done = 1; st->reason = R_DIV_NANINF; return; }
-  if (eta == 0.0 || ((eta > 0.0) != (st->eta > 0.0))) { st->done = 1; st->reason = R_DIV_INDEF_MAT; return; }
+  if (eta == 0.0 || (!st->relaxed && ((eta > 0.0) != (st->eta > 0.0)))) {
+    st->done = 1;
+    st->reason = R_DIV_INDEF_MAT;
+    return;
+  }
   st->beta = beta;
   st->gamma = gamma;
   st->eta = eta;
@@ -241,7 +245,7 @@ __device__ __forceinline__ void lag_update_lean(const PcgState* st, const double
   const double dp = sqrt(lag[0]);
   const double b = lag[1];
   const bool stop = (st->done != 0) | !isfinite(dp) | (dp <= st->ttol) | (dp >= st->dtol * st->rnorm0) |
-                    (st->it + 1 >= st->max_it) | (b == 0.0) | (b * st->betaold < 0.0);
+                    (st->it + 1 >= st->max_it) | (b == 0.0) | (!st->relaxed & (b * st->betaold < 0.0));
   done = stop ? 1 : 0;
   beta = stop ? st->beta : b;
 }
@@ -317,31 +321,6 @@ __device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
   if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
   if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
   return add;
-}
-
-// D^-1 at local node t + df.t_off (DiagFly): stored on the physical boundary,
-// 1 / diag(M + dt alpha K) from the axis tables elsewhere
-__device__ __forceinline__ double dinv_fly(const DiagFly& df, const double* __restrict__ dinv, int64_t t) {
-  const int nd = (int)(t + df.t_off);
-  const int plane = df.n0 * df.n1;
-  int k = (int)((double)nd * df.inv_plane);
-  k -= (k * plane > nd) ? 1 : 0;
-  k += ((k + 1) * plane <= nd) ? 1 : 0;
-  const int rem = nd - k * plane;
-  int j = (int)((double)rem * df.inv_n0);
-  j -= (j * df.n0 > rem) ? 1 : 0;
-  j += ((j + 1) * df.n0 <= rem) ? 1 : 0;
-  const int i = rem - j * df.n0;
-  const bool bnd = (i == 0 && df.bnd[0][0]) || (i == df.n0 - 1 && df.bnd[0][1]) || (j == 0 && df.bnd[1][0]) ||
-                   (j == df.n1 - 1 && df.bnd[1][1]) || (k == 0 && df.bnd[2][0]) || (k == df.n2 - 1 && df.bnd[2][1]);
-  if (bnd) return __builtin_nontemporal_load(&dinv[t]);
-  const double* cx = df.coef[0] + (int64_t)i * C_NCOEF;
-  const double* cy = df.coef[1] + (int64_t)j * C_NCOEF;
-  const double* cz = df.coef[2] + (int64_t)k * C_NCOEF;
-  const double d = cx[C_MDI] * cy[C_MDI] * cz[C_MDI] +
-                   df.dt_alpha * (cx[C_KDI] * cy[C_MDI] * cz[C_MDI] + cx[C_MDI] * cy[C_KDI] * cz[C_MDI] +
-                                  cx[C_MDI] * cy[C_MDI] * cz[C_KDI]);
-  return 1.0 / d;
 }
 
 // the same at local node (i, j, k) (coordinates known)

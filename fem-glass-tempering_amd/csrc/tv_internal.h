@@ -111,6 +111,9 @@ struct PcgState {
   int it, done, reason, max_it;
   int post;                   // the post-solve group queued behind the batches has run (pcg_solve_mg)
   int accept_its;             // ksp_fixed_its > 0: a solve ending at max_it (DIVERGED_ITS) is a good outcome
+  int relaxed;                // the measurement stub (tv_comm_init_stub): no indefiniteness breakdowns --
+                              // its zeroed ghosts make the slab's operator inconsistent, the fixed
+                              // iterations are timed, not used
   double dx_norm2;            // ||dx||^2 of the last Newton update
   double a_prev;              // step length of the previous iteration (dx is updated every 2nd)
   // single-reduction form (k_cgs_march): gamma = (r, z) and eta = (p, A p) of
@@ -193,8 +196,14 @@ struct UmGrid {
   // any coordinates -- a jittered / warped plate, an extruded or transfinite
   // gmsh mesh): V as 27 stencil slots per row, V27[slot nv + r] for column
   // r + di + s1 dj + s2 dk, slot = (di + 1) + 3 (dj + 1) + 9 (dk + 1); no column
-  // indices (216 instead of ~330 B per row); nullptr: SELL only
+  // indices (216 instead of ~330 B per row); nullptr: SELL only.  J27 = V27
+  // with the Robin facet Jacobian of J(T) folded into the boundary rows'
+  // slots (launch_um_robin27, once per Newton iteration): the J x kernels then
+  // run no facet quadrature (brow: the nbr boundary rows)
   const double* V27;
+  double* J27;
+  const int64_t* brow;
+  int64_t nbr;
   int64_t s1, s2;
   // Robin terms
   const int* fv;         // [m][facet] facet vertex ids, facet-local tensor order
@@ -253,6 +262,9 @@ int um_rcb(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* ce
            std::string& err);
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s);
+// J27 <- V27 + the Robin facet Jacobian at T (structured topology; a no-op else):
+// before the J x launches of a Newton iteration (J(T) is fixed inside a solve)
+void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s);
 void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hipStream_t s);
 // p <- z + beta p (iteration it_host's parity buffer), w <- J p, p.w; the
 // reduction tail (rt.counter != nullptr) reduces the records and runs the
@@ -362,22 +374,6 @@ struct FaceAdd {
 };
 FaceAdd cg_face_add(const CgGrid& g, int64_t t_off);
 
-// The Jacobi diagonal of a box level formed on the fly by a pointwise kernel
-// (instead of streaming the stored dinv): off the physical boundary diag J =
-// diag(M + dt alpha K) is the per-axis product of diag_value<3, false>
-// (tv_cg.hip), the same expression; the boundary nodes (Robin facet terms,
-// T-dependent, rewritten every Newton iteration; 0 on Dirichlet rows) read the
-// stored value.  on = 0: the stored dinv everywhere (unstructured levels).
-struct DiagFly {
-  int on;
-  int n0, n1, n2;
-  int64_t t_off;             // local index of the kernel's first node
-  double inv_n0, inv_plane;
-  const double* coef[3];
-  double dt_alpha;
-  int bnd[3][2];
-};
-DiagFly cg_diag_fly(const CgGrid& g, int64_t t_off);
 
 // ---- geometric multigrid on the box hierarchy (tv_mg.hip, tv_pcg.hip) ----
 // Transfer between a level and the next coarser one (nested rectilinear grids:
@@ -482,7 +478,7 @@ void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x,
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
                       int it_host, int init, hipStream_t s, const double* lag = nullptr,
-                      unsigned* counter = nullptr, const DiagFly* df = nullptr);
+                      unsigned* counter = nullptr);
 // the single-reduction form's update (k_mg_update_cgs, tv_pcg.hip): s <- u + beta s,
 // p <- z + beta p, dx <- dx + a p, r <- r - a s, x0 <- omega dinv r (first: s = u,
 // p = z, dx = a p); lag: the all-reduced sums whose logic (lag_kind 6 / 7) this

@@ -508,10 +508,9 @@ int mg_iteration_dist(Ctx* c, const double* T, int it, bool fold, bool lag3) {
                       0, c->stream);
   } else {
     const FaceAdd fa = c->um ? FaceAdd{} : cg_face_add(c->cg, off);  // unstructured: w is complete
-    const DiagFly df = c->um ? DiagFly{} : cg_diag_fly(c->cg, off);
     launch_mg_update(n, c->st, c->pA + off, c->pB + off, c->w + off, &fa, c->dinv + off, c->mg_omega0, c->r + off,
                      c->f[TV_F_DX].ptr + off, c->mgx + off, it, 0, c->stream, lag2 ? c->sums : nullptr,
-                     lag2 ? c->counters + kUpdateCounter : nullptr, &df);
+                     lag2 ? c->counters + kUpdateCounter : nullptr);
   }
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 0, nullptr};
   return mg_apply0_dist(c, T, &t2);

@@ -459,11 +459,9 @@ int mg_iteration(Ctx* c, const double* T, int it) {
   if (c->dggface)
     launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
                       c->stream);
-  else {
-    const DiagFly df = c->um ? DiagFly{} : cg_diag_fly(c->cg, 0);  // D^-1 off the boundary from the axis tables
+  else
     launch_mg_update(n, c->st, c->pA, c->pB, c->w, &fa, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, it, 0,
-                     c->stream, nullptr, nullptr, &df);
-  }
+                     c->stream);
   RedTail t2{c->counters + kTailCounters, c->partials, c->sums, c->st, 3, nullptr};
   mg_apply0(c, T, &t2);  // z <- V(r); z.z, z.r; beta, convergence
   return TV_OK;
@@ -481,11 +479,9 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
   if (c->dggface)
     launch_dg_bupdate(c->dg, c->st, c->pA, c->pB, c->w, c->dggface, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
                       c->stream);  // dx <- 0, x0 <- omega B^-1 r
-  else {
-    const DiagFly df = c->um ? DiagFly{} : cg_diag_fly(c->cg, 0);
+  else
     launch_mg_update(n, c->st, c->pA, c->pB, c->w, nullptr, c->dinv, c->mg_omega0, c->r, c->f[TV_F_DX].ptr, c->mgx, 0, 1,
-                     c->stream, nullptr, nullptr, &df);  // x0 <- omega dinv r
-  }
+                     c->stream);  // dx <- 0, x0 <- omega dinv r
   RedTail t0{c->counters + kTailCounters, c->partials, c->sums, c->st, 1, nullptr};
   mg_apply0(c, T, &t0);  // z <- V(r); dp, beta (KSPCG init)
   if (c->ktime && c->ts_next + c->O.ksp_max_it + 8 > kTsCap)

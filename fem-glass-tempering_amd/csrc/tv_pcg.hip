@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
                                                       const double* __restrict__ dinv, double omega,
                                                       double* __restrict__ r, double* __restrict__ dx,
                                                       double* __restrict__ x0, int it_host, const double* lag,
-                                                      unsigned* counter, PcgState* st_w, DiagFly df) {
+                                                      unsigned* counter, PcgState* st_w) {
   double a = 0.0, ap = 0.0;
   if (!INIT && lag != nullptr) {
     const PcgState ls = lagged_state(st, lag, 2);
@@ -178,11 +178,13 @@ __global__ __launch_bounds__(kBlock) void k_mg_update(int64_t n, const PcgState*
   }
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
   const double* __restrict__ pp = (it_host & 1) ? pA : pB;
-  // v = {r, w, dinv, dx, p_prev, p}; D^-1 formed on the fly off the physical
-  // boundary (DiagFly: 8 B per node fewer, 40 -> 32 / 72 -> 64 B)
+  // v = {r, w, dinv, dx, p_prev, p}.  (D^-1 formed on the fly from the axis
+  // tables instead of this stream -- 8 B per node fewer -- measured slower:
+  // C4 10.72 / 10.77 vs 10.71 / 10.66 ms, the per-lane index decode, table
+  // gathers and the divide cost more than the stream)
   auto load = [&](int64_t q, double (&v)[6]) {
     v[0] = r[q];
-    v[2] = df.on ? dinv_fly(df, dinv, q) : ldc<true>(&dinv[q]);
+    v[2] = ldc<true>(&dinv[q]);
     if (!INIT) v[1] = ldc<true>(&w[q]);
     if (DXU) {
       v[3] = FIRST ? 0.0 : ldc<true>(&dx[q]);
@@ -437,16 +439,14 @@ void launch_pcg_init(int64_t n, const double* r, const double* dinv, double* z, 
 
 void launch_mg_update(int64_t n, const PcgState* st, const double* pA, const double* pB, const double* w,
                       const FaceAdd* fa, const double* dinv, double omega, double* r, double* dx, double* x0,
-                      int it_host, int init, hipStream_t s, const double* lag, unsigned* counter,
-                      const DiagFly* dfp) {
+                      int it_host, int init, hipStream_t s, const double* lag, unsigned* counter) {
   const FaceAdd f = (fa && fa->on) ? *fa : FaceAdd{};
-  const DiagFly df = dfp ? *dfp : DiagFly{};
   const dim3 g(vec_blocks(n)), b(kBlock);
   const bool odd = (it_host & 1) != 0;
   const bool first = it_host == 1;
 #define TV_MGU(F, I, D, FI) \
   hipLaunchKernelGGL((k_mg_update<F, I, D, FI>), g, b, 0, s, n, st, pA, pB, w, f, dinv, omega, r, dx, x0, it_host, \
-                     lag, counter, const_cast<PcgState*>(st), df)
+                     lag, counter, const_cast<PcgState*>(st))
   if (init) TV_MGU(false, true, false, false);
   else if (f.on) {
     if (first) TV_MGU(true, false, true, true);

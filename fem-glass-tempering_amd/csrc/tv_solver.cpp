@@ -22,7 +22,10 @@ void op_diag(Ctx* c, const double* T, double* d, int invert) {
   else launch_dg_diag(c->dg, T, d, invert, c->stream);
 }
 void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
-  if (c->um) launch_um_japply(c->umg, T, x, y, c->stream);
+  if (c->um) {  // (structured topology: the Robin terms at this T folded into the stencil first)
+    launch_um_robin27(c->umg, T, c->stream);
+    launch_um_japply(c->umg, T, x, y, c->stream);
+  }
   else if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
   else launch_dg_japply(c->dg, T, x, y, partials, np, c->stream);
 }
@@ -58,6 +61,7 @@ PcgState pcg_state_init(const Ctx* c) {
     h.dtol = 1e300;
     h.max_it = c->O.ksp_fixed_its;
     h.accept_its = 1;
+    h.relaxed = c->comm_stub ? 1 : 0;
   }
   return h;
 }
@@ -364,6 +368,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
         c->dinv_interior = true;
       } else {
         op_diag(c, T, c->dinv, 1);
+        if (c->um) launch_um_robin27(c->umg, T, c->stream);  // J(u) of the solve (structured topology)
       }
     }
     dinv_fresh = false;

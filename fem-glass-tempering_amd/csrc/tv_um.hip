@@ -390,11 +390,12 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
         acc += __builtin_nontemporal_load(&ms[64 * k]) * (xc - up[c]);
         acc2 += __builtin_nontemporal_load(&ks[64 * k]) * xc;
       }
-    } else if (MODE != UM_DIAG && g.V27 != nullptr) {
-      // structured topology: the 27 slots in column order (the SELL row's sorted
-      // columns, absent neighbours as zeros: the same sum, term by term)
+    } else if (MODE != UM_DIAG && g.J27 != nullptr) {
+      // structured topology: the 27 slots of J(T) in column order (the SELL row's
+      // sorted columns, absent neighbours as zeros), the Robin facet terms of the
+      // boundary rows folded in (no robin_row below)
       if (r < g.nv) {
-        const double* __restrict__ vs = g.V27 + r;
+        const double* __restrict__ vs = g.J27 + r;
 #pragma unroll
         for (int q = 0; q < 27; ++q) {
           const int64_t o = (int64_t)(q % 3 - 1) + g.s1 * ((q / 3) % 3 - 1) + g.s2 * (q / 9 - 1);
@@ -430,7 +431,8 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
       if (MODE == UM_DIAG) val = g.vdiag[r];
       else if (MODE == UM_RES) val = (acc + acc2) - g.dt_f * g.bvec[r];
       else val = acc;
-      val += robin_row<D, MODE>(g, r, (MODE == UM_RES) ? u : T, xget);
+      if (MODE == UM_RES || MODE == UM_DIAG || g.J27 == nullptr)  // (J27: folded in)
+        val += robin_row<D, MODE>(g, r, (MODE == UM_RES) ? u : T, xget);
       if (MODE == UM_DIAG && invert) val = 1.0 / val;
       if (MODE == UM_FUSED) pw += u[r] * val;
       out[r] = val;
@@ -526,6 +528,63 @@ int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, do
   const double* p = (it_host & 1) ? pB : pA;
   launch_rows<UM_FUSED>(g, T, p, nullptr, w, st, partials, rt, 0, s);
   return row_blocks(g);
+}
+
+// J27 = V27 + the Robin facet Jacobian dt int_f g'(T_h) phi_r phi_m ds of each
+// boundary row r (the terms robin_row<UM_JAC> applies to x), one thread per
+// boundary row: its 27 slots copied from V27, then per boundary incidence the
+// 3^(d-1)-point facet quadrature accumulated into the slots of the facet's
+// vertices (race-free: a row's slots belong to its thread)
+__global__ __launch_bounds__(kBlock) void k_um_robin27(UmGrid g, const double* __restrict__ T) {
+  constexpr int NF = 4, NQ = 9;
+  for (int64_t b = blockIdx.x * (int64_t)kBlock + threadIdx.x; b < g.nbr; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = g.brow[b];
+#pragma unroll
+    for (int q = 0; q < 27; ++q) g.J27[(int64_t)q * g.nv + r] = g.V27[(int64_t)q * g.nv + r];
+    const int t1 = g.boff[r + 1];
+    for (int t = g.boff[r]; t < t1; ++t) {
+      const int code = g.binc[t];
+      const int64_t f = code >> 2;
+      const int m = code & 3;
+      double Tn[NF];
+      int64_t vn[NF];
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        vn[n] = g.fv[(int64_t)n * g.nf + f];
+        Tn[n] = T[vn[n]];
+      }
+      double cn[NF] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+      for (int q = 0; q < NQ; ++q) {
+        double Tq = 0.0, pm = 0.0, ph[NF];
+#pragma unroll
+        for (int n = 0; n < NF; ++n) {
+          ph[n] = fphi(n, q, 3);
+          Tq += ph[n] * Tn[n];
+          if (n == m) pm = ph[n];
+        }
+        const double wq = g.fw[(int64_t)q * g.nf + f] * um_dg(g, Tq) * pm;
+#pragma unroll
+        for (int n = 0; n < NF; ++n) cn[n] += wq * ph[n];
+      }
+#pragma unroll
+      for (int n = 0; n < NF; ++n) {
+        const int64_t off = vn[n] - r;
+        const int64_t dk = (off + g.s2 / 2 + g.s2) / g.s2 - 1;
+        const int64_t rem = off - dk * g.s2;
+        const int64_t dj = (rem + g.s1 / 2 + g.s1) / g.s1 - 1;
+        const int64_t di = rem - dj * g.s1;
+        const int sl = (int)((di + 1) + 3 * (dj + 1) + 9 * (dk + 1));
+        g.J27[(int64_t)sl * g.nv + r] += g.dt * cn[n];
+      }
+    }
+  }
+}
+
+void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s) {
+  if (g.J27 == nullptr || g.nbr == 0) return;
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.nbr + kBlock - 1) / kBlock, 4096));
+  hipLaunchKernelGGL(k_um_robin27, dim3(nb), dim3(kBlock), 0, s, g, T);
 }
 
 // SELL rows -> the 27 stencil slots of a structured-topology mesh (V27 zeroed
@@ -835,13 +894,20 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   }
   UMC(hipGetLastError());
   // structured topology on one partition: J x from the 27 stencil slots
-  int64_t ss1 = 0, ss2 = 0;
-  double* V27 = nullptr;
+  int64_t ss1 = 0, ss2 = 0, nbr = 0;
+  double *V27 = nullptr, *J27 = nullptr;
+  int64_t* brow_d = nullptr;
   if (nrow == nv && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
-    if (um_alloc(d, (size_t)27 * nv, &V27, err)) return 1;
+    if (um_alloc(d, (size_t)27 * nv, &V27, err) || um_alloc(d, (size_t)27 * nv, &J27, err)) return 1;
     UMC(hipMemsetAsync(V27, 0, sizeof(double) * 27 * (size_t)nv, s));
     hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V27);
     UMC(hipGetLastError());
+    UMC(hipMemcpyAsync(J27, V27, sizeof(double) * 27 * (size_t)nv, hipMemcpyDeviceToDevice, s));
+    std::vector<int64_t> brow;
+    for (int64_t v = 0; v < nv; ++v)
+      if (boff[(size_t)v + 1] > boff[(size_t)v]) brow.push_back(v);
+    nbr = (int64_t)brow.size();
+    if (um_upload(d, brow, &brow_d, err)) return 1;
   }
   UMC(hipStreamSynchronize(s));
   // setup-only arrays
@@ -862,6 +928,9 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   g.bvec = bvec;
   g.vdiag = vdiag;
   g.V27 = V27;
+  g.J27 = J27;
+  g.brow = brow_d;
+  g.nbr = nbr;
   g.s1 = ss1;
   g.s2 = ss2;
   g.fv = fv_d;
