@@ -136,7 +136,8 @@ def main():
                               verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,
                               mg_coupling=a.mg_coupling,
                               write_output=a.output is not None, output_dir=a.output or "output", **kw)
-    single = prob.pcg_variant == "single"
+    mg_single = pc == "gmg" and prob.pcg_variant == "single"  # GMG-PCG, Chronopoulos-Gear form (deep-ghost slabs)
+    single = prob.pcg_variant == "single" and not mg_single
     lib, ctx = prob._lib, prob._ctx
     if a.share > 1:  # the multi-rank launch sequence with the transport stubbed (tv_comm_init_stub)
         N.check(lib.tv_comm_init_stub(ctx), ctx)
@@ -264,8 +265,9 @@ def main():
         traffic_src = "committed rocprofv3 --pmc record " + os.path.relpath(pmc_file, ROOT)
     roofline = {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": ("jacobian_apply_unstructured (y <- J(T) x, isoparametric 27-point cells, coloured "
-                           "scatter; algorithmic bytes 16/vertex (x, y) + 24/vertex (coords) + 32/cell (ids))" if um else
+                "kernel": ("jacobian_apply_unstructured (y <- J(T) x; structured topology: the 14 upper slots of "
+                           "the symmetric 27-point stencil of J(T) per row, 128 B/vertex with x and y; else SELL-64, "
+                           "12 B per stored entry + 16 B/vertex)" if um else
                            "pcg_iteration_single_reduction (s, p, x, r, z updates; w <- J(T) z; (r,z), (z,w), (z,z))"
                            if single else "pcg_matvec_fused (p <- z + b p; w <- J(T) p; p.w)"),
                 "bytes_per_launch": dom["bytes"], "ms_per_launch": dom["ms"],
@@ -325,6 +327,8 @@ def main():
                                        else "PETSc KSPCG Jacobi-PCG" if pc == "jacobi"
                                        else "PETSc KSPCG, smoothed-aggregation AMG preconditioner (additive "
                                        "level 0)" if pc == "amg"
+                                       else "single-reduction (Chronopoulos-Gear) CG, geometric-multigrid V-cycle "
+                                       "preconditioner, three ghost planes per slab interface" if mg_single
                                        else "PETSc KSPCG, geometric-multigrid V-cycle preconditioner"),
                        "preconditioner": pc,
                        "visco_fields": "state (T, Tf, Tf_partial, phi, xi, s_tilde, sigma_tilde, sigma)"},

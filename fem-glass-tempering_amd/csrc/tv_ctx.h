@@ -85,6 +85,7 @@ struct Ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evp[2] = {nullptr, nullptr};  // PCG convergence polls (double-buffered)
   hipEvent_t evn = nullptr;                 // Newton: ||dx|| copied to the host
+  const double* nrm_dev = nullptr;          // ... from here (||dx||^2, final on every rank behind evn)
   tv_params P{};
   tv_options O{};
   int dim = 1;
@@ -295,8 +296,12 @@ bool op_japply_fused(Ctx* c, const double* T, int* np, const RedTail* tail = nul
 PcgState pcg_state_init(const Ctx* c);
 int ts_flush(Ctx* c);
 CgsBuffers cgs_buffers(Ctx* c, const double* T, int it);
-int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv);
-int visco(Ctx* c, bool copy_Tprev);
+// step_end (tv_step): 0 none, 1 the visco update, 2 T_prev <- T (thermal only).
+// At the Newton iteration the last step predicts to be the final one, the step's
+// end is queued before the host reads ||dx||, gated on the device's Newton test
+// (NewtonGate); *end_queued tells tv_step that it ran (the step is done)
+int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end = 0, bool* end_queued = nullptr);
+int visco(Ctx* c, bool copy_Tprev, const NewtonGate& gate = NewtonGate{});
 void launch_bc_mask(Ctx* c, double* dinv);  // dinv = 0 on the Dirichlet-constrained rows
 
 // ---- tv_mgsolve.cpp ----

@@ -155,6 +155,20 @@ struct ViscoConst {
 };
 
 // Pointers of the viscoelastic state (component-major, stride = n_local).
+// the incremental Newton test of newton() on the device: sqrt(*nrm2) / r0 < rtol
+// or sqrt(*nrm2) < atol (nrm2 == nullptr: always true)
+struct NewtonGate {
+  const double* nrm2 = nullptr;
+  double r0 = 1.0, rtol = 0.0, atol = 0.0;
+};
+#ifdef __HIPCC__
+__device__ __forceinline__ bool newton_gate_open(const NewtonGate& g) {
+  if (g.nrm2 == nullptr) return true;
+  const double rn = sqrt(*g.nrm2);
+  return (rn / g.r0 < g.rtol) || (rn < g.atol);
+}
+#endif
+
 struct ViscoFields {
   int64_t n;                  // dofs processed (owned range length)
   int64_t off_T, off_S;       // first processed dof in T-space / sigma-space arrays
@@ -172,6 +186,10 @@ struct ViscoFields {
   // device word: 0 = s_tilde and sigma_tilde hold +0.0 at every dof (quirk Q3
   // keeps them there), so the update neither reads nor rewrites them; 1 = general
   int* tflag;
+  // Newton gate (queued before the host has read ||dx||, newton()): the launch
+  // runs only if the Newton test on the device's ||dx||^2 passes -- the same
+  // operations as the host's test, so both decide alike; nullptr: ungated
+  NewtonGate gate;
 };
 
 // Unstructured CG1 mesh (quadrilaterals / hexahedra of any shape, tv_um.hip).
@@ -194,14 +212,21 @@ struct UmGrid {
   const double* vdiag;   // diag V
   // topologically structured hexahedra (vertex i + s1 j + s2 k, the box's cells,
   // any coordinates -- a jittered / warped plate, an extruded or transfinite
-  // gmsh mesh): V as 27 stencil slots per row, V27[slot nv + r] for column
-  // r + di + s1 dj + s2 dk, slot = (di + 1) + 3 (dj + 1) + 9 (dk + 1); no column
-  // indices (216 instead of ~330 B per row); nullptr: SELL only.  J27 = V27
-  // with the Robin facet Jacobian of J(T) folded into the boundary rows'
-  // slots (launch_um_robin27, once per Newton iteration): the J x kernels then
-  // run no facet quadrature (brow: the nbr boundary rows)
-  const double* V27;
-  double* J27;
+  // gmsh mesh): the operators as stencil slots, no column indices.  Slot q =
+  // (di + 1) + 3 (dj + 1) + 9 (dk + 1) couples row r to column r + o_q, o_q =
+  // di + s1 dj + s2 dk; the operators are symmetric and o_{26-q} = -o_q, so only
+  // the upper half q = 13 .. 26 is stored, X14[(q - 13) nv + r], and the lower
+  // slot q of row r is the upper slot 26 - q of row r + o_q (read from the
+  // neighbour row's stream, a cache hit): 112 B per row and operator from HBM
+  // instead of ~330 B of SELL.  J14 = V14 with the Robin facet Jacobian of J(T)
+  // folded into the boundary rows' slots (launch_um_robin27, once per Newton
+  // iteration): the J x kernels then run no facet quadrature (brow: the nbr
+  // boundary rows).  M14 / K14: the residual's mass and dt alpha K.  nullptr:
+  // SELL only.
+  const double* V14;
+  double* J14;
+  const double* M14;
+  const double* K14;
   const int64_t* brow;
   int64_t nbr;
   int64_t s1, s2;
@@ -262,7 +287,7 @@ int um_rcb(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* ce
            std::string& err);
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s);
-// J27 <- V27 + the Robin facet Jacobian at T (structured topology; a no-op else):
+// J14 <- V14 + the Robin facet Jacobian at T (structured topology; a no-op else):
 // before the J x launches of a Newton iteration (J(T) is fixed inside a solve)
 void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s);
 void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hipStream_t s);
@@ -542,5 +567,7 @@ void output_release(Output* o, int set);  // an acquired set whose write is aban
 bool output_submit(Output* o, int set, double t, hipStream_t compute, std::string& err);
 std::string output_destroy(Output* o);
 void launch_copy(double* dst, const double* src, int64_t n, hipStream_t s);
+// the same, gated on the Newton test (tv_visco.hip)
+void launch_copy_gated(double* dst, const double* src, int64_t n, const NewtonGate& g, hipStream_t s);
 
 }  // namespace tv

@@ -28,9 +28,12 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
   switch (kernel) {
     case 0:  // J(T) x : read x, write y (geometry implicit, T only on boundary nodes)
     case 10:  // the same, timed with the Infinity Cache flushed (tv_time_kernel)
-      // unstructured: + the assembled cell operator (8 B value + 4 B column per
-      // stored SELL entry, padding included) and the Robin data of the boundary
-      *bytes = c->um ? 16.0 * n + 12.0 * (double)um_nnz(c->umd) : 16.0 * n;
+      // unstructured: + the assembled operator -- structured topology: the 14
+      // upper stencil slots of J(T) per row (112 B; the lower slots are the
+      // neighbour rows' upper slots, counted once); else 8 B value + 4 B column
+      // per stored SELL entry, padding included
+      *bytes = !c->um ? 16.0 * n
+                      : (c->umg.J14 ? (16.0 + 112.0) * n : 16.0 * n + 12.0 * (double)um_nnz(c->umd));
       break;
     case 1: {  // fused visco update, per dof
       int tf = 1;
@@ -42,8 +45,8 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       *bytes = per * n;
       break;
     }
-    case 2:  // residual: read T, Tp, write F
-      *bytes = 24.0 * n;
+    case 2:  // residual: read T, Tp, write F (+ structured topology: the M and K half stencils)
+      *bytes = (c->um && c->umg.J14) ? (24.0 + 224.0) * n : 24.0 * n;
       break;
     case 3:  // fused PCG matvec: read z, p_old, write p, w (T on boundary nodes only)
       // single-reduction iteration: read r, s, w, diag^-1, p, x; write r, s, p, x, w
@@ -273,7 +276,7 @@ int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches) {
 int tv_pcg_variant(void* ctx, int* variant) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !variant) return TV_ERR_ARG;
-  *variant = c->cgs ? TV_PCG_SINGLE_REDUCTION : TV_PCG_KSPCG;
+  *variant = (c->cgs || c->mg_cgs) ? TV_PCG_SINGLE_REDUCTION : TV_PCG_KSPCG;
   return TV_OK;
 }
 

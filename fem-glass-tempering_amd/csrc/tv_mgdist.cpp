@@ -583,6 +583,7 @@ static int pcg_solve_mg_dist_cgs(Ctx* c, const double* T, int* its, int* reason,
       if (int e = allreduce(c, nrm, 1)) return e;
       HIPC(hipMemcpyAsync(c->h_sums, nrm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
       HIPC(hipEventRecord(c->evn, c->stream));
+      c->nrm_dev = nrm;
     }
     return TV_OK;
   };
@@ -677,6 +678,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post)
       if (int e = allreduce(c, nrm, 1)) return e;  // collective on every rank, run or gated off
       HIPC(hipMemcpyAsync(c->h_sums, nrm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
       HIPC(hipEventRecord(c->evn, c->stream));
+      c->nrm_dev = nrm;
     }
     return TV_OK;
   };

@@ -504,6 +504,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
       launch_post_group(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, c->f[TV_F_T].ptr, c->partials, c->sums, c->stream);
       HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
       HIPC(hipEventRecord(c->evn, c->stream));
+      c->nrm_dev = c->sums;
     }
     return TV_OK;
   };

@@ -335,8 +335,30 @@ int dirichlet_pre(Ctx* c, const double* T) {
   return TV_OK;
 }
 
+// the end of a time step (tv_step): the visco update with T_prev <- T, or the
+// copy alone (thermal only), optionally gated on the device's Newton test; the
+// visco update's HIP events bracket it (the previous pair is read first: it is
+// long done by now, and reading it at the step's start made the host wait for
+// the previous update -- an 18 us gap before the step's first residual)
+int queue_step_end(Ctx* c, int step_end, const NewtonGate& gate) {
+  if (step_end == 2) {
+    if (gate.nrm2) launch_copy_gated(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, gate, c->stream);
+    else launch_copy(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, c->stream);
+    return TV_OK;
+  }
+  if (int e = visco_timing_flush(c)) return e;
+  if (c->ktime) HIPC(hipEventRecord(c->vev[0], c->stream));
+  if (int e = visco(c, true, gate)) return e;  // includes T_prev <- T (ThermoViscoProblem.py:378-379)
+  if (c->ktime) {
+    HIPC(hipEventRecord(c->vev[1], c->stream));
+    c->vev_pending = true;  // read at the next step / tv_kernel_stats (no host wait here)
+  }
+  return TV_OK;
+}
+
 // dolfinx NewtonSolver::solve, convergence_criterion = "incremental"
-int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
+int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, bool* end_queued) {
+  if (end_queued) *end_queued = false;
   if (int e = require_comm(c, "Newton solve")) return e;
   if (int e = refresh_dirty_ghosts(c)) return e;
   if (c->um && c->n_parts > 1 && c->O.preconditioner == TV_PC_AMG && !c->amg_on)
@@ -398,6 +420,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
       if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
       HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
       HIPC(hipEventRecord(c->evn, c->stream));
+      c->nrm_dev = c->sums;
     }
     if (int e = halo(c, T)) return e;
     // the next F queued before the host reads ||dx|| when the previous step
@@ -406,6 +429,19 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     // A wrong guess costs one residual, whose result is simply not used.
     const bool spec = its + 1 < c->newton_pred && its + 1 < c->O.newton_max_it;
     if (spec) dinv_fresh = residual();
+    // at (or past) the iteration the last step ended with, the step's end is
+    // queued now, gated on the device's copy of this iteration's test (an
+    // iteration that reaches newton_max_it without error_on_nonconvergence ends
+    // the solve either way: ungated); the host's test below takes the same
+    // decision from the same ||dx||^2, so a gated-off launch is simply not used
+    bool end_q = false, end_always = false;
+    if (step_end && !spec && its >= 1 && its + 1 >= c->newton_pred && c->nrm_dev) {
+      end_always = its + 1 >= c->O.newton_max_it && !c->O.error_on_nonconvergence;
+      NewtonGate g;
+      if (!end_always) g = NewtonGate{c->nrm_dev, r0, c->O.newton_rtol, c->O.newton_atol};
+      if (int e = queue_step_end(c, step_end, g)) return e;
+      end_q = true;
+    }
     // the host waits for ||dx|| only, not for the queued residual: it decides
     // and queues the next Newton iteration while the GPU computes F (the C4
     // trace showed the GPU idle ~27 us per Newton iteration behind a stream sync)
@@ -418,6 +454,10 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv) {
     } else {
       const double rel = rn / r0;
       conv = (rel < c->O.newton_rtol) || (rn < c->O.newton_atol);
+    }
+    if (end_q) {
+      if (conv || end_always) *end_queued = true;
+      else c->vev_pending = false;  // gated off: its events bracket nothing
     }
     // dolfinx assembles F after every update; in the incremental criterion that
     // last F is never read, so it is assembled only when another iteration follows.
@@ -482,10 +522,15 @@ void visco_setup(Ctx* c, ViscoConst& k, ViscoFields& v) {
   v.Tfo = c->Tfo;
 }
 
-int visco(Ctx* c, bool copy_Tprev) {
+int visco(Ctx* c, bool copy_Tprev, const NewtonGate& gate) {
   ViscoConst k;
   ViscoFields v;
   visco_setup(c, k, v);
+  v.gate = gate;
+  auto copy = [&](double* d, const double* s, int64_t n) {
+    if (gate.nrm2) launch_copy_gated(d, s, n, gate, c->stream);
+    else launch_copy(d, s, n, c->stream);
+  };
   const int all = c->O.materialize ? 1 : 0;
   if (c->um && c->n_parts > 1) {
     // partitioned unstructured mesh: every local vertex, ghosts included (their
@@ -503,11 +548,11 @@ int visco(Ctx* c, bool copy_Tprev) {
     v.copy_Tprev = copy_Tprev ? 1 : 0;
     launch_visco(c->dim, all, k, v, c->stream);
     if (copy_Tprev && c->ownT_off > 0) {  // ghost planes of T_prev
-      launch_copy(v.Tp, v.T, c->ownT_off, c->stream);
+      copy(v.Tp, v.T, c->ownT_off);
     }
     if (copy_Tprev && c->nT > c->ownT_off + c->ownT_n) {
       const int64_t o = c->ownT_off + c->ownT_n;
-      launch_copy(v.Tp + o, v.T + o, c->nT - o, c->stream);
+      copy(v.Tp + o, v.T + o, c->nT - o);
     }
   } else {
     // mixed families; on a slab partition (setup_mixed_part) the T pass covers
@@ -520,7 +565,7 @@ int visco(Ctx* c, bool copy_Tprev) {
     v.off_S = c->mixed_part ? 0 : c->ownS_off;
     v.map = c->map;
     launch_visco_Spass(c->dim, all, k, v, c->stream);
-    if (copy_Tprev) launch_copy(v.Tp, v.T, c->nT, c->stream);
+    if (copy_Tprev) copy(v.Tp, v.T, c->nT);
   }
   HIPC(hipGetLastError());
   return TV_OK;
@@ -590,19 +635,12 @@ int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c) return TV_ERR_ARG;
   hipSetDevice(c->device);
-  if (int e = visco_timing_flush(c)) return e;  // the previous step's visco events are long done
   int conv = 0;
-  if (int e = newton(c, newton_its, krylov_its, &conv)) return e;
-  if (!thermal_only) {
-    if (c->ktime) HIPC(hipEventRecord(c->vev[0], c->stream));
-    if (int e = visco(c, true)) return e;  // includes T_prev <- T (ThermoViscoProblem.py:378-379)
-    if (c->ktime) {
-      HIPC(hipEventRecord(c->vev[1], c->stream));
-      c->vev_pending = true;  // read at the next step / tv_kernel_stats (no host wait here)
-    }
-  } else {
-    launch_copy(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, c->stream);
-  }
+  bool done = false;
+  const int step_end = thermal_only ? 2 : 1;
+  if (int e = newton(c, newton_its, krylov_its, &conv, step_end, &done)) return e;
+  if (!done)
+    if (int e = queue_step_end(c, step_end, NewtonGate{})) return e;
   HIPC(hipGetLastError());
   // no stream synchronisation: the visco update (and T_prev <- T) finishes
   // behind the host, which queues the next step's residual meanwhile (the

@@ -212,6 +212,7 @@ __device__ __forceinline__ void fused_loop(const ViscoConst& c, const ViscoField
 
 template <int D, bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_fused(ViscoConst c, ViscoFields f) {
+  if (!newton_gate_open(f.gate)) return;
   if (c.paper) {
     fused_loop<D, ALL, false, true>(c, f);
     return;
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_visco_fused(ViscoConst c, ViscoField
 // per T dof (f.Tfo, a work array) for the sigma pass's thermal strain
 template <bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_T(ViscoConst c, ViscoFields f) {
+  if (!newton_gate_open(f.gate)) return;
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < f.n; t += (int64_t)gridDim.x * kBlock) {
     if (c.paper) {
       const TState ts = t_part<ALL, true>(c, f, f.off_T + t);
@@ -255,9 +257,16 @@ __device__ __forceinline__ void s_loop(const ViscoConst& c, const ViscoFields& f
 
 template <int D, bool ALL>
 __global__ __launch_bounds__(kBlock) void k_visco_S(ViscoConst c, ViscoFields f) {
+  if (!newton_gate_open(f.gate)) return;
   if (c.paper) s_loop<D, ALL, false, true>(c, f);
   else if (*f.tflag == 0) s_loop<D, ALL, true>(c, f);
   else s_loop<D, ALL, false>(c, f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_gated(double* __restrict__ d, const double* __restrict__ s, int64_t n,
+                                                       NewtonGate g) {
+  if (!newton_gate_open(g)) return;
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) d[t] = s[t];
 }
 
 int blocks_for(int64_t n) {
@@ -275,6 +284,11 @@ void launch_visco(int dim, int all, const ViscoConst& c, const ViscoFields& f, h
   else if (dim == 2) { if (all) TV_V(2, true); else TV_V(2, false); }
   else { if (all) TV_V(3, true); else TV_V(3, false); }
 #undef TV_V
+}
+
+void launch_copy_gated(double* dst, const double* src, int64_t n, const NewtonGate& g, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_copy_gated, dim3(blocks_for(n)), dim3(kBlock), 0, s, dst, src, n, g);
 }
 
 void launch_visco_Tpass(int dim, int all, const ViscoConst& c, const ViscoFields& f, hipStream_t s) {

@@ -462,9 +462,12 @@ int tv_kernel_timing(void* ctx, int on);
 int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches);
 /* counters of the last tv_step / tv_solve_T */
 int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm);
-/* the Krylov iteration form in use (TV_PCG_KSPCG or TV_PCG_SINGLE_REDUCTION);
- * with SINGLE_REDUCTION, kernel id 3 of tv_time_kernel / tv_kernel_bytes /
- * tv_kernel_stats is the fused single-reduction iteration and id 4 is unused */
+/* the Krylov iteration form in use (TV_PCG_KSPCG or TV_PCG_SINGLE_REDUCTION:
+ * the Jacobi march form, or with TV_PC_GMG the single-reduction GMG-PCG of
+ * deep-ghost slabs); with the Jacobi SINGLE_REDUCTION form, kernel id 3 of
+ * tv_time_kernel / tv_kernel_bytes / tv_kernel_stats is the fused
+ * single-reduction iteration and id 4 is unused (GMG: the ids keep their
+ * meaning) */
 int tv_pcg_variant(void* ctx, int* variant);
 
 #ifdef __cplusplus
