@@ -221,12 +221,9 @@ struct UmGrid {
   // instead of ~330 B of SELL.  J14 = V14 with the Robin facet Jacobian of J(T)
   // folded into the boundary rows' slots (launch_um_robin27, once per Newton
   // iteration): the J x kernels then run no facet quadrature (brow: the nbr
-  // boundary rows).  M14 / K14: the residual's mass and dt alpha K.  nullptr:
-  // SELL only.
+  // boundary rows).  nullptr: SELL only (the residual always runs on SELL).
   const double* V14;
   double* J14;
-  const double* M14;
-  const double* K14;
   const int64_t* brow;
   int64_t nbr;
   int64_t s1, s2;

@@ -45,8 +45,8 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       *bytes = per * n;
       break;
     }
-    case 2:  // residual: read T, Tp, write F (+ structured topology: the M and K half stencils)
-      *bytes = (c->um && c->umg.J14) ? (24.0 + 224.0) * n : 24.0 * n;
+    case 2:  // residual: read T, Tp, write F
+      *bytes = 24.0 * n;
       break;
     case 3:  // fused PCG matvec: read z, p_old, write p, w (T on boundary nodes only)
       // single-reduction iteration: read r, s, w, diag^-1, p, x; write r, s, p, x, w

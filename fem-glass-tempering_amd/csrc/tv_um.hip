@@ -381,11 +381,13 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
     const int wdt = (int)((g.soff[s + 1] - so) >> 6);
     const int* __restrict__ cs = g.cols + so + lane;  // entry k of this row: cs[64 k]
     double acc = 0.0, acc2 = 0.0;
-    if (MODE != UM_DIAG && g.J14 != nullptr) {
-      // structured topology, symmetric half stencils: upper slot k of row r
-      // (column r + o) and of row r - o (its column r: the lower slot of row r).
-      // Absent neighbours hold zeros; a row outside the mesh reads nothing.
+    if (MODE != UM_DIAG && MODE != UM_RES && g.J14 != nullptr) {
+      // structured topology, symmetric half stencil of J(T): upper slot k of
+      // row r (column r + o) and of row r - o (its column r: the lower slot of
+      // row r).  Absent neighbours hold zeros; a row outside the mesh reads nothing.
       if (r < g.nv) {
+        // fully unrolled (127 VGPRs, 4 waves per SIMD: every slot's loads in
+        // flight; unrolled by 2, 64 VGPRs: 524 vs 388 us per J x at 8.2M rows)
 #pragma unroll
         for (int k = 0; k < 14; ++k) {
           const int q = 13 + k;
@@ -393,18 +395,8 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
           const int64_t cu = r + o < g.nv ? r + o : r;
           const int64_t cl = r - o >= 0 ? r - o : r;
           const int64_t ku = (int64_t)k * g.nv;
-          if (MODE == UM_RES) {
-            const double du = u[cu] - up[cu];
-            acc += g.M14[ku + r] * du;
-            acc2 += g.K14[ku + r] * u[cu];
-            if (k > 0 && r - o >= 0) {
-              acc += g.M14[ku + cl] * (u[cl] - up[cl]);
-              acc2 += g.K14[ku + cl] * u[cl];
-            }
-          } else {
-            acc += g.J14[ku + r] * u[cu];
-            if (k > 0) acc += (r - o >= 0 ? g.J14[ku + cl] : 0.0) * u[cl];
-          }
+          acc += g.J14[ku + r] * u[cu];
+          if (k > 0) acc += (r - o >= 0 ? g.J14[ku + cl] : 0.0) * u[cl];
         }
       }
     } else if (MODE == UM_RES) {
@@ -477,55 +469,6 @@ __global__ __launch_bounds__(kBlock) void k_um_pvec(int64_t n, const PcgState* _
     p[t] = first ? z[t] : z[t] + b * po[t];
 }
 
-// The fused PCG matvec on the half stencils (structured topology): p = z +
-// beta p_old formed where it is read -- at the row itself (stored) and at each
-// of its 26 neighbours (recomputed from z and p_old, which the neighbouring
-// rows read too: cache hits) -- so no separate p pass and no re-read of p;
-// w = J p, p.w records and the reduction tail as k_um_rows<UM_FUSED>
-__global__ __launch_bounds__(kBlock) void k_um_fused14(UmGrid g, const double* __restrict__ z,
-                                                       const double* __restrict__ po, double* __restrict__ p,
-                                                       double* __restrict__ w, const PcgState* __restrict__ st,
-                                                       double* __restrict__ partials, RedTail rt, int first) {
-  stamp_start(rt);
-  if (st->done) return;
-  const double b = first ? 0.0 : st->beta / st->betaold;
-  auto pv = [&](int64_t c) -> double { return first ? z[c] : z[c] + b * po[c]; };
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  constexpr int WPB = kBlock / 64;
-  const int blk = xcd_remap(blockIdx.x, gridDim.x);
-  const int64_t nw = (int64_t)gridDim.x * WPB;
-  const int64_t gw = (int64_t)blk * WPB + wave;
-  const int64_t chunk = (g.nslice + nw - 1) / nw;
-  const int64_t s0 = gw * chunk, s1 = std::min<int64_t>(s0 + chunk, g.nslice);
-  double pw = 0.0;
-  for (int64_t s = s0; s < s1; ++s) {
-    const int64_t r = s * 64 + lane;
-    if (r >= g.nv) continue;
-    double acc = 0.0, pr = 0.0;
-#pragma unroll
-    for (int k = 0; k < 14; ++k) {
-      const int q = 13 + k;
-      const int64_t o = (int64_t)(q % 3 - 1) + g.s1 * ((q / 3) % 3 - 1) + g.s2 * (q / 9 - 1);
-      const int64_t cu = r + o < g.nv ? r + o : r;
-      const int64_t cl = r - o >= 0 ? r - o : r;
-      const int64_t ku = (int64_t)k * g.nv;
-      const double pu = pv(cu);
-      if (k == 0) pr = pu;
-      acc += g.J14[ku + r] * pu;
-      if (k > 0) acc += (r - o >= 0 ? g.J14[ku + cl] : 0.0) * pv(cl);
-    }
-    p[r] = pr;
-    w[r] = acc;
-    pw += pr * acc;
-  }
-  __shared__ double red[WPB];
-  const double sw = wave_sum64(pw);
-  if (lane == 0) red[wave] = sw;
-  __syncthreads();
-  if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
-  fused_reduce_tail<1>(rt, gridDim.x);
-}
-
 // the owned values the neighbours hold as ghosts, gathered into the send buffer
 __global__ __launch_bounds__(kBlock) void k_um_pack(const int64_t* __restrict__ idx, int64_t n,
                                                     const double* __restrict__ v, double* __restrict__ out) {
@@ -585,13 +528,6 @@ void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hip
 int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, double* pA, double* pB, double* w,
                            const PcgState* st, double* partials, int it_host, const RedTail* tail, hipStream_t s) {
   const RedTail rt = tail ? *tail : RedTail{};
-  if (g.J14 != nullptr) {  // structured topology: p formed inside the matvec
-    double* p = (it_host & 1) ? pB : pA;
-    const double* po = (it_host & 1) ? pA : pB;
-    hipLaunchKernelGGL(k_um_fused14, dim3(row_blocks(g)), dim3(kBlock), 0, s, g, z, po, p, w, st, partials, rt,
-                       it_host == 0 ? 1 : 0);
-    return row_blocks(g);
-  }
   const int vb = (int)std::max<int64_t>(1, std::min<int64_t>((g.nv + kBlock - 1) / kBlock, 2048));
   hipLaunchKernelGGL(k_um_pvec, dim3(vb), dim3(kBlock), 0, s, g.nv, st, z, pA, pB, it_host, rt);
   const double* p = (it_host & 1) ? pB : pA;
@@ -658,12 +594,14 @@ void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s) {
   hipLaunchKernelGGL(k_um_robin27, dim3(nb), dim3(kBlock), 0, s, g, T);
 }
 
-// SELL rows -> the upper stencil slots of a structured-topology mesh (X14
-// zeroed first; a row's padding entries -- column r, value 0 -- add 0 to its
-// centre; the lower entries are the neighbours' upper slots)
+// SELL rows -> the stencil slots of a structured-topology mesh: all 27, or
+// (half) the upper 14 (X zeroed first; a row's padding entries -- column r,
+// value 0 -- add 0 to its centre; the lower entries of a half stencil are the
+// neighbours' upper slots)
 __global__ __launch_bounds__(kBlock) void k_um_to_stencil(int64_t nrow, const int64_t* __restrict__ soff,
                                                           const int* __restrict__ cols, const double* __restrict__ V,
-                                                          int64_t s1, int64_t s2, int64_t nv, double* __restrict__ X14) {
+                                                          int64_t s1, int64_t s2, int64_t nv, double* __restrict__ X,
+                                                          int half) {
   for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < nrow; r += (int64_t)gridDim.x * kBlock) {
     const int64_t sl = r >> 6, lane = r & 63, so = soff[sl];
     const int wdt = (int)((soff[sl + 1] - so) >> 6);
@@ -675,7 +613,8 @@ __global__ __launch_bounds__(kBlock) void k_um_to_stencil(int64_t nrow, const in
       const int64_t dj = (rem + s1 / 2 + s1) / s1 - 1;  // |di| < s1 / 2
       const int64_t di = rem - dj * s1;
       const int q = (int)((di + 1) + 3 * (dj + 1) + 9 * (dk + 1));
-      if (q >= 13) X14[(int64_t)(q - 13) * nv + r] += V[e];
+      if (!half) X[(int64_t)q * nv + r] += V[e];
+      else if (q >= 13) X[(int64_t)(q - 13) * nv + r] += V[e];
     }
   }
 }
@@ -965,19 +904,19 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
                                Xd[2], fv_d, fw);
   }
   UMC(hipGetLastError());
-  // structured topology on one partition: J x and F from the half stencils
+  // structured topology on one partition: J x from the half stencil (the
+  // residual stays on SELL: its 27-slot M and K stencils measured no faster,
+  // 1.03-1.14 vs 1.01 ms -- the boundary rows' facet quadrature bounds it --
+  // and their half forms slower, 1.35 ms: the lower slots' re-reads a plane
+  // apart miss L2)
   int64_t ss1 = 0, ss2 = 0, nbr = 0;
-  double *V14 = nullptr, *J14 = nullptr, *M14 = nullptr, *K14 = nullptr;
+  double *V14 = nullptr, *J14 = nullptr;
   int64_t* brow_d = nullptr;
   if (nrow == nv && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
     const size_t n14 = (size_t)14 * nv;
-    if (um_alloc(d, n14, &V14, err) || um_alloc(d, n14, &J14, err) || um_alloc(d, n14, &M14, err) ||
-        um_alloc(d, n14, &K14, err))
-      return 1;
-    for (double* X : {V14, M14, K14}) UMC(hipMemsetAsync(X, 0, sizeof(double) * n14, s));
-    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V14);
-    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, M, ss1, ss2, nv, M14);
-    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, K, ss1, ss2, nv, K14);
+    if (um_alloc(d, n14, &V14, err) || um_alloc(d, n14, &J14, err)) return 1;
+    UMC(hipMemsetAsync(V14, 0, sizeof(double) * n14, s));
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V14, 1);
     UMC(hipGetLastError());
     UMC(hipMemcpyAsync(J14, V14, sizeof(double) * n14, hipMemcpyDeviceToDevice, s));
     std::vector<int64_t> brow;
@@ -1006,8 +945,6 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   g.vdiag = vdiag;
   g.V14 = V14;
   g.J14 = J14;
-  g.M14 = M14;
-  g.K14 = K14;
   g.brow = brow_d;
   g.nbr = nbr;
   g.s1 = ss1;

@@ -10,9 +10,21 @@ from collections import defaultdict
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+def dur(r):
+    return int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+
+
 vis = [i for i, r in enumerate(rows) if "k_visco_fused" in r["Kernel_Name"]]
-k = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(vis) // 2 - 1)
-a, b = vis[k], vis[k + 1]
+if not vis:  # thermal only: the step ends with T_prev <- T
+    vis = [i for i, r in enumerate(rows) if "k_copy" in r["Kernel_Name"]]
+# step boundaries: visco launches that did the update (a speculative launch the
+# device's Newton test gated off exits at once), and windows that hold a whole
+# step (not the back-to-back timing launches after the timed region)
+dmax = max(dur(rows[i]) for i in vis)
+vis = [i for i in vis if dur(rows[i]) > 0.2 * dmax]
+wins = [(a, b) for a, b in zip(vis, vis[1:]) if b - a > 20]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(wins) // 2)
+a, b = wins[k]
 win = rows[a + 1:b + 1]
 t0 = int(rows[a]["End_Timestamp"])
 t1 = int(rows[b]["End_Timestamp"])
