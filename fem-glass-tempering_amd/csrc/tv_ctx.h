@@ -73,6 +73,7 @@ struct MgLevel {
 struct AmgLevel {
   int64_t n = 0;
   Sell A, P, R;
+  UmGrid sg{};  // geometric levels: A as a half stencil (sg.J14 != nullptr: applied so instead of A)
   int64_t a_nnz = 0, p_nnz = 0, r_nnz = 0;
   double omega = 0.0;
   double *dinv = nullptr, *b = nullptr, *x = nullptr, *w = nullptr;

@@ -284,6 +284,10 @@ int um_rcb(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* ce
            std::string& err);
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s);
+// a structured grid's half-stencil operator (g.J14, g.nv, g.s1, g.s2): y = A x, or
+// with b != nullptr the Jacobi step y = x + omega dinv (b - A x)
+void launch_sg_apply(const UmGrid& g, const PcgState* st, const double* x, const double* b, const double* dinv,
+                     double omega, double* y, hipStream_t s);
 // J14 <- V14 + the Robin facet Jacobian at T (structured topology; a no-op else):
 // before the J x launches of a Newton iteration (J(T) is fixed inside a solve)
 void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s);

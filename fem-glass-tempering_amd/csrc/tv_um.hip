@@ -594,6 +594,38 @@ void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s) {
   hipLaunchKernelGGL(k_um_robin27, dim3(nb), dim3(kBlock), 0, s, g, T);
 }
 
+// A structured grid's operator as a half stencil (the coarse levels of the
+// algebraic multigrid's geometric hierarchy, tv_amg.cpp): one row per thread;
+// POST: the damped Jacobi step y = x + omega dinv (b - A x) in the epilogue
+template <bool POST>
+__global__ __launch_bounds__(kBlock) void k_sg_rows(UmGrid g, const PcgState* __restrict__ st,
+                                                   const double* __restrict__ x, const double* __restrict__ b,
+                                                   const double* __restrict__ dinv, double omega,
+                                                   double* __restrict__ y) {
+  if (st != nullptr && st->done) return;
+  for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < g.nv; r += (int64_t)gridDim.x * kBlock) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+      const int q = 13 + k;
+      const int64_t o = (int64_t)(q % 3 - 1) + g.s1 * ((q / 3) % 3 - 1) + g.s2 * (q / 9 - 1);
+      const int64_t cu = r + o < g.nv ? r + o : r;
+      const int64_t cl = r - o >= 0 ? r - o : r;
+      const int64_t ku = (int64_t)k * g.nv;
+      acc += g.J14[ku + r] * x[cu];
+      if (k > 0) acc += (r - o >= 0 ? g.J14[ku + cl] : 0.0) * x[cl];
+    }
+    y[r] = POST ? x[r] + omega * dinv[r] * (b[r] - acc) : acc;
+  }
+}
+
+void launch_sg_apply(const UmGrid& g, const PcgState* st, const double* x, const double* b, const double* dinv,
+                     double omega, double* y, hipStream_t s) {
+  const dim3 gr((unsigned)std::max<int64_t>(1, std::min<int64_t>((g.nv + kBlock - 1) / kBlock, 8192)));
+  if (b) hipLaunchKernelGGL(k_sg_rows<true>, gr, dim3(kBlock), 0, s, g, st, x, b, dinv, omega, y);
+  else hipLaunchKernelGGL(k_sg_rows<false>, gr, dim3(kBlock), 0, s, g, st, x, nullptr, nullptr, 0.0, y);
+}
+
 // SELL rows -> the stencil slots of a structured-topology mesh: all 27, or
 // (half) the upper 14 (X zeroed first; a row's padding entries -- column r,
 // value 0 -- add 0 to its centre; the lower entries of a half stencil are the

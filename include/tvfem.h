@@ -208,8 +208,8 @@ typedef struct {
  * ThermoViscoProblem.py:343-346; PETSc's GAMG is not reproducible here):
  *   JACOBI  point Jacobi (the oracle's PETSc KSPCG + PCJACOBI restatement; the
  *           Krylov iteration counts the parity tests compare);
- *   GMG     geometric multigrid V-cycle on the box hierarchy (3D CG1
- *           rectilinear meshes on one partition): the box coarsened by two
+ *   GMG     geometric multigrid V-cycle on the box hierarchy (3D CG1 and DG1
+ *           rectilinear meshes, one partition or slabs): the box coarsened by two
  *           along every axis with an even cell count until the coarsest level
  *           is mass-dominated (dt alpha / h^2 <= 0.5) or cannot coarsen, damped
  *           Jacobi smoothing (Gershgorin-bounded weight), coarse operators
@@ -218,7 +218,10 @@ typedef struct {
  *           iterations per solve at C4. */
 #define TV_PC_JACOBI 0
 #define TV_PC_GMG 1
-#define TV_PC_AMG 2   /* smoothed-aggregation AMG (csrc/tv_amg.cpp), the PCGAMG of ThermoViscoProblem.py:344 */
+#define TV_PC_AMG 2   /* algebraic multigrid (csrc/tv_amg.cpp), the PCGAMG of ThermoViscoProblem.py:344:
+                         smoothed aggregation; on a mesh with structured topology
+                         (one partition) index-space geometric transfers with
+                         Galerkin coarse operators */
 
 /* Model semantics.  REFERENCE reproduces the reference as it runs, quirks
  * included.  PAPER (opt-in, never the default) applies

@@ -20,6 +20,11 @@ Algorithm (each step as tv_amg.cpp states it):
   * coarse weights omega_l = 2 / (1.1 lambda_max(D^-1 A_l)) (20 Lanczos steps);
     level-0 weight 2 / (1.1 lambda_max(D^-1 J(T))) (30 iterations, the
     device's mg_dg_lambda);
+  * structured topology (build(V, dims=(N0, N1, N2)), vertex i + N0 (j + N1 k)):
+    P = the geometric prolongation of the index space instead (tv_amg.cpp
+    geometric_p: every other vertex kept per axis plus the last when the cell
+    count is odd, the others at 1/2 from their two kept neighbours), every
+    coarse level again a structured grid;
   * cycle: z = omega0 D0^-1 r + P_0 V_1(R_0 r); V_l: x = omega D^-1 b,
     w = A x, b_c = R (b - w), x += P V_{l+1}(b_c), x += omega D^-1 (b - A x);
     the coarsest level x = omega D^-1 b.
@@ -135,7 +140,24 @@ def aggregate(A):
     return agg, na
 
 
-def build(V, max_levels=12):
+def geometric_p1(n):
+    """1D index-space prolongation of n nodes (tv_amg.cpp geometric_p, per axis)."""
+    keep = list(range(0, n, 2))
+    if keep[-1] != n - 1:
+        keep.append(n - 1)
+    pos = {f: c for c, f in enumerate(keep)}
+    rows, cols, vals = [], [], []
+    for i in range(n):
+        if i in pos:
+            rows.append(i), cols.append(pos[i]), vals.append(1.0)
+        else:
+            rows += [i, i]
+            cols += [pos[i - 1], pos[i + 1]]
+            vals += [0.5, 0.5]
+    return sp.csr_matrix((vals, (rows, cols)), shape=(n, len(keep))), len(keep)
+
+
+def build(V, max_levels=12, dims=None):
     """The hierarchy below the fine level: list of (A_l, P_l, R_l, dinv_l, omega_l)."""
     A = sp.csr_matrix(V)
     A.eliminate_zeros()
@@ -143,12 +165,19 @@ def build(V, max_levels=12):
     levels = []
     while len(levels) + 1 < max_levels and A.shape[0] > COARSE_ROWS:
         dinv = 1.0 / A.diagonal()
-        agg, na = aggregate(A)
-        if na < 1 or na * 10 > A.shape[0] * 7:
-            break
-        lam = lam_max_host(A, dinv, 20)
-        P0 = sp.csr_matrix((np.ones(A.shape[0]), (np.arange(A.shape[0]), agg)), shape=(A.shape[0], na))
-        P = sp.csr_matrix(P0 - (4.0 / (3.0 * lam)) * (sp.diags(dinv) @ (A @ P0)))
+        if dims is not None:
+            (Px, cx), (Py, cy), (Pz, cz) = (geometric_p1(n) for n in dims)
+            P = sp.csr_matrix(sp.kron(Pz, sp.kron(Py, Px)))
+            if P.shape[1] * 10 > A.shape[0] * 7:
+                break
+            dims = (cx, cy, cz)
+        else:
+            agg, na = aggregate(A)
+            if na < 1 or na * 10 > A.shape[0] * 7:
+                break
+            lam = lam_max_host(A, dinv, 20)
+            P0 = sp.csr_matrix((np.ones(A.shape[0]), (np.arange(A.shape[0]), agg)), shape=(A.shape[0], na))
+            P = sp.csr_matrix(P0 - (4.0 / (3.0 * lam)) * (sp.diags(dinv) @ (A @ P0)))
         P.data = P.data.astype(np.float32).astype(np.float64)  # the device stores the transfers in float32
         R = sp.csr_matrix(P.T)
         Ac = sp.csr_matrix(R @ (A @ P))

@@ -63,8 +63,10 @@ def test_amg_restatement_builds_a_spd_hierarchy():
 # the third is a stretched plate (cells 0.5 x 0.1 x 0.05, aspect ratio 10), whose
 # clustered top eigenvalues a power-iteration estimate of lambda_max
 # under-estimates (the weights 2 / (1.1 lambda) must stay below 2 / lambda_max)
+# "structured": a plane-by-plane numbered plate (structured topology): the
+# geometric index-space transfers (tv_amg.cpp geometric_p) instead of aggregation
 VCYCLE_CASES = {"two_levels": ((16, 14, 12), (2.0, 2.0, 1.0)), "three_levels": ((56, 56, 40), (4.0, 4.0, 3.0)),
-                "stretched": ((60, 10, 5), (30.0, 1.0, 0.25))}
+                "stretched": ((60, 10, 5), (30.0, 1.0, 0.25)), "structured": ((40, 36, 12), (4.0, 4.0, 1.0))}
 
 
 @pytest.mark.gpu
@@ -73,7 +75,8 @@ def test_amg_vcycle_matches_restatement(case):
     torch = _torch()
     from tvfem.problem import ThermoViscoProblem
     n, L = VCYCLE_CASES[case]
-    m = _mesh(n, L, seed=2)
+    structured = case == "structured"
+    m = _mesh(n, L, seed=2, shuffle=not structured)
     mp = dict(O.MAIN_MODEL_PARAMS)
     p = ThermoViscoProblem(m, (0.0, 1.0), 0.1, {"T": CG, "sigma": CG}, mp, verbose=False, preconditioner="amg")
     p.setup()
@@ -85,7 +88,7 @@ def test_amg_vcycle_matches_restatement(case):
     om = _omesh(m)
     V = O.HeatForm(O.Space(om, "CG"), 0.1, O.ThermalParams.from_dict({**mp, "epsilon": 0.0, "htc": 0.0})).jacobian(T)
     J = O.HeatForm(O.Space(om, "CG"), 0.1, O.ThermalParams.from_dict(mp)).jacobian(T)
-    levels = OA.build(V)
+    levels = OA.build(V, dims=tuple(c + 1 for c in n) if structured else None)
     d0 = 1.0 / J.diagonal()
     om0 = 2.0 / (1.1 * OA.lam_max_device(J, d0))
     r, y = rng.standard_normal((2, nv))
@@ -100,7 +103,7 @@ def test_amg_vcycle_matches_restatement(case):
     sym = abs(y @ z_r - r @ z_y) / abs(y @ z_r)
     print(f"[amg] V-cycle {case}: {len(levels) + 1} levels ({[lv[0].shape[0] for lv in levels]}), vs numpy {e:.2e}, "
           f"symmetry {sym:.1e}")
-    assert len(levels) + 1 == {"two_levels": 2, "three_levels": 3, "stretched": 2}[case]
+    assert len(levels) + 1 == {"two_levels": 2, "three_levels": 3, "stretched": 2, "structured": 3}[case]
     assert e < 1e-10, e
     assert sym < 1e-12, sym
     assert r @ z_r > 0.0
