@@ -19,6 +19,12 @@ oracle cannot run a Newton solve at these sizes in a test's time):
     Jacobi give the same T (Newton to 1e-12 either way, so only the Krylov
     iterates differ) and the same Newton count, and the converged residual is
     small against the first one.
+
+C4 and C5 at full size are also pinned to the C/OpenMP port of the oracle
+(oracle/tv_cpu.c, itself pinned to the numpy oracle by tests/test_cpu_port.py):
+two coupled steps of the whole 8M-dof plate on both, the same Newton counts,
+T, phi and Tf at 1e-10, xi and sigma by check_field
+(test_fullsize_step_pinned_to_cpu_port).
 """
 import numpy as np
 import pytest
@@ -176,3 +182,45 @@ def test_c3_fullsize_steps_pinned_to_oracle(pc):
         check_field("xi", dev.get_field("xi"), ref.functions["xi"], mT, min_frac=0.9)
         check_field("sigma", dev.get_field("sigma"), ref.functions_next["sigma"], mT, bs=9, min_frac=0.9)
     dev.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["C4", "C5"])
+def test_fullsize_step_pinned_to_cpu_port(case):
+    """One coupled step of C4 (CG1, 8.2M dofs) / C5 (DG1, 8M dofs) on the GPU
+    (the bench's GMG) and on the oracle's C/OpenMP port (GMG for CG1, Jacobi for
+    DG1: the preconditioner moves only the Krylov iterates, Newton converges to
+    1e-12 either way): the same Newton count, T / phi / Tf to 1e-10, xi and
+    sigma on the dofs whose temperature moved (parity_util.check_field).
+    part_axis=2 keeps the device's storage order equal to the port's dof order."""
+    _torch()
+    from parity_util import check_field, cond_mask, relerr
+    from oracle import tv_cpu
+    fam, nc = SIZES[case]
+    p = _problem(fam, nc, "gmg", part_axis=2)
+    p.setup()
+    T0 = p.get_field("T")
+    p.solve_timestep()
+    dev = {k: p.get_field(k) for k in ("T", "phi", "xi", "Tf", "sigma")}
+    nd = p.last_newton_iterations
+    p.close()
+    axes = [np.linspace(0.0, l, n + 1) for l, n in zip(L, nc)]
+    cpu = tv_cpu.CpuProblem(axes, dict(O.MAIN_MODEL_PARAMS), 0.1, fam, pc="gmg" if fam == "CG" else "jacobi")
+    try:
+        nit, kit = cpu.step()
+        nl = 8
+
+        def host(a, bs=1):  # port layout (DG: l * ncell + cell) -> the problem's (cell-major)
+            return a if fam == "CG" else a.reshape(nl, -1, bs).transpose(1, 0, 2).reshape(-1)
+        ref = {k: host(cpu.get(k), 9 if k == "sigma" else 1) for k in ("T", "phi", "xi", "Tf", "sigma")}
+    finally:
+        cpu.close()
+    errs = {k: relerr(dev[k], ref[k]) for k in ("T", "phi", "Tf")}
+    print(f"[fullsize] {case} vs CPU port: Newton {nd} / {nit}, Krylov (port) {kit}, "
+          + ", ".join(f"{k} {v:.1e}" for k, v in errs.items()))
+    assert nd == nit, (nd, nit)
+    for k, v in errs.items():
+        assert v < 1e-10, (k, v)
+    mT, _ = cond_mask(ref["T"], T0)
+    check_field(f"xi[{case} full size, cpu port]", dev["xi"], ref["xi"], mT, min_frac=0.9)
+    check_field(f"sigma[{case} full size, cpu port]", dev["sigma"], ref["sigma"], mT, bs=9, min_frac=0.9)
