@@ -436,8 +436,11 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
       if (MODE == UM_DIAG) val = g.vdiag[r];
       else if (MODE == UM_RES) val = (acc + acc2) - g.dt_f * g.bvec[r];
       else val = acc;
-      if (MODE == UM_RES || MODE == UM_DIAG || g.J14 == nullptr)  // (J14: folded in)
-        val += robin_row<D, MODE>(g, r, (MODE == UM_RES) ? u : T, xget);
+      // Robin terms: the residual's in a pass over the boundary rows of their
+      // own (k_um_robin_res: no divergent facet quadrature in this kernel's
+      // waves); the Jacobian's folded into J14 on structured topology
+      if (MODE == UM_DIAG || (MODE != UM_RES && g.J14 == nullptr))
+        val += robin_row<D, MODE>(g, r, T, xget);
       if (MODE == UM_DIAG && invert) val = 1.0 / val;
       if (MODE == UM_FUSED) pw += u[r] * val;
       out[r] = val;
@@ -467,6 +470,18 @@ __global__ __launch_bounds__(kBlock) void k_um_pvec(int64_t n, const PcgState* _
   const double* po = (it_host & 1) ? pA : pB;
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock)
     p[t] = first ? z[t] : z[t] + b * po[t];
+}
+
+// the residual's Robin terms (ThermoViscoProblem.py:302-304) on the boundary rows,
+// added to the cell part k_um_rows<UM_RES> wrote: F[r] = (cell part) + Robin,
+// the same association as a single pass
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_um_robin_res(UmGrid g, const double* __restrict__ u, double* __restrict__ F) {
+  auto xget = [&](int64_t c) -> double { return u[c]; };
+  for (int64_t b = blockIdx.x * (int64_t)kBlock + threadIdx.x; b < g.nbr; b += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = g.brow[b];
+    F[r] += robin_row<D, UM_RES>(g, r, u, xget);
+  }
 }
 
 // the owned values the neighbours hold as ghosts, gathered into the send buffer
@@ -515,6 +530,10 @@ int64_t um_boundary_vertices(const UmDevice* d, std::vector<unsigned char>& mask
 
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
   launch_rows<UM_RES>(g, T, T, Tp, F, nullptr, nullptr, RedTail{}, 0, s);
+  if (g.nbr == 0) return;
+  const dim3 gr((unsigned)std::max<int64_t>(1, std::min<int64_t>((g.nbr + kBlock - 1) / kBlock, 4096)));
+  if (g.dim == 2) hipLaunchKernelGGL(k_um_robin_res<2>, gr, dim3(kBlock), 0, s, g, T, F);
+  else hipLaunchKernelGGL(k_um_robin_res<3>, gr, dim3(kBlock), 0, s, g, T, F);
 }
 
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s) {
@@ -951,11 +970,13 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
     hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V14, 1);
     UMC(hipGetLastError());
     UMC(hipMemcpyAsync(J14, V14, sizeof(double) * n14, hipMemcpyDeviceToDevice, s));
+  }
+  {  // the owned rows with boundary incidences (the Robin passes)
     std::vector<int64_t> brow;
-    for (int64_t v = 0; v < nv; ++v)
+    for (int64_t v = 0; v < nrow; ++v)
       if (boff[(size_t)v + 1] > boff[(size_t)v]) brow.push_back(v);
     nbr = (int64_t)brow.size();
-    if (um_upload(d, brow, &brow_d, err)) return 1;
+    if (nbr > 0 && um_upload(d, brow, &brow_d, err)) return 1;
   }
   UMC(hipStreamSynchronize(s));
   // setup-only arrays
