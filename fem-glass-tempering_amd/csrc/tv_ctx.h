@@ -224,6 +224,7 @@ struct Ctx {
   // pattern of counts, e.g. 6 5 5 4: the previous solve's count over-queues
   // early-exit iterations, ~25 launches each), and the index of the current one
   int mg_hint[16] = {0};
+  int jac_hint[16] = {0};  // the same for the Jacobi-PCG solves
   int newton_k = 0;
   int newton_pred = 0;  // the previous step's Newton count (speculative residual, newton())
 

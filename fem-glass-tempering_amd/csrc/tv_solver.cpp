@@ -161,7 +161,12 @@ int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   // the host's turnaround (~30 us) is well inside one iteration (~130 us at C4),
   // and every iteration queued past convergence costs two early-exit launches
   const int small = std::max(1, c->O.pcg_batch / 8);
-  if (int e = enqueue(std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
+  // first batch: one short of the count this Newton index took in the last
+  // step (the counts repeat from step to step, and decrease along a step's
+  // Newton iterations, so the previous solve's count over-queues)
+  const int hk = std::min(c->newton_k, 15);
+  const int hint = c->jac_hint[hk] > 0 ? c->jac_hint[hk] : c->pcg_hint;
+  if (int e = enqueue(std::max(1, hint > 4 ? hint - 1 : c->O.pcg_batch), 0)) return e;
   for (;;) {
     if (int e = enqueue(small, slot ^ 1)) return e;
     HIPC(hipEventSynchronize(c->evp[slot]));
@@ -174,6 +179,7 @@ int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   *reason = c->h_st[slot].reason;
   launch_pcg_dx_tail(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
   c->pcg_hint = c->h_st[slot].it;
+  c->jac_hint[hk] = c->pcg_hint;
   if (c->ktime) {  // productive iterations only (launches queued behind convergence exit at once)
     for (int it = 0; it < *its; it += c->kstride)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
@@ -241,7 +247,9 @@ int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
   // every poll (see pcg_solve); multi-rank the state lags one launch
   const int lag = multi_rank(c) ? 1 : 0;
   const int small = 1 + lag;
-  if (int e = enqueue(1 + std::max(1, c->pcg_hint > 4 ? c->pcg_hint - 3 : c->O.pcg_batch), 0)) return e;
+  const int hk = std::min(c->newton_k, 15);  // as pcg_solve: this Newton index's count in the last step
+  const int hint = c->jac_hint[hk] > 0 ? c->jac_hint[hk] : c->pcg_hint;
+  if (int e = enqueue(1 + std::max(1, hint > 4 ? hint - 1 : c->O.pcg_batch), 0)) return e;
   for (;;) {
     if (int e = enqueue(small, slot ^ 1)) return e;
     HIPC(hipEventSynchronize(c->evp[slot]));
@@ -252,6 +260,7 @@ int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
   *its = c->h_st[slot].it;
   *reason = c->h_st[slot].reason;
   c->pcg_hint = *its;
+  c->jac_hint[hk] = *its;
   if (c->ktime) {
     for (int it = 1; it <= *its; it += c->kstride)  // productive iterations (iteration 0 is the init launch)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);

@@ -22,7 +22,11 @@ rows = list(csv.DictReader(open(os.path.join(prof, "run_kernel_trace.csv"))))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 pats = {"pcg_matvec_fused": "k_cg_march<1, true", "pcg_update": "k_pcg_update<", "visco_update": "k_visco_fused<"}
 
-visco_end = [int(r["End_Timestamp"]) for r in rows if pats["visco_update"] in r["Kernel_Name"]]
+vis = [r for r in rows if pats["visco_update"] in r["Kernel_Name"]]
+dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in vis]
+# the updates that ran: a step's end is queued speculatively, gated on the
+# device's Newton test, and a gated-off launch exits at once
+visco_end = [int(r["End_Timestamp"]) for r, d in zip(vis, dur) if d > 0.2 * max(dur)]
 w, k = bench["warmup"], bench["steps"]
 window = (visco_end[w - 1] if w > 0 else 0, visco_end[w + k - 1]) if len(visco_end) >= w + k else None
 
