@@ -161,12 +161,13 @@ int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
   // the host's turnaround (~30 us) is well inside one iteration (~130 us at C4),
   // and every iteration queued past convergence costs two early-exit launches
   const int small = std::max(1, c->O.pcg_batch / 8);
-  // first batch: one short of the count this Newton index took in the last
-  // step (the counts repeat from step to step, and decrease along a step's
-  // Newton iterations, so the previous solve's count over-queues)
+  // first batch: the count this Newton index took in the last step (the counts
+  // repeat from step to step, and decrease along a step's Newton iterations,
+  // so the previous solve's count over-queues; measured: previous count - 3
+  // C2 0.97-0.99 ms, this index's count - 1 0.90-0.92, its count 0.88-0.89)
   const int hk = std::min(c->newton_k, 15);
   const int hint = c->jac_hint[hk] > 0 ? c->jac_hint[hk] : c->pcg_hint;
-  if (int e = enqueue(std::max(1, hint > 4 ? hint - 1 : c->O.pcg_batch), 0)) return e;
+  if (int e = enqueue(std::max(1, hint > 4 ? hint : c->O.pcg_batch), 0)) return e;
   for (;;) {
     if (int e = enqueue(small, slot ^ 1)) return e;
     HIPC(hipEventSynchronize(c->evp[slot]));
@@ -249,7 +250,7 @@ int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
   const int small = 1 + lag;
   const int hk = std::min(c->newton_k, 15);  // as pcg_solve: this Newton index's count in the last step
   const int hint = c->jac_hint[hk] > 0 ? c->jac_hint[hk] : c->pcg_hint;
-  if (int e = enqueue(1 + std::max(1, hint > 4 ? hint - 1 : c->O.pcg_batch), 0)) return e;
+  if (int e = enqueue(1 + std::max(1, hint > 4 ? hint : c->O.pcg_batch), 0)) return e;
   for (;;) {
     if (int e = enqueue(small, slot ^ 1)) return e;
     HIPC(hipEventSynchronize(c->evp[slot]));
