@@ -70,9 +70,10 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
         break;
       }
       // level 0: J x0 (16), restriction reads r, w (16), prolongation x0 -> x (16),
-      // then CG: J x with the post-smoothing in its epilogue (x, r, dinv in, z out: 32),
+      // then CG: J x with the post-smoothing in its epilogue (x, r in, z out: 24;
+      // D^-1 formed in the kernel off the physical boundary),
       // DG: J x (16) + the cell-block post-smoothing (x0, r, w in, z out: 32)
-      double b = (c->mg_dg ? 16.0 + 16 + 16 + 16 + 32 : 16.0 + 16 + 16 + 32) * n;
+      double b = (c->mg_dg ? 16.0 + 16 + 16 + 16 + 32 : 16.0 + 16 + 16 + 24) * n;
       for (size_t l = 0; l < c->mg.size(); ++l) {
         const double nl = (double)c->mg[l].n;
         b += 24.0 * nl;  // the restriction's outputs b, x (pre-smoothing) and the dinv it reads
