@@ -219,7 +219,7 @@ struct UmGrid {
   // slot q of row r is the upper slot 26 - q of row r + o_q (read from the
   // neighbour row's stream, a cache hit): 112 B per row and operator from HBM
   // instead of ~330 B of SELL.  J14 = V14 with the Robin facet Jacobian of J(T)
-  // folded into the boundary rows' slots (launch_um_robin27, once per Newton
+  // folded into the boundary rows' slots (launch_um_robin_fold, once per Newton
   // iteration): the J x kernels then run no facet quadrature (brow: the nbr
   // boundary rows).  nullptr: SELL only (the residual always runs on SELL).
   const double* V14;
@@ -290,7 +290,7 @@ void launch_sg_apply(const UmGrid& g, const PcgState* st, const double* x, const
                      double omega, double* y, hipStream_t s);
 // J14 <- V14 + the Robin facet Jacobian at T (structured topology; a no-op else):
 // before the J x launches of a Newton iteration (J(T) is fixed inside a solve)
-void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s);
+void launch_um_robin_fold(const UmGrid& g, const double* T, hipStream_t s);
 void launch_um_diag(const UmGrid& g, const double* T, double* d, int invert, hipStream_t s);
 // p <- z + beta p (iteration it_host's parity buffer), w <- J p, p.w; the
 // reduction tail (rt.counter != nullptr) reduces the records and runs the

@@ -105,7 +105,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
   // the J x of a solve: on a structured-topology unstructured mesh the Robin
   // terms at the current T are folded into the stencil once (as each Newton
   // iteration does), and the matvec alone is timed
-  if (c->um && (kernel == 0 || kernel == 10)) launch_um_robin27(c->umg, c->f[TV_F_T].ptr, c->stream);
+  if (c->um && (kernel == 0 || kernel == 10)) launch_um_robin_fold(c->umg, c->f[TV_F_T].ptr, c->stream);
   auto jx = [&]() {
     if (c->um) launch_um_japply(c->umg, c->f[TV_F_T].ptr, c->pA, c->w, c->stream);
     else op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr);

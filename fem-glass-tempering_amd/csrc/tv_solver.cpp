@@ -23,7 +23,7 @@ void op_diag(Ctx* c, const double* T, double* d, int invert) {
 }
 void op_japply(Ctx* c, const double* T, const double* x, double* y, double* partials, int* np) {
   if (c->um) {  // (structured topology: the Robin terms at this T folded into the stencil first)
-    launch_um_robin27(c->umg, T, c->stream);
+    launch_um_robin_fold(c->umg, T, c->stream);
     launch_um_japply(c->umg, T, x, y, c->stream);
   }
   else if (c->fam_T == TV_CG) launch_cg_japply(c->cg, T, x, y, partials, np, c->stream);
@@ -400,7 +400,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
         c->dinv_interior = true;
       } else {
         op_diag(c, T, c->dinv, 1);
-        if (c->um) launch_um_robin27(c->umg, T, c->stream);  // J(u) of the solve (structured topology)
+        if (c->um) launch_um_robin_fold(c->umg, T, c->stream);  // J(u) of the solve (structured topology)
       }
     }
     dinv_fresh = false;

@@ -561,7 +561,7 @@ int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, do
 // facet's vertices (race-free: a row's slots belong to its thread; the lower
 // couplings are the upper slots of the facet's other rows, which are boundary
 // rows too)
-__global__ __launch_bounds__(kBlock) void k_um_robin27(UmGrid g, const double* __restrict__ T) {
+__global__ __launch_bounds__(kBlock) void k_um_robin_fold(UmGrid g, const double* __restrict__ T) {
   constexpr int NF = 4, NQ = 9;
   for (int64_t b = blockIdx.x * (int64_t)kBlock + threadIdx.x; b < g.nbr; b += (int64_t)gridDim.x * kBlock) {
     const int64_t r = g.brow[b];
@@ -607,10 +607,10 @@ __global__ __launch_bounds__(kBlock) void k_um_robin27(UmGrid g, const double* _
   }
 }
 
-void launch_um_robin27(const UmGrid& g, const double* T, hipStream_t s) {
+void launch_um_robin_fold(const UmGrid& g, const double* T, hipStream_t s) {
   if (g.J14 == nullptr || g.nbr == 0) return;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.nbr + kBlock - 1) / kBlock, 4096));
-  hipLaunchKernelGGL(k_um_robin27, dim3(nb), dim3(kBlock), 0, s, g, T);
+  hipLaunchKernelGGL(k_um_robin_fold, dim3(nb), dim3(kBlock), 0, s, g, T);
 }
 
 // A structured grid's operator as a half stencil (the coarse levels of the
