@@ -386,17 +386,20 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
       // row r (column r + o) and of row r - o (its column r: the lower slot of
       // row r).  Absent neighbours hold zeros; a row outside the mesh reads nothing.
       if (r < g.nv) {
-        // fully unrolled (127 VGPRs, 4 waves per SIMD: every slot's loads in
-        // flight; unrolled by 2, 64 VGPRs: 524 vs 388 us per J x at 8.2M rows)
+        // fully unrolled (every slot's loads in flight; unrolled by 2, 64 VGPRs:
+        // 524 vs 388 us per J x at 8.2M rows); 32-bit unsigned element indices
+        // (14 nv elements < 2^32 / 8, checked at setup)
+        const double* __restrict__ J = g.J14;
+        const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2, ru = (unsigned)r;
 #pragma unroll
         for (int k = 0; k < 14; ++k) {
           const int q = 13 + k;
-          const int64_t o = (int64_t)(q % 3 - 1) + g.s1 * ((q / 3) % 3 - 1) + g.s2 * (q / 9 - 1);
-          const int64_t cu = r + o < g.nv ? r + o : r;
-          const int64_t cl = r - o >= 0 ? r - o : r;
-          const int64_t ku = (int64_t)k * g.nv;
-          acc += g.J14[ku + r] * u[cu];
-          if (k > 0) acc += (r - o >= 0 ? g.J14[ku + cl] : 0.0) * u[cl];
+          const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
+          const bool hi = ru + o < nv, lo = ru >= o;
+          const unsigned cu = hi ? ru + o : ru, cl = lo ? ru - o : ru;
+          const unsigned ku = (unsigned)k * nv;
+          acc += J[ku + ru] * u[cu];
+          if (k > 0) acc += (lo ? J[ku + cl] : 0.0) * u[cl];
         }
       }
     } else if (MODE == UM_RES) {
@@ -494,6 +497,83 @@ int row_blocks(const UmGrid& g) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((g.nslice + 3) / 4, kUmBlocksMax));
 }
 
+// Structured topology: the half-stencil J x with one wave per column of rows --
+// an x segment of 64 vertices at row j -- marching the planes k (in kch chunks
+// of the plane axis).  Row r's lower slots a plane back are the upper slots of
+// rows this wave read one plane step earlier (L1 / L2 hits; in row order they
+// come back ~160K rows later and miss, 72 B per row), and the neighbouring
+// columns j +- 1 run on the same XCD (consecutive waves).
+struct March14 {
+  int64_t n0, n1, n2;
+  int nseg, kch, kper;
+  int64_t ncol;
+};
+March14 march14(const UmGrid& g) {
+  March14 m;
+  m.n0 = g.s1;
+  m.n1 = g.s2 / g.s1;
+  m.n2 = g.nv / g.s2;
+  m.nseg = (int)((m.n0 + 63) / 64);
+  m.ncol = (int64_t)m.nseg * m.n1;
+  // enough waves for the chip (>= ~4K), at most 4 chunks of the plane axis
+  m.kch = (int)std::max<int64_t>(1, std::min<int64_t>({4, m.n2, (4096 + m.ncol - 1) / m.ncol}));
+  m.kper = (int)((m.n2 + m.kch - 1) / m.kch);
+  return m;
+}
+int march_blocks(const UmGrid& g) {
+  if (g.J14 == nullptr) return 1;
+  const March14 m = march14(g);
+  return (int)std::max<int64_t>(1, std::min<int64_t>((m.ncol * m.kch + 3) / 4, kUmBlocksMax));
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_um_march14(UmGrid g, March14 m, const double* __restrict__ u,
+                                                       double* __restrict__ out, const PcgState* __restrict__ st,
+                                                       double* __restrict__ partials, RedTail rt) {
+  if (MODE == UM_FUSED && st->done) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int WPB = kBlock / 64;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  double pw = 0.0;
+  for (int64_t gw = (int64_t)blk * WPB + wave; gw < m.ncol * m.kch; gw += nw) {
+    const int64_t seg = gw % m.nseg, t = gw / m.nseg;  // segment fastest, then row j, then chunk
+    const int64_t j = t % m.n1, ch = t / m.n1;
+    const int64_t i = seg * 64 + lane;
+    if (i >= m.n0) continue;
+    const int64_t k1 = std::min<int64_t>(m.n2, (ch + 1) * m.kper);
+    // 32-bit unsigned element indices (14 nv < 2^31 and 8 x that < 2^32: checked
+    // at setup): uniform base + 32-bit offset loads, no 64-bit address VGPRs
+    const double* __restrict__ J = g.J14;
+    const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2;
+#pragma unroll 1
+    for (int64_t k = ch * m.kper; k < k1; ++k) {
+      const unsigned r = (unsigned)(i + m.n0 * j + g.s2 * k);
+      double acc = 0.0;
+#pragma unroll
+      for (int q14 = 0; q14 < 14; ++q14) {
+        const int q = 13 + q14;
+        const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
+        const bool hi = r + o < nv, lo = r >= o;  // (o >= 0 for the upper slots)
+        const unsigned cu = hi ? r + o : r, cl = lo ? r - o : r;
+        const unsigned ku = (unsigned)q14 * nv;
+        acc += J[ku + r] * u[cu];
+        if (q14 > 0) acc += (lo ? J[ku + cl] : 0.0) * u[cl];
+      }
+      out[r] = acc;
+      if (MODE == UM_FUSED) pw += u[r] * acc;
+    }
+  }
+  if (MODE == UM_FUSED) {
+    __shared__ double red[WPB];
+    const double sw = wave_sum64(pw);
+    if (lane == 0) red[wave] = sw;
+    __syncthreads();
+    if (threadIdx.x == 0) store_partial(&partials[blockIdx.x], (red[0] + red[1]) + (red[2] + red[3]));
+    fused_reduce_tail<1>(rt, gridDim.x);
+  }
+}
+
 template <int MODE>
 void launch_rows(const UmGrid& g, const double* T, const double* u, const double* up, double* out,
                  const PcgState* st, double* partials, const RedTail& rt, int invert, hipStream_t s) {
@@ -506,7 +586,7 @@ void launch_rows(const UmGrid& g, const double* T, const double* u, const double
 
 }  // namespace
 
-int um_num_blocks(const UmGrid& g) { return row_blocks(g); }
+int um_num_blocks(const UmGrid& g) { return std::max(row_blocks(g), march_blocks(g)); }
 Sell um_operator(const UmGrid& g) {
   Sell m;
   m.nrow = g.nrow;
@@ -537,6 +617,11 @@ void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, doub
 }
 
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s) {
+  if (g.J14 != nullptr) {
+    hipLaunchKernelGGL(k_um_march14<UM_JAC>, dim3(march_blocks(g)), dim3(kBlock), 0, s, g, march14(g), x, y,
+                       nullptr, nullptr, RedTail{});
+    return;
+  }
   launch_rows<UM_JAC>(g, T, x, nullptr, y, nullptr, nullptr, RedTail{}, 0, s);
 }
 
@@ -550,6 +635,11 @@ int launch_um_japply_fused(const UmGrid& g, const double* T, const double* z, do
   const int vb = (int)std::max<int64_t>(1, std::min<int64_t>((g.nv + kBlock - 1) / kBlock, 2048));
   hipLaunchKernelGGL(k_um_pvec, dim3(vb), dim3(kBlock), 0, s, g.nv, st, z, pA, pB, it_host, rt);
   const double* p = (it_host & 1) ? pB : pA;
+  if (g.J14 != nullptr) {
+    const int nb = march_blocks(g);
+    hipLaunchKernelGGL(k_um_march14<UM_FUSED>, dim3(nb), dim3(kBlock), 0, s, g, march14(g), p, w, st, partials, rt);
+    return nb;
+  }
   launch_rows<UM_FUSED>(g, T, p, nullptr, w, st, partials, rt, 0, s);
   return row_blocks(g);
 }
@@ -963,7 +1053,8 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   int64_t ss1 = 0, ss2 = 0, nbr = 0;
   double *V14 = nullptr, *J14 = nullptr;
   int64_t* brow_d = nullptr;
-  if (nrow == nv && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
+  // (32-bit element offsets into the 14 slot arrays: 14 nv * 8 B < 4 GiB)
+  if (nrow == nv && nv * 14 * 8 < ((int64_t)1 << 32) && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
     const size_t n14 = (size_t)14 * nv;
     if (um_alloc(d, n14, &V14, err) || um_alloc(d, n14, &J14, err)) return 1;
     UMC(hipMemsetAsync(V14, 0, sizeof(double) * n14, s));
