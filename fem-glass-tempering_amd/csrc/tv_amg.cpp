@@ -541,6 +541,7 @@ static int amg_build(Ctx* c, Csr A, int64_t row0, int64_t nrow, const int64_t* g
   while ((int)c->amg.size() + 1 < max_levels && A.n > kAmgCoarseRows) {
     int64_t na = 0;
     Csr P;
+    int64_t fdims[3] = {dims[0], dims[1], dims[2]};
     if (grid) {
       int64_t cd[3];
       P = geometric_p(dims, cd);
@@ -589,6 +590,15 @@ static int amg_build(Ctx* c, Csr A, int64_t row0, int64_t nrow, const int64_t* g
     // a geometric level's operator is a 27-point stencil of a structured grid:
     // applied as a half stencil (112 B per row instead of ~12 B x 27 of SELL)
     if (grid) half_stencil(c, Ac, dims, L.sg);
+    // level 0's transfers by index arithmetic (stored as SELL they were the
+    // cycle's largest streams: V-cycle 472-475 -> 320-324 us at distorted C4)
+    if (grid && c->amg.size() == 1 && !part) {
+      L.geo0 = true;
+      for (int a = 0; a < 3; ++a) {
+        L.gfine[a] = fdims[a];
+        L.gcoarse[a] = dims[a];
+      }
+    }
     const std::vector<double> dc = diag_inv(Ac);
     for (double v : dc)
       if (!(v > 0.0) || !std::isfinite(v)) return c->fail(TV_ERR_ARG, "AMG: coarse operator not positive definite");
@@ -736,10 +746,14 @@ int amg_apply0(Ctx* c, const RedTail* tail) {
     launch_amg_restrict(L1.R, c->st, c->r, nullptr, nullptr, 0.0, L1.b, nullptr, c->stream);
     if (int e = allreduce_vec(c, L1.b, L1.n)) return -e;
     launch_mg_jacobi(L1.n, c->st, L1.b, nullptr, nullptr, L1.dinv, L1.omega, L1.x, 0, c->stream);
+  } else if (L1.geo0) {
+    launch_geo_restrict0(L1.gfine, L1.gcoarse, c->st, c->r, L1.dinv, L1.omega, L1.b, L1.x, c->stream);
   } else {
     launch_amg_restrict(L1.R, c->st, c->r, nullptr, L1.dinv, L1.omega, L1.b, L1.x, c->stream);
   }
   const double* x1 = amg_level(c, 1);
+  if (L1.geo0)
+    return launch_geo_prolong0(L1.gfine, L1.gcoarse, c->st, x1, c->mgx, c->r, c->z, c->partials, tail, c->stream);
   return launch_amg_prolong0(L1.P, c->st, x1, c->mgx, c->r, c->z, c->partials, tail, c->stream);
 }
 
@@ -750,8 +764,11 @@ int amg_apply0(Ctx* c, const RedTail* tail) {
 double amg_cycle_bytes(const Ctx* c) {
   const double n0 = (double)c->nT;
   const AmgLevel& L1 = c->amg[0];
-  double b = 8.0 * (double)L1.r_nnz + 8.0 * n0 + 24.0 * (double)L1.n;         // R_0 (r in; b, x, dinv of level 1)
-  b += 8.0 * (double)L1.p_nnz + 8.0 * (double)L1.n + 24.0 * n0;  // P_0 (x_1 in; x0, r in, z out)
+  // R_0 (r in; b, x, dinv of level 1) and P_0 (x_1 in; x0, r in, z out): stored
+  // transfers, or (geo0) applied by index arithmetic -- the vectors only
+  const double t0 = L1.geo0 ? 0.0 : 8.0;
+  double b = t0 * (double)L1.r_nnz + 8.0 * n0 + 24.0 * (double)L1.n;
+  b += t0 * (double)L1.p_nnz + 8.0 * (double)L1.n + 24.0 * n0;
   for (size_t l = 0; l + 1 < c->amg.size(); ++l) {
     const AmgLevel& L = c->amg[l];
     const AmgLevel& C = c->amg[l + 1];

@@ -74,6 +74,10 @@ struct AmgLevel {
   int64_t n = 0;
   Sell A, P, R;
   UmGrid sg{};  // geometric levels: A as a half stencil (sg.J14 != nullptr: applied so instead of A)
+  // the first geometric level: its grid and the fine one's (the level-0
+  // transfers applied by index arithmetic, launch_geo_*); geo0 = false: SELL P, R
+  bool geo0 = false;
+  int64_t gfine[3] = {0, 0, 0}, gcoarse[3] = {0, 0, 0};
   int64_t a_nnz = 0, p_nnz = 0, r_nnz = 0;
   double omega = 0.0;
   double *dinv = nullptr, *b = nullptr, *x = nullptr, *w = nullptr;

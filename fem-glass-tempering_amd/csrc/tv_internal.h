@@ -284,6 +284,16 @@ int um_rcb(int dim, int64_t nv, const double* xyz, int64_t nc, const int64_t* ce
            std::string& err);
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s);
 void launch_um_japply(const UmGrid& g, const double* T, const double* x, double* y, hipStream_t s);
+// The level-0 transfers of the geometric hierarchy (tv_amg.cpp geometric_p) on
+// a structured grid of fn[0] x fn[1] x fn[2] vertices, its coarse grid cn[],
+// applied by index arithmetic (no stored matrix): b_c = P^T r, x_c = omega_c
+// dinv_c b_c; and z = x0 + P x_c with the (z.z, z.r) records and the KSPCG
+// tail (returns the record count)
+void launch_geo_restrict0(const int64_t (&fn)[3], const int64_t (&cn)[3], const PcgState* st, const double* r,
+                          const double* dinv_c, double omega_c, double* b_c, double* x_c, hipStream_t s);
+int launch_geo_prolong0(const int64_t (&fn)[3], const int64_t (&cn)[3], const PcgState* st, const double* x_c,
+                        const double* x0, const double* r, double* z, double* partials, const RedTail* tail,
+                        hipStream_t s);
 // a structured grid's half-stencil operator (g.J14, g.nv, g.s1, g.s2): y = A x, or
 // with b != nullptr the Jacobi step y = x + omega dinv (b - A x)
 void launch_sg_apply(const UmGrid& g, const PcgState* st, const double* x, const double* b, const double* dinv,

@@ -586,6 +586,174 @@ void launch_rows(const UmGrid& g, const double* T, const double* u, const double
 
 }  // namespace
 
+// A structured grid's half-stencil operator, one row per thread (the small
+// coarse grids of the geometric hierarchy: every row in flight at once);
+// POST: the damped Jacobi step y = x + omega dinv (b - A x)
+template <bool POST>
+__global__ __launch_bounds__(kBlock) void k_sg_rows(UmGrid g, const PcgState* __restrict__ st,
+                                                   const double* __restrict__ x, const double* __restrict__ b,
+                                                   const double* __restrict__ dinv, double omega,
+                                                   double* __restrict__ y) {
+  if (st != nullptr && st->done) return;
+  const double* __restrict__ J = g.J14;
+  const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2;
+  for (unsigned r = blockIdx.x * kBlock + threadIdx.x; r < nv; r += gridDim.x * kBlock) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+      const int q = 13 + k;
+      const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
+      const bool hi = r + o < nv, lo = r >= o;
+      const unsigned cu = hi ? r + o : r, cl = lo ? r - o : r;
+      const unsigned ku = (unsigned)k * nv;
+      acc += J[ku + r] * x[cu];
+      if (k > 0) acc += (lo ? J[ku + cl] : 0.0) * x[cl];
+    }
+    y[r] = POST ? x[r] + omega * dinv[r] * (b[r] - acc) : acc;
+  }
+}
+
+// ---- index-space transfers of the geometric hierarchy (level 0) ----------------
+// per axis: fine node i is kept (a coarse node) when even or the last one; a
+// kept node's coarse index is i / 2, the odd last one's nc - 1; the others
+// interpolate their two kept neighbours at 1/2 (tv_amg.cpp geometric_p)
+struct GeoDims {
+  int f[3], c[3];
+};
+__device__ __forceinline__ int geo_cidx(int i, int nf, int nc) { return (i == nf - 1 && (i & 1)) ? nc - 1 : i >> 1; }
+__device__ __forceinline__ bool geo_kept(int i, int nf) { return !(i & 1) || i == nf - 1; }
+
+// b_c[I] = sum over the (<= 3)^3 fine nodes that interpolate from I, one thread per coarse node
+__global__ __launch_bounds__(kBlock) void k_geo_restrict0(GeoDims d, const PcgState* __restrict__ st,
+                                                          const double* __restrict__ r,
+                                                          const double* __restrict__ dinv_c, double omega_c,
+                                                          double* __restrict__ b_c, double* __restrict__ x_c) {
+  if (st != nullptr && st->done) return;
+  const int64_t nc = (int64_t)d.c[0] * d.c[1] * d.c[2];
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nc; t += (int64_t)gridDim.x * kBlock) {
+    const int ci[3] = {(int)(t % d.c[0]), (int)((t / d.c[0]) % d.c[1]), (int)(t / ((int64_t)d.c[0] * d.c[1]))};
+    int fi[3][3];
+    double wi[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const int nf = d.f[a];
+      const int f = (ci[a] == d.c[a] - 1 && ((nf - 1) & 1)) ? nf - 1 : 2 * ci[a];
+      fi[a][0] = f - 1; fi[a][1] = f; fi[a][2] = f + 1;
+      wi[a][0] = (f - 1 >= 0 && !geo_kept(f - 1, nf)) ? 0.5 : 0.0;
+      wi[a][1] = 1.0;
+      wi[a][2] = (f + 1 < nf && !geo_kept(f + 1, nf)) ? 0.5 : 0.0;
+      if (wi[a][0] == 0.0) fi[a][0] = f;
+      if (wi[a][2] == 0.0) fi[a][2] = f;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        double row = 0.0;
+        const int64_t base = (int64_t)d.f[0] * (fi[1][jj] + (int64_t)d.f[1] * fi[2][kk]);
+#pragma unroll
+        for (int ii = 0; ii < 3; ++ii) row += wi[0][ii] * r[base + fi[0][ii]];
+        acc += (wi[2][kk] * wi[1][jj]) * row;
+      }
+    b_c[t] = acc;
+    if (x_c) x_c[t] = omega_c * dinv_c[t] * acc;
+  }
+}
+
+// z = x0 + P x_c, one thread per fine node; (z.z, z.r) per workgroup and the tail
+__global__ __launch_bounds__(kBlock) void k_geo_prolong0(GeoDims d, const PcgState* __restrict__ st,
+                                                         const double* __restrict__ x_c,
+                                                         const double* __restrict__ x0, const double* __restrict__ r,
+                                                         double* __restrict__ z, double* __restrict__ partials,
+                                                         RedTail rt) {
+  if (st->done) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int WPB = kBlock / 64;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t nf = (int64_t)d.f[0] * d.f[1] * d.f[2];
+  const int64_t per = ((nf + gridDim.x - 1) / gridDim.x + 63) / 64 * 64;  // a contiguous range per workgroup
+  const int64_t t0 = (int64_t)blk * per, t1 = std::min<int64_t>(t0 + per, nf);
+  double zz = 0.0, zr = 0.0;
+  for (int64_t t = t0 + threadIdx.x; t < t1; t += kBlock) {
+    const int fi[3] = {(int)(t % d.f[0]), (int)((t / d.f[0]) % d.f[1]), (int)(t / ((int64_t)d.f[0] * d.f[1]))};
+    int c[3][2];
+    double w[3][2];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const int i = fi[a], n = d.f[a], m = d.c[a];
+      if (geo_kept(i, n)) {
+        c[a][0] = c[a][1] = geo_cidx(i, n, m);
+        w[a][0] = 1.0;
+        w[a][1] = 0.0;
+      } else {
+        c[a][0] = geo_cidx(i - 1, n, m);
+        c[a][1] = geo_cidx(i + 1, n, m);
+        w[a][0] = w[a][1] = 0.5;
+      }
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int64_t base = (int64_t)d.c[0] * (c[1][jj] + (int64_t)d.c[1] * c[2][kk]);
+        const double row = w[0][0] * x_c[base + c[0][0]] + w[0][1] * x_c[base + c[0][1]];
+        acc += (w[2][kk] * w[1][jj]) * row;
+      }
+    const double zv = x0[t] + acc;
+    z[t] = zv;
+    zz += zv * zv;
+    zr += zv * r[t];
+  }
+  __shared__ double red[2][WPB];
+  const double s_zz = wave_sum64(zz), s_zr = wave_sum64(zr);
+  if (lane == 0) {
+    red[0][wave] = s_zz;
+    red[1][wave] = s_zr;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2)
+    store_partial(&partials[2 * (int64_t)blockIdx.x + threadIdx.x],
+                  (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]));
+  fused_reduce_tail<2>(rt, gridDim.x);
+}
+
+GeoDims geo_dims(const int64_t (&fn)[3], const int64_t (&cn)[3]) {
+  GeoDims d;
+  for (int a = 0; a < 3; ++a) {
+    d.f[a] = (int)fn[a];
+    d.c[a] = (int)cn[a];
+  }
+  return d;
+}
+
+void launch_geo_restrict0(const int64_t (&fn)[3], const int64_t (&cn)[3], const PcgState* st, const double* r,
+                          const double* dinv_c, double omega_c, double* b_c, double* x_c, hipStream_t s) {
+  const int64_t nc = cn[0] * cn[1] * cn[2];
+  const dim3 gr((unsigned)std::max<int64_t>(1, std::min<int64_t>((nc + kBlock - 1) / kBlock, 8192)));
+  hipLaunchKernelGGL(k_geo_restrict0, gr, dim3(kBlock), 0, s, geo_dims(fn, cn), st, r, dinv_c, omega_c, b_c, x_c);
+}
+
+int launch_geo_prolong0(const int64_t (&fn)[3], const int64_t (&cn)[3], const PcgState* st, const double* x_c,
+                        const double* x0, const double* r, double* z, double* partials, const RedTail* tail,
+                        hipStream_t s) {
+  const int64_t nf = fn[0] * fn[1] * fn[2];
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nf + kBlock - 1) / kBlock, kUmBlocksMax));
+  const RedTail rt = tail ? *tail : RedTail{};
+  hipLaunchKernelGGL(k_geo_prolong0, dim3(nb), dim3(kBlock), 0, s, geo_dims(fn, cn), st, x_c, x0, r, z, partials, rt);
+  return nb;
+}
+
+void launch_sg_apply(const UmGrid& g, const PcgState* st, const double* x, const double* b, const double* dinv,
+                     double omega, double* y, hipStream_t s) {
+  // (the plane-marching kernel of the fine level on these grids: V-cycle 351-355
+  // vs 320-324 us at distorted C4 -- 7 planes per wave, too few to pay)
+  const dim3 gr((unsigned)std::max<int64_t>(1, std::min<int64_t>((g.nv + kBlock - 1) / kBlock, 8192)));
+  if (b) hipLaunchKernelGGL(k_sg_rows<true>, gr, dim3(kBlock), 0, s, g, st, x, b, dinv, omega, y);
+  else hipLaunchKernelGGL(k_sg_rows<false>, gr, dim3(kBlock), 0, s, g, st, x, nullptr, nullptr, 0.0, y);
+}
+
 int um_num_blocks(const UmGrid& g) { return std::max(row_blocks(g), march_blocks(g)); }
 Sell um_operator(const UmGrid& g) {
   Sell m;
@@ -701,38 +869,6 @@ void launch_um_robin_fold(const UmGrid& g, const double* T, hipStream_t s) {
   if (g.J14 == nullptr || g.nbr == 0) return;
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((g.nbr + kBlock - 1) / kBlock, 4096));
   hipLaunchKernelGGL(k_um_robin_fold, dim3(nb), dim3(kBlock), 0, s, g, T);
-}
-
-// A structured grid's operator as a half stencil (the coarse levels of the
-// algebraic multigrid's geometric hierarchy, tv_amg.cpp): one row per thread;
-// POST: the damped Jacobi step y = x + omega dinv (b - A x) in the epilogue
-template <bool POST>
-__global__ __launch_bounds__(kBlock) void k_sg_rows(UmGrid g, const PcgState* __restrict__ st,
-                                                   const double* __restrict__ x, const double* __restrict__ b,
-                                                   const double* __restrict__ dinv, double omega,
-                                                   double* __restrict__ y) {
-  if (st != nullptr && st->done) return;
-  for (int64_t r = blockIdx.x * (int64_t)kBlock + threadIdx.x; r < g.nv; r += (int64_t)gridDim.x * kBlock) {
-    double acc = 0.0;
-#pragma unroll
-    for (int k = 0; k < 14; ++k) {
-      const int q = 13 + k;
-      const int64_t o = (int64_t)(q % 3 - 1) + g.s1 * ((q / 3) % 3 - 1) + g.s2 * (q / 9 - 1);
-      const int64_t cu = r + o < g.nv ? r + o : r;
-      const int64_t cl = r - o >= 0 ? r - o : r;
-      const int64_t ku = (int64_t)k * g.nv;
-      acc += g.J14[ku + r] * x[cu];
-      if (k > 0) acc += (r - o >= 0 ? g.J14[ku + cl] : 0.0) * x[cl];
-    }
-    y[r] = POST ? x[r] + omega * dinv[r] * (b[r] - acc) : acc;
-  }
-}
-
-void launch_sg_apply(const UmGrid& g, const PcgState* st, const double* x, const double* b, const double* dinv,
-                     double omega, double* y, hipStream_t s) {
-  const dim3 gr((unsigned)std::max<int64_t>(1, std::min<int64_t>((g.nv + kBlock - 1) / kBlock, 8192)));
-  if (b) hipLaunchKernelGGL(k_sg_rows<true>, gr, dim3(kBlock), 0, s, g, st, x, b, dinv, omega, y);
-  else hipLaunchKernelGGL(k_sg_rows<false>, gr, dim3(kBlock), 0, s, g, st, x, nullptr, nullptr, 0.0, y);
 }
 
 // SELL rows -> the stencil slots of a structured-topology mesh: all 27, or
