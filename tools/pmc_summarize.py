@@ -23,7 +23,8 @@ GROUPS = {
     "jacobian_apply": ("k_cg_march<1, false",),  # plain J x (+ k_cg_addfaces, a few KB)
     "dg_matvec_fused": ("k_dg_tile<true",),
     "pcg_iteration_single_reduction": ("k_cgs_march<false",),
-    "jacobian_apply_unstructured": ("k_um_rows<3, 1>",),  # SELL-64 J x of tv_um.hip
+    "jacobian_apply_unstructured": ("k_um_march14<1>",),  # half-stencil J x (structured topology, tv_um.hip)
+    "jacobian_apply_unstructured_sell": ("k_um_rows<3, 1>",),  # SELL-64 J x (general meshes)
     # multigrid kernels (pmc_kernels.py --pc gmg)
     "mg_update": ("k_mg_update",),
     "mg_post_march": ("k_cg_march<1, false, 8, 1, 2, true",),
