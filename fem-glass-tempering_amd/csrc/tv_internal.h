@@ -221,9 +221,12 @@ struct UmGrid {
   // instead of ~330 B of SELL.  J14 = V14 with the Robin facet Jacobian of J(T)
   // folded into the boundary rows' slots (launch_um_robin_fold, once per Newton
   // iteration): the J x kernels then run no facet quadrature (brow: the nbr
-  // boundary rows).  nullptr: SELL only (the residual always runs on SELL).
+  // boundary rows).  M14 / K14: the residual's mass and dt alpha K, the same
+  // way (marched along the planes, k_um_res14).  nullptr: SELL only.
   const double* V14;
   double* J14;
+  const double* M14;
+  const double* K14;
   const int64_t* brow;
   int64_t nbr;
   int64_t s1, s2;

@@ -574,6 +574,50 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
 }
 
+// The residual's cell part on the half stencils of M and dt alpha K (structured
+// topology), marched like k_um_march14: F = M (T - T_prev) + K T - dt f b (the
+// same grouping as k_um_rows<UM_RES>, M and K apart so T - T_prev is formed
+// first); the Robin terms follow in k_um_robin_res
+__global__ __launch_bounds__(kBlock) void k_um_res14(UmGrid g, March14 m, const double* __restrict__ u,
+                                                       const double* __restrict__ up, double* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int WPB = kBlock / 64;
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  const double* __restrict__ Mh = g.M14;
+  const double* __restrict__ Kh = g.K14;
+  const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2;
+  for (int64_t gw = (int64_t)blk * WPB + wave; gw < m.ncol * m.kch; gw += nw) {
+    const int64_t seg = gw % m.nseg, t = gw / m.nseg;
+    const int64_t j = t % m.n1, ch = t / m.n1;
+    const int64_t i = seg * 64 + lane;
+    if (i >= m.n0) continue;
+    const int64_t k1 = std::min<int64_t>(m.n2, (ch + 1) * m.kper);
+#pragma unroll 1
+    for (int64_t k = ch * m.kper; k < k1; ++k) {
+      const unsigned r = (unsigned)(i + m.n0 * j + g.s2 * k);
+      double acc = 0.0, acc2 = 0.0;
+#pragma unroll 7
+      for (int q14 = 0; q14 < 14; ++q14) {
+        const int q = 13 + q14;
+        const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
+        const bool hi = r + o < nv, lo = r >= o;
+        const unsigned cu = hi ? r + o : r, cl = lo ? r - o : r;
+        const unsigned ku = (unsigned)q14 * nv;
+        const double xu = u[cu];
+        acc += Mh[ku + r] * (xu - up[cu]);
+        acc2 += Kh[ku + r] * xu;
+        if (q14 > 0) {
+          const double xl = u[cl];
+          acc += (lo ? Mh[ku + cl] : 0.0) * (xl - up[cl]);
+          acc2 += (lo ? Kh[ku + cl] : 0.0) * xl;
+        }
+      }
+      out[r] = (acc + acc2) - g.dt_f * g.bvec[r];
+    }
+  }
+}
+
 template <int MODE>
 void launch_rows(const UmGrid& g, const double* T, const double* u, const double* up, double* out,
                  const PcgState* st, double* partials, const RedTail& rt, int invert, hipStream_t s) {
@@ -777,7 +821,10 @@ int64_t um_boundary_vertices(const UmDevice* d, std::vector<unsigned char>& mask
 }
 
 void launch_um_residual(const UmGrid& g, const double* T, const double* Tp, double* F, hipStream_t s) {
-  launch_rows<UM_RES>(g, T, T, Tp, F, nullptr, nullptr, RedTail{}, 0, s);
+  if (g.M14 != nullptr)
+    hipLaunchKernelGGL(k_um_res14, dim3(march_blocks(g)), dim3(kBlock), 0, s, g, march14(g), T, Tp, F);
+  else
+    launch_rows<UM_RES>(g, T, T, Tp, F, nullptr, nullptr, RedTail{}, 0, s);
   if (g.nbr == 0) return;
   const dim3 gr((unsigned)std::max<int64_t>(1, std::min<int64_t>((g.nbr + kBlock - 1) / kBlock, 4096)));
   if (g.dim == 2) hipLaunchKernelGGL(k_um_robin_res<2>, gr, dim3(kBlock), 0, s, g, T, F);
@@ -1187,14 +1234,18 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   // and their half forms slower, 1.35 ms: the lower slots' re-reads a plane
   // apart miss L2)
   int64_t ss1 = 0, ss2 = 0, nbr = 0;
-  double *V14 = nullptr, *J14 = nullptr;
+  double *V14 = nullptr, *J14 = nullptr, *M14 = nullptr, *K14 = nullptr;
   int64_t* brow_d = nullptr;
   // (32-bit element offsets into the 14 slot arrays: 14 nv * 8 B < 4 GiB)
   if (nrow == nv && nv * 14 * 8 < ((int64_t)1 << 32) && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
     const size_t n14 = (size_t)14 * nv;
-    if (um_alloc(d, n14, &V14, err) || um_alloc(d, n14, &J14, err)) return 1;
-    UMC(hipMemsetAsync(V14, 0, sizeof(double) * n14, s));
+    if (um_alloc(d, n14, &V14, err) || um_alloc(d, n14, &J14, err) || um_alloc(d, n14, &M14, err) ||
+        um_alloc(d, n14, &K14, err))
+      return 1;
+    for (double* X : {V14, M14, K14}) UMC(hipMemsetAsync(X, 0, sizeof(double) * n14, s));
     hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V14, 1);
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, M, ss1, ss2, nv, M14, 1);
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, K, ss1, ss2, nv, K14, 1);
     UMC(hipGetLastError());
     UMC(hipMemcpyAsync(J14, V14, sizeof(double) * n14, hipMemcpyDeviceToDevice, s));
   }
@@ -1225,6 +1276,8 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   g.vdiag = vdiag;
   g.V14 = V14;
   g.J14 = J14;
+  g.M14 = M14;
+  g.K14 = K14;
   g.brow = brow_d;
   g.nbr = nbr;
   g.s1 = ss1;
