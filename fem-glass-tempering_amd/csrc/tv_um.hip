@@ -381,28 +381,7 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
     const int wdt = (int)((g.soff[s + 1] - so) >> 6);
     const int* __restrict__ cs = g.cols + so + lane;  // entry k of this row: cs[64 k]
     double acc = 0.0, acc2 = 0.0;
-    if (MODE != UM_DIAG && MODE != UM_RES && g.J14 != nullptr) {
-      // structured topology, symmetric half stencil of J(T): upper slot k of
-      // row r (column r + o) and of row r - o (its column r: the lower slot of
-      // row r).  Absent neighbours hold zeros; a row outside the mesh reads nothing.
-      if (r < g.nv) {
-        // fully unrolled (every slot's loads in flight; unrolled by 2, 64 VGPRs:
-        // 524 vs 388 us per J x at 8.2M rows); 32-bit unsigned element indices
-        // (14 nv elements < 2^32 / 8, checked at setup)
-        const double* __restrict__ J = g.J14;
-        const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2, ru = (unsigned)r;
-#pragma unroll
-        for (int k = 0; k < 14; ++k) {
-          const int q = 13 + k;
-          const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
-          const bool hi = ru + o < nv, lo = ru >= o;
-          const unsigned cu = hi ? ru + o : ru, cl = lo ? ru - o : ru;
-          const unsigned ku = (unsigned)k * nv;
-          acc += J[ku + ru] * u[cu];
-          if (k > 0) acc += (lo ? J[ku + cl] : 0.0) * u[cl];
-        }
-      }
-    } else if (MODE == UM_RES) {
+    if (MODE == UM_RES) {
       const double* __restrict__ ms = g.M + so + lane;
       const double* __restrict__ ks = g.K + so + lane;
       for (int k = 0; k < wdt; ++k) {
@@ -441,8 +420,9 @@ __global__ __launch_bounds__(kBlock) void k_um_rows(UmGrid g, const double* __re
       else val = acc;
       // Robin terms: the residual's in a pass over the boundary rows of their
       // own (k_um_robin_res: no divergent facet quadrature in this kernel's
-      // waves); the Jacobian's folded into J14 on structured topology
-      if (MODE == UM_DIAG || (MODE != UM_RES && g.J14 == nullptr))
+      // waves); structured topology runs J x on the half stencil instead
+      // (k_um_march14, the Robin Jacobian folded in)
+      if (MODE != UM_RES)
         val += robin_row<D, MODE>(g, r, T, xget);
       if (MODE == UM_DIAG && invert) val = 1.0 / val;
       if (MODE == UM_FUSED) pw += u[r] * val;
