@@ -248,6 +248,19 @@ def main():
                "unit": "GB/s", "frac": fl_by.value / (fl_ms.value * 1e-3) / 1e9 / HBM_PEAK_GBS,
                "timing": "HBM (flushed): 512 MiB write + read sweep before each of 21 launches, HIP events "
                          "around each launch (dispatch included), median"}
+    # the same flushed launches under the rocprofv3 kernel trace of this command
+    # (kernel time, no dispatch), from the committed profile summary of the
+    # bench default (tools/profile_summary.py; the trace cannot run inside the
+    # timed process)
+    prof_file = os.path.join(ROOT, "profiles", "r05_profile_summary.json")
+    if not um and a.share <= 1 and nc == [400, 400, 50] and a.family == "CG" and os.path.exists(prof_file):
+        with open(prof_file) as fh:
+            pf = json.load(fh).get("hbm_flushed")
+        if pf:
+            flushed["rocprof_median_us"] = pf["rocprof_median_us"]
+            flushed["rocprof_frac"] = pf["rocprof_frac"]
+            flushed["rocprof_source"] = ("committed rocprofv3 --kernel-trace of the C4 bench default, median of "
+                                         f"{pf['launches']} flushed launches: " + os.path.relpath(prof_file, ROOT))
     dom = kern[names[0] if um else names[3]]
     # traffic: HBM bytes per launch of this kernel from the rocprofv3 --pmc passes
     # (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md HBM section) of this same
