@@ -59,6 +59,39 @@ def test_amg_restatement_builds_a_spd_hierarchy():
     assert x @ bx > 0
 
 
+def test_geometric_hierarchy_restatement():
+    """CPU: the index-space geometric hierarchy of structured-topology meshes
+    (tv_amg.cpp geometric_p, restated in oracle/amg.py build(dims=...)): every
+    P interpolates constants exactly (rows sum to 1), keeps every other vertex
+    per axis plus the last one of an odd cell count, weights in {1, 1/2, 1/4,
+    1/8} (exact in float32), and each Galerkin operator is symmetric positive
+    definite with at most 27 couplings per row (a 27-point stencil again)."""
+    n = (15, 12, 9)  # odd and even cell counts
+    m = _mesh(n, (2.0, 2.0, 1.0), seed=3, shuffle=False)
+    mp = dict(O.MAIN_MODEL_PARAMS)
+    V = O.HeatForm(O.Space(_omesh(m), "CG"), 0.1,
+                   O.ThermalParams.from_dict({**mp, "epsilon": 0.0, "htc": 0.0})).jacobian(np.full(m.num_vertices, 800.0))
+    old = OA.COARSE_ROWS
+    OA.COARSE_ROWS = 30
+    try:
+        levels = OA.build(V, dims=tuple(c + 1 for c in n))
+    finally:
+        OA.COARSE_ROWS = old
+    dims = [c + 1 for c in n]
+    for A, P, R, d, om in levels:
+        kept = [len(range(0, k, 2)) + (1 if (k - 1) % 2 else 0) for k in dims]
+        assert P.shape == (int(np.prod(dims)), int(np.prod(kept)))
+        assert np.allclose(np.asarray(P.sum(axis=1)).ravel(), 1.0, rtol=0, atol=1e-15)
+        assert set(np.unique(P.data)) <= {1.0, 0.5, 0.25, 0.125}
+        assert abs(R - P.T).max() == 0.0
+        assert abs(A - A.T).max() <= 1e-12 * abs(A).max()
+        assert np.diff(A.indptr).max() <= 27
+        assert np.all(np.linalg.eigvalsh(A.toarray()) > 0.0)
+        assert 0.0 < om < 2.0 / 1.05
+        dims = kept
+    assert len(levels) >= 2
+
+
 # the second case has > 2000 rows on level 1 (aggregates of ~30 vertices): three levels;
 # the third is a stretched plate (cells 0.5 x 0.1 x 0.05, aspect ratio 10), whose
 # clustered top eigenvalues a power-iteration estimate of lambda_max
