@@ -1250,4 +1250,43 @@ int tv_sync(void* ctx) {
   return TV_OK;
 }
 
+
+int tv_get_options(void* ctx, tv_options* out) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !out) return TV_ERR_ARG;
+  *out = c->O;
+  return TV_OK;
+}
+
+
+// the attributes of the reference's problem.solver (dolfinx NewtonSolver,
+// ThermoViscoProblem.py:334-337): read at the next solve; the gated step end
+// queues its test with the values in force then
+int tv_set_newton_tolerances(void* ctx, double rtol, double atol, int max_it, int error_on_nonconvergence) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (!(rtol >= 0.0) || !(atol >= 0.0) || max_it < 1)
+    return c->fail(TV_ERR_ARG, "Newton tolerances: rtol >= 0, atol >= 0 and max_it >= 1");
+  c->O.newton_rtol = rtol;
+  c->O.newton_atol = atol;
+  c->O.newton_max_it = max_it;
+  c->O.error_on_nonconvergence = error_on_nonconvergence ? 1 : 0;
+  return TV_OK;
+}
+
+
+// problem.ksp.setTolerances (PETSc KSPSetTolerances on the solver's KSP,
+// ThermoViscoProblem.py:339): pcg_state_init reads them at every solve
+int tv_set_ksp_tolerances(void* ctx, double rtol, double atol, double dtol, int max_it) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c) return TV_ERR_ARG;
+  if (!(rtol >= 0.0) || !(atol >= 0.0) || !(dtol > 0.0) || max_it < 1)
+    return c->fail(TV_ERR_ARG, "KSP tolerances: rtol >= 0, atol >= 0, dtol > 0 and max_it >= 1");
+  c->O.ksp_rtol = rtol;
+  c->O.ksp_atol = atol;
+  c->O.ksp_dtol = dtol;
+  c->O.ksp_max_it = max_it;
+  return TV_OK;
+}
+
 }  // extern "C"

@@ -222,6 +222,7 @@ struct Ctx {
   // stats
   int last_newton = 0, last_krylov = 0;
   double last_dx = 0.0;
+  int last_conv = 0;  // the last Newton solve met its test (tv_last_converged)
   int pcg_hint = 0;
   // multigrid solves: the Krylov count of the Newton iteration with the same
   // index in the previous time step (the solves of a step take a repeating

@@ -291,4 +291,12 @@ int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm) 
   return TV_OK;
 }
 
+
+int tv_last_converged(void* ctx, int* converged) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  if (!c || !converged) return TV_ERR_ARG;
+  *converged = c->last_conv;
+  return TV_OK;
+}
+
 }  // extern "C"

@@ -478,6 +478,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
   c->last_newton = its;
   c->last_krylov = kits;
   c->last_dx = rn;
+  c->last_conv = conv ? 1 : 0;
   if (out_its) *out_its = its;
   if (out_kits) *out_kits = kits;
   if (out_conv) *out_conv = conv ? 1 : 0;

@@ -19,7 +19,7 @@ TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
 TV_PC_JACOBI, TV_PC_GMG, TV_PC_AMG = 0, 1, 2
 TV_DG_KERNEL_AUTO, TV_DG_KERNEL_TILE, TV_DG_KERNEL_CELLS = 0, 1, 2
 TV_MG_COUPLING_AUTO, TV_MG_COUPLING_GLOBAL, TV_MG_COUPLING_LOCAL = 0, 1, 2
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -37,8 +37,9 @@ EXPORTS = [
     "tv_field_device_ptr", "tv_set_initial_condition", "tv_sync", "tv_residual", "tv_jacobian_apply",
     "tv_jacobian_diag", "tv_precond_apply", "tv_solve_T", "tv_visco_update", "tv_step", "tv_comm_unique_id_size",
     "tv_comm_get_unique_id", "tv_comm_init", "tv_comm_init_stub", "tv_comm_init_loopback", "tv_comm_check", "tv_comm_time", "tv_halo_exchange", "tv_time_kernel", "tv_kernel_bytes", "tv_kernel_timing", "tv_kernel_stats",
-    "tv_last_stats", "tv_comm_init_host", "tv_partition_layout", "tv_pcg_variant",
-    "tv_set_dirichlet", "tv_output_open", "tv_output_open_named", "tv_output_write", "tv_output_close", "tv_xdmf_open",
+    "tv_last_stats", "tv_last_converged", "tv_comm_init_host", "tv_partition_layout", "tv_pcg_variant",
+    "tv_set_dirichlet", "tv_get_options", "tv_set_newton_tolerances", "tv_set_ksp_tolerances",
+    "tv_output_open", "tv_output_open_named", "tv_output_write", "tv_output_close", "tv_xdmf_open",
     "tv_xdmf_add_field", "tv_xdmf_append", "tv_xdmf_close",
 ]
 
@@ -158,10 +159,14 @@ def load_library():
         "tv_kernel_timing": (C.c_int, [vp, C.c_int]),
         "tv_kernel_stats": (C.c_int, [vp, C.c_int, dp, C.POINTER(C.c_int64)]),
         "tv_last_stats": (C.c_int, [vp, ip, ip, dp]),
+        "tv_last_converged": (C.c_int, [vp, ip]),
         "tv_comm_init_host": (C.c_int, [vp, C.c_int, C.c_int, HOST_ALLREDUCE_FN, HOST_SENDRECV_FN, vp]),
         "tv_partition_layout": (C.c_int, [C.POINTER(MeshDesc), i64p]),
         "tv_pcg_variant": (C.c_int, [vp, ip]),
         "tv_set_dirichlet": (C.c_int, [vp, C.c_int, C.c_double]),
+        "tv_get_options": (C.c_int, [vp, C.POINTER(Options)]),
+        "tv_set_newton_tolerances": (C.c_int, [vp, C.c_double, C.c_double, C.c_int, C.c_int]),
+        "tv_set_ksp_tolerances": (C.c_int, [vp, C.c_double, C.c_double, C.c_double, C.c_int]),
         "tv_output_open": (C.c_int, [vp, C.c_char_p, ip, C.c_int]),
         "tv_output_open_named": (C.c_int, [vp, C.c_char_p, ip, C.POINTER(C.c_char_p), C.c_int]),
         "tv_output_write": (C.c_int, [vp, C.c_double]),

@@ -368,6 +368,10 @@ class ThermoViscoProblem:
         self._outfile_names = (outfile_name, outfile_name1)
         if self.write_output:
             self._write_initial_output(t=self.t)
+        # _setup_solver (ThermoViscoProblem.py:330-346): problem.solver / problem.ksp
+        from .solver import NewtonSolver
+        self.solver = NewtonSolver(self)
+        self.ksp = self.solver.krylov_solver
 
     # the reference's five series (ThermoViscoProblem.py:246-276): T, phi, Tf,
     # xi and sigma, as XDMF over raw binary (tvfem.xdmf reads them back)
@@ -428,6 +432,12 @@ class ThermoViscoProblem:
         N.check(rc, self._ctx)
         self.last_newton_iterations = nits.value
         self.last_krylov_iterations = kits.value
+        if self._newton_fixed_its == 0:
+            # solver.error_on_nonconvergence = False: dolfinx returns (n, False)
+            # and _solve_T fails its assert(converged) (ThermoViscoProblem.py:390)
+            conv = C.c_int()
+            N.check(self._lib.tv_last_converged(self._ctx, C.byref(conv)), self._ctx)
+            assert conv.value, "Newton solver did not converge"
         if self._output_open:  # ThermoViscoProblem.py:374
             self._write_output()
 

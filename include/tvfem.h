@@ -51,11 +51,13 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 6  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+#define TV_ABI_VERSION 7  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
                             3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its;
                             4: tv_upart_desc / tv_create_unstructured_part;
                             5: tv_comm_init_loopback, tv_comm_check, tv_options.mg_coupling;
-                            6: tv_comm_time */
+                            6: tv_comm_time;
+                            7: tv_get_options, tv_set_newton_tolerances, tv_set_ksp_tolerances,
+                               tv_last_converged */
 
 /* status codes */
 #define TV_OK 0
@@ -341,6 +343,17 @@ int tv_set_initial_condition(void* ctx, double T0);
 int tv_set_dirichlet(void* ctx, int enable, double value);
 int tv_sync(void* ctx);
 
+/* Solver settings after creation: the options in force (tv_get_options), and
+ * the tolerances a caller of the reference sets on problem.solver -- dolfinx
+ * NewtonSolver rtol / atol / max_it / error_on_nonconvergence, the object
+ * _setup_solver creates at ThermoViscoProblem.py:334-337 [3P] -- and on
+ * problem.ksp = solver.krylov_solver (:339; PETSc KSPSetTolerances rtol,
+ * abstol, dtol, max_it [3P]).  They take effect at the next solve;
+ * TV_ERR_ARG for a negative tolerance, dtol <= 0 or max_it < 1. */
+int tv_get_options(void* ctx, tv_options* out);
+int tv_set_newton_tolerances(void* ctx, double rtol, double atol, int max_it, int error_on_nonconvergence);
+int tv_set_ksp_tolerances(void* ctx, double rtol, double atol, double dtol, int max_it);
+
 /* ---- operators (device pointers, owned T-dofs, length n_owned) ----------
  * The context stream is non-blocking: these calls first wait for all work
  * already queued on the device (hipDeviceSynchronize), so inputs written on
@@ -363,7 +376,12 @@ int tv_visco_update(void* ctx);
 /* one time step (solve_timestep minus I/O); returns once the Newton solve has
  * converged, with the visco update still queued on the context's stream:
  * tv_get_field / tv_set_field / the operator calls / tv_field_device_ptr order
- * themselves behind it, tv_sync waits for it */
+ * themselves behind it, tv_sync waits for it.  A Newton solve that reaches
+ * newton_max_it unconverged returns TV_ERR_NOT_CONVERGED with the step's end
+ * not run (dolfinx raises; T_prev and the visco state stay those of the
+ * previous step), or -- error_on_nonconvergence = 0 -- ends the step anyway
+ * (tv_last_converged tells; the reference's _solve_T would then fail its
+ * assert(converged), ThermoViscoProblem.py:390) */
 int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its);
 
 /* ---- time-series output -------------------------------------------------------
@@ -465,6 +483,9 @@ int tv_kernel_timing(void* ctx, int on);
 int tv_kernel_stats(void* ctx, int kernel, double* ms_avg, int64_t* launches);
 /* counters of the last tv_step / tv_solve_T */
 int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm);
+/* whether the last tv_step / tv_solve_T met the Newton test (with
+ * error_on_nonconvergence = 0 an unconverged solve returns TV_OK) */
+int tv_last_converged(void* ctx, int* converged);
 /* the Krylov iteration form in use (TV_PCG_KSPCG or TV_PCG_SINGLE_REDUCTION:
  * the Jacobi march form, or with TV_PC_GMG the single-reduction GMG-PCG of
  * deep-ghost slabs); with the Jacobi SINGLE_REDUCTION form, kernel id 3 of
