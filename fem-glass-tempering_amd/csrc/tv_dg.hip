@@ -59,6 +59,13 @@ __device__ __forceinline__ double kloc(double h, int a, int b) { return (a == b 
 // SIPG penalty / sqrt(q) without the FP64 sqrt + divide sequences (~25
 // instructions each, a third of the tile kernels' per-cell VALU count): v_rsq_f64
 // refined by two Newton steps (relative error ~1e-16, not bitwise the IEEE quotient)
+// a read-only table entry through the constant address space: a wave-uniform
+// index becomes a scalar load (counted by lgkmcnt, so waiting for it does not
+// wait for the vector loads in flight)
+__device__ __forceinline__ double kld(const double* p, int i) {
+  return ((const __attribute__((address_space(4))) double*)p)[i];
+}
+
 __device__ __forceinline__ double pen_rsq(double penalty, double q) {
   double r = __builtin_amdgcn_rsq(q);
   r = r * (1.5 - (0.5 * q) * (r * r));
@@ -570,6 +577,16 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
     }
   };
   if (HL) hfetch(q0);
+  // cell lengths: the x axis per lane and the row axis per wave do not change
+  // along the march (loaded once; the x neighbours' by DPP); the march axis'
+  // per plane by scalar loads.  Vector loads of the tables inside the march
+  // made every plane wait for the plane prefetch too (vmcnt counts in order)
+  const int icl = min(max(i, 0), g.c0 - 1);
+  const double h0 = g.h[0][icl], ih0 = g.ih[0][icl];
+  const int rlo = max(rcl - 1, 0), rhi = min(rcl + 1, cn[ra] - 1);
+  const double hr = kld(g.h[ra], rcl), ihr = kld(g.ih[ra], rcl);
+  const double hr_lo = kld(g.h[ra], rlo), ihr_lo = kld(g.ih[ra], rlo);
+  const double hr_hi = kld(g.h[ra], rhi), ihr_hi = kld(g.ih[ra], rhi);
   double xl[8], x[8], xu[8];  // planes L - 1, L, L + 1
   double rz[8], ro[8];        // raw loads of plane L + 2, in flight during step L
   {  // prologue: the loads of the first three planes in flight together
@@ -604,11 +621,14 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
       ci[0] = valid ? i : 0;
       ci[ra] = valid ? r : 0;
       ci[pa] = L;
-      double h[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e) h[e] = g.h[e][ci[e]];
+      double h[3], ih[3];
+      h[0] = h0;
+      ih[0] = ih0;
+      h[ra] = hr;
+      ih[ra] = ihr;
+      h[pa] = kld(g.h[pa], L);
+      ih[pa] = kld(g.ih[pa], L);
       const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
-      const double ih[3] = {g.ih[0][ci[0]], g.ih[1][ci[1]], g.ih[2][ci[2]]};
       const double pen_up = pen_rsq(g.penalty, hd2);  // upper facets: this cell is '+'
       double y[8];
       // ---- cell term: Mz(My Mx x + da (My Kx x + Ky Mx x)) + da Kz (My Mx x) ----
@@ -639,16 +659,23 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
         for (int side = 0; side < 2; ++side) {
           const int nbi = ci[k] + (side ? 1 : -1);
           const bool interior = valid && nbi >= 0 && nbi < cn[k];
-          double xn[8];
+          double xn[8], hn, ihn;  // the neighbour's values and lengths along k
           if (k == 0) {  // lane +- 1 (all lanes)
 #pragma unroll
             for (int l = 0; l < 8; ++l) xn[l] = side ? shl1(x[l]) : shr1(x[l]);
+            hn = side ? shl1(h0) : shr1(h0);
+            ihn = side ? shl1(ih0) : shr1(ih0);
           } else if (k == ra) {
 #pragma unroll
             for (int l = 0; l < 8; ++l) xn[l] = sX[sb][slot + (side ? 1 : -1)][l][lane];
+            hn = side ? hr_hi : hr_lo;
+            ihn = side ? ihr_hi : ihr_lo;
           } else {
 #pragma unroll
             for (int l = 0; l < 8; ++l) xn[l] = side ? xu[l] : xl[l];
+            const int Ln = min(max(L + (side ? 1 : -1), 0), npl - 1);
+            hn = kld(g.h[pa], Ln);
+            ihn = kld(g.ih[pa], Ln);
           }
           if (interior) {
             // SIPG facet rows, '+' = L = lower cell: with J = (0, 1, -1, 0) and
@@ -656,8 +683,7 @@ __global__ __launch_bounds__(512) void k_dg_tile(DgGrid g, const double* __restr
             // pen J J^T - G J^T - J G^T reduces per tangential dof pair to the
             // jump j = x_L1 - x_R0 and the normal differences d = x_1 - x_0 of
             // both cells; then the tangential masses (they commute)
-            const double hn = g.h[k][nbi];
-            const double gO = 0.5 * ih[k], gN = 0.5 * g.ih[k][nbi];
+            const double gO = 0.5 * ih[k], gN = 0.5 * ihn;
             double U[8];
             if (side) {  // upper facet: this cell is L, the neighbour R
               const double pen = pen_up;

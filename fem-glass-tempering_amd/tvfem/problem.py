@@ -368,10 +368,21 @@ class ThermoViscoProblem:
         self._outfile_names = (outfile_name, outfile_name1)
         if self.write_output:
             self._write_initial_output(t=self.t)
-        # _setup_solver (ThermoViscoProblem.py:330-346): problem.solver / problem.ksp
+        self._setup_solver()
+
+    def _setup_solver(self) -> None:
+        """ThermoViscoProblem.py:330-346: ``problem.solver`` (NewtonSolver:
+        incremental criterion, rtol 1e-12, report) and ``problem.ksp`` (its CG
+        KSP), whose tolerances reach the context (tvfem/solver.py)."""
         from .solver import NewtonSolver
         self.solver = NewtonSolver(self)
         self.ksp = self.solver.krylov_solver
+
+    def _update_values(self, current: Function, previous: Function) -> None:
+        """ThermoViscoProblem.py:349-354: ghost update, then previous <- current
+        (host round trip; the step's own copies run on the device)."""
+        current.x.scatter_forward()
+        previous.x.array[:] = current.x.array[:]
 
     # the reference's five series (ThermoViscoProblem.py:246-276): T, phi, Tf,
     # xi and sigma, as XDMF over raw binary (tvfem.xdmf reads them back)

@@ -51,6 +51,13 @@ def test_solver_objects_defaults_and_checks():
         k.setTolerances(rtol=-1.0)
     with pytest.raises(NotImplementedError):
         s.convergence_criterion = "residual"
+    # _update_values (ThermoViscoProblem.py:349-354): previous <- current
+    s.max_it = 50
+    k.setTolerances(rtol=1e-5)
+    dev.solve_timestep()
+    dev._update_values(dev.functions_current["T"], dev.functions_next["T"])
+    dev._flush()
+    assert np.array_equal(dev.get_field("T_next"), dev.get_field("T"))
     dev.close()
 
 
