@@ -61,6 +61,7 @@ def parse():
                          "one GPU), jacobi, or auto (gmg where it applies and the mesh has >= 4M T-dofs, at "
                          "every rank count; amg for --mesh distorted on one GPU)")
     ap.add_argument("--mg-levels", type=int, default=0, help="GMG levels incl. the fine one (0: automatic)")
+    ap.add_argument("--dg-tile-chunk", type=int, default=0, help="DG1 J x tile: planes per march chunk (0: automatic)")
     ap.add_argument("--mg-coupling", choices=["auto", "global", "local"], default="auto",
                     help="partitioned GMG: global = the distributed V-cycle of the whole box (the N = 1 "
                          "preconditioner), local = each slab's own V-cycle (block Jacobi, no exchange inside the "
@@ -134,7 +135,7 @@ def main():
               "ksp_fixed_its": kk}
     prob = ThermoViscoProblem(mesh, (0.0, 50.0), 0.1, cfg, mp, device=device, materialize=False,
                               verbose=False, pcg_variant=a.pcg, preconditioner=pc, mg_levels=a.mg_levels,
-                              mg_coupling=a.mg_coupling,
+                              mg_coupling=a.mg_coupling, dg_tile_chunk=a.dg_tile_chunk,
                               write_output=a.output is not None, output_dir=a.output or "output", **kw)
     mg_single = pc == "gmg" and prob.pcg_variant == "single"  # GMG-PCG, Chronopoulos-Gear form (deep-ghost slabs)
     single = prob.pcg_variant == "single" and not mg_single
