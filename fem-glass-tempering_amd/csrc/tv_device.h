@@ -20,6 +20,14 @@ __device__ __forceinline__ double shl1(double v) {  // lane l <- lane l+1
   return __hiloint2double(hi, lo);
 }
 
+// A read-only table entry through the constant address space: a wave-uniform
+// index becomes a scalar load (counted by lgkmcnt, so waiting for it does not
+// wait for the vector loads in flight -- vmcnt counts in order)
+template <class T>
+__device__ __forceinline__ T kld(const T* p, int i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
 // Blocks are dispatched round-robin over the 8 XCDs; remap so that each XCD
 // gets a contiguous range of tile ids (bijective for any grid size), keeping
 // the halo rows / columns shared by neighbouring tiles in one L2.

@@ -59,13 +59,6 @@ __device__ __forceinline__ double kloc(double h, int a, int b) { return (a == b 
 // SIPG penalty / sqrt(q) without the FP64 sqrt + divide sequences (~25
 // instructions each, a third of the tile kernels' per-cell VALU count): v_rsq_f64
 // refined by two Newton steps (relative error ~1e-16, not bitwise the IEEE quotient)
-// a read-only table entry through the constant address space: a wave-uniform
-// index becomes a scalar load (counted by lgkmcnt, so waiting for it does not
-// wait for the vector loads in flight)
-__device__ __forceinline__ double kld(const double* p, int i) {
-  return ((const __attribute__((address_space(4))) double*)p)[i];
-}
-
 __device__ __forceinline__ double pen_rsq(double penalty, double q) {
   double r = __builtin_amdgcn_rsq(q);
   r = r * (1.5 - (0.5 * q) * (r * r));

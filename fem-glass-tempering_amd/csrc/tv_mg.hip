@@ -19,6 +19,7 @@
 // level) + 8 / 8 (coarse write), prolongation 16 (+ coarse reads, cached),
 // Jacobi step 24 / 40.
 #include <algorithm>
+#include <type_traits>
 
 #include "tv_stencil.h"
 
@@ -204,7 +205,9 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
   const int64_t fpl = (int64_t)nf * x.fn[1];
   const int64_t o = (int64_t)I + (int64_t)cn * (J + (int64_t)x.cn[1] * K);
   // the output's coarse diagonal first: its load overlaps the gathers below
-  const double dci = (xc != nullptr && ok) ? dinv_c[o] : 0.0;
+  // (clamped address, no branch around the load)
+  const double dcl = (xc != nullptr) ? dinv_c[(int64_t)II + (int64_t)cn * (J + (int64_t)x.cn[1] * K)] : 0.0;
+  const double dci = ok ? dcl : 0.0;
   // fine rows / planes of the 3 x 3 gather: closed form along axis 1 (always a
   // whole axis) and, on a whole-box level, along axis 2 -- no table load ahead
   // of the gathers (a partitioned level's local axis-2 window keeps its table)
@@ -216,16 +219,31 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
 #pragma unroll
     for (int c = 0; c < 3; ++c) fkr[c] = x.ri[2][3 * K + c];
   }
+  // all 9 rows' loads first, then the arithmetic: loads under a per-lane
+  // branch (the odd tail lane's single node) made every row wait for the one
+  // before (vmcnt counts in order) -- 9 memory round trips per wave.  The tail
+  // lane loads the pair ending at its node (always inside the row) and keeps .y
+  d2a8 rv[9], wv[9], mv[9];
+  int fjq[9], fkq[9];
   double dc[9], dr[9], wq[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const int c = q / 3, b = q % 3;
     wq[q] = x.rw[2][3 * K + c] * x.rw[1][3 * J + b];
-    const int fj = fjr[b], fk = fkr[c];
-    const int64_t f = (int64_t)fj * nf + fpl * fk + f1;
+    fjq[q] = fjr[b];
+    fkq[q] = fkr[c];
+    const int64_t f = (int64_t)fjr[b] * nf + fpl * fkr[c] + f1;
+    const int64_t fp = pair ? f : f - 1;
+    rv[q] = ld_pair(bf + fp);
+    wv[q] = (wf != nullptr) ? ld_pair(wf + fp) : d2a8{0.0, 0.0};  // wf null: bf is the residual itself
+    if (MASK) mv[q] = ld_pair(mask + fp);
+  }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) {
+    const int fj = fjq[q], fk = fkq[q];
     if (pair) {
-      const d2a8 r = ld_pair(bf + f);
-      d2a8 w = (wf != nullptr) ? ld_pair(wf + f) : d2a8{0.0, 0.0};  // wf null: bf is the residual itself
+      const d2a8 r = rv[q];
+      d2a8 w = wv[q];
       if (FACES) {
         const bool rowface = (fa.ff[2] && fj == 0) || (fa.ff[3] && fj == fa.n1 - 1) || (fa.ff[4] && fk == 0) ||
                              (fa.ff[5] && fk == fa.n2 - 1);  // wave-uniform
@@ -235,15 +253,15 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
       dc[q] = r.x - w.x;
       dr[q] = r.y - w.y;
       if (MASK) {
-        const d2a8 m = ld_pair(mask + f);
+        const d2a8 m = mv[q];
         if (m.x == 0.0) dc[q] = 0.0;
         if (m.y == 0.0) dr[q] = 0.0;
       }
     } else {
-      double wt = (wf != nullptr) ? wf[f] : 0.0;
+      double wt = wv[q].y;
       if (FACES) wt += face_at(fa, f1, fj, fk);  // the row's last node: an x-face node
-      double d = bf[f] - wt;
-      if (MASK && mask[f] == 0.0) d = 0.0;
+      double d = rv[q].y - wt;
+      if (MASK && mv[q].y == 0.0) d = 0.0;
       dc[q] = dr[q] = d;
     }
   }
@@ -343,20 +361,46 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgSta
   const double wl = x.pw[0][2 * i1c], wr = x.pw[0][2 * i1c + 1];
   const int64_t cpl = (int64_t)cn * x.cn[1];
   const int jc1 = min(jb + 1, x.cn[1] - 1), kc1 = min(kb + 1, x.cn[2] - 1);
-  double v[4];
+  // every load first, then the arithmetic (loads under per-lane branches, or
+  // after a branchy face_at, made each wait for the ones before: vmcnt counts
+  // in order): the four coarse x-runs (and the post-smoothing operands), then
+  // the four fine rows' old values -- the lone-node lane at the row's odd end
+  // loads the pair ending at its node, rows past the grid a clamped row (not
+  // stored); the fine-row weights are wave-uniform scalar loads
+  double v[4], cw[4], cd[4], cb[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
     const int64_t o = cc + (int64_t)cn * jcq + cpl * kcq;
     v[q] = xc[o];
     if (SMOOTH) {
-      const double wt = cp.w[o] + face_at(cp.fa, cc, jcq, kcq);
-      v[q] += cp.omega * cp.dinv[o] * (cp.b[o] - wt);
+      cw[q] = cp.w[o];
+      cd[q] = cp.dinv[o];
+      cb[q] = cp.b[o];
+    }
+  }
+  bool rj[2], rk[2];
+  int64_t f[4];
+  d2a8 xo[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int a = r & 1, b = r >> 1;
+    const int jr = min(2 * jb + a, x.fn[1] - 1), kr = min(2 * kb + b, x.f_ke - 1);
+    f[r] = (int64_t)i0 + (int64_t)nf * (jr + (int64_t)x.fn[1] * kr);
+    const int64_t fp = (int64_t)(has1 ? i0 : nf - 2) + (int64_t)nf * (jr + (int64_t)x.fn[1] * kr);
+    const d2a8 t = ld_pair(xf + fp);
+    xo[r] = d2a8{has1 ? t.x : (has0 ? t.y : 0.0), has1 ? t.y : 0.0};
+  }
+  if (SMOOTH) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
+      const double wt = cw[q] + face_at(cp.fa, cc, jcq, kcq);
+      v[q] += cp.omega * cd[q] * (cb[q] - wt);
     }
   }
   // per fine row of the block: its weights on coarse rows jb / jb + 1 (kb / kb + 1)
   double wy[2][2], wz[2][2];
-  bool rj[2], rk[2];
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
     const int j = 2 * jb + a, k = 2 * kb + a;
@@ -366,29 +410,17 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgSta
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       if (rj[a]) {
-        const int ci = x.pi[1][2 * j + e];
-        const double w = x.pw[1][2 * j + e];
+        const int ci = kld(x.pi[1], 2 * j + e);
+        const double w = kld(x.pw[1], 2 * j + e);
         wy[a][0] += ci == jb ? w : 0.0;
         wy[a][1] += ci == jb + 1 ? w : 0.0;
       }
       if (rk[a]) {
-        const int ci = x.pi[2][2 * k + e];
-        const double w = x.pw[2][2 * k + e];
+        const int ci = kld(x.pi[2], 2 * k + e);
+        const double w = kld(x.pw[2], 2 * k + e);
         wz[a][0] += ci == kb ? w : 0.0;
         wz[a][1] += ci == kb + 1 ? w : 0.0;
       }
-    }
-  }
-  int64_t f[4];
-  d2a8 xo[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int a = r & 1, b = r >> 1;
-    f[r] = (int64_t)i0 + (int64_t)nf * ((2 * jb + a) + (int64_t)x.fn[1] * (2 * kb + b));
-    xo[r] = d2a8{0.0, 0.0};
-    if (rj[a] && rk[b]) {
-      if (has1) xo[r] = ld_pair(xf + f[r]);
-      else if (has0) xo[r].x = xf[f[r]];
     }
   }
   // x-interpolated coarse values: even fine node (coarse c), odd (c, c + 1)
@@ -506,22 +538,39 @@ __global__ __launch_bounds__(kBlock) void k_mg_dg_restrict(DgGrid g, const PcgSt
   if (st != nullptr && st->done) return;
   const int c0 = g.c0, c1 = g.c1, n0 = c0 + 1, n1 = c1 + 1;
   const int64_t nv = (int64_t)n0 * n1 * (v1 - v0);
-  for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
-    const int i = (int)(v % n0), j = (int)((v / n0) % n1), K = v0 + (int)(v / ((int64_t)n0 * n1));
-    double acc = 0.0;
+  // (the mask test a compile-time choice: a load under a run-time test, even a
+  // uniform one, ended in a wait for every load before it)
+  auto run = [&](auto masked) {
+    constexpr bool MASKED = decltype(masked)::value;
+    for (int64_t v = blockIdx.x * (int64_t)kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
+      const int i = (int)(v % n0), j = (int)((v / n0) % n1), K = v0 + (int)(v / ((int64_t)n0 * n1));
+      // the 8 cells' copies loaded together (clamped addresses, no branch around
+      // a load), then summed in the same order over the cells that exist: with
+      // a branch per copy each load waited for the one before (vmcnt counts in
+      // order).  Adding +0.0 for a missing copy is exact (acc never is -0.0)
+      const int64_t o = i + (int64_t)n0 * (j + (int64_t)n1 * (K + kg0));
+      double bv[8], wv[8], mv[8];
+      bool in[8];
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
-      const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = K - (l >> 2);
-      if (ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < ck0 || ck >= ck1) continue;
-      const DgL a = dg_lay(g, ck);
-      const int64_t f = a.base + (int64_t)l * a.stride + ci + (int64_t)c0 * cj;
-      if (mask != nullptr && mask[f] == 0.0) continue;
-      acc += bf[f] - wf[f];
+      for (int l = 0; l < 8; ++l) {
+        const int ci = i - (l & 1), cj = j - ((l >> 1) & 1), ck = K - (l >> 2);
+        in[l] = !(ci < 0 || ci >= c0 || cj < 0 || cj >= c1 || ck < ck0 || ck >= ck1);
+        const DgL a = dg_lay(g, min(max(ck, ck0), ck1 - 1));
+        const int64_t f =
+            a.base + (int64_t)l * a.stride + min(max(ci, 0), c0 - 1) + (int64_t)c0 * min(max(cj, 0), c1 - 1);
+        bv[l] = bf[f];
+        wv[l] = wf[f];
+        mv[l] = MASKED ? mask[f] : 1.0;
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int l = 0; l < 8; ++l) acc += (in[l] && mv[l] != 0.0) ? bv[l] - wv[l] : 0.0;
+      bc[o] = acc;
+      if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;
     }
-    const int64_t o = i + (int64_t)n0 * (j + (int64_t)n1 * (K + kg0));
-    bc[o] = acc;
-    if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * acc;
-  }
+  };
+  if (mask != nullptr) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // every cell-local copy of the cells of local layers [ck0, ck1) takes its
@@ -533,16 +582,32 @@ __global__ __launch_bounds__(kBlock) void k_mg_dg_prolong(DgGrid g, const PcgSta
   if (st != nullptr && st->done) return;
   const int c0 = g.c0, c1 = g.c1, n0 = c0 + 1, n1 = c1 + 1;
   const int64_t pc = (int64_t)c0 * c1, ncell = pc * (ck1 - ck0);
-  for (int64_t cell = blockIdx.x * (int64_t)kBlock + threadIdx.x; cell < ncell; cell += (int64_t)gridDim.x * kBlock) {
-    const int i = (int)(cell % c0), j = (int)((cell / c0) % c1), k = ck0 + (int)(cell / pc);
-    const DgL a = dg_lay(g, k);
+  auto run = [&](auto masked) {
+    constexpr bool MASKED = decltype(masked)::value;
+    for (int64_t cell = blockIdx.x * (int64_t)kBlock + threadIdx.x; cell < ncell; cell += (int64_t)gridDim.x * kBlock) {
+      const int i = (int)(cell % c0), j = (int)((cell / c0) % c1), k = ck0 + (int)(cell / pc);
+      const DgL a = dg_lay(g, k);
+      // every load before the first store (a store to xf, then the next copy's
+      // load from xf: the compiler cannot prove them apart, so each load waited
+      // for the store and the load before it)
+      double xv[8], cv[8], mv[8];
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
-      const int64_t v = (i + (l & 1)) + (int64_t)n0 * ((j + ((l >> 1) & 1)) + (int64_t)n1 * (k + kg0 + (l >> 2)));
-      const int64_t f = a.base + (int64_t)l * a.stride + i + (int64_t)c0 * j;
-      xf[f] = (mask != nullptr && mask[f] == 0.0) ? 0.0 : xf[f] + xc[v];
+      for (int l = 0; l < 8; ++l) {
+        const int64_t v = (i + (l & 1)) + (int64_t)n0 * ((j + ((l >> 1) & 1)) + (int64_t)n1 * (k + kg0 + (l >> 2)));
+        const int64_t f = a.base + (int64_t)l * a.stride + i + (int64_t)c0 * j;
+        xv[l] = xf[f];
+        cv[l] = xc[v];
+        mv[l] = MASKED ? mask[f] : 1.0;
+      }
+#pragma unroll
+      for (int l = 0; l < 8; ++l) {
+        const int64_t f = a.base + (int64_t)l * a.stride + i + (int64_t)c0 * j;
+        xf[f] = (MASKED && mv[l] == 0.0) ? 0.0 : xv[l] + cv[l];
+      }
     }
-  }
+  };
+  if (mask != nullptr) run(std::true_type{});
+  else run(std::false_type{});
 }
 
 // T of the CG level: the mean of the cell-local copies at each vertex of local

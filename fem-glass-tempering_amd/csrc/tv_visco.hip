@@ -58,6 +58,16 @@ __device__ __forceinline__ TState t_part(const ViscoConst& c, const ViscoFields&
   const double T = f.T[t];
   const double Tp = f.Tp[t];
   const double Tfo = PAPER ? f.Tf[t] : 0.0;
+  // the six previous partial fictive temperatures loaded with T and T_prev,
+  // before any store: loaded one by one, each load waited behind the store
+  // before it (the compiler cannot prove that i sT + t and (i + 1) sT + t
+  // differ) -- six memory round trips per dof
+  double prev6[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) prev6[i] = f.Tfp[i * f.sT + t];
+  // (without the fence the scheduler sinks each load to just before its first
+  // use, between the divisions: one round trip per load again)
+  __builtin_amdgcn_sched_barrier(0);
   // Eq. 5 (VEM:156-161)
   const double phi = exp(c.H_over_Rg * (c.inv_Tb - 1.0 / T));
   // Eq. 25 (VEM:100-108), overwritten by Eq. 5 in the reference (Q1)
@@ -66,7 +76,7 @@ __device__ __forceinline__ TState t_part(const ViscoConst& c, const ViscoFields&
   double Tf = 0.0;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const double prev = f.Tfp[i * f.sT + t];
+    const double prev = prev6[i];
     const double cur = (c.lambda_m[i] * prev + T * c.dt * phi_tf) / (c.lambda_m[i] + c.dt * phi_tf);
     f.Tfp[i * f.sT + t] = cur;
     Tf = Tf + c.m_n[i] * cur;  // Eq. 26 inner(m, Tf_partial) (VEM:122-125)
