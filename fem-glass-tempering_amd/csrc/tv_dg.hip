@@ -389,23 +389,31 @@ __device__ __forceinline__ void fdm_mul(const DgGrid& g, const double* __restric
                                         const double (&v)[8], double (&y)[8]) {
   const int cn[3] = {g.c0, g.c1, g.c2};
   const int ci[3] = {(int)(cid % g.c0), (int)((cid / g.c0) % g.c1), (int)(cid / ((int64_t)g.c0 * g.c1))};
-  double h[3];
+  // every table value first (the neighbours' lengths at clamped indices):
+  // loaded where used, under the facet branches, each waited for the load
+  // before it -- six dependent round trips per cell
+  double h[3], ihk[3], hnb[3][2];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) h[k] = g.h[k][ci[k]];
+  for (int k = 0; k < 3; ++k) {
+    h[k] = g.h[k][ci[k]];
+    ihk[k] = g.ih[k][ci[k]];
+    hnb[k][0] = g.h[k][max(ci[k] - 1, 0)];
+    hnb[k][1] = g.h[k][min(ci[k] + 1, cn[k] - 1)];
+  }
   const double hd2 = h[0] * h[0] + h[1] * h[1] + h[2] * h[2];
   int64_t off[4];
   gface_offsets(g, off);
   double V[3][4], lam[3][2];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const double hk = h[k], ih = g.ih[k][ci[k]];
+    const double hk = h[k], ih = ihk[k];
     double a00 = ih, a01 = -ih, a11 = ih;  // 1D stiffness
     const int ea = k == 0 ? 1 : 0, eb = k == 2 ? 1 : 2;
 #pragma unroll
     for (int side = 0; side < 2; ++side) {
       const int nbi = ci[k] + (side ? 1 : -1);
       if (nbi >= 0 && nbi < cn[k]) {  // SIPG self terms of the facet (rows of k_dg_diag)
-        const double hn = g.h[k][nbi];
+        const double hn = hnb[k][side];
         const double pen = g.penalty * frsq(side ? hd2 : hd2 - hk * hk + hn * hn);
         a01 += 0.5 * ih;
         if (side) a11 += pen - ih;
@@ -912,21 +920,29 @@ __global__ __launch_bounds__(kBlock) void k_dg_bupdate(DgGrid g, const PcgState*
   const double* __restrict__ p = (it_host & 1) ? pB : pA;
   const double* __restrict__ pp = (it_host & 1) ? pA : pB;
   for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
-    double v[8], y[8];
+    // every load of the cell before the first store (a store to r, then the
+    // next copy's load from r: the compiler cannot prove them apart, so each
+    // load waited for the store and the loads before it)
+    double v[8], y[8], wv[8], dv[8], ppv[8], pv[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       const int64_t o = l * ncell + c;
-      double rr = r[o];
-      if (!INIT) {
-        rr -= a * __builtin_nontemporal_load(&w[o]);
-        r[o] = rr;
-        if (DXU) {
-          const double d0 = FIRST ? 0.0 : __builtin_nontemporal_load(&dx[o]);
-          __builtin_nontemporal_store((d0 + ap * __builtin_nontemporal_load(&pp[o])) + a * __builtin_nontemporal_load(&p[o]),
-                                      &dx[o]);
-        }
+      v[l] = r[o];
+      if (!INIT) wv[l] = __builtin_nontemporal_load(&w[o]);
+      if (DXU) {
+        dv[l] = FIRST ? 0.0 : __builtin_nontemporal_load(&dx[o]);
+        ppv[l] = __builtin_nontemporal_load(&pp[o]);
+        pv[l] = __builtin_nontemporal_load(&p[o]);
       }
-      v[l] = rr;
+    }
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const int64_t o = l * ncell + c;
+      if (!INIT) {
+        v[l] -= a * wv[l];
+        r[o] = v[l];
+        if (DXU) __builtin_nontemporal_store((dv[l] + ap * ppv[l]) + a * pv[l], &dx[o]);
+      }
     }
     fdm_mul(g, gface, c + c_loc, v, y);
 #pragma unroll
@@ -946,16 +962,19 @@ __global__ __launch_bounds__(kBlock) void k_dg_bpost(DgGrid g, const PcgState* _
   if (st->done) return;
   double acc[2] = {0.0, 0.0};
   for (int64_t c = blockIdx.x * (int64_t)kBlock + threadIdx.x; c < ncell; c += (int64_t)gridDim.x * kBlock) {
-    double v[8], y[8], rr[8];
+    // x0 loaded with r and w, before the smoother's table loads (it was
+    // loaded after them: one more round trip per cell)
+    double v[8], y[8], rr[8], xv[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       rr[l] = r[l * ncell + c];
       v[l] = rr[l] - w[l * ncell + c];
+      xv[l] = x0[l * ncell + c];
     }
     fdm_mul(g, gface, c + c_loc, v, y);
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-      const double zz = x0[l * ncell + c] + omega * y[l];
+      const double zz = xv[l] + omega * y[l];
       z[l * ncell + c] = zz;
       acc[0] += zz * zz;
       acc[1] += zz * rr[l];
