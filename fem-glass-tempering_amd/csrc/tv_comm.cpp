@@ -37,7 +37,7 @@ int refresh_dirty_ghosts(Ctx* c) {
   for (int f = 0; f < TV_NUM_FIELDS; ++f) {
     if (fl[f] == 0.0 || !c->f[f].ptr || f == TV_F_T || f == TV_F_T_PREV) continue;
     if (c->mixed_part && c->f[f].space != 0) continue;  // the sigma space of a mixed slab has no ghosts
-    const int64_t stride = c->f[f].space == 0 ? c->nT : c->nS;  // unstructured: the same vertex set (CG1 / CG1)
+    const int64_t stride = field_stride(c, c->f[f].space);  // unstructured: the same vertex set (CG1 / CG1)
     for (int k = 0; k < c->f[f].bs; ++k)
       if (int e = halo(c, c->f[f].ptr + k * stride)) return e;
     tilde = tilde || f == TV_F_S_TILDE || f == TV_F_S_TILDE_NEXT || f == TV_F_SIGMA_TILDE || f == TV_F_SIGMA_TILDE_NEXT;

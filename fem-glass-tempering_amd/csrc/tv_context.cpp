@@ -58,7 +58,7 @@ int alloc_field(Ctx* c, int id, int space, int bs) {
   FieldInfo& fi = c->f[id];
   fi.space = space;
   fi.bs = bs;
-  const int64_t n = (space == 0 ? c->nT : c->nS);
+  const int64_t n = field_stride(c, space);
   // every field starts at its own offset inside a 2 MiB page (id x 132 KiB):
   // the fused visco update streams ~26 fields at the same index at once, and
   // page-aligned starts put all of them on the same HBM channels together
@@ -566,7 +566,7 @@ int transfer(Ctx* c, int field, double* host, size_t n, int dir) {
   if (!fi.ptr) return c->fail(TV_ERR_STATE, "field not materialized (options.materialize = 0 keeps state fields only)");
   const int64_t ndof = (fi.space == 0) ? c->ownT_n : c->ownS_n;
   const int64_t off = (fi.space == 0) ? c->ownT_off : c->ownS_off;
-  const int64_t stride = (fi.space == 0) ? c->nT : c->nS;
+  const int64_t stride = field_stride(c, fi.space);
   const size_t need = (size_t)ndof * fi.bs;
   if (n != need)
     return c->fail(TV_ERR_ARG, "size mismatch: expected " + std::to_string(need) + " values, got " + std::to_string(n));
@@ -1077,7 +1077,7 @@ int tv_field_device_ptr(void* ctx, int field, void** dev_ptr, int64_t* comp_stri
   hipSetDevice(c->device);
   HIPC(hipStreamSynchronize(c->stream));  // the queued steps are complete when the consumer reads
   if (dev_ptr) *dev_ptr = c->f[field].ptr;
-  if (comp_stride) *comp_stride = c->f[field].space == 0 ? c->nT : c->nS;
+  if (comp_stride) *comp_stride = field_stride(c, c->f[field].space);
   return TV_OK;
 }
 
@@ -1090,7 +1090,7 @@ int tv_set_initial_condition(void* ctx, double T0) {
   launch_fill(c->f[TV_F_T].ptr, c->nT, T0, c->stream);
   launch_fill(c->f[TV_F_T_PREV].ptr, c->nT, T0, c->stream);
   launch_fill(c->f[TV_F_TF].ptr, c->nT, T0, c->stream);
-  launch_fill(c->f[TV_F_TF_PARTIAL].ptr, c->nT * 6, T0, c->stream);
+  launch_fill(c->f[TV_F_TF_PARTIAL].ptr, field_stride(c, 0) * 6, T0, c->stream);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(c->stream));
   return TV_OK;
@@ -1189,7 +1189,7 @@ int tv_output_write(void* ctx, double t) {
                          : c->mixed_part ? (fi.space == 0 ? c->outT_n : c->outS_n)
                                          : (fi.space == 0) ? c->ownT_n : c->ownS_n;
     const int64_t off = local_all ? 0 : (fi.space == 0) ? c->ownT_off : c->ownS_off;
-    const int64_t stride = (fi.space == 0) ? c->nT : c->nS;
+    const int64_t stride = field_stride(c, fi.space);
     const bool dgsp = (fi.space == 0 ? c->fam_T : c->fam_S) == TV_DG;
     const int nl = dgsp ? (1 << c->dim) : 0;
     const int64_t ncell = dgsp ? ndof / nl : 0;

@@ -519,8 +519,8 @@ void visco_setup(Ctx* c, ViscoConst& k, ViscoFields& v) {
     k.lambda_k[i] = P.lambda_k[i]; k.k_n[i] = P.k_n[i];
   }
   std::memset(&v, 0, sizeof(v));
-  v.sT = c->nT;
-  v.sS = c->nS;
+  v.sT = field_stride(c, 0);
+  v.sS = field_stride(c, 1);
   v.T = c->f[TV_F_T].ptr; v.Tp = c->f[TV_F_T_PREV].ptr; v.Tn = c->f[TV_F_T_NEXT].ptr;
   v.phi = c->f[TV_F_PHI].ptr; v.phin = c->f[TV_F_PHI_NEXT].ptr; v.xi = c->f[TV_F_XI].ptr;
   v.Tf = c->f[TV_F_TF].ptr; v.Tfp = c->f[TV_F_TF_PARTIAL].ptr;
