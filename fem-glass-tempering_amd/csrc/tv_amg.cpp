@@ -519,7 +519,6 @@ bool half_stencil(Ctx* c, const Csr& A, const int64_t (&d)[3], UmGrid& sg) {
   sg.nv = sg.nrow = n;
   sg.s1 = s1;
   sg.s2 = s2;
-  sg.s14 = n;  // host-built slot arrays: stride n
   sg.V14 = dX;
   sg.J14 = dX;
   return true;

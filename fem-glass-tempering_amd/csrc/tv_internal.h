@@ -230,7 +230,6 @@ struct UmGrid {
   const int64_t* brow;
   int64_t nbr;
   int64_t s1, s2;
-  int64_t s14;  // slot stride of the X14 arrays: nv rounded up to 64 (each slot 512-byte aligned)
   // Robin terms
   const int* fv;         // [m][facet] facet vertex ids, facet-local tensor order
   const double* fw;      // [q][facet] w_q |J_s|(q), 3^(d-1) points

@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // 32-bit unsigned element indices (14 nv < 2^31 and 8 x that < 2^32: checked
     // at setup): uniform base + 32-bit offset loads, no 64-bit address VGPRs
     const double* __restrict__ J = g.J14;
-    const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2, ss = (unsigned)g.s14;
+    const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2;
 #pragma unroll 1
     for (int64_t k = ch * m.kper; k < k1; ++k) {
       const unsigned r = (unsigned)(i + m.n0 * j + g.s2 * k);
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
         const bool hi = r + o < nv, lo = r >= o;  // (o >= 0 for the upper slots)
         const unsigned cu = hi ? r + o : r, cl = lo ? r - o : r;
-        const unsigned ku = (unsigned)q14 * ss;
+        const unsigned ku = (unsigned)q14 * nv;
         acc += J[ku + r] * u[cu];
         if (q14 > 0) acc += (lo ? J[ku + cl] : 0.0) * u[cl];
       }
@@ -566,7 +566,7 @@ __global__ __launch_bounds__(kBlock) void k_um_res14(UmGrid g, March14 m, const 
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const double* __restrict__ Mh = g.M14;
   const double* __restrict__ Kh = g.K14;
-  const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2, ss = (unsigned)g.s14;
+  const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2;
   for (int64_t gw = (int64_t)blk * WPB + wave; gw < m.ncol * m.kch; gw += nw) {
     const int64_t seg = gw % m.nseg, t = gw / m.nseg;
     const int64_t j = t % m.n1, ch = t / m.n1;
@@ -583,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void k_um_res14(UmGrid g, March14 m, const 
         const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
         const bool hi = r + o < nv, lo = r >= o;
         const unsigned cu = hi ? r + o : r, cl = lo ? r - o : r;
-        const unsigned ku = (unsigned)q14 * ss;
+        const unsigned ku = (unsigned)q14 * nv;
         const double xu = u[cu];
         acc += Mh[ku + r] * (xu - up[cu]);
         acc2 += Kh[ku + r] * xu;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kBlock) void k_sg_rows(UmGrid g, const PcgState* __
                                                    double* __restrict__ y) {
   if (st != nullptr && st->done) return;
   const double* __restrict__ J = g.J14;
-  const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2, ss = (unsigned)g.s14;
+  const unsigned nv = (unsigned)g.nv, s1 = (unsigned)g.s1, s2 = (unsigned)g.s2;
   for (unsigned r = blockIdx.x * kBlock + threadIdx.x; r < nv; r += gridDim.x * kBlock) {
     double acc = 0.0;
 #pragma unroll
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(kBlock) void k_sg_rows(UmGrid g, const PcgState* __
       const unsigned o = (unsigned)(q % 3 - 1) + s1 * (unsigned)((q / 3) % 3 - 1) + s2 * (unsigned)(q / 9 - 1);
       const bool hi = r + o < nv, lo = r >= o;
       const unsigned cu = hi ? r + o : r, cl = lo ? r - o : r;
-      const unsigned ku = (unsigned)k * ss;
+      const unsigned ku = (unsigned)k * nv;
       acc += J[ku + r] * x[cu];
       if (k > 0) acc += (lo ? J[ku + cl] : 0.0) * x[cl];
     }
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_um_robin_fold(UmGrid g, const double
   for (int64_t b = blockIdx.x * (int64_t)kBlock + threadIdx.x; b < g.nbr; b += (int64_t)gridDim.x * kBlock) {
     const int64_t r = g.brow[b];
 #pragma unroll
-    for (int k = 0; k < 14; ++k) g.J14[(int64_t)k * g.s14 + r] = g.V14[(int64_t)k * g.s14 + r];
+    for (int k = 0; k < 14; ++k) g.J14[(int64_t)k * g.nv + r] = g.V14[(int64_t)k * g.nv + r];
     const int t1 = g.boff[r + 1];
     for (int t = g.boff[r]; t < t1; ++t) {
       const int code = g.binc[t];
@@ -886,7 +886,7 @@ __global__ __launch_bounds__(kBlock) void k_um_robin_fold(UmGrid g, const double
         const int64_t dj = (rem + g.s1 / 2 + g.s1) / g.s1 - 1;
         const int64_t di = rem - dj * g.s1;
         const int sl = (int)((di + 1) + 3 * (dj + 1) + 9 * (dk + 1));
-        if (sl >= 13) g.J14[(int64_t)(sl - 13) * g.s14 + r] += g.dt * cn[n];
+        if (sl >= 13) g.J14[(int64_t)(sl - 13) * g.nv + r] += g.dt * cn[n];
       }
     }
   }
@@ -1217,16 +1217,15 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   double *V14 = nullptr, *J14 = nullptr, *M14 = nullptr, *K14 = nullptr;
   int64_t* brow_d = nullptr;
   // (32-bit element offsets into the 14 slot arrays: 14 nv * 8 B < 4 GiB)
-  const int64_t s14 = (nv + 63) / 64 * 64;
-  if (nrow == nv && s14 * 14 * 8 < ((int64_t)1 << 32) && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
-    const size_t n14 = (size_t)14 * s14;
+  if (nrow == nv && nv * 14 * 8 < ((int64_t)1 << 32) && structured_topology(dim, nv, nc, cells, &ss1, &ss2)) {
+    const size_t n14 = (size_t)14 * nv;
     if (um_alloc(d, n14, &V14, err) || um_alloc(d, n14, &J14, err) || um_alloc(d, n14, &M14, err) ||
         um_alloc(d, n14, &K14, err))
       return 1;
     for (double* X : {V14, M14, K14}) UMC(hipMemsetAsync(X, 0, sizeof(double) * n14, s));
-    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, s14, V14, 1);
-    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, M, ss1, ss2, s14, M14, 1);
-    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, K, ss1, ss2, s14, K14, 1);
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, V, ss1, ss2, nv, V14, 1);
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, M, ss1, ss2, nv, M14, 1);
+    hipLaunchKernelGGL(k_um_to_stencil, gr_v, bl, 0, s, nrow, soff_d, cols_d, K, ss1, ss2, nv, K14, 1);
     UMC(hipGetLastError());
     UMC(hipMemcpyAsync(J14, V14, sizeof(double) * n14, hipMemcpyDeviceToDevice, s));
   }
@@ -1259,7 +1258,6 @@ int um_setup(int dim, int64_t nv, int64_t nrow, const double* xyz, int64_t nc, c
   g.J14 = J14;
   g.M14 = M14;
   g.K14 = K14;
-  g.s14 = s14;
   g.brow = brow_d;
   g.nbr = nbr;
   g.s1 = ss1;
