@@ -237,3 +237,38 @@ def test_sipg_plus_side_sensitivity():
         out[name] = np.linalg.norm(T["lower"] - T["higher"]) / np.linalg.norm(T["lower"])
     assert out["uniform"] < 1e-14, out
     assert 1e-7 < out["graded"] < 1e-4, out
+
+
+def test_newton_settings_of_the_restatement():
+    """problem.solver / problem.ksp settings (ThermoViscoProblem.py:334-346) in
+    the oracle: max_it below the step's count raises with error_on_nonconvergence
+    (dolfinx's RuntimeError) and returns unconverged without it; a looser rtol
+    takes fewer iterations; the KSP tolerances reach pcg_jacobi"""
+    axes = [np.linspace(0.0, 2.0, 5), np.linspace(0.0, 1.0, 3), np.linspace(0.0, 0.5, 3)]
+    cfg = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
+
+    def prob():
+        p = O.OracleProblem(O.rectilinear_mesh(axes), (0.0, 1.0), 0.1, cfg, dict(O.MAIN_MODEL_PARAMS), linear="pcg")
+        p.setup()
+        return p
+
+    ref = prob()
+    ref.solve_T()
+    n, k = ref.newton_history[0]
+    assert n >= 3
+    p = prob()
+    p.newton["max_it"] = n - 1
+    with pytest.raises(O.NewtonNotConverged):
+        p.solve_T()
+    p = prob()
+    p.newton.update(max_it=n - 1, error_on_nonconvergence=False)
+    p.solve_T()
+    assert p.newton_history[0][0] == n - 1
+    p = prob()
+    p.newton["rtol"] = 1e-4
+    p.solve_T()
+    assert p.newton_history[0][0] < n
+    p = prob()
+    p.ksp = {"rtol": 1e-9}
+    p.solve_T()
+    assert p.newton_history[0][0] == n and p.newton_history[0][1] > k
