@@ -968,8 +968,8 @@ __global__ __launch_bounds__(kBlock) void k_dg_bpost(DgGrid g, const PcgState* _
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
       rr[l] = r[l * ncell + c];
-      v[l] = rr[l] - w[l * ncell + c];
-      xv[l] = x0[l * ncell + c];
+      v[l] = rr[l] - __builtin_nontemporal_load(&w[l * ncell + c]);  // w and x0: not read again
+      xv[l] = __builtin_nontemporal_load(&x0[l * ncell + c]);
     }
     fdm_mul(g, gface, c + c_loc, v, y);
 #pragma unroll
