@@ -173,6 +173,8 @@ typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
 constexpr int kPairSeg = kWave - 1;  // outputs per wave
 
 __device__ __forceinline__ d2a8 ld_pair(const double* p) { return *reinterpret_cast<const d2a8*>(p); }
+// a pair not read again: non-temporal (leaves the caches to the vectors that are)
+__device__ __forceinline__ d2a8 ld_pair_nt(const double* p) { return __builtin_nontemporal_load(reinterpret_cast<const d2a8*>(p)); }
 
 // Restriction, one wave per (coarse row, 63-node x segment); lane l is coarse
 // node I = 63 seg - 1 + l (lane 0 = the halo lane whose right fine node is
@@ -235,7 +237,7 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
     const int64_t f = (int64_t)fjr[b] * nf + fpl * fkr[c] + f1;
     const int64_t fp = pair ? f : f - 1;
     rv[q] = ld_pair(bf + fp);
-    wv[q] = (wf != nullptr) ? ld_pair(wf + fp) : d2a8{0.0, 0.0};  // wf null: bf is the residual itself
+    wv[q] = (wf != nullptr) ? ld_pair_nt(wf + fp) : d2a8{0.0, 0.0};  // wf null: bf is the residual itself
     if (MASK) mv[q] = ld_pair(mask + fp);
   }
 #pragma unroll
