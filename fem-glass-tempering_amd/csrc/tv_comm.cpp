@@ -93,6 +93,23 @@ int halo_host(Ctx* c, const CgGrid& g, double* v) {
     return c->fail(TV_ERR_COMM, "host sendrecv failed");
   if (nhi && c->host_sendrecv(s_hi, (size_t)nhi, c->rank + 1, r_hi, (size_t)nhi, c->rank + 1, c->host_user))
     return c->fail(TV_ERR_COMM, "host sendrecv failed");
+  if (c->comm_self && g.g_lo && g.g_hi) {  // loopback, both sides: periodic images (see group_planes)
+    HIPC(hipMemcpyAsync(v, r_hi, nlo * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPC(hipMemcpyAsync(v + plane * g.k_end, r_lo, nhi * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return TV_OK;
+  }
+  if (c->comm_self && (g.g_lo > 1 || g.g_hi > 1)) {
+    // loopback, one side: the received planes land mirrored (see group_planes)
+    for (int j = 0; j < g.g_lo; ++j)  // ghost plane k_begin - 1 - j <- owned plane k_begin + j
+      HIPC(hipMemcpyAsync(v + plane * (g.k_begin - 1 - j), r_lo + plane * j, plane * sizeof(double),
+                          hipMemcpyHostToDevice, c->stream));
+    for (int j = 0; j < g.g_hi; ++j)  // ghost plane k_end + j <- owned plane k_end - 1 - j
+      HIPC(hipMemcpyAsync(v + plane * (g.k_end + j), r_hi + plane * (g.g_hi - 1 - j), plane * sizeof(double),
+                          hipMemcpyHostToDevice, c->stream));
+    HIPC(hipStreamSynchronize(c->stream));
+    return TV_OK;
+  }
   if (nlo) HIPC(hipMemcpyAsync(v, r_lo, nlo * sizeof(double), hipMemcpyHostToDevice, c->stream));
   if (nhi) HIPC(hipMemcpyAsync(v + plane * g.k_end, r_hi, nhi * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
@@ -103,6 +120,35 @@ int halo_host(Ctx* c, const CgGrid& g, double* v) {
 static int group_planes(Ctx* c, const CgGrid& g, double* v) {
   const int64_t plane = (int64_t)g.n0 * g.n1;
   const size_t nlo = (size_t)(plane * g.g_lo), nhi = (size_t)(plane * g.g_hi);
+  if (c->comm_self && g.g_lo && g.g_hi) {
+    // loopback, a slab with neighbours on both sides: the neighbours are this
+    // slab's own periodic images (ghost planes below <- the top owned planes,
+    // ghost planes above <- the bottom ones), so the slab solves one period of
+    // a y-periodic plate -- symmetric on every grid of the multigrid hierarchy
+    // whose owned planes are a translate of the fine slab (tools/loopback_check.py)
+    NCCLC(ncclSend(v + plane * (g.k_end - g.g_lo), nlo, ncclDouble, 0, c->comm, c->stream));
+    NCCLC(ncclRecv(v, nlo, ncclDouble, 0, c->comm, c->stream));
+    NCCLC(ncclSend(v + plane * g.k_begin, nhi, ncclDouble, 0, c->comm, c->stream));
+    NCCLC(ncclRecv(v + plane * g.k_end, nhi, ncclDouble, 0, c->comm, c->stream));
+    return TV_OK;
+  }
+  if (c->comm_self && (g.g_lo > 1 || g.g_hi > 1)) {
+    // loopback, one neighbour, several ghost planes: the slab's MIRROR image
+    // across the interface (ghost plane k_begin - 1 - j = owned plane k_begin + j),
+    // the even extension about the interface midplane, whose operator on the
+    // owned planes stays symmetric (a shifted copy of the boundary planes is
+    // not).  One send / receive pair per plane; self pairs match in issue order.
+    // (One ghost plane: the mirror is the plain copy below.)
+    for (int j = 0; j < g.g_lo; ++j) {
+      NCCLC(ncclSend(v + plane * (g.k_begin + j), (size_t)plane, ncclDouble, 0, c->comm, c->stream));
+      NCCLC(ncclRecv(v + plane * (g.k_begin - 1 - j), (size_t)plane, ncclDouble, 0, c->comm, c->stream));
+    }
+    for (int j = 0; j < g.g_hi; ++j) {
+      NCCLC(ncclSend(v + plane * (g.k_end - 1 - j), (size_t)plane, ncclDouble, 0, c->comm, c->stream));
+      NCCLC(ncclRecv(v + plane * (g.k_end + j), (size_t)plane, ncclDouble, 0, c->comm, c->stream));
+    }
+    return TV_OK;
+  }
   if (nlo) {  // neighbour rank - 1: send the first g_lo owned planes, receive the ghost planes below
     NCCLC(ncclSend(v + plane * g.k_begin, nlo, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
     NCCLC(ncclRecv(v, nlo, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
@@ -345,8 +391,12 @@ void check_ids(const Ctx* c, const CgGrid& g, const std::vector<double>& h, int6
   const int64_t plane = (int64_t)g.n0 * g.n1;
   for (int k = 0; k < g.n2; ++k) {
     int64_t src = first_plane + k;                                  // global plane the values must come from
-    if (k < g.k_begin && c->comm_self) src = first_plane + g.k_begin + k;  // this rank's first g_lo planes
-    if (k >= g.k_end && c->comm_self) src = first_plane + g.k_end - g.g_hi + (k - g.k_end);
+    // loopback (group_planes): periodic images of the slab when it has both
+    // neighbours, else the mirror image of its boundary planes
+    const int S = g.k_end - g.k_begin;
+    const bool per = g.g_lo && g.g_hi;
+    if (k < g.k_begin && c->comm_self) src = first_plane + (per ? k + S : g.k_begin + (g.k_begin - 1 - k));
+    if (k >= g.k_end && c->comm_self) src = first_plane + (per ? k - S : g.k_end - 1 - (k - g.k_end));
     if ((k < g.k_begin && !g.g_lo) || (k >= g.k_end && !g.g_hi)) continue;
     for (int64_t e = 0; e < plane; ++e) {
       ++*n_chk;
@@ -541,19 +591,23 @@ int cgs_exchange(Ctx* c, double* wout, const double* fout) {
       return c->fail(TV_ERR_COMM, "host sendrecv failed");
     if (g.g_hi && c->host_sendrecv(s_hi, (size_t)plane, c->rank + 1, r_hi, (size_t)plane, c->rank + 1, c->host_user))
       return c->fail(TV_ERR_COMM, "host sendrecv failed");
-    if (g.g_lo) HIPC(hipMemcpyAsync(wout, r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    if (g.g_hi) HIPC(hipMemcpyAsync(wout + plane * g.k_end, r_hi, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    const bool per = c->comm_self && g.g_lo && g.g_hi;  // loopback: periodic images (group_planes)
+    if (g.g_lo) HIPC(hipMemcpyAsync(wout, per ? r_hi : r_lo, plane * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (g.g_hi)
+      HIPC(hipMemcpyAsync(wout + plane * g.k_end, per ? r_lo : r_hi, plane * sizeof(double), hipMemcpyHostToDevice,
+                          c->stream));
     return TV_OK;
   }
   // one group: the 3-scalar all-reduce and the ghost planes of w (<= 2 peers)
   NCCLC(ncclGroupStart());
   NCCLC(ncclAllReduce(c->sums, c->sums, 3, ncclDouble, ncclSum, c->comm, c->stream));
+  const bool per = c->comm_self && g.g_lo && g.g_hi;  // loopback: periodic images (group_planes)
   if (g.g_lo) {
-    NCCLC(ncclSend(c->wsend, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
+    NCCLC(ncclSend(c->wsend + (per ? plane : 0), plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
     NCCLC(ncclRecv(wout, plane, ncclDouble, peer(c, c->rank - 1), c->comm, c->stream));
   }
   if (g.g_hi) {
-    NCCLC(ncclSend(c->wsend + plane, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
+    NCCLC(ncclSend(c->wsend + (per ? 0 : plane), plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
     NCCLC(ncclRecv(wout + plane * g.k_end, plane, ncclDouble, peer(c, c->rank + 1), c->comm, c->stream));
   }
   NCCLC(ncclGroupEnd());
@@ -637,11 +691,16 @@ int tv_comm_init_host(void* ctx, int n_ranks, int rank, tv_host_allreduce_fn all
                       tv_host_sendrecv_fn sendrecv_fn, void* user) {
   Ctx* c = static_cast<Ctx*>(ctx);
   if (!c || !allreduce_fn || !sendrecv_fn) return TV_ERR_ARG;
-  if (n_ranks != c->n_parts || rank != c->part)
+  // n_ranks = 1 on a partition of a partitioned mesh: a host-staged LOOPBACK
+  // (every neighbour is this rank itself, as tv_comm_init_loopback over RCCL),
+  // with the same mirrored ghost planes
+  const bool self = n_ranks == 1 && rank == 0 && c->n_parts > 1;
+  if (!self && (n_ranks != c->n_parts || rank != c->part))
     return c->fail(TV_ERR_ARG, "communicator size/rank must match the mesh partition (n_parts/part)");
   hipSetDevice(c->device);
-  c->nranks = n_ranks;
-  c->rank = rank;
+  c->nranks = c->n_parts;
+  c->rank = c->part;
+  c->comm_self = self;
   c->host_allreduce = allreduce_fn;
   c->host_sendrecv = sendrecv_fn;
   c->host_user = user;

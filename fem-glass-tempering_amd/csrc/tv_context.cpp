@@ -306,11 +306,23 @@ int setup_mesh(Ctx* c, const tv_mesh_desc* m) {
     // deep ghosts (three planes per interface) for the distributed multigrid
     // with global coupling: the level-0 vectors of a V-cycle are then computed
     // on the ghost planes too and need no exchange of their own (tv_mgdist.cpp)
+    // Every rank takes the same decision: from the SMALLEST slab of the global
+    // partition (part_planes hands out sizes that differ by one plane), so a
+    // partition too thin for deep ghosts gives every rank the one-ghost-plane
+    // form instead of failing some ranks' creation while the others wait in
+    // their first collective
+    int min_slab = N2;
+    for (int q = 0; q < P; ++q) {
+      int q0, q1;
+      part_planes(N2, P, q, &q0, &q1);
+      min_slab = std::min(min_slab, q1 - q0);
+    }
+    // (an explicit SINGLE_REDUCTION with GMG is refused by mg_setup: the
+    // single-reduction GMG-PCG is AUTO's choice on deep-ghost slabs)
     const bool deep = P > 1 && d == 3 && c->O.preconditioner == TV_PC_GMG && c->O.mg_coupling != TV_MG_COUPLING_LOCAL &&
-                      c->O.pcg_variant != TV_PCG_SINGLE_REDUCTION;
+                      min_slab >= kDeepGhosts;
     c->ghost_depth = deep ? kDeepGhosts : 1;
     const int G = c->ghost_depth;
-    if (deep && b1 - b0 < G) return c->fail(TV_ERR_ARG, "partitioned GMG: fewer owned planes than the ghost depth (3)");
     const int g_lo = (p > 0) ? G : 0, g_hi = (p < P - 1) ? G : 0;
     if (int e = build_cg_grid(c, d, X, b0 - g_lo, (b1 - b0) + g_lo + g_hi, g_lo, g_hi, p == 0, p == P - 1, g, c->coef,
                               &c->bnodes, c->ffbuf))
@@ -491,6 +503,8 @@ int setup_fields(Ctx* c) {
   // records of width <= 3 per workgroup + the shard records of the two-level tail
   HIPC(hipMalloc(&c->partials, sizeof(double) * 3 * ((size_t)np + 2 * kShards)));
   HIPC(hipMalloc(&c->sums, sizeof(double) * 8));
+  HIPC(hipMalloc(&c->ngate, sizeof(double) * 2));
+  HIPC(hipMemset(c->ngate, 0, sizeof(double) * 2));
   HIPC(hipMalloc(&c->counters, sizeof(unsigned) * kCounterWords));
   HIPC(hipMemsetAsync(c->counters, 0, sizeof(unsigned) * kCounterWords, c->stream));
   HIPC(hipMalloc(&c->st, sizeof(PcgState)));
@@ -944,7 +958,7 @@ int tv_destroy(void* ctx) {
   if (c->mgx) hipFree(c->mgx);
   if (c->mg_s) hipFree(c->mg_s);
   if (c->dggface) hipFree(c->dggface);
-  for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->scratch})
+  for (double* p : {c->r, c->z, c->pA, c->pB, c->w, c->dinv, c->partials, c->sums, c->ngate, c->scratch})
     if (p) hipFree(p);
   for (int s = 0; s < 3; ++s) {
     if (c->coef[s]) hipFree(c->coef[s]);

@@ -91,6 +91,13 @@ struct Ctx {
   hipEvent_t evp[2] = {nullptr, nullptr};  // PCG convergence polls (double-buffered)
   hipEvent_t evn = nullptr;                 // Newton: ||dx|| copied to the host
   const double* nrm_dev = nullptr;          // ... from here (||dx||^2, final on every rank behind evn)
+  // the device's Newton test (queue_newton_norm): ngate[0] = ||dx||^2, ngate[1] =
+  // the decision; gate_dev points at the decision of the last queued norm
+  // (nullptr: iteration 1, no test), gate_r0 = ||dx_1|| once known
+  double* ngate = nullptr;
+  const double* gate_dev = nullptr;
+  double gate_r0 = 0.0;
+  bool gate_ready = false;
   tv_params P{};
   tv_options O{};
   int dim = 1;
@@ -318,6 +325,9 @@ CgsBuffers cgs_buffers(Ctx* c, const double* T, int it);
 // (NewtonGate); *end_queued tells tv_step that it ran (the step is done)
 int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end = 0, bool* end_queued = nullptr);
 int visco(Ctx* c, bool copy_Tprev, const NewtonGate& gate = NewtonGate{});
+// the Newton iteration's ||dx||^2 (final on every rank at nrm2) to the host,
+// with the device's convergence decision when r0 is known; records evn
+int queue_newton_norm(Ctx* c, const double* nrm2);
 void launch_bc_mask(Ctx* c, double* dinv);  // dinv = 0 on the Dirichlet-constrained rows
 
 // ---- tv_mgsolve.cpp ----

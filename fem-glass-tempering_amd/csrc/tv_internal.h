@@ -155,17 +155,17 @@ struct ViscoConst {
 };
 
 // Pointers of the viscoelastic state (component-major, stride = n_local).
-// the incremental Newton test of newton() on the device: sqrt(*nrm2) / r0 < rtol
-// or sqrt(*nrm2) < atol (nrm2 == nullptr: always true)
+// the incremental Newton test of newton(), decided ONCE on the device
+// (k_newton_test, tv_solver.cpp): *flag != 0 when sqrt(||dx||^2) / r0 < rtol or
+// sqrt(||dx||^2) < atol; the host copies the same flag and takes it as its own
+// convergence decision, so a gated launch and the host never disagree
+// (flag == nullptr: always open)
 struct NewtonGate {
-  const double* nrm2 = nullptr;
-  double r0 = 1.0, rtol = 0.0, atol = 0.0;
+  const double* flag = nullptr;
 };
 #ifdef __HIPCC__
 __device__ __forceinline__ bool newton_gate_open(const NewtonGate& g) {
-  if (g.nrm2 == nullptr) return true;
-  const double rn = sqrt(*g.nrm2);
-  return (rn / g.r0 < g.rtol) || (rn < g.atol);
+  return g.flag == nullptr || *g.flag != 0.0;
 }
 #endif
 

@@ -13,6 +13,16 @@ __global__ __launch_bounds__(kBlock) void k_read_sweep(const double* __restrict_
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) acc += a[t];
   if (acc == 12345.678) out[blockIdx.x] = acc;  // practically never: keeps the loads
 }
+// launch audit (tv_time_kernel ids 12-17): a one-thread kernel that holds the
+// stream for `ticks` of the 100 MHz REALTIME clock, so that the chain queued
+// behind it is timed as the GPU runs it, not at the host's enqueue rate
+__global__ void k_spin(uint64_t ticks) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+  }
+}
+__global__ void k_noop() {}
 
 }  // namespace tv
 
@@ -183,6 +193,50 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     }
     for (auto& e : ev) hipEventDestroy(e);
     *ms = sum / reps;
+    return TV_OK;
+  }
+  if (kernel >= 12 && kernel <= 17) {
+    // launch audit: `reps` back-to-back launches of one
+    // kind queued behind k_spin, HIP events around the chain, per launch =
+    // elapsed / reps -- the dependent-launch cost as the GPU pays it, unprofiled.
+    //   12 an empty one-thread kernel        13 k_set_state (one thread, 160-B argument)
+    //   14 the one-block reduce + KSPCG logic 15 k_mg_jacobi on the coarsest GMG level
+    //   16 J x on GMG level 1 (march)        17 J x on the fine grid (march + faces)
+    if ((kernel >= 15 && kernel <= 16) && (!c->mg_on || c->mg.empty() || c->amg_on || c->mg_dg))
+      return c->fail(TV_ERR_ARG, "kernel ids 15-16: CG GMG levels required");
+    if (kernel == 17 && (c->um || c->fam_T != TV_CG)) return c->fail(TV_ERR_ARG, "kernel 17: CG box mesh");
+    PcgState h{};
+    h.max_it = 1 << 30;  // running: the GMG kernels do their work
+    HIPC(hipMemcpyAsync(c->st, &h, sizeof(PcgState), hipMemcpyHostToDevice, c->stream));
+    auto launch = [&]() {
+      switch (kernel) {
+        case 12: hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, c->stream); break;
+        case 13: launch_set_state(c->st, h, c->stream); break;
+        case 14: launch_reduce_logic(c->partials, 256, 2, c->sums, c->st, 0, 0, c->stream); break;
+        case 15: {
+          MgLevel& L = c->mg.back();
+          launch_mg_jacobi(L.n, c->st, L.b, nullptr, nullptr, L.dinv, L.omega, L.x, 0, c->stream);
+          break;
+        }
+        case 16: {
+          MgLevel& L = c->mg[0];
+          launch_cg_japply(L.g, L.T, L.x, L.w, nullptr, nullptr, c->stream, c->st);
+          break;
+        }
+        default: op_japply(c, c->f[TV_F_T].ptr, c->pA, c->w, nullptr, nullptr); break;
+      }
+    };
+    for (int i = 0; i < 3; ++i) launch();  // warm-up
+    HIPC(hipStreamSynchronize(c->stream));
+    // ~8 us of host enqueue per launch at most: the chain is queued before the spin ends
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, c->stream, (uint64_t)reps * 800 + 20000);
+    HIPC(hipEventRecord(c->ev0, c->stream));
+    for (int i = 0; i < reps; ++i) launch();
+    HIPC(hipEventRecord(c->ev1, c->stream));
+    HIPC(hipEventSynchronize(c->ev1));
+    float t = 0.f;
+    HIPC(hipEventElapsedTime(&t, c->ev0, c->ev1));
+    *ms = (double)t / reps;
     return TV_OK;
   }
   if (kernel == 10) {

@@ -434,6 +434,13 @@ int mg_apply0_dist(Ctx* c, const double* T, const RedTail* tail) {
     MgLevel& C = c->mg[l];
     // every local fine plane, ghost planes included (their inputs are local)
     launch_mg_prolong(C.xf, c->st, r.x, C.x, l == 0 ? dmask : nullptr, s);
+    // loopback transport test only (tv_comm_init_loopback: the neighbours are
+    // this slab's periodic images): the ghost planes prolongated from the
+    // replicated GLOBAL level are not the images of the owned ones, so they are
+    // refreshed from them -- on a real partition the exchange would deliver
+    // exactly what the prolongation computed there (a no-op, never issued)
+    if (c->comm_self && l + 1 == A && A < L)
+      if (int e = vhalo(*r.g, r.x)) return e;
     // level 0: J x, the post-smoothing and the (z.z, z.r) records in the march
     // epilogue (+ the side-face pass with the reduction tail), as on one partition
     if (l == 0 && launch_cg_japply_post(*r.g, r.T, r.x, r.b, r.dinv, r.omega, c->z, c->st, c->partials, tail, s) >= 0)
@@ -581,9 +588,7 @@ static int pcg_solve_mg_dist_cgs(Ctx* c, const double* T, int* its, int* reason,
       launch_post_group(n, c->st, nullptr, nullptr, c->f[TV_F_DX].ptr + off, c->f[TV_F_T].ptr + off, c->partials, nrm,
                         c->stream);
       if (int e = allreduce(c, nrm, 1)) return e;
-      HIPC(hipMemcpyAsync(c->h_sums, nrm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPC(hipEventRecord(c->evn, c->stream));
-      c->nrm_dev = nrm;
+      if (int e = queue_newton_norm(c, nrm)) return e;
     }
     return TV_OK;
   };
@@ -676,9 +681,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post)
       launch_post_group(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, c->f[TV_F_T].ptr + off,
                         c->partials, nrm, c->stream);
       if (int e = allreduce(c, nrm, 1)) return e;  // collective on every rank, run or gated off
-      HIPC(hipMemcpyAsync(c->h_sums, nrm, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPC(hipEventRecord(c->evn, c->stream));
-      c->nrm_dev = nrm;
+      if (int e = queue_newton_norm(c, nrm)) return e;
     }
     return TV_OK;
   };

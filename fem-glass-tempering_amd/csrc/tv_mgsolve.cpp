@@ -502,9 +502,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
     HIPC(hipEventRecord(c->evp[0], c->stream));
     if (post) {  // the Newton iteration's next work, queued before the host's poll (it runs once)
       launch_post_group(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, c->f[TV_F_T].ptr, c->partials, c->sums, c->stream);
-      HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPC(hipEventRecord(c->evn, c->stream));
-      c->nrm_dev = c->sums;
+      if (int e = queue_newton_norm(c, c->sums)) return e;
     }
     return TV_OK;
   };

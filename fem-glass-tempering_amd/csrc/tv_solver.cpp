@@ -345,6 +345,33 @@ int dirichlet_pre(Ctx* c, const double* T) {
   return TV_OK;
 }
 
+// the Newton test on the device (one thread): the only place the decision is
+// taken -- the gated step-end launches read out[1], the host copies it
+__global__ void k_newton_test(const double* __restrict__ nrm2, double r0, double rtol, double atol,
+                              double* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    const double v = *nrm2;
+    const double rn = sqrt(v);
+    out[0] = v;
+    out[1] = ((rn / r0 < rtol) || (rn < atol)) ? 1.0 : 0.0;
+  }
+}
+
+int queue_newton_norm(Ctx* c, const double* nrm2) {
+  c->nrm_dev = nrm2;
+  if (c->gate_ready) {
+    hipLaunchKernelGGL(k_newton_test, dim3(1), dim3(64), 0, c->stream, nrm2, c->gate_r0, c->O.newton_rtol,
+                       c->O.newton_atol, c->ngate);
+    HIPC(hipMemcpyAsync(c->h_sums, c->ngate, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    c->gate_dev = c->ngate + 1;
+  } else {
+    HIPC(hipMemcpyAsync(c->h_sums, nrm2, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    c->gate_dev = nullptr;
+  }
+  HIPC(hipEventRecord(c->evn, c->stream));
+  return TV_OK;
+}
+
 // the end of a time step (tv_step): the visco update with T_prev <- T, or the
 // copy alone (thermal only), optionally gated on the device's Newton test; the
 // visco update's HIP events bracket it (the previous pair is read first: it is
@@ -352,7 +379,7 @@ int dirichlet_pre(Ctx* c, const double* T) {
 // the previous update -- an 18 us gap before the step's first residual)
 int queue_step_end(Ctx* c, int step_end, const NewtonGate& gate) {
   if (step_end == 2) {
-    if (gate.nrm2) launch_copy_gated(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, gate, c->stream);
+    if (gate.flag) launch_copy_gated(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, gate, c->stream);
     else launch_copy(c->f[TV_F_T_PREV].ptr, c->f[TV_F_T].ptr, c->nT, c->stream);
     return TV_OK;
   }
@@ -383,6 +410,8 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
   int its = 0, kits = 0;
   bool conv = false;
   double r0 = 0.0, rn = 0.0;
+  c->gate_ready = false;  // r0 unknown until iteration 1's ||dx|| is read
+  c->gate_dev = nullptr;
   // F(u); on the CG march path the residual's boundary pass also rewrites the
   // boundary rows of dinv for the same u once the interior is in place
   auto residual = [&]() -> bool {
@@ -428,9 +457,7 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
     if (!post_in_solve) {
       launch_newton_update(n, T + off, c->f[TV_F_DX].ptr + off, c->partials, c->stream);
       if (int e = reduce_logic(c, pcg_vec_blocks(n), 1, 0, 0)) return e;
-      HIPC(hipMemcpyAsync(c->h_sums, c->sums, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPC(hipEventRecord(c->evn, c->stream));
-      c->nrm_dev = c->sums;
+      if (int e = queue_newton_norm(c, c->sums)) return e;
     }
     if (int e = halo(c, T)) return e;
     // the next F queued before the host reads ||dx|| when the previous step
@@ -440,16 +467,14 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
     const bool spec = its + 1 < c->newton_pred && its + 1 < c->O.newton_max_it;
     if (spec) dinv_fresh = residual();
     // at (or past) the iteration the last step ended with, the step's end is
-    // queued now, gated on the device's copy of this iteration's test (an
-    // iteration that reaches newton_max_it without error_on_nonconvergence ends
-    // the solve either way: ungated); the host's test below takes the same
-    // decision from the same ||dx||^2, so a gated-off launch is simply not used
-    bool end_q = false, end_always = false;
-    if (step_end && !spec && its >= 1 && its + 1 >= c->newton_pred && c->nrm_dev) {
-      end_always = its + 1 >= c->O.newton_max_it && !c->O.error_on_nonconvergence;
-      NewtonGate g;
-      if (!end_always) g = NewtonGate{c->nrm_dev, r0, c->O.newton_rtol, c->O.newton_atol};
-      if (int e = queue_step_end(c, step_end, g)) return e;
+    // queued now, gated on the device's test of this iteration (k_newton_test);
+    // the host below takes the SAME decision (the flag copied with ||dx||^2), so
+    // a gated-off launch is simply not used.  A solve that ends unconverged never
+    // runs the step end (_solve_T's assert(converged), ThermoViscoProblem.py:390,
+    // fires before _solve_Tf and the stress updates)
+    bool end_q = false;
+    if (step_end && !spec && its >= 1 && its + 1 >= c->newton_pred && c->gate_dev) {
+      if (int e = queue_step_end(c, step_end, NewtonGate{c->gate_dev})) return e;
       end_q = true;
     }
     // the host waits for ||dx|| only, not for the queued residual: it decides
@@ -461,12 +486,13 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
     if (its == 1) {
       r0 = rn;  // residual0 = ||dx_1||; no test at the first iteration
       conv = false;
+      c->gate_r0 = r0;
+      c->gate_ready = true;  // every later norm is tested on the device
     } else {
-      const double rel = rn / r0;
-      conv = (rel < c->O.newton_rtol) || (rn < c->O.newton_atol);
+      conv = c->h_sums[1] != 0.0;  // the device's decision (queue_newton_norm)
     }
     if (end_q) {
-      if (conv || end_always) *end_queued = true;
+      if (conv) *end_queued = true;
       else c->vev_pending = false;  // gated off: its events bracket nothing
     }
     // dolfinx assembles F after every update; in the incremental criterion that
@@ -539,7 +565,7 @@ int visco(Ctx* c, bool copy_Tprev, const NewtonGate& gate) {
   visco_setup(c, k, v);
   v.gate = gate;
   auto copy = [&](double* d, const double* s, int64_t n) {
-    if (gate.nrm2) launch_copy_gated(d, s, n, gate, c->stream);
+    if (gate.flag) launch_copy_gated(d, s, n, gate, c->stream);
     else launch_copy(d, s, n, c->stream);
   };
   const int all = c->O.materialize ? 1 : 0;
@@ -650,7 +676,10 @@ int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its) {
   bool done = false;
   const int step_end = thermal_only ? 2 : 1;
   if (int e = newton(c, newton_its, krylov_its, &conv, step_end, &done)) return e;
-  if (!done)
+  // an unconverged solve (error_on_nonconvergence = False) stops here, as the
+  // reference's _solve_T assert does (ThermoViscoProblem.py:390): T holds the
+  // last Newton iterate, T_prev and the viscoelastic state keep the previous step
+  if (!done && conv)
     if (int e = queue_step_end(c, step_end, NewtonGate{})) return e;
   HIPC(hipGetLastError());
   // no stream synchronisation: the visco update (and T_prev <- T) finishes

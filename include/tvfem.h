@@ -244,7 +244,10 @@ typedef struct {
  *   AUTO              SINGLE_REDUCTION (Jacobi) on 3D CG1 box meshes partitioned
  *                     into slabs of <= 3M owned nodes (one communication round
  *                     per iteration) or on one partition of <= 1.5M nodes (one
- *                     launch per iteration), else KSPCG. */
+ *                     launch per iteration), else KSPCG.  With TV_PC_GMG on a
+ *                     slab partition AUTO selects the single-reduction GMG-PCG
+ *                     (deep-ghost slabs); an explicit SINGLE_REDUCTION is the
+ *                     Jacobi form only and is refused with TV_PC_GMG. */
 #define TV_PCG_AUTO 0
 #define TV_PCG_KSPCG 1
 #define TV_PCG_SINGLE_REDUCTION 2
@@ -431,10 +434,16 @@ int tv_comm_init_stub(void* ctx);   /* needs options.ksp_fixed_its > 0; tv_get_f
 /* Transport test on ONE GPU: a one-rank RCCL communicator (id from
  * tv_comm_get_unique_id) on which every neighbour of this partition is the rank
  * itself -- the production RCCL groups run unchanged with self send/recv pairs
- * and one-rank all-reduces, so each ghost plane receives the boundary plane
- * this partition sends (the plane next to it, not the neighbour's).  The
- * host-staged transport with a callback that copies a send into its receive
- * gives the same exchanges (tests/test_loopback.py compares the two). */
+ * and one-rank all-reduces, so each ghost plane receives a boundary plane
+ * this partition sends: a slab with neighbours on both sides sees its own
+ * periodic images (ghost planes below <- its top owned planes, above <- its
+ * bottom ones: one period of a periodic plate), a slab with one neighbour its
+ * MIRROR image across the interface (ghost plane k_begin-1-j <- owned plane
+ * k_begin+j, one send / receive pair per plane) -- either way the operator on
+ * the owned planes stays symmetric.  tv_comm_init_host with n_ranks = 1 (rank 0)
+ * on a partition is the same loopback over the host-staged transport, its
+ * callback copying a send into its receive (tests/test_loopback.py compares
+ * the two). */
 int tv_comm_init_loopback(void* ctx, const char* id);
 /* Collective check of the transport (every rank calls it): the exchange
  * patterns the solver issues -- ghost planes of the fine grid and of every
@@ -467,8 +476,12 @@ int tv_comm_time(void* ctx, int pattern, int reps, double* us_per_call);
  * 2 = residual, 3 = fused PCG matvec (p <- z + b p; w <- J p; p.w),
  * 4 = PCG vector update, 10 = Jacobian apply with the 256 MiB Infinity Cache
  * flushed (512 MiB write) before every launch, events around the launch alone,
- * the MEDIAN over the reps.  Writes the duration per launch in ms (the mean,
- * except 10). */
+ * the MEDIAN over the reps, 11 = one GMG V-cycle.  Launch audit, 12-17: `reps`
+ * back-to-back launches queued behind a spin kernel (timed as the GPU runs them,
+ * not at the host's enqueue rate), events around the chain: 12 an empty
+ * one-thread kernel, 13 the solver-state upload kernel, 14 the one-block
+ * reduction, 15 a Jacobi sweep of the coarsest GMG level, 16 J x of GMG level 1,
+ * 17 the fine J x.  Writes the duration per launch in ms (the mean, except 10). */
 int tv_time_kernel(void* ctx, int kernel, int reps, double* ms_per_launch);
 /* algorithmic bytes moved by one launch of `kernel` */
 int tv_kernel_bytes(void* ctx, int kernel, double* bytes);
@@ -488,7 +501,7 @@ int tv_last_stats(void* ctx, int* newton_its, int* krylov_its, double* dx_norm);
 int tv_last_converged(void* ctx, int* converged);
 /* the Krylov iteration form in use (TV_PCG_KSPCG or TV_PCG_SINGLE_REDUCTION:
  * the Jacobi march form, or with TV_PC_GMG the single-reduction GMG-PCG of
- * deep-ghost slabs); with the Jacobi SINGLE_REDUCTION form, kernel id 3 of
+ * deep-ghost slabs, which only pcg_variant AUTO selects); with the Jacobi SINGLE_REDUCTION form, kernel id 3 of
  * tv_time_kernel / tv_kernel_bytes / tv_kernel_stats is the fused
  * single-reduction iteration and id 4 is unused (GMG: the ids keep their
  * meaning) */

@@ -44,10 +44,11 @@ def test_rccl_loopback_groups_match_host_transport():
               f"(host {r['its_host']}); form {r['krylov_form']}, pc {r['pc']}; err {r['err_rccl']}")
         assert r["checked"] > 0 and r["bad"] == 0, r
         assert r["err_rccl"] == r["err_host"], r
-        # the CG slabs' reflected-ghost problem is SPD: its steps converge (the DG
-        # ghost layer and the three ghost planes of a multigrid slab are shifted
-        # copies, not reflections; there agreement is what counts)
-        assert r["err_rccl"] is None or r["case"].startswith("dg") or r["pc"] == "gmg", r
+        # the CG slabs' mirrored-ghost problem is symmetric: every CG step converges,
+        # the distributed multigrid ones (three deep ghost planes, single-reduction
+        # GMG-PCG) included; the DG ghost layer is a shifted copy
+        # of the cell layer (its local vertex order is not mirrored): agreement counts
+        assert r["err_rccl"] is None or r["case"].startswith("dg"), r
         if r["pc"] == "gmg":  # the distributed V-cycle itself, every exchange of it, through both transports
             assert r["vcycle_bitwise"] and r["vcycle_norm"] > 0.0, r
         assert r["its_rccl"] == r["its_host"], r

@@ -115,23 +115,30 @@ def test_newton_failure_keeps_step_state(after_converged_step):
     dev.close()
 
 
-def test_error_off_ends_step_then_asserts():
-    """error_on_nonconvergence off: the step ends (visco update, T_prev <- T)
-    after max_it iterations, as the oracle's step with the same settings, and
-    solve_timestep raises the AssertionError of _solve_T (:390)"""
+def test_error_off_keeps_step_state_then_asserts():
+    """error_on_nonconvergence off: dolfinx returns (max_it, False) and
+    _solve_T's assert(converged) (ThermoViscoProblem.py:390) fires before
+    _solve_Tf and the stress updates (:372-381) -- so T holds the last Newton
+    iterate (the oracle's T after the same iterations) while T_prev and the
+    viscoelastic state keep the previous step's values (the step end
+    used to run ungated here)"""
     _torch()
     n1 = _first_step_newton_count()
     dev, ref = make_pair(AXES["3d"], {"T": CG, "sigma": CG})
+    before = _state(dev)
     dev.solver.max_it = n1 - 1
     dev.solver.error_on_nonconvergence = False
     ref.newton.update(max_it=n1 - 1, error_on_nonconvergence=False)
     with pytest.raises(AssertionError):
         dev.solve_timestep()
-    ref.solve_timestep()
+    ref.solve_T()  # the oracle's Newton solve alone: the reference stops at the assert
     assert dev.last_newton_iterations == n1 - 1
     st = _state(dev)
     assert relerr(st["T"], ref.functions_current["T"]) < 1e-10
-    assert np.array_equal(st["T_prev"], st["T"])
-    assert relerr(st["phi"], ref.functions["phi"]) < 1e-9
-    assert relerr(st["Tf"], ref.functions_current["Tf"]) < 1e-10
+    for f in ("T_prev", "phi", "Tf", "xi", "sigma"):
+        assert np.array_equal(st[f], before[f], equal_nan=True), f
+    # the context stays usable: with the default max_it the next step converges
+    dev.solver.max_it = 50
+    dev.solver.error_on_nonconvergence = True
+    dev.solve_timestep()
     dev.close()

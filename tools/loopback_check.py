@@ -16,10 +16,17 @@ Per case:
   3. multigrid cases: the partitioned V-cycle (tv_precond_apply, every
      exchange of the distributed cycle) applied to the same vector on both
      transports gives bitwise identical results.
-A deep-ghost slab (the distributed multigrid keeps three ghost planes on its
-fine grid) receives under self-loopback a SHIFTED copy of its boundary planes,
-not a mirror: the reflected operator is not symmetric, and its Krylov solves
-may stop as indefinite -- on both transports alike, which is what is compared.
+Loopback semantics (tv_comm_init_loopback): a slab with neighbours on both
+sides receives its own periodic images (the ghost planes below hold its top
+owned planes, those above its bottom ones), so it solves one period of a
+y-periodic plate; a slab with one neighbour receives its mirror image.  Both
+keep the operator on the owned planes symmetric.  The multigrid cases use a
+slab of 8 node planes (24 cells, 3 parts: planes [8, 16)) so that the owned
+planes of every distributed level are a translate of it (4 and 2 planes) and
+the periodic image is consistent on every level: the distributed GMG-PCG --
+deep ghost planes, the single-reduction form -- then runs to convergence over
+RCCL.  (Rounds 4-5 sent a shifted copy of the three deep ghost planes: not
+symmetric, its GMG solves stopped as indefinite.)
 
     python tools/loopback_check.py [--case NAME ...]     (prints LOOPBACK <json> per case)
 """
@@ -45,26 +52,27 @@ MP = {"f": 0.0, "epsilon": 0.93, "sigma": 5.670e-8, "T_ambient": 600.0, "T_0": 8
       "alpha_liquid": 25.1e-6}
 CFG = {"T": {"element": "CG", "degree": 1}, "sigma": {"element": "CG", "degree": 1}}
 
-# name: (mesh kind, cells, parts, part, Krylov form, preconditioner, replication bound[, family])
+# name: (mesh kind, cells, parts, part, Krylov form, preconditioner, replication bound, multigrid levels[, family])
 CASES = {
-    "dg_mid": ("box", (8, 12, 3), 3, 1, "kspcg", "jacobi", 0, "DG"),
-    "box_single_mid": ("box", (10, 30, 5), 3, 1, "single", "jacobi", 0),
-    "box_kspcg_mid": ("box", (10, 30, 5), 3, 1, "kspcg", "jacobi", 0),
-    "box_kspcg_first": ("box", (10, 30, 5), 2, 0, "kspcg", "jacobi", 0),
-    "box_gmg_replicated": ("box", (10, 30, 5), 3, 1, "kspcg", "gmg", 0),
-    "box_gmg_distributed": ("box", (10, 30, 5), 3, 1, "kspcg", "gmg", 1),
-    "box_gmg_single_reduction": ("box", (10, 30, 5), 3, 1, "auto", "gmg", 1),
-    "um_first": ("distorted", (6, 12, 3), 2, 0, "kspcg", "jacobi", 0),
-    "um_mid": ("distorted", (6, 12, 3), 3, 1, "kspcg", "jacobi", 0),
+    "dg_mid": ("box", (8, 12, 3), 3, 1, "kspcg", "jacobi", 0, 0, "DG"),
+    "box_single_mid": ("box", (10, 30, 5), 3, 1, "single", "jacobi", 0, 0),
+    "box_kspcg_mid": ("box", (10, 30, 5), 3, 1, "kspcg", "jacobi", 0, 0),
+    "box_kspcg_first": ("box", (10, 30, 5), 2, 0, "kspcg", "jacobi", 0, 0),
+    "box_gmg_replicated": ("box", (10, 24, 5), 3, 1, "kspcg", "gmg", 0, 3),
+    "box_gmg_distributed": ("box", (10, 24, 5), 3, 1, "kspcg", "gmg", 1, 3),
+    "box_gmg_single_reduction": ("box", (10, 24, 5), 3, 1, "auto", "gmg", 1, 3),
+    "um_first": ("distorted", (6, 12, 3), 2, 0, "kspcg", "jacobi", 0, 0),
+    "um_mid": ("distorted", (6, 12, 3), 3, 1, "kspcg", "jacobi", 0, 0),
 }
 
 
-def _problem(kind, cells, parts, part, pcg, pc, rep, family="CG"):
+def _problem(kind, cells, parts, part, pcg, pc, rep, levels, family="CG"):
     mesh = (distorted_box_mesh if kind == "distorted" else box_mesh)([2.0, 6.0, 1.0], list(cells))
     kw = {} if kind == "distorted" else {"part_axis": 1}
     cfg = {"T": {"element": family, "degree": 1}, "sigma": {"element": family, "degree": 1}}
     return ThermoViscoProblem(mesh, (0, 1), 0.1, cfg, MP, n_parts=parts, part=part, verbose=False,
-                              pcg_variant=pcg, preconditioner=pc, mg_replicate_nodes=rep, write_output=False, **kw)
+                              pcg_variant=pcg, preconditioner=pc, mg_replicate_nodes=rep, mg_levels=levels,
+                              write_output=False, **kw)
 
 
 def _host_loopback(p):
@@ -78,7 +86,8 @@ def _host_loopback(p):
         C.memmove(rptr, sptr, 8 * ns)
         return 0
     p._host_cbs = (N.HOST_ALLREDUCE_FN(allreduce), N.HOST_SENDRECV_FN(sendrecv))
-    N.check(p._lib.tv_comm_init_host(p._ctx, p._n_parts, p._part, p._host_cbs[0], p._host_cbs[1], None), p._ctx)
+    # n_ranks = 1: the library's host-staged loopback (mirrored ghost planes, as over RCCL)
+    N.check(p._lib.tv_comm_init_host(p._ctx, 1, 0, p._host_cbs[0], p._host_cbs[1], None), p._ctx)
 
 
 def _steps(p, steps):
@@ -106,19 +115,19 @@ def _vcycle(p):
 
 
 def run_case(name, steps=3):
-    kind, cells, parts, part, pcg, pc, rep, *fam = CASES[name]
+    kind, cells, parts, part, pcg, pc, rep, levels, *fam = CASES[name]
     lib = N.load_library()
     box_gmg = pc == "gmg" and kind == "box" and not fam
 
     def rccl():
-        q = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
+        q = _problem(kind, cells, parts, part, pcg, pc, rep, levels, *fam)
         uid = C.create_string_buffer(lib.tv_comm_unique_id_size())
         N.check(lib.tv_comm_get_unique_id(uid))
         N.check(lib.tv_comm_init_loopback(q._ctx, uid.raw), q._ctx)
         return q
 
     def host():
-        q = _problem(kind, cells, parts, part, pcg, pc, rep, *fam)
+        q = _problem(kind, cells, parts, part, pcg, pc, rep, levels, *fam)
         _host_loopback(q)
         return q
     # RCCL loopback
