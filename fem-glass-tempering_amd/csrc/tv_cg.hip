@@ -1849,6 +1849,24 @@ __global__ __launch_bounds__(kBlock) void k_mg_prep_diag(MgPrep p) {
   p.dinv[l][n] = 1.0 / diag_value<3, true>(g, p.T[l], n);
 }
 
+
+// Robin facet Jacobian terms of x on EVERY physical face: fface[f][c_t1 + fn1
+// c_t2] = dt sum over the node's facets in face f of int g'(T_h) phi_I x_h ds,
+// by the face workgroups of the marching launch (face_block: per facet, 3 x 3
+// Gauss, four corners at once) over all six faces -- the marching tiles
+// integrate the faces normal to their march axis themselves; the fused
+// residual restriction (k_mg_rrestrict, tv_mg.hip) reads all six from here.
+// (One thread per face node with facet_direct: 15.9 us at C4.)
+template <int R>
+__global__ __launch_bounds__(R * kWave) void k_cg_faces_all(CgGrid g, const double* __restrict__ T,
+                                                            const double* __restrict__ x, FaceOff fo,
+                                                            const PcgState* __restrict__ st) {
+  if (st != nullptr && st->done) return;
+  __shared__ double fsm[(8 * R + 8) * kWave];
+  __shared__ double red[R];
+  face_block<false, R>(g, T, x, x, x, 0.0, nullptr, RedTail{}, 0, (int)blockIdx.x, fo, fsm, red, 0);
+}
+
 }  // namespace
 
 int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, const double* r, const double* dinv,
@@ -1926,6 +1944,20 @@ bool launch_cg_japply_tail(const CgGrid& g, const double* T, const double* x, do
   // march) with the x.(J x) records of the march tiles and face workgroups
   // reduced by the tail into tail->out[0]
   return launch_rows<MODE_JAC, false>(g, T, x, nullptr, y, nullptr, st, partials, false, s, tail, 0, true);
+}
+
+void launch_cg_facet_faces(const CgGrid& g, const double* T, const double* x, const PcgState* st, hipStream_t s) {
+  const FaceOff fo = face_offsets(g, kRows, -1);  // all six faces
+  if (fo.off[6] <= 0) return;
+  hipLaunchKernelGGL(k_cg_faces_all<kRows>, dim3(fo.off[6]), dim3(kRows * kWave), 0, s, g, T, x, fo, st);
+}
+
+// the six face arrays as a FaceAdd (every physical face, fface[] of g)
+FaceAdd cg_face_add_all(const CgGrid& g) {
+  FaceAdd fa = cg_face_add(g, 0);
+  if (!fa.on) return fa;
+  for (int f = 0; f < 6; ++f) fa.ff[f] = g.fface[f];
+  return fa;
 }
 
 void launch_cg_japply_partial(const CgGrid& g, const double* T, const double* x, double* y, const PcgState* st,

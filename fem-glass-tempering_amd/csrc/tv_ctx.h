@@ -66,6 +66,9 @@ struct MgLevel {
   int first2 = 0;
   int inj0 = 0, inj1 = 0;
   double* mask = nullptr;    // the level above the replicated ones: 1 owned / 0 ghost
+  // the fused residual restriction INTO this level (RRArgs, tv_mg.hip): rr.on
+  // where the transfer's geometry allows it (one partition, tv_mgsolve.cpp)
+  RRArgs rr{};
 };
 
 // level l >= 1 of the algebraic multigrid (tv_amg.cpp): A_l, the prolongation

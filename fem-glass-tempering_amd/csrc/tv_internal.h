@@ -440,6 +440,30 @@ struct MgXfer {
 void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, const double* wf, const FaceAdd* fa,
                         const double* mask, double* bc, const double* dinv_c, double omega_c, double* xc,
                         hipStream_t s);
+// Fused residual restriction (tv_mg.hip k_mg_rrestrict): b_c = R (b - J x) on a
+// rectilinear level WITHOUT forming J x.  On the box R = Rq (x) Rr (x) Rx and J
+// is a sum of Kronecker products of the 1D mass / stiffness rows, so R J is a
+// sum of Kronecker products of the per-axis operators (R_a M_a), (R_a K_a):
+// five fine nodes wide per coarse node, applied by sum factorisation (x in the
+// lanes, the row axis over five fine rows per wave, the march axis over a
+// sliding five-plane window).  The Robin facet part of J x comes from
+// k_cg_facet_faces (fface of all six faces), subtracted from b on the face nodes.
+struct RRAxis {
+  const int* f0;     // [cn]: first fine node of coarse node I's window (its fine node - 2)
+  const double* w;   // [cn][15]: (R M), (R K), R over fine nodes f0 .. f0 + 4 (0 outside the axis)
+};
+struct RRArgs {
+  int on;
+  int fn[3], cn[3];
+  RRAxis ax[3];
+  double da;           // dt alpha
+  int raxis, nseg, qchunk;
+};
+void launch_mg_rrestrict(const RRArgs& a, const PcgState* st, const double* b, const double* x, const FaceAdd& fa,
+                         double* bc, const double* dinv_c, double omega_c, double* xc, hipStream_t s);
+void launch_cg_facet_faces(const CgGrid& g, const double* T, const double* x, const PcgState* st, hipStream_t s);
+FaceAdd cg_face_add_all(const CgGrid& g);  // the facet terms of every physical face (fface[] of g)
+
 // The coarse level's post-smoothing operands: the prolongation applies
 // xc + omega dinv (b - (w + facet terms fa)) instead of xc
 struct CoarsePost {

@@ -83,12 +83,16 @@ int tv_kernel_bytes(void* ctx, int kernel, double* bytes) {
       // then CG: J x with the post-smoothing in its epilogue (x, r in, z out: 24;
       // D^-1 formed in the kernel off the physical boundary),
       // DG: J x (16) + the cell-block post-smoothing (x0, r, w in, z out: 32)
-      double b = (c->mg_dg ? 16.0 + 16 + 16 + 16 + 32 : 16.0 + 16 + 16 + 24) * n;
+      // (a fused residual restriction, RRArgs: no J x0, the restriction reads r
+      // and x0 -- 16 B instead of 32; the facet terms it needs touch the faces only)
+      const bool rr0 = !c->mg_dg && !c->mg.empty() && c->mg[0].rr.on;
+      double b = (c->mg_dg ? 16.0 + 16 + 16 + 16 + 32 : (rr0 ? 0.0 : 16.0) + 16 + 16 + 24) * n;
       for (size_t l = 0; l < c->mg.size(); ++l) {
         const double nl = (double)c->mg[l].n;
         b += 24.0 * nl;  // the restriction's outputs b, x (pre-smoothing) and the dinv it reads
+        const bool rr = l + 1 < c->mg.size() && c->mg[l + 1].rr.on;
         if (l + 1 < c->mg.size())  // J x (16), restriction reads (16), partial J x (16), prolongation in (16),
-          b += (16.0 + 16 + 16 + 16 + 24) * nl;  // post-smoothing operands b, w, dinv (24)
+          b += ((rr ? 0.0 : 16.0) + 16 + 16 + 16 + 24) * nl;  // post-smoothing operands b, w, dinv (24)
       }
       *bytes = b;
       break;

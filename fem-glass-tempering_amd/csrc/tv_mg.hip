@@ -19,6 +19,7 @@
 // level) + 8 / 8 (coarse write), prolongation 16 (+ coarse reads, cached),
 // Jacobi step 24 / 40.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "tv_stencil.h"
@@ -661,6 +662,251 @@ int blocks_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>((
 // measured 24 us at 143k coarse nodes)
 int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kBlock - 1) / kBlock); }
 
+// ---- fused residual restriction (RRArgs, tv_internal.h) ----------------------
+// A workgroup of kRRWaves waves = kRRWaves consecutive coarse rows Jc0 .. of the
+// row axis, one 62-node coarse x segment and a chunk of coarse planes of the
+// march axis.  Lane l holds coarse x node I = 62 seg - 1 + l and its fine pair
+// (2I, 2I + 1) (the fine x cell count is even); the window 2I - 2 .. 2I + 2
+// comes from lanes l - 1 / l + 1 by DPP (lanes 0 and 63 are halo lanes).  Per
+// fine plane of the march window:
+//   1. the workgroup's fine rows (2 kRRWaves + 3 on a coarsened row axis) are
+//      loaded ONCE, spread over the waves (x and b as 16-byte pairs), the facet
+//      terms subtracted from b on the face nodes, and each row x-reduced to
+//        p = Rx Mx x,  q = Rx Kx x,  s = Rx (b - F x)
+//      into a double-buffered LDS slab (one barrier per plane);
+//   2. each wave folds its coarse row's five fine rows from the slab:
+//        U = RrMr (p + da q) + da RrKr p,  V = RrMr p,  S = Rr s
+//      and accumulates b_c(Q) = sum over the window of Rq S - RqMq U - da RqKq V
+//      (two accumulators: an even plane 2k completes coarse k - 2, opens k).
+// The loads of plane P + 1 are in flight while plane P is reduced and folded.
+constexpr int kRRSeg = kWave - 2;
+constexpr int kRRWaves = 8;
+constexpr int kRRRows = 2 * kRRWaves + 3;          // fine rows per plane (coarsened row axis)
+constexpr int kRRPer = (kRRRows + kRRWaves - 1) / kRRWaves;  // rows loaded per wave
+constexpr int kRRQMax = 64;  // coarse march planes per chunk (LDS weight stage)
+
+// buffer resource of a level vector (32-bit byte offsets: a per-lane x offset in
+// a VGPR plus a wave-uniform row / plane offset in an SGPR)
+using rr_buf = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rr_buf rr_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ d2a8 rr_ld2(rr_buf r, uint32_t voff, uint32_t soff) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+  return __builtin_bit_cast(d2a8, v);
+}
+
+struct RRSet {
+  d2a8 xv[kRRPer], bv[kRRPer];
+  double fx[kRRPer];  // the x-face facet term of each row at this lane's node (x-face lanes only)
+};
+
+template <int RA>
+__global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, const PcgState* __restrict__ st,
+                                                                   const double* __restrict__ b,
+                                                                   const double* __restrict__ x, FaceAdd fa,
+                                                                   double* __restrict__ bc,
+                                                                   const double* __restrict__ dinv_c, double omega_c,
+                                                                   double* __restrict__ xc) {
+  if (st != nullptr && st->done) return;
+  __shared__ double sq[kRRQMax][15];        // the chunk's march-axis windows
+  __shared__ double sr[kRRWaves][15];       // each wave's row-axis window
+  __shared__ double red[2][3][kRRRows][kWave];  // x-reduced rows (p, q, s), two planes
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  constexpr int ra = RA, qa = 3 - RA;
+  const int ncr = a.cn[ra], ncq = a.cn[qa];
+  const int nrb = (ncr + kRRWaves - 1) / kRRWaves;
+  // order: x segment fastest, then row block, then chunk; contiguous per XCD
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int seg = bid % a.nseg;
+  const int t = bid / a.nseg;
+  const int rb = t % nrb, chunk = t / nrb;
+  const int Jc0 = rb * kRRWaves;
+  const int Jc = Jc0 + wave;
+  const bool row_ok = Jc < ncr;
+  const int Jcc = row_ok ? Jc : ncr - 1;
+  const int Q0 = chunk * a.qchunk, Q1 = min(Q0 + a.qchunk, ncq);
+  const int nf0 = a.fn[0], ncx = a.cn[0];
+  const int nfr = a.fn[ra], nfq = a.fn[qa];
+  const int I = seg * kRRSeg - 1 + lane;
+  const bool Iok = I >= 0 && I < ncx;
+  const int e0 = 2 * I;
+  {
+    const int tid = threadIdx.x;
+    for (int e = tid; e < 15 * (Q1 - Q0); e += kRRWaves * kWave) sq[e / 15][e % 15] = a.ax[qa].w[15 * Q0 + e];
+    if (lane < 15) sr[wave][lane] = row_ok ? a.ax[ra].w[15 * Jcc + lane] : 0.0;
+  }
+  // the workgroup's fine rows: fr_first .. fr_first + nrows - 1 (clamped to the axis)
+  const int Jlast = min(Jc0 + kRRWaves, ncr) - 1;
+  const int fr_first = kld(a.ax[ra].f0, Jc0);
+  const int nrows = kld(a.ax[ra].f0, Jlast) + 5 - fr_first;  // <= kRRRows (rr_setup)
+  const int my0 = kld(a.ax[ra].f0, Jcc) - fr_first;           // this wave's first row in the slab
+  const int sR = (ra == 1) ? nf0 : nf0 * a.fn[1];
+  const int sQ = (ra == 1) ? nf0 * a.fn[1] : nf0;
+  // the rows this wave loads: slab rows wave, wave + kRRWaves, ...
+  int frow[kRRPer];
+  uint32_t rowoff[kRRPer];
+  bool rload[kRRPer];
+#pragma unroll
+  for (int u = 0; u < kRRPer; ++u) {
+    const int sl = wave + u * kRRWaves;
+    rload[u] = sl < nrows;
+    frow[u] = min(max(fr_first + sl, 0), nfr - 1);  // clamped (weight 0 outside the axis)
+    rowoff[u] = (uint32_t)(sR * frow[u]) * 8u;
+  }
+  const uint32_t nbytes = (uint32_t)a.fn[0] * (uint32_t)a.fn[1] * (uint32_t)a.fn[2] * 8u;
+  const rr_buf rx = rr_rsrc(x, nbytes), rbv = rr_rsrc(b, nbytes);
+  // the lane's fine pair (e0, e0 + 1) straight from the row; the last lane's
+  // e0 + 1 is the next row's first node (weight 0), the lanes outside the axis
+  // carry an out-of-range offset (the range check returns 0)
+  const uint32_t voff = Iok ? (uint32_t)e0 * 8u : 0x40000000u;
+  // facet terms: the x faces at the lanes holding fine x node 0 / nf0 - 1 (in
+  // the waves that have one: loaded with the plane), the row-axis faces on the
+  // axis' first / last row and the march-axis faces on the first / last fine
+  // plane (wave-uniform branches, rare)
+  const bool xl0 = fa.ff[0] != nullptr && e0 == 0, xl1 = fa.ff[1] != nullptr && e0 == nf0 - 1;
+  const bool xwave = __ballot(xl0 || xl1) != 0;  // wave-uniform
+  const double* fxp = xl0 ? fa.ff[0] : (xl1 ? fa.ff[1] : b);
+  const int n1 = a.fn[1];
+  const uint32_t nfa = nbytes / (uint32_t)nfr, nfb = nbytes / (uint32_t)nfq;  // face array bytes
+  const rr_buf frl = rr_rsrc(fa.ff[2 * ra], fa.ff[2 * ra] ? nfa : 0u);
+  const rr_buf frh = rr_rsrc(fa.ff[2 * ra + 1], fa.ff[2 * ra + 1] ? nfa : 0u);
+  const rr_buf fql = rr_rsrc(fa.ff[2 * qa], fa.ff[2 * qa] ? nfb : 0u);
+  const rr_buf fqh = rr_rsrc(fa.ff[2 * qa + 1], fa.ff[2 * qa + 1] ? nfb : 0u);
+  const bool hrl = fa.ff[2 * ra] != nullptr, hrh = fa.ff[2 * ra + 1] != nullptr;
+  const bool hql = fa.ff[2 * qa] != nullptr, hqh = fa.ff[2 * qa + 1] != nullptr;
+  const int f0q = kld(a.ax[qa].f0, Q0);
+  const int np = 2 * (Q1 - Q0) + 3;  // fine planes f0q .. f0q + np - 1
+  auto fetch = [&](int P, RRSet& S) {
+    const int fq = min(max(f0q + P, 0), nfq - 1);
+    const uint32_t po = (uint32_t)(sQ * fq) * 8u;
+#pragma unroll
+    for (int u = 0; u < kRRPer; ++u) {
+      S.xv[u] = rr_ld2(rx, rload[u] ? voff : 0x40000000u, rowoff[u] + po);
+      S.bv[u] = rr_ld2(rbv, rload[u] ? voff : 0x40000000u, rowoff[u] + po);
+    }
+#pragma unroll
+    for (int u = 0; u < kRRPer; ++u) {
+      // storage (j, k) of (row frow[u], plane fq): the x-face index j + n1 k
+      const int j = (ra == 1) ? frow[u] : fq, k = (ra == 1) ? fq : frow[u];
+      S.fx[u] = 0.0;
+      if (xwave) {
+        const double v = fxp[(xl0 || xl1) ? j + n1 * k : 0];
+        S.fx[u] = (xl0 || xl1) ? v : 0.0;
+      }
+    }
+  };
+  // the lane's x weights in registers (read for every loaded row)
+  double wx[15];
+#pragma unroll
+  for (int m = 0; m < 15; ++m) wx[m] = (Iok ? a.ax[0].w[15 * (Iok ? I : 0) + m] : 0.0);
+  // the loaded rows of plane P: facet terms, x-reduction into slab buffer P & 1
+  auto reduce = [&](int P, const RRSet& S) {
+    const int fqr = f0q + P;
+    const int fqc = min(max(fqr, 0), nfq - 1);
+    const bool qlo = hql && fqr == 0, qhi = hqh && fqr == nfq - 1;  // wave-uniform
+    d2a8 sv[kRRPer];
+#pragma unroll
+    for (int u = 0; u < kRRPer; ++u) {
+      sv[u] = S.bv[u];
+      sv[u].x -= S.fx[u];
+      const int fr = fr_first + wave + u * kRRWaves;
+      const bool rlo = hrl && fr == 0, rhi = hrh && fr == nfr - 1;  // wave-uniform
+      if (rlo || rhi) {  // a row-axis face row (face index i + n0 * plane)
+        const d2a8 f = rr_ld2(rlo ? frl : frh, voff, (uint32_t)(nf0 * fqc) * 8u);
+        sv[u].x -= f.x;
+        sv[u].y -= f.y;
+      }
+      if (qlo || qhi) {  // a march-axis face plane (face index i + n0 * row)
+        const d2a8 f = rr_ld2(qlo ? fql : fqh, voff, (uint32_t)(nf0 * frow[u]) * 8u);
+        sv[u].x -= f.x;
+        sv[u].y -= f.y;
+      }
+    }
+    const int buf = P & 1;
+#pragma unroll
+    for (int u = 0; u < kRRPer; ++u) {
+      const d2a8 xv = S.xv[u];
+      // x window (2I - 2, 2I - 1, 2I, 2I + 1, 2I + 2)
+      const double x0 = shr1(xv.x), x1 = shr1(xv.y), x4 = shl1(xv.x);
+      const double s0 = shr1(sv[u].x), s1 = shr1(sv[u].y), s4 = shl1(sv[u].x);
+      const double p = ((wx[0] * x0 + wx[1] * x1) + wx[2] * xv.x) + (wx[3] * xv.y + wx[4] * x4);
+      const double q = ((wx[5] * x0 + wx[6] * x1) + wx[7] * xv.x) + (wx[8] * xv.y + wx[9] * x4);
+      const double s = ((wx[10] * s0 + wx[11] * s1) + wx[12] * sv[u].x) + (wx[13] * sv[u].y + wx[14] * s4);
+      const int sl = wave + u * kRRWaves;
+      if (sl < kRRRows) {  // (compile-time true for all but the last u)
+        red[buf][0][sl][lane] = p;
+        red[buf][1][sl][lane] = q;
+        red[buf][2][sl][lane] = s;
+      }
+    }
+  };
+  // this wave's coarse row from the slab: (U, V, S)
+  auto fold = [&](int P, double& U, double& V, double& Sv) {
+    const int buf = P & 1;
+    double um = 0.0, uk = 0.0, vv = 0.0, ss = 0.0;
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      const int sl = min(my0 + m, kRRRows - 1);
+      const double p = red[buf][0][sl][lane], q = red[buf][1][sl][lane], s = red[buf][2][sl][lane];
+      um += sr[wave][m] * (p + a.da * q);
+      uk += sr[wave][5 + m] * p;
+      vv += sr[wave][m] * p;
+      ss += sr[wave][10 + m] * s;
+    }
+    U = um + a.da * uk;
+    V = vv;
+    Sv = ss;
+  };
+  // window-position contribution of a fine plane to coarse plane Q (weights of Q's window slot m)
+  auto contrib = [&](int Q, int m, double U, double V, double Sv) {
+    const double* w = sq[Q - Q0];
+    return w[10 + m] * Sv - (w[m] * U + a.da * (w[5 + m] * V));
+  };
+  const bool out_lane = row_ok && Iok && lane >= 1 && lane <= kRRSeg;
+  const int nQ = Q1 - Q0;
+  // fine plane P feeds coarse planes Q0 + k with 2k <= P <= 2k + 4.  X = the
+  // older, Y = the newer live coarse plane; an even plane 2k completes coarse
+  // k - 2 (written out) and opens coarse k.
+  double X = 0.0, Y = 0.0;
+  RRSet A, B;
+  fetch(0, A);
+  __syncthreads();  // the weight stages
+#pragma unroll 1
+  for (int P = 0; P < np; ++P) {
+    fetch(min(P + 1, np - 1), B);  // in flight during this plane
+    reduce(P, A);
+    __syncthreads();
+    double U, V, Sv;
+    fold(P, U, V, Sv);
+    const int k = P >> 1;
+    if ((P & 1) == 0) {
+      if (k - 2 >= 0 && k - 2 < nQ) X += contrib(Q0 + k - 2, 4, U, V, Sv);
+      if (k - 1 >= 0 && k - 1 < nQ) Y += contrib(Q0 + k - 1, 2, U, V, Sv);
+      const double Z = (k < nQ) ? contrib(Q0 + k, 0, U, V, Sv) : 0.0;
+      if (k - 2 >= 0 && out_lane) {  // coarse Q0 + k - 2 complete
+        const int Q = Q0 + k - 2;
+        const int J1 = (ra == 1) ? Jc : Q, K2 = (ra == 1) ? Q : Jc;
+        const int64_t o = (int64_t)I + (int64_t)ncx * (J1 + (int64_t)a.cn[1] * K2);
+        bc[o] = X;
+        if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * X;  // the coarse pre-smoothing step from 0
+      }
+      X = Y;
+      Y = Z;
+    } else {
+      if (k - 1 >= 0 && k - 1 < nQ) X += contrib(Q0 + k - 1, 3, U, V, Sv);
+      if (k < nQ) Y += contrib(Q0 + k, 1, U, V, Sv);
+    }
+    A = B;
+  }
+}
+
 }  // namespace
 
 
@@ -699,6 +945,17 @@ void launch_mg_restrict(const MgXfer& x, const PcgState* st, const double* bf, c
 }
 
 bool mg_restrict_folds_faces(const MgXfer& x) { return x.coarse[0] && x.fn[0] >= 3; }
+
+void launch_mg_rrestrict(const RRArgs& a, const PcgState* st, const double* b, const double* x, const FaceAdd& fa,
+                         double* bc, const double* dinv_c, double omega_c, double* xc, hipStream_t s) {
+  const int ncr = a.cn[a.raxis], ncq = a.cn[3 - a.raxis];
+  const int nrb = (ncr + kRRWaves - 1) / kRRWaves;
+  if (a.qchunk > kRRQMax) return;  // (rr_setup keeps it below)
+  const int nch = (ncq + a.qchunk - 1) / a.qchunk;
+  const dim3 g((unsigned)((int64_t)a.nseg * nrb * nch)), bl(kRRWaves * kWave);
+  if (a.raxis == 1) hipLaunchKernelGGL(k_mg_rrestrict<1>, g, bl, 0, s, a, st, b, x, fa, bc, dinv_c, omega_c, xc);
+  else hipLaunchKernelGGL(k_mg_rrestrict<2>, g, bl, 0, s, a, st, b, x, fa, bc, dinv_c, omega_c, xc);
+}
 
 bool mg_prolong_blocks(const MgXfer& x) {
   return x.aligned && x.coarse[0] && x.coarse[1] && x.coarse[2] && x.fn[0] >= 3 && x.f_kb == 0;

@@ -1,6 +1,8 @@
 // Geometric multigrid on the box hierarchy: setup, per-Newton preparation and
 // the multigrid-preconditioned KSPCG (the reference's PCGAMG,
 // ThermoViscoProblem.py:343-346, replaced for rectilinear 3D meshes).
+#include <cstdlib>
+
 #include "tv_ctx.h"
 
 namespace tv {
@@ -202,6 +204,99 @@ void mg_axis_tables(const std::vector<double>& Xf, const std::vector<char>& is_c
   }
 }
 
+// Tables of the fused residual restriction (RRArgs) along one axis: for coarse
+// node I (fine node fc = ri[3I + 1]) the window fc - 2 .. fc + 2 and the weights
+// of (R M), (R K) and R over it, from the fine 1D rows and the restriction
+// weights.  False when a product reaches outside the window (not a nested pair).
+static bool rr_axis(const std::vector<double>& Xf, const std::vector<int>& ri, const std::vector<double>& rw,
+                    std::vector<int>& f0, std::vector<double>& w) {
+  const int nf = (int)Xf.size(), nc = (int)ri.size() / 3;
+  std::vector<double> cf;
+  axis_coefs(Xf, 0, nf, cf);
+  f0.assign(nc, 0);
+  w.assign(15 * (size_t)nc, 0.0);
+  for (int I = 0; I < nc; ++I) {
+    f0[I] = ri[3 * I + 1] - 2;
+    for (int q = 0; q < 3; ++q) {
+      const int f = ri[3 * I + q];
+      const double wt = rw[3 * I + q];
+      if (wt == 0.0) continue;
+      const double* cc = &cf[(size_t)f * C_NCOEF];
+      auto add = [&](int col, int fi, double v) -> bool {
+        if (v == 0.0) return true;
+        const int m = fi - f0[I];
+        if (fi < 0 || fi >= nf || m < 0 || m > 4) return false;
+        w[15 * (size_t)I + 5 * col + m] += wt * v;
+        return true;
+      };
+      if (!(add(0, f - 1, cc[C_MLO]) && add(0, f, cc[C_MDI]) && add(0, f + 1, cc[C_MUP]) &&
+            add(1, f - 1, cc[C_KLO]) && add(1, f, cc[C_KDI]) && add(1, f + 1, cc[C_KUP]) && add(2, f, 1.0)))
+        return false;
+    }
+  }
+  return true;
+}
+
+// The fused residual restriction from fine coordinates Xp into coarse level L
+// (single partition): x needs even fine cell counts (lanes own fine pairs
+// 2I, 2I + 1), the march axis consecutive windows two fine planes apart (every
+// coarsened axis: the odd tail's window too); the row axis is free.
+static int rr_setup(Ctx* c, MgLevel& L, const std::vector<double> (&Xp)[3], const std::vector<int> (&ri)[3],
+                    const std::vector<double> (&rw)[3]) {
+  RRArgs& a = L.rr;
+  a = RRArgs{};
+  const MgXfer& x = L.xf;
+  if (!x.coarse[0] || x.fn[0] < 5 || !(x.fn[0] & 1)) return TV_OK;
+  std::vector<int> f0[3];
+  std::vector<double> w[3];
+  for (int s = 0; s < 3; ++s)
+    if (!rr_axis(Xp[s], ri[s], rw[s], f0[s], w[s])) return TV_OK;
+  auto regular = [&](int s) {
+    if (!x.coarse[s] || x.cn[s] < 2) return false;
+    for (int I = 0; I + 1 < x.cn[s]; ++I)
+      if (f0[s][I + 1] - f0[s][I] != 2) return false;
+    return true;
+  };
+  int qa = (x.cn[1] <= x.cn[2]) ? 1 : 2;
+  if (!regular(qa)) qa = 3 - qa;
+  if (!regular(qa)) return TV_OK;
+  a.raxis = 3 - qa;
+  for (int I = 0; I + 1 < x.cn[a.raxis]; ++I)  // the row axis: windows 1 or 2 fine rows apart (slab bound)
+    if (f0[a.raxis][I + 1] - f0[a.raxis][I] > 2) return TV_OK;
+  for (int s = 0; s < 3; ++s) {
+    a.fn[s] = x.fn[s];
+    a.cn[s] = x.cn[s];
+    if (int e = mg_upload(c, L, f0[s], &a.ax[s].f0)) return e;
+    if (int e = mg_upload(c, L, w[s], &a.ax[s].w)) return e;
+  }
+  a.da = L.g.dt_alpha;
+  a.nseg = (x.cn[0] + 61) / 62;
+  // chunks of the march axis: about `target` workgroups of 8 waves (2 fit a CU:
+  // 67 KB of LDS each), >= 3 coarse planes per chunk (TVFEM_RR_WG overrides)
+  // (256 measured best at C4: V-cycle 226 us against 240 / 231 us at 128 / 512)
+  const char* te = std::getenv("TVFEM_RR_WG");
+  const int target = te ? std::max(1, std::atoi(te)) : 256;
+  const int64_t rowblocks = (x.cn[a.raxis] + 7) / 8;
+  a.qchunk = std::min(x.cn[qa], 64);  // <= kRRQMax (tv_mg.hip)
+  while ((int64_t)a.nseg * rowblocks * ((x.cn[qa] + a.qchunk - 1) / a.qchunk) < target && a.qchunk > 3)
+    a.qchunk = (a.qchunk + 1) / 2;
+  a.on = 1;
+  return TV_OK;
+}
+
+// Levels whose restriction runs fused (bit l: from level l into level l + 1):
+// level 0 on fine grids of >= kRRMinNodes nodes.  Measured (C4, 8.2M nodes,
+// interleaved): V-cycle 249 -> 226 us, step 10.22 -> 9.85 ms; at C3 (1M nodes)
+// 3.15 -> 3.21 ms and on the coarse levels slower (their J x launches are
+// latency-bound, the facet launch adds one), so not there.  TVFEM_MG_RR (a bit
+// mask, read at setup) overrides, for tests and A/B measurement.
+constexpr int64_t kRRMinNodes = 3000000;
+static unsigned rr_levels(int64_t fine_nodes) {
+  const char* e = std::getenv("TVFEM_MG_RR");
+  if (e) return (unsigned)std::strtoul(e, nullptr, 0);
+  return fine_nodes >= kRRMinNodes ? 1u : 0u;
+}
+
 // T, b, x, w, dinv of a level (local size L.n), zeroed
 int mg_level_vectors(Ctx* c, MgLevel& L) {
   const CgGrid& f = c->cg;  // thermal constants (set by setup_mesh for both families)
@@ -262,14 +357,16 @@ int mg_setup(Ctx* c) {
     L.omega = mg_omega(mg_gershgorin(L.X, da));
     // transfer maps (finer level Xp -> this level)
     MgXfer& x = L.xf;
+    std::vector<int> ri[3];
+    std::vector<double> rw[3];
     for (int s = 0; s < 3; ++s) {
-      std::vector<int> pi, ri;
-      std::vector<double> pw, rw;
-      mg_axis_tables(Xp[s], is_c[s], pi, pw, ri, rw);
+      std::vector<int> pi;
+      std::vector<double> pw;
+      mg_axis_tables(Xp[s], is_c[s], pi, pw, ri[s], rw[s]);
       if (int e = mg_upload(c, L, pi, &x.pi[s])) return e;
       if (int e = mg_upload(c, L, pw, &x.pw[s])) return e;
-      if (int e = mg_upload(c, L, ri, &x.ri[s])) return e;
-      if (int e = mg_upload(c, L, rw, &x.rw[s])) return e;
+      if (int e = mg_upload(c, L, ri[s], &x.ri[s])) return e;
+      if (int e = mg_upload(c, L, rw[s], &x.rw[s])) return e;
       x.fn[s] = (int)Xp[s].size();
       x.cn[s] = (int)L.X[s].size();
       x.coarse[s] = coarse[s];
@@ -279,6 +376,11 @@ int mg_setup(Ctx* c) {
     x.c_kb = 0;
     x.c_ke = x.cn[2];
     x.aligned = 1;
+    // the fused residual restriction into this level (CG levels of a CG box;
+    // the DG1 -> CG1 transfer is the cell-vertex one)
+    const size_t from = c->mg.size() - 1 - (dg ? 1 : 0);  // index of the finer level (0: the fine grid)
+    if (!dg && ((rr_levels(c->nT) >> from) & 1u))
+      if (int e = rr_setup(c, L, Xp, ri, rw)) return e;
     for (int s = 0; s < 3; ++s) Xp[s] = L.X[s];
   }
   c->mg_on = true;
@@ -373,7 +475,10 @@ void mg_level(Ctx* c, size_t l) {
   if (l < c->mg.size()) {
     const MgLevel& C = c->mg[l];
     const FaceAdd fa = cg_face_add(L.g, 0);
-    if (fa.on && mg_restrict_folds_faces(C.xf)) {  // the restriction adds the facet terms (no k_cg_addfaces)
+    if (C.rr.on && fa.on) {  // fused residual restriction (no J x of this level)
+      launch_cg_facet_faces(L.g, L.T, L.x, c->st, s);
+      launch_mg_rrestrict(C.rr, c->st, L.b, L.x, cg_face_add_all(L.g), C.b, C.dinv, C.omega, C.x, s);
+    } else if (fa.on && mg_restrict_folds_faces(C.xf)) {  // the restriction adds the facet terms (no k_cg_addfaces)
       launch_cg_japply_partial(L.g, L.T, L.x, L.w, c->st, s);
       launch_mg_restrict(C.xf, c->st, L.b, L.w, &fa, nullptr, C.b, C.dinv, C.omega, C.x, s);
     } else {
@@ -427,7 +532,12 @@ int mg_apply0(Ctx* c, const double* T, const RedTail* tail) {
     // below kMgFoldFacesNodes the restriction adds the face-workgroup facet
     // terms itself, as on the coarse levels (one launch fewer where the V-cycle
     // is launch-bound); at C4 a complete J x (k_cg_addfaces) measured the same
-    if (fa.on && mg_restrict_folds_faces(C.xf) && n < kMgFoldFacesNodes) {
+    if (C.rr.on && mask == nullptr && fa.on) {
+      // b_1 = R (r - J x0) without J x0: the facet terms of x0 on every face,
+      // then the fused residual restriction (RRArgs) with level 1's pre-smoothing
+      launch_cg_facet_faces(c->cg, T, c->mgx, c->st, s);
+      launch_mg_rrestrict(C.rr, c->st, c->r, c->mgx, cg_face_add_all(c->cg), C.b, C.dinv, C.omega, C.x, s);
+    } else if (fa.on && mg_restrict_folds_faces(C.xf) && n < kMgFoldFacesNodes) {
       launch_cg_japply_partial(c->cg, T, c->mgx, c->w, c->st, s);
       launch_mg_restrict(C.xf, c->st, c->r, c->w, &fa, mask, C.b, C.dinv, C.omega, C.x, s);
     } else {

@@ -49,9 +49,13 @@ CASES = {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", list(CASES))
-def test_gmg_steps_match_oracle(case):
+@pytest.mark.parametrize("case", list(CASES) + ["plate+fused", "graded+fused"])
+def test_gmg_steps_match_oracle(case, monkeypatch):
+    """"+fused": level 0's fused residual restriction forced (k_mg_rrestrict, the
+    default from 3M nodes)"""
     _torch()
+    case, _, fused = case.partition("+")
+    monkeypatch.setenv("TVFEM_MG_RR", "1" if fused else "0")
     axes = CASES[case]
     dev, ref = _pair(axes, preconditioner="gmg")
     jac, _ = _pair(axes)
@@ -232,12 +236,17 @@ VCYCLE_CASES = {
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fused", [False, True], ids=["jx_restrict", "fused_restrict"])
 @pytest.mark.parametrize("case", list(VCYCLE_CASES))
-def test_gmg_vcycle_operator_matches_numpy_restatement(case):
+def test_gmg_vcycle_operator_matches_numpy_restatement(case, fused, monkeypatch):
     """tv_precond_apply (one V-cycle: the PCApply of the solve) against the numpy
     V-cycle above at a non-uniform T, to 1e-11; the operator is symmetric (CG
-    needs it) and positive."""
+    needs it) and positive.  fused: level 0's restriction as the fused residual
+    restriction b_1 = R (r - J x0) without J x0 (k_mg_rrestrict, on by default
+    from 3M nodes; forced here, where the geometry allows it: thin_x_4 keeps the
+    J x path)"""
     torch = _torch()
+    monkeypatch.setenv("TVFEM_MG_RR", "1" if fused else "0")
     from tvfem import RectilinearMesh
     from tvfem.problem import ThermoViscoProblem
     axes, levels = VCYCLE_CASES[case]
@@ -274,7 +283,8 @@ def test_gmg_vcycle_operator_matches_numpy_restatement(case):
     z_r, z_y = out
     e = relerr(z_r, B(r))
     sym = abs(y @ z_r - r @ z_y) / abs(y @ z_r)
-    print(f"[gmg] V-cycle {case}: {nlev} levels, vs numpy {e:.2e}, symmetry {sym:.1e}, r.Br {r @ z_r:.3e}")
+    print(f"[gmg] V-cycle {case} ({'fused' if fused else 'J x'} restriction): {nlev} levels, vs numpy {e:.2e}, "
+          f"symmetry {sym:.1e}, r.Br {r @ z_r:.3e}")
     assert e < 1e-11, e
     assert sym < 1e-12, sym
     assert r @ z_r > 0.0

@@ -20,7 +20,7 @@ GROUPS = {
     "pcg_matvec_fused": ("k_cg_march<1, true",),  # marching tiles + face workgroups, one launch
     "pcg_update": ("k_pcg_update",),
     "visco_update": ("k_visco_fused",),
-    "jacobian_apply": ("k_cg_march<1, false",),  # plain J x (+ k_cg_addfaces, a few KB)
+    "jacobian_apply": ("k_cg_march<1, false, 8, 1, 2, false",),  # the FINE-grid plain J x (largest grid; V-cycle x0)
     "dg_matvec_fused": ("k_dg_tile<true",),
     "pcg_iteration_single_reduction": ("k_cgs_march<false",),
     "jacobian_apply_unstructured": ("k_um_march14<1>",),  # half-stencil J x (structured topology, tv_um.hip)
@@ -36,7 +36,15 @@ GROUPS = {
 VCYCLE = ("k_cg_march<1, false", "k_cg_addfaces", "k_mg_restrict", "k_mg_prolong", "k_mg_jacobi", "k_mg_post_faces")
 
 
+# a dispatch that did no work: a gated-off step-end launch (the visco update
+# queued behind a Newton iteration that did not converge exits at its first
+# instruction) or a launch queued behind a converged Krylov solve.  Such
+# dispatches are dropped: below this fraction of the group's largest dispatch
+IDLE_FRAC = 0.02
+
+
 def per_kernel(d, counter):
+    """{kernel name: [(grid size, value), ...]} in dispatch order"""
     vals = defaultdict(list)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -46,11 +54,15 @@ def per_kernel(d, counter):
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") != counter:
                     continue
-                vals[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+                grid = int(float(row.get("Grid_Size") or row.get("Grid_Size_X") or 0))
+                vals[row["Kernel_Name"]].append((grid, float(row["Counter_Value"])))
     return vals
 
 
-def group_avg(vals, pats):
+def group_avg(vals, pats, grid_sel=None):
+    """mean per dispatch of each pattern's working dispatches (idle ones dropped),
+    summed over the patterns; grid_sel: "max" keeps the largest grid only (the
+    fine-grid launch of a kernel that also runs on the coarse multigrid levels)"""
     tot = 0.0
     found = []
     for pat in pats:
@@ -58,8 +70,13 @@ def group_avg(vals, pats):
         if not ks:
             return None, found
         v = [x for k in ks for x in vals[k]]
-        found.append((ks[0][:80], len(v)))
-        tot += sum(v) / len(v)
+        if grid_sel == "max":
+            gmax = max(g for g, _ in v)
+            v = [x for x in v if x[0] == gmax]
+        top = max(x for _, x in v)
+        work = [x for _, x in v if x >= IDLE_FRAC * top]
+        found.append((ks[0][:80], len(work), len(v) - len(work)))
+        tot += sum(work) / len(work)
     return tot, found
 
 
@@ -70,21 +87,27 @@ def main():
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), tools/pmc_kernels.py",
            "correction": "FETCH_SIZE x2 (gfx950 wide-read halving), KB -> bytes x1024", "kernels": {}}
     for name, pats in GROUPS.items():
-        fb, ff = group_avg(fetch, pats)
-        wb, wf = group_avg(write, pats)
+        sel = "max" if name == "jacobian_apply" else None
+        fb, ff = group_avg(fetch, pats, sel)
+        wb, wf = group_avg(write, pats, sel)
         if fb is None or wb is None:
             continue
         rd = 2.0 * fb * 1024.0
         wr = wb * 1024.0
         res["kernels"][name] = {"fetch_bytes": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
-                                "dispatches": ff}
+                                "dispatches": ff,
+                                "dispatch_note": "(name, working dispatches averaged, idle dispatches dropped)"
+                                                 + ("; the largest grid only (the fine level)" if sel else "")}
     ncyc = sum(len(v) for k, v in fetch.items() if "k_mg_post_faces" in k)
-    if ncyc:
-        fsum = sum(sum(v) for k, v in fetch.items() if any(p in k for p in VCYCLE))
-        wsum = sum(sum(v) for k, v in write.items() if any(p in k for p in VCYCLE))
+    if ncyc:  # (idle dispatches of a converged solve add ~0 bytes to the sums)
+        fsum = sum(x for k, v in fetch.items() if any(p in k for p in VCYCLE) for _, x in v)
+        wsum = sum(x for k, v in write.items() if any(p in k for p in VCYCLE) for _, x in v)
         res["kernels"]["mg_vcycle"] = {"fetch_bytes": 2.0 * fsum * 1024.0 / ncyc, "write_bytes": wsum * 1024.0 / ncyc,
                                        "hbm_bytes_per_launch": (2.0 * fsum + wsum) * 1024.0 / ncyc,
                                        "dispatches": [("V-cycles (k_mg_post_faces dispatches)", ncyc)]}
+    # the code the counters were collected on (the GPU box's copy has no .git:
+    # the caller passes the commit in TVFEM_GIT_HEAD)
+    res["git_head"] = os.environ.get("TVFEM_GIT_HEAD")
     dom = sys.argv[4] if len(sys.argv) > 4 else "pcg_matvec_fused"
     if dom in res["kernels"]:
         res["dominant"] = dom
