@@ -331,6 +331,8 @@ int visco(Ctx* c, bool copy_Tprev, const NewtonGate& gate = NewtonGate{});
 // the Newton iteration's ||dx||^2 (final on every rank at nrm2) to the host,
 // with the device's convergence decision when r0 is known; records evn
 int queue_newton_norm(Ctx* c, const double* nrm2);
+// dev_src -> pinned host_dst on the context stream (a one-wave kernel; bytes % 4 == 0)
+int publish(Ctx* c, void* host_dst, const void* dev_src, size_t bytes);
 void launch_bc_mask(Ctx* c, double* dinv);  // dinv = 0 on the Dirichlet-constrained rows
 
 // ---- tv_mgsolve.cpp ----

@@ -581,7 +581,7 @@ static int pcg_solve_mg_dist_cgs(Ctx* c, const double* T, int* its, int* reason,
       pending = 0;
     }
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, &c->h_st[0], c->st, sizeof(PcgState))) return e;
     HIPC(hipEventRecord(c->evp[0], c->stream));
     if (post) {  // dx is complete (the updates apply it); the group zeroes it after a 0-iteration solve
       double* nrm = c->sums + 6;
@@ -674,7 +674,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post)
     }
     launched += nb;
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, &c->h_st[0], c->st, sizeof(PcgState))) return e;
     HIPC(hipEventRecord(c->evp[0], c->stream));
     if (post) {  // the Newton iteration's next work, gated on the (all-reduced, rank-identical) state
       double* nrm = c->sums + 6;  // not c->sums: the lagged logic reads those across the batch boundary

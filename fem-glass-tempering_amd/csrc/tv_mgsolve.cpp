@@ -608,7 +608,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
       if (int e = mg_iteration(c, T, launched + b)) return e;
     launched += nb;
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(&c->h_st[0], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, &c->h_st[0], c->st, sizeof(PcgState))) return e;
     HIPC(hipEventRecord(c->evp[0], c->stream));
     if (post) {  // the Newton iteration's next work, queued before the host's poll (it runs once)
       launch_post_group(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, c->f[TV_F_T].ptr, c->partials, c->sums, c->stream);

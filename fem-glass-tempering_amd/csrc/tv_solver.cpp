@@ -4,6 +4,8 @@
 //   pcg_solve            PETSc KSPSolve_CG + PCJACOBI restated on the device
 //   pcg_solve_cgs        the single-reduction (Chronopoulos-Gear) form
 //   visco                _solve_Tf .. _solve_stress (ThermoViscoProblem.py:393-595)
+#include <cstdlib>
+
 #include "tv_ctx.h"
 
 namespace tv {
@@ -153,7 +155,7 @@ int pcg_solve(Ctx* c, const double* T, int* its, int* reason) {
       if (int e = pcg_iteration(c, T, launched + b, fold && b > 0, fold && b + 1 < nb)) return e;
     launched += nb;
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, &c->h_st[k], c->st, sizeof(PcgState))) return e;
     HIPC(hipEventRecord(c->evp[k], c->stream));
     return TV_OK;
   };
@@ -240,7 +242,7 @@ int pcg_solve_cgs(Ctx* c, const double* T, int* its, int* reason) {
       if (int e = cgs_iteration(c, T, launched + b)) return e;
     launched += nb;
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(&c->h_st[k], c->st, sizeof(PcgState), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, &c->h_st[k], c->st, sizeof(PcgState))) return e;
     HIPC(hipEventRecord(c->evp[k], c->stream));
     return TV_OK;
   };
@@ -345,6 +347,32 @@ int dirichlet_pre(Ctx* c, const double* T) {
   return TV_OK;
 }
 
+// Host-visible copies of the solver's scalars (the PCG state for the convergence
+// polls, ||dx||^2 and the Newton decision) written by a one-wave kernel with
+// system-scope stores straight into the pinned host slot, instead of a
+// hipMemcpyAsync: a copy in the stream left the GPU idle ~5 us each (C4 trace:
+// the gaps before k_dx_finish_gated and before every residual), a launch
+// costs ~1.5 us (profiles/r06_launch_audit.json).  TVFEM_PUBLISH=0: the copies.
+__global__ void k_publish(const uint32_t* __restrict__ src, uint32_t* dst, int n) {
+  const int t = threadIdx.x;
+  if (t < n) __hip_atomic_store(dst + t, src[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int publish(Ctx* c, void* host_dst, const void* dev_src, size_t bytes) {
+  static const bool on = [] {
+    const char* e = std::getenv("TVFEM_PUBLISH");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  if (!on || bytes % 4 != 0 || bytes > 4 * 256) {
+    HIPC(hipMemcpyAsync(host_dst, dev_src, bytes, hipMemcpyDeviceToHost, c->stream));
+    return TV_OK;
+  }
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, c->stream, static_cast<const uint32_t*>(dev_src),
+                     static_cast<uint32_t*>(host_dst), (int)(bytes / 4));
+  HIPC(hipGetLastError());
+  return TV_OK;
+}
+
 // the Newton test on the device (one thread): the only place the decision is
 // taken -- the gated step-end launches read out[1], the host copies it
 __global__ void k_newton_test(const double* __restrict__ nrm2, double r0, double rtol, double atol,
@@ -362,10 +390,10 @@ int queue_newton_norm(Ctx* c, const double* nrm2) {
   if (c->gate_ready) {
     hipLaunchKernelGGL(k_newton_test, dim3(1), dim3(64), 0, c->stream, nrm2, c->gate_r0, c->O.newton_rtol,
                        c->O.newton_atol, c->ngate);
-    HIPC(hipMemcpyAsync(c->h_sums, c->ngate, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, c->h_sums, c->ngate, 2 * sizeof(double))) return e;
     c->gate_dev = c->ngate + 1;
   } else {
-    HIPC(hipMemcpyAsync(c->h_sums, nrm2, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (int e = publish(c, c->h_sums, nrm2, sizeof(double))) return e;
     c->gate_dev = nullptr;
   }
   HIPC(hipEventRecord(c->evn, c->stream));
@@ -678,8 +706,10 @@ int tv_step(void* ctx, int thermal_only, int* newton_its, int* krylov_its) {
   if (int e = newton(c, newton_its, krylov_its, &conv, step_end, &done)) return e;
   // an unconverged solve (error_on_nonconvergence = False) stops here, as the
   // reference's _solve_T assert does (ThermoViscoProblem.py:390): T holds the
-  // last Newton iterate, T_prev and the viscoelastic state keep the previous step
-  if (!done && conv)
+  // last Newton iterate, T_prev and the viscoelastic state keep the previous step.
+  // Timing runs with fixed iteration counts (ksp_fixed_its > 0, bench.py --share:
+  // Newton tolerances 0, so never "converged") end every step as a solve would.
+  if (!done && (conv || c->O.ksp_fixed_its > 0))
     if (int e = queue_step_end(c, step_end, NewtonGate{})) return e;
   HIPC(hipGetLastError());
   // no stream synchronisation: the visco update (and T_prev <- T) finishes

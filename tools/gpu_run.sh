@@ -88,11 +88,15 @@ for MODE in "$@"; do
           timeout -s KILL 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${fam}_gmg_$ctr -o run --output-format csv -- \
             python3 tools/pmc_kernels.py --pc gmg --family $fam --cells $cells > $OUT/pmc_${fam}_gmg_$ctr.log 2>&1 ||
             { tail -5 $OUT/pmc_${fam}_gmg_$ctr.log; exit 1; }
+          step "pmc $fam jx $ctr"
+          timeout -s KILL 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${fam}_jx_$ctr -o run --output-format csv -- \
+            python3 tools/pmc_kernels.py --jx-only --family $fam --cells $cells > $OUT/pmc_${fam}_jx_$ctr.log 2>&1 ||
+            { tail -5 $OUT/pmc_${fam}_jx_$ctr.log; exit 1; }
         done
         dom=pcg_matvec_fused; [ $fam = DG ] && dom=dg_matvec_fused
         f=pmc_pcg_matvec_fused_${fam}_${cells//,/x}_n1_gmg.json
         python3 tools/pmc_summarize.py $OUT/pmc_${fam}_gmg_FETCH_SIZE $OUT/pmc_${fam}_gmg_WRITE_SIZE $OUT/$f $dom \
-          > $OUT/pmc_${fam}_gmg_summary.log 2>&1 || exit 1
+          $OUT/pmc_${fam}_jx_FETCH_SIZE $OUT/pmc_${fam}_jx_WRITE_SIZE > $OUT/pmc_${fam}_gmg_summary.log 2>&1 || exit 1
       done
       ;;
     ab)

@@ -35,6 +35,9 @@ ap.add_argument("--pc", choices=["jacobi", "gmg"], default="jacobi",
                 help="gmg: the bench line's solver -- whole coupled steps under the counters (the fused "
                      "matvec and every V-cycle kernel in the cache state of the multigrid solve)")
 ap.add_argument("--steps", type=int, default=2)
+ap.add_argument("--jx-only", action="store_true",
+                help="only `reps` plain J x launches with the Infinity Cache flushed (tv_time_kernel 10): the fine-grid "
+                     "J x record (with --pc gmg at C4 the V-cycle no longer runs a fine J x: the fused restriction)")
 a = ap.parse_args()
 nc = [int(v) for v in a.cells.split(",")]
 cfg = {"T": {"element": a.family, "degree": 1}, "sigma": {"element": a.family, "degree": 1}}
@@ -45,6 +48,12 @@ prob = ThermoViscoProblem(mesh, (0.0, 1.0), 0.1, cfg, dict(MP), materialize=Fals
 prob.setup()
 prob.solve_timestep()
 lib, ctx = prob._lib, prob._ctx
+if a.jx_only:
+    ms = C.c_double()
+    N.check(lib.tv_time_kernel(ctx, 10, a.reps, C.byref(ms)), ctx)
+    print(10, ms.value, flush=True)
+    prob.close()
+    sys.exit(0)
 if a.pc == "gmg":  # whole steps of the bench's solve and nothing else (the
     # V-cycle aggregate of pmc_summarize.py counts every level-0 J x launch)
     for _ in range(a.steps):

@@ -4,7 +4,11 @@ per launch for the hot-path kernels, with the gfx950 correction of
 streaming reads: doubled here; WRITE_SIZE taken as is).  Counter values are in
 KB (rocprofv3 derived-counter unit) -> bytes x1024.
 
-    python tools/pmc_summarize.py FETCH_DIR WRITE_DIR OUT.json [DOMINANT]
+    python tools/pmc_summarize.py FETCH_DIR WRITE_DIR OUT.json [DOMINANT [JX_FETCH_DIR JX_WRITE_DIR]]
+
+JX_*: passes of `pmc_kernels.py --jx-only` (flushed plain J x launches): the
+jacobian_apply record comes from them (the multigrid solve itself may run no
+fine-grid J x: the fused residual restriction).
 
 DOMINANT (default pcg_matvec_fused) names the group whose per-launch bytes are
 the record's top-level hbm_bytes_per_launch (bench.py's roofline.traffic).
@@ -33,7 +37,8 @@ GROUPS = {
 }
 # one V-cycle (tv_mgsolve.cpp mg_apply0): every launch of these, all levels, per
 # k_mg_post_faces dispatch (one per V-cycle)
-VCYCLE = ("k_cg_march<1, false", "k_cg_addfaces", "k_mg_restrict", "k_mg_prolong", "k_mg_jacobi", "k_mg_post_faces")
+VCYCLE = ("k_cg_march<1, false", "k_cg_addfaces", "k_mg_restrict", "k_mg_rrestrict", "k_cg_faces_all", "k_mg_prolong",
+          "k_mg_jacobi", "k_mg_post_faces")
 
 
 # a dispatch that did no work: a gated-off step-end launch (the visco update
@@ -108,6 +113,19 @@ def main():
     # the code the counters were collected on (the GPU box's copy has no .git:
     # the caller passes the commit in TVFEM_GIT_HEAD)
     res["git_head"] = os.environ.get("TVFEM_GIT_HEAD")
+    if len(sys.argv) > 6:  # the fine J x from its own (flushed) passes
+        jf = per_kernel(sys.argv[5], "FETCH_SIZE")
+        jw = per_kernel(sys.argv[6], "WRITE_SIZE")
+        pats = GROUPS["jacobian_apply"]
+        if not any(pats[0] in k for k in jf):  # DG1: the plain J x tile
+            pats = ("k_dg_tile<false",)
+        fb, ff = group_avg(jf, pats, "max")
+        wb, _ = group_avg(jw, pats, "max")
+        if fb is not None and wb is not None:
+            res["kernels"]["jacobian_apply"] = {
+                "fetch_bytes": 2.0 * fb * 1024.0, "write_bytes": wb * 1024.0,
+                "hbm_bytes_per_launch": (2.0 * fb + wb) * 1024.0, "dispatches": ff,
+                "dispatch_note": "pmc_kernels.py --jx-only: plain fine-grid J x, Infinity Cache flushed before each"}
     dom = sys.argv[4] if len(sys.argv) > 4 else "pcg_matvec_fused"
     if dom in res["kernels"]:
         res["dominant"] = dom

@@ -22,7 +22,7 @@ if not vis:  # thermal only: the step ends with T_prev <- T
 # step (not the back-to-back timing launches after the timed region)
 dmax = max(dur(rows[i]) for i in vis)
 vis = [i for i in vis if dur(rows[i]) > 0.2 * dmax]
-wins = [(a, b) for a, b in zip(vis, vis[1:]) if b - a > 20]
+wins = [(a, b) for a, b in zip(vis, vis[1:]) if b - a > 20] or list(zip(vis, vis[1:]))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else max(0, len(wins) // 2)
 a, b = wins[k]
 win = rows[a + 1:b + 1]
