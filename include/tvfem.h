@@ -178,7 +178,8 @@ typedef struct {
   int ksp_fixed_its;      /* > 0: every Krylov solve runs exactly this many
                              iterations, with no convergence test (PETSc
                              KSP_NORM_NONE + max_it; timing of partition shares
-                             with the communication stubbed)                    */
+                             with the communication stubbed); tv_step then ends
+                             every step (visco update) whatever the Newton test */
   int mg_coupling;        /* partitioned GMG: TV_MG_COUPLING_AUTO / _GLOBAL / _LOCAL */
 } tv_options;
 
