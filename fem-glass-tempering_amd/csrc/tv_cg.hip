@@ -660,7 +660,7 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
                                                         double* __restrict__ out, double* pout,
                                                         const PcgState* __restrict__ st,
                                                         double* __restrict__ partials, int nseg, int raxis,
-                                                        int qchunk, int qsub, RedTail rt, int nrec, int nmarch,
+                                                        int qchunk, RedTail rt, int nrec, int nmarch,
                                                         FaceOff fo, int it_host, PostArgs pa) {
   static_assert(!POST || (MODE == MODE_JAC && !FUSEP), "POST: plain Jacobian march only");
   stamp_start(rt);
@@ -720,31 +720,15 @@ __global__ __launch_bounds__(R * kWave) __attribute__((amdgpu_waves_per_eu(WPE))
   // runs and share their halo rows in L2 (measured at C4 against chunk-fastest:
   // step 11.22 / 11.34 -> 10.99 / 10.85 ms, flushed J x 53.5 -> 50.9-52.6 us;
   // segment, then chunk: 11.08 / 11.17 ms)
-  // chunks along the march axis: qchunk planes each; with qsub > 0 (plan():
-  // split_middle) the chunks between the two face chunks are cut into
-  // sub-chunks of qsub planes, which march_tile dispatches after the face-chunk
-  // tiles -- shorter tiles in the launch's last round (a shorter drain)
-  const int nch0 = (nQ + qchunk - 1) / qchunk;
-  const int mid = (nch0 - 2) * qchunk;  // planes between the face chunks
-  const bool split = qsub > 0 && nch0 > 2;
-  const int nch = split ? 2 + (mid + qsub - 1) / qsub : nch0;
+  const int nch = (nQ + qchunk - 1) / qchunk;
   const int nrbk = (nR + R - 1) / R;
   int seg, rb, chunk;
   march_tile(bid, nmarch, nseg, nrbk, nch, seg, rb, chunk);
   const int r0 = rb * R;
   const int r = r0 + wave;
   const bool row_ok = r < nR;
-  int q0 = chunk * qchunk;
-  int q1 = min(q0 + qchunk, nQ);
-  if (split && chunk > 0) {
-    if (chunk == nch - 1) {
-      q0 = qchunk * (nch0 - 1);
-      q1 = nQ;
-    } else {
-      q0 = qchunk + (chunk - 1) * qsub;
-      q1 = min(q0 + qsub, qchunk * (nch0 - 1));
-    }
-  }
+  const int q0 = chunk * qchunk;
+  const int q1 = min(q0 + qchunk, nQ);
   const int i = seg * kSeg - 1 + lane;
   const bool col_ok = (i >= 0) && (i < n0);
   const bool writer = col_ok && lane >= 1 && lane <= kSeg;
@@ -1654,18 +1638,7 @@ struct Launch {
   int nparts;  // partial records written (JAC)
   bool march;
   int raxis, qchunk;
-  // k_cg_march's tiles: the middle chunks split into sub-chunks of qsub planes
-  // (0: none; the single-reduction march keeps `blocks`)
-  int qsub, mblocks;
 };
-
-// sub-chunk length of the middle march chunks (0: no split); TVFEM_MARCH_QSUB
-// overrides
-int march_qsub(int qchunk, int nchunks) {
-  const char* e = std::getenv("TVFEM_MARCH_QSUB");
-  const int q = e ? std::atoi(e) : 0;
-  return (q > 0 && q < qchunk && nchunks > 2) ? q : 0;
-}
 
 bool use_march(const CgGrid& g) {
   // the marching kernel addresses the fields with 32-bit buffer offsets
@@ -1702,11 +1675,8 @@ Launch plan(const CgGrid& g, bool ghosts) {
     L.qchunk = (nQ + nchunks - 1) / nchunks;
     nchunks = (nQ + L.qchunk - 1) / L.qchunk;
     L.blocks = L.nseg * nrb * nchunks;
-    L.qsub = march_qsub(L.qchunk, nchunks);
-    const int nmid = L.qsub ? ((nchunks - 2) * L.qchunk + L.qsub - 1) / L.qsub : nchunks - 2;
-    L.mblocks = L.qsub ? L.nseg * nrb * (nmid + 2) : L.blocks;
     // Jacobian partial records: one per marching tile and face workgroup
-    L.nparts = L.mblocks + face_offsets(g, L.rows, 3 - L.raxis).off[6];
+    L.nparts = L.blocks + face_offsets(g, L.rows, 3 - L.raxis).off[6];
     return L;
   }
   L.kfirst = ghosts ? g.k_begin - g.g_lo : g.k_begin;
@@ -1719,8 +1689,6 @@ Launch plan(const CgGrid& g, bool ghosts) {
     L.blocks = (int)((waves + 3) / 4);
   }
   L.nparts = L.blocks;
-  L.mblocks = L.blocks;
-  L.qsub = 0;
   return L;
 }
 
@@ -1738,12 +1706,12 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     RedTail rt{};
     if (folded && tail && partials) rt = *tail;
     const FaceOff fo = folded ? face_offsets(g, L.rows, 3 - L.raxis) : FaceOff{};
-    const int grid = L.mblocks + fo.off[6];
+    const int grid = L.blocks + fo.off[6];
     // R = 8 rows, prefetch depth 2 (measured best, round 1-2: R = 16, PF 3 / 4,
     // 8 waves per SIMD and an LDS-DMA plane ring were all slower)
     hipLaunchKernelGGL((k_cg_march<MODE, FUSEP, kRows, 1, 2>), dim3(grid), dim3(kRows * kWave), 0, s, g, T, in0, in1,
-                       out, pout, st, partials, L.nseg, L.raxis, L.qchunk, L.qsub, rt, L.nparts, L.mblocks, fo,
-                       it_host, PostArgs{});
+                       out, pout, st, partials, L.nseg, L.raxis, L.qchunk, rt, L.nparts, L.blocks, fo, it_host,
+                       PostArgs{});
     if (folded && !FUSEP && addfaces && fo.off[6] > 0) {  // complete J x (else the consumer adds them)
       const int64_t nodes = 2 * ((int64_t)g.n1 * (g.w_end - g.w_begin) + (int64_t)g.n0 * std::max(g.n1, g.n2));
       const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, 1024));
@@ -1753,7 +1721,7 @@ bool launch_rows(const CgGrid& g, const double* T, const double* in0, const doub
     if (g.n_bnodes > 0) {
       hipLaunchKernelGGL((k_cg_boundary<MODE, FUSEP>), dim3(bnd_blocks(g)), dim3(kBlock), 0, s, g, g.bnodes,
                          g.n_bnodes, T, FUSEP ? in1 : in0, pout, out, st,
-                         partials ? partials + L.mblocks : nullptr, dinv_bnd);
+                         partials ? partials + L.blocks : nullptr, dinv_bnd);
     }
     return false;
   }
@@ -1910,11 +1878,11 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
   // the ghost planes)
   if (!L.march || g.n0 < 3) return -1;
   const FaceOff fo = face_offsets(g, L.rows, 3 - L.raxis);
-  const int grid = L.mblocks + fo.off[6];
+  const int grid = L.blocks + fo.off[6];
   const PostArgs pa{r, dinv, omega};
   hipLaunchKernelGGL((k_cg_march<MODE_JAC, false, 8, 1, 2, true>), dim3(grid), dim3(8 * kWave), 0, s, g, T, x,
-                     nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, L.qsub, RedTail{}, L.nparts,
-                     L.mblocks, fo, 0, pa);
+                     nullptr, z, nullptr, st, partials, L.nseg, L.raxis, L.qchunk, RedTail{}, L.nparts, L.blocks, fo,
+                     0, pa);
   const FaceAdd fa = cg_face_add(g, 0);
   const int nO = (L.raxis == 2) ? g.n1 : g.n2;
   const int64_t nodes = 2 * (int64_t)g.n1 * g.n2 + 2 * (int64_t)(g.n0 - 2) * nO;
@@ -1924,8 +1892,8 @@ int launch_cg_japply_post(const CgGrid& g, const double* T, const double* x, con
   const int nb = (int)std::max<int64_t>(1, std::min<int64_t>((nodes + kBlock - 1) / kBlock, cap));
   const RedTail rt = tail ? *tail : RedTail{};
   hipLaunchKernelGGL(k_mg_post_faces, dim3(nb), dim3(kBlock), 0, s, fa, L.raxis, r, dinv, omega, z, partials,
-                     L.mblocks, rt, st, g.k_begin, g.k_end, g.w_begin, g.w_end);
-  return L.mblocks + nb;
+                     L.blocks, rt, st, g.k_begin, g.k_end, g.w_begin, g.w_end);
+  return L.blocks + nb;
 }
 
 bool cg_uses_march(const CgGrid& g) { return use_march(g); }
