@@ -45,8 +45,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--kernel-reps", type=int, default=20)
-    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
-                    help="rccl (production) or host-staged gloo transport (rehearsal on one GPU)")
+    ap.add_argument("--comm", choices=["rccl", "host", "loopback"], default="rccl",
+                    help="rccl (production) or host-staged gloo transport (rehearsal on one GPU); with --share: "
+                         "loopback = the share's solve with the production RCCL groups on a one-rank communicator "
+                         "(tv_comm_init_loopback: the neighbours are the slab's periodic images) instead of the stub")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the hot kernels inside the timed steps")
     ap.add_argument("--output", default=None, metavar="DIR",
@@ -140,7 +142,13 @@ def main():
     mg_single = pc == "gmg" and prob.pcg_variant == "single"  # GMG-PCG, Chronopoulos-Gear form (deep-ghost slabs)
     single = prob.pcg_variant == "single" and not mg_single
     lib, ctx = prob._lib, prob._ctx
-    if a.share > 1:  # the multi-rank launch sequence with the transport stubbed (tv_comm_init_stub)
+    if a.share > 1 and a.comm == "loopback":  # the production RCCL groups, self send / receive pairs
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        uid = C.create_string_buffer(lib.tv_comm_unique_id_size())
+        with _StdoutToStderr():
+            N.check(lib.tv_comm_get_unique_id(uid))
+            N.check(lib.tv_comm_init_loopback(ctx, uid.raw), ctx)
+    elif a.share > 1:  # the multi-rank launch sequence with the transport stubbed (tv_comm_init_stub)
         N.check(lib.tv_comm_init_stub(ctx), ctx)
     if world > 1:
         from tvfem.parallel import init_host_comm, init_rccl
@@ -149,7 +157,8 @@ def main():
         else:
             # production transport; no silent fallback: a failed RCCL init ends the run
             try:
-                init_rccl(prob, rank, world, dist)
+                with _StdoutToStderr():
+                    init_rccl(prob, rank, world, dist)
             except Exception as e:
                 print(f"[bench rank {rank}] RCCL init failed: {e}", file=sys.stderr, flush=True)
                 raise SystemExit(3)
@@ -344,9 +353,13 @@ def main():
                                    f"({n_global} T-dofs), dt 0.1, "
                                    + ("thermal-only" if a.thermal_only else "coupled 6-term Prony"),
                        "parallelism": (f"ONE rank's share (partition {a.share // 2} of {a.share}, its slab of "
-                                       f"{n_owned} owned T-dofs) on one GPU, communication stubbed, iterations "
-                                       f"fixed at {a.share_its} (Newton per step, Krylov per solve): the per-rank "
-                                       "compute floor, not a multi-GPU measurement"
+                                       f"{n_owned} owned T-dofs) on one GPU, "
+                                       + ("the production RCCL groups on a one-rank loopback communicator "
+                                          "(self send/receive pairs; one-rank all-reduces are local copies)"
+                                          if a.comm == "loopback" else "communication stubbed")
+                                       + f", iterations fixed at {a.share_its} (Newton per step, Krylov per solve): "
+                                       "the per-rank step without cross-GPU transfer time, not a multi-GPU "
+                                       "measurement"
                                        if a.share > 1 else
                                        "single GPU, one partition (no communication)" if world == 1 else
                                        (f"RCB cell partition x{world} with a ghost-cell layer ("
@@ -369,6 +382,20 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
+
+
+class _StdoutToStderr:
+    """fd 1 -> fd 2 while RCCL initialises (its version banner goes to stdout;
+    the bench's stdout must hold the JSON line only)"""
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
 
 
 def latest_profile_summary():
