@@ -6,6 +6,8 @@
 //   tv_set_initial_condition  _set_initial_condition (:187-233)
 //   tv_output_*          _write_initial_output / _write_output / _finalize
 //                        (:246-276, :357-364, :614-620)
+#include <cstdlib>
+
 #include "tv_ctx.h"
 
 namespace tv {
@@ -503,8 +505,9 @@ int setup_fields(Ctx* c) {
   // records of width <= 3 per workgroup + the shard records of the two-level tail
   HIPC(hipMalloc(&c->partials, sizeof(double) * 3 * ((size_t)np + 2 * kShards)));
   HIPC(hipMalloc(&c->sums, sizeof(double) * 8));
-  HIPC(hipMalloc(&c->ngate, sizeof(double) * 2));
-  HIPC(hipMemset(c->ngate, 0, sizeof(double) * 2));
+  HIPC(hipMalloc(&c->ngate, sizeof(double) * 8));
+  HIPC(hipMemset(c->ngate, 0, sizeof(double) * 8));
+  if (const char* e = std::getenv("TVFEM_NEWTON_AHEAD")) c->newton_ahead = std::atoi(e) != 0;
   HIPC(hipMalloc(&c->counters, sizeof(unsigned) * kCounterWords));
   HIPC(hipMemsetAsync(c->counters, 0, sizeof(unsigned) * kCounterWords, c->stream));
   HIPC(hipMalloc(&c->st, sizeof(PcgState)));
@@ -512,7 +515,7 @@ int setup_fields(Ctx* c) {
   HIPC(hipMemsetAsync(c->tflag, 0, sizeof(int), c->stream));  // the tilde fields start at +0.0
   HIPC(hipHostMalloc(&c->h_st, 3 * sizeof(PcgState)));
   for (int k = 0; k < 2; ++k) HIPC(hipEventCreateWithFlags(&c->evp[k], hipEventDisableTiming));
-  HIPC(hipEventCreateWithFlags(&c->evn, hipEventDisableTiming));
+  for (hipEvent_t& e : c->evn) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPC(hipHostMalloc(&c->h_sums, sizeof(double) * 8));
   const int var = c->O.pcg_variant;
   const bool can = c->fam_T == TV_CG && !c->um && cg_cgs_supported(c->cg);
@@ -985,7 +988,8 @@ int tv_destroy(void* ctx) {
     if (c->evp[k]) hipEventDestroy(c->evp[k]);
     if (c->vev[k]) hipEventDestroy(c->vev[k]);
   }
-  if (c->evn) hipEventDestroy(c->evn);
+  for (hipEvent_t e : c->evn)
+    if (e) hipEventDestroy(e);
   if (c->d_ts) hipFree(c->d_ts);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;

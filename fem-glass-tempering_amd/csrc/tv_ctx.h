@@ -92,15 +92,23 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t evp[2] = {nullptr, nullptr};  // PCG convergence polls (double-buffered)
-  hipEvent_t evn = nullptr;                 // Newton: ||dx|| copied to the host
+  hipEvent_t evn[2] = {nullptr, nullptr};  // Newton: ||dx|| and the decision copied to the host (slot)
   const double* nrm_dev = nullptr;          // ... from here (||dx||^2, final on every rank behind evn)
-  // the device's Newton test (queue_newton_norm): ngate[0] = ||dx||^2, ngate[1] =
-  // the decision; gate_dev points at the decision of the last queued norm
-  // (nullptr: iteration 1, no test), gate_r0 = ||dx_1|| once known
+  // the device's Newton test (queue_newton_norm), two slots by the parity of
+  // the Newton iteration: ngate[2 s] = ||dx||^2, ngate[2 s + 1] = the decision;
+  // ngate[4] = ||dx_1||^2 (r0 of the incremental test, recorded on the device).
+  // gate_dev points at the decision of the last queued norm (nullptr:
+  // iteration 1, no test); solve_gate is the decision the next solve's state
+  // launch is gated on (a solve queued before the host read that decision)
   double* ngate = nullptr;
   const double* gate_dev = nullptr;
-  double gate_r0 = 0.0;
-  bool gate_ready = false;
+  const double* solve_gate = nullptr;
+  int newton_slot = 0;
+  bool newton_first = true;
+  // queue the predicted next Newton iteration's solve ahead of the host's read
+  // (multigrid paths); TVFEM_NEWTON_AHEAD=0 at creation: wait at every boundary
+  // (a test / measurement switch, tests/test_multigrid.py)
+  bool newton_ahead = true;
   tv_params P{};
   tv_options O{};
   int dim = 1;
@@ -325,11 +333,13 @@ CgsBuffers cgs_buffers(Ctx* c, const double* T, int it);
 // step_end (tv_step): 0 none, 1 the visco update, 2 T_prev <- T (thermal only).
 // At the Newton iteration the last step predicts to be the final one, the step's
 // end is queued before the host reads ||dx||, gated on the device's Newton test
-// (NewtonGate); *end_queued tells tv_step that it ran (the step is done)
+// (NewtonGate); *end_queued tells tv_step that it ran (the step is done).  On
+// the multigrid paths an iteration the last step predicts is queued before the
+// host reads the previous test, its solve gated on that test (solve_gate)
 int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end = 0, bool* end_queued = nullptr);
 int visco(Ctx* c, bool copy_Tprev, const NewtonGate& gate = NewtonGate{});
-// the Newton iteration's ||dx||^2 (final on every rank at nrm2) to the host,
-// with the device's convergence decision when r0 is known; records evn
+// the Newton iteration's ||dx||^2 (final on every rank at nrm2) and the device's
+// convergence decision (k_newton_test) to the host slot newton_slot; records evn[slot]
 int queue_newton_norm(Ctx* c, const double* nrm2);
 // dev_src -> pinned host_dst on the context stream (a one-wave kernel; bytes % 4 == 0)
 int publish(Ctx* c, void* host_dst, const void* dev_src, size_t bytes);
@@ -341,7 +351,7 @@ int mg_prepare(Ctx* c, const double* T);
 int mg_dg_weight(Ctx* c, const double* T);
 int mg_apply0(Ctx* c, const double* T, const RedTail* tail);
 // post: queue the Newton iteration's post-solve group (launch_post_group, ||dx||
-// copied to h_sums, evn recorded) behind every batch, gated on the device state
+// copied to h_sums, evn[slot] recorded) behind every batch, gated on the device state
 int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post = false);
 bool mg_next_level(const std::vector<double> (&Xp)[3], double da, bool automatic, std::vector<double> (&Xc)[3],
                    std::vector<char> (&is_c)[3], int coarse[3]);

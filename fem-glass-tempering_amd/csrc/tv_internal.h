@@ -144,6 +144,9 @@ enum PcgReason {
   R_RUNNING = 0,
   R_CONV_RTOL = 2, R_CONV_ATOL = 3,
   R_DIV_ITS = -3, R_DIV_DTOL = -4, R_DIV_INDEF_PC = -8, R_DIV_NANINF = -9, R_DIV_INDEF_MAT = -10,
+  // not a PETSc reason: a solve queued ahead of the Newton test of the previous
+  // iteration, which found Newton converged (k_set_state's gate): nothing ran
+  R_SKIPPED = -100,
 };
 
 // Viscoelastic constants (ViscoelasticModel.py:15-83), uploaded as a kernel argument.
@@ -579,7 +582,9 @@ void launch_mg_dx_finish(int64_t n, const PcgState* st, const double* pA, const 
 void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgState* st, int kind,
                          int check_done, hipStream_t s);
 void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s);
-void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s);
+// gate: a Newton decision word (k_newton_test); nonzero -> the solve is marked
+// done with R_SKIPPED, so every launch queued behind it exits at once
+void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s, const double* gate = nullptr);
 // T <- T - dx, ||dx||^2 partials; with `tail` the last workgroup reduces them into tail->out
 void launch_newton_update(int64_t n, double* T, const double* dx, double* partials, hipStream_t s,
                           const RedTail* tail = nullptr);

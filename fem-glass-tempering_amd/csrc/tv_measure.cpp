@@ -215,7 +215,7 @@ int tv_time_kernel(void* ctx, int kernel, int reps, double* ms) {
     auto launch = [&]() {
       switch (kernel) {
         case 12: hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, c->stream); break;
-        case 13: launch_set_state(c->st, h, c->stream); break;
+        case 13: launch_set_state(c->st, h, c->stream, nullptr); break;
         case 14: launch_reduce_logic(c->partials, 256, 2, c->sums, c->st, 0, 0, c->stream); break;
         case 15: {
           MgLevel& L = c->mg.back();

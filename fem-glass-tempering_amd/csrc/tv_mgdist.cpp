@@ -540,7 +540,7 @@ static int pcg_solve_mg_dist_cgs(Ctx* c, const double* T, int* its, int* reason,
   fine_window(c, &woff, &nwin);
   const PcgState h = pcg_state_init(c);
   c->h_st[2] = h;
-  launch_set_state(c->st, h, c->stream);
+  launch_set_state(c->st, h, c->stream, c->solve_gate);
   if (int e = mg_prepare_dist(c, T)) return e;
   if (c->dir_on)
     if (int e = halo(c, c->dinv)) return e;
@@ -603,8 +603,10 @@ static int pcg_solve_mg_dist_cgs(Ctx* c, const double* T, int* its, int* reason,
   *its = c->h_st[0].it;
   *reason = c->h_st[0].reason;
   if (!post && *its == 0) launch_fill(c->f[TV_F_DX].ptr + off, n, 0.0, c->stream);
-  c->pcg_hint = std::max(1, c->h_st[0].it);
-  c->mg_hint[hk] = c->pcg_hint;
+  if (*reason != R_SKIPPED) {  // a solve gated off by the Newton test says nothing of the count
+    c->pcg_hint = std::max(1, c->h_st[0].it);
+    c->mg_hint[hk] = c->pcg_hint;
+  }
   if (c->ktime) {
     for (int it = 0; it < *its; it += c->kstride)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);
@@ -620,7 +622,7 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post)
   fine_window(c, &woff, &nwin);
   const PcgState h = pcg_state_init(c);
   c->h_st[2] = h;
-  launch_set_state(c->st, h, c->stream);
+  launch_set_state(c->st, h, c->stream, c->solve_gate);
   if (c->amg_on) {  // the algebraic hierarchy is T-independent; level 0's weight at the first solve
     if (int e = mg_dg_weight(c, T)) return e;
   } else if (int e = mg_prepare_dist(c, T)) {
@@ -696,8 +698,10 @@ int pcg_solve_mg_dist(Ctx* c, const double* T, int* its, int* reason, bool post)
   *its = c->h_st[0].it;
   *reason = c->h_st[0].reason;
   if (!post) launch_mg_dx_finish(n, c->st, c->pA + off, c->pB + off, c->f[TV_F_DX].ptr + off, *its, c->stream);
-  c->pcg_hint = std::max(1, c->h_st[0].it);
-  c->mg_hint[hk] = c->pcg_hint;
+  if (*reason != R_SKIPPED) {  // a solve gated off by the Newton test says nothing of the count
+    c->pcg_hint = std::max(1, c->h_st[0].it);
+    c->mg_hint[hk] = c->pcg_hint;
+  }
   if (c->ktime) {
     for (int it = 0; it < *its; it += c->kstride)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);

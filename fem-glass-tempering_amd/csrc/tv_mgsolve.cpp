@@ -583,7 +583,7 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
   // from pinned memory (an asynchronous upload; a pageable source is staged by
   // the runtime -- no step-time change measured at C2 / C3 / C4)
   c->h_st[2] = h;
-  launch_set_state(c->st, h, c->stream);
+  launch_set_state(c->st, h, c->stream, c->solve_gate);
   if (int e = mg_prepare(c, T)) return e;
   if (int e = mg_dg_weight(c, T)) return e;
   if (c->dggface)
@@ -629,8 +629,10 @@ int pcg_solve_mg(Ctx* c, const double* T, int* its, int* reason, bool post) {
   // level 0 updates dx in pairs of iterations from iteration 1 on (k_mg_update /
   // k_dg_bupdate DXU): solves of 0 / 1 iterations and the last step of an odd-length one
   if (!post) launch_mg_dx_finish(n, c->st, c->pA, c->pB, c->f[TV_F_DX].ptr, *its, c->stream);
-  c->pcg_hint = std::max(1, c->h_st[0].it);
-  c->mg_hint[hk] = c->pcg_hint;
+  if (*reason != R_SKIPPED) {  // a solve gated off by the Newton test says nothing of the count
+    c->pcg_hint = std::max(1, c->h_st[0].it);
+    c->mg_hint[hk] = c->pcg_hint;
+  }
   if (c->ktime) {
     for (int it = 0; it < *its; it += c->kstride)
       if (c->ts_next + it < kTsCap) c->ts_pending.push_back(c->ts_next + it);

@@ -404,7 +404,13 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
 }
 
 __global__ void k_logic(PcgState* st, const double* sums, int kind) { apply_logic(st, sums, kind); }
-__global__ void k_set_state(PcgState* st, PcgState h) { *st = h; }
+__global__ void k_set_state(PcgState* st, PcgState h, const double* __restrict__ gate) {
+  if (gate != nullptr && *gate != 0.0) {
+    h.done = 1;
+    h.reason = R_SKIPPED;
+  }
+  *st = h;
+}
 
 __global__ __launch_bounds__(kBlock) void k_fill(double* x, int64_t n, double v) {
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) x[t] = v;
@@ -555,8 +561,8 @@ void launch_reduce_logic(const double* partials, int n, int W, double* out, PcgS
 // host-to-device copy: the copy of a pinned 160-byte struct was followed by a
 // ~45 us gap before the next kernel in the C4 trace (the runtime's copy path),
 // a launch is queued like every other kernel
-void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s) {
-  hipLaunchKernelGGL(k_set_state, dim3(1), dim3(1), 0, s, st, h);
+void launch_set_state(PcgState* st, const PcgState& h, hipStream_t s, const double* gate) {
+  hipLaunchKernelGGL(k_set_state, dim3(1), dim3(1), 0, s, st, h, gate);
 }
 
 void launch_logic(PcgState* st, const double* sums, int kind, hipStream_t s) {

@@ -374,29 +374,33 @@ int publish(Ctx* c, void* host_dst, const void* dev_src, size_t bytes) {
 }
 
 // the Newton test on the device (one thread): the only place the decision is
-// taken -- the gated step-end launches read out[1], the host copies it
-__global__ void k_newton_test(const double* __restrict__ nrm2, double r0, double rtol, double atol,
-                              double* __restrict__ out) {
+// taken -- the gated step-end launches and a solve queued ahead of the host's
+// read (k_set_state) read out[1], the host copies it.  Iteration 1 records
+// r0^2 = ||dx_1||^2 (no test there, dolfinx's incremental criterion)
+__global__ void k_newton_test(const double* __restrict__ nrm2, double* __restrict__ r0sq, int first, double rtol,
+                              double atol, double* __restrict__ out) {
   if (threadIdx.x == 0) {
     const double v = *nrm2;
-    const double rn = sqrt(v);
     out[0] = v;
-    out[1] = ((rn / r0 < rtol) || (rn < atol)) ? 1.0 : 0.0;
+    if (first) {
+      *r0sq = v;
+      out[1] = 0.0;
+    } else {
+      const double rn = sqrt(v), r0 = sqrt(*r0sq);
+      out[1] = ((rn / r0 < rtol) || (rn < atol)) ? 1.0 : 0.0;
+    }
   }
 }
 
 int queue_newton_norm(Ctx* c, const double* nrm2) {
   c->nrm_dev = nrm2;
-  if (c->gate_ready) {
-    hipLaunchKernelGGL(k_newton_test, dim3(1), dim3(64), 0, c->stream, nrm2, c->gate_r0, c->O.newton_rtol,
-                       c->O.newton_atol, c->ngate);
-    if (int e = publish(c, c->h_sums, c->ngate, 2 * sizeof(double))) return e;
-    c->gate_dev = c->ngate + 1;
-  } else {
-    if (int e = publish(c, c->h_sums, nrm2, sizeof(double))) return e;
-    c->gate_dev = nullptr;
-  }
-  HIPC(hipEventRecord(c->evn, c->stream));
+  const int sl = c->newton_slot;
+  double* out = c->ngate + 2 * sl;
+  hipLaunchKernelGGL(k_newton_test, dim3(1), dim3(64), 0, c->stream, nrm2, c->ngate + 4, c->newton_first ? 1 : 0,
+                     c->O.newton_rtol, c->O.newton_atol, out);
+  if (int e = publish(c, c->h_sums + 2 * sl, out, 2 * sizeof(double))) return e;
+  c->gate_dev = c->newton_first ? nullptr : out + 1;
+  HIPC(hipEventRecord(c->evn[sl], c->stream));
   return TV_OK;
 }
 
@@ -435,11 +439,11 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
   if (int e = halo(c, T)) return e;
   if (int e = halo(c, c->f[TV_F_T_PREV].ptr)) return e;
   const int64_t off = c->ownT_off, n = c->ownT_n;
-  int its = 0, kits = 0;
+  int its = 0, kits = 0;  // its: Newton iterations whose test the host has read
   bool conv = false;
-  double r0 = 0.0, rn = 0.0;
-  c->gate_ready = false;  // r0 unknown until iteration 1's ||dx|| is read
+  double rn = 0.0;
   c->gate_dev = nullptr;
+  c->solve_gate = nullptr;
   // F(u); on the CG march path the residual's boundary pass also rewrites the
   // boundary rows of dinv for the same u once the interior is in place
   auto residual = [&]() -> bool {
@@ -448,8 +452,19 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
     op_residual(c, T, Tp, c->r);
     return false;
   };
+  // the host's read of Newton iteration q's test (its slot's event has fired
+  // once a later launch's poll returned): ||dx||, the device's decision
+  auto read_test = [&](int q) -> int {
+    HIPC(hipEventSynchronize(c->evn[q & 1]));
+    rn = std::sqrt(c->h_sums[2 * (q & 1)]);
+    ++its;
+    conv = q > 0 && c->h_sums[2 * (q & 1) + 1] != 0.0;  // no test at the first iteration
+    return TV_OK;
+  };
   bool dinv_fresh = residual();
-  while (!conv && its < c->O.newton_max_it) {
+  int q = 0;          // Newton iterations queued
+  int pending = -1;   // a queued iteration whose test the host has not read yet
+  for (;;) {
     if (!c->dggface) {  // J(u) (matrix-free) + Jacobi PC setup (DG GMG: cell blocks)
       if (!c->um && c->fam_T == TV_CG) {
         // the T-independent interior of dinv is written once; then the boundary nodes only
@@ -465,15 +480,28 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
     if (dir)
       if (int e = dirichlet_pre(c, T)) return e;
     int k = 0, reason = 0;
-    c->newton_k = its;  // the multigrid solves queue the count this Newton index took last step
+    c->newton_k = q;  // the multigrid solves queue the count this Newton index took last step
+    c->newton_slot = q & 1;
+    c->newton_first = q == 0;
     // multigrid (one partition or distributed): the post-solve group (dx,
     // u <- u - dx, ||dx||) is queued behind every batch and runs behind the
     // one that ends the solve, and only if it ended well (post_gate)
     const bool post_in_solve = c->mg_on && !dir;
-    if (int e = (c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason, post_in_solve)
-                                            : pcg_solve_mg(c, T, &k, &reason, post_in_solve))
-                          : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason))))
-      return e;
+    // a solve queued before the host read the previous iteration's test runs
+    // only if that test did not end the Newton solve (iteration 1 has no test)
+    c->solve_gate = pending >= 1 ? c->ngate + 2 * (pending & 1) + 1 : nullptr;
+    const int e_solve = c->mg_on ? (c->n_parts > 1 ? pcg_solve_mg_dist(c, T, &k, &reason, post_in_solve)
+                                                   : pcg_solve_mg(c, T, &k, &reason, post_in_solve))
+                                 : (c->cgs ? pcg_solve_cgs(c, T, &k, &reason) : pcg_solve(c, T, &k, &reason));
+    c->solve_gate = nullptr;
+    if (e_solve) return e_solve;
+    if (pending >= 0) {
+      if (int e = read_test(pending)) return e;
+      pending = -1;
+      if ((reason == R_SKIPPED) != conv)
+        return c->fail(TV_ERR_STATE, "Newton: a solve queued ahead disagrees with the Newton test (internal)");
+      if (conv) break;  // that solve was gated off on the device: T is the converged iterate
+    }
     kits += k;
     if (reason < 0 && !(reason == R_DIV_ITS && c->O.ksp_fixed_its > 0))
       return c->fail(TV_ERR_KSP, std::string("Krylov solver did not converge (") + reason_str(reason) + ")");
@@ -488,12 +516,23 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
       if (int e = queue_newton_norm(c, c->sums)) return e;
     }
     if (int e = halo(c, T)) return e;
+    ++q;
     // the next F queued before the host reads ||dx|| when the previous step
     // took more Newton iterations than this one has so far (the counts repeat
     // from step to step): the GPU does not idle through the host's turnaround.
     // A wrong guess costs one residual, whose result is simply not used.
-    const bool spec = its + 1 < c->newton_pred && its + 1 < c->O.newton_max_it;
+    const bool spec = q < c->newton_pred && q < c->O.newton_max_it;
     if (spec) dinv_fresh = residual();
+    // ... and on the multigrid paths the next iteration's solve too, gated on
+    // the device's test of this one (k_set_state): the host reads this test
+    // after that solve's first poll, so it never waits at a Newton boundary
+    // with the GPU drained (the C4 trace showed the GPU catching up with the
+    // host's enqueue of the next solve's first V-cycle there).  A wrong guess
+    // costs one batch of launches that exit at once.
+    if (spec && post_in_solve && c->newton_ahead) {
+      pending = q - 1;
+      continue;
+    }
     // at (or past) the iteration the last step ended with, the step's end is
     // queued now, gated on the device's test of this iteration (k_newton_test);
     // the host below takes the SAME decision (the flag copied with ||dx||^2), so
@@ -501,31 +540,22 @@ int newton(Ctx* c, int* out_its, int* out_kits, int* out_conv, int step_end, boo
     // runs the step end (_solve_T's assert(converged), ThermoViscoProblem.py:390,
     // fires before _solve_Tf and the stress updates)
     bool end_q = false;
-    if (step_end && !spec && its >= 1 && its + 1 >= c->newton_pred && c->gate_dev) {
+    if (step_end && !spec && q >= 2 && q >= c->newton_pred && c->gate_dev) {
       if (int e = queue_step_end(c, step_end, NewtonGate{c->gate_dev})) return e;
       end_q = true;
     }
     // the host waits for ||dx|| only, not for the queued residual: it decides
     // and queues the next Newton iteration while the GPU computes F (the C4
     // trace showed the GPU idle ~27 us per Newton iteration behind a stream sync)
-    HIPC(hipEventSynchronize(c->evn));
-    rn = std::sqrt(c->h_sums[0]);
-    ++its;
-    if (its == 1) {
-      r0 = rn;  // residual0 = ||dx_1||; no test at the first iteration
-      conv = false;
-      c->gate_r0 = r0;
-      c->gate_ready = true;  // every later norm is tested on the device
-    } else {
-      conv = c->h_sums[1] != 0.0;  // the device's decision (queue_newton_norm)
-    }
+    if (int e = read_test(q - 1)) return e;
     if (end_q) {
       if (conv) *end_queued = true;
       else c->vev_pending = false;  // gated off: its events bracket nothing
     }
+    if (conv || its >= c->O.newton_max_it) break;
     // dolfinx assembles F after every update; in the incremental criterion that
     // last F is never read, so it is assembled only when another iteration follows.
-    if (!conv && its < c->O.newton_max_it && !spec) dinv_fresh = residual();
+    if (!spec) dinv_fresh = residual();
   }
   HIPC(hipGetLastError());
   c->newton_pred = its;

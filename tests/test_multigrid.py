@@ -79,6 +79,39 @@ def test_gmg_steps_match_oracle(case, monkeypatch):
         p.close()
 
 
+@pytest.mark.gpu
+def test_gmg_newton_ahead_mispredicted(monkeypatch):
+    """The next Newton iteration's solve is queued before the host reads the
+    previous test when the last step took more iterations (newton(), gated on
+    the device's test by k_set_state).  A looser Newton rtol makes step 2 end
+    before the predicted count (the solve queued ahead is gated off), then the
+    default rtol makes step 3 take more than predicted; every state field must
+    be bitwise the one of a context that waits at every Newton boundary
+    (TVFEM_NEWTON_AHEAD=0), with the same Newton and Krylov counts."""
+    _torch()
+    axes = CASES["plate"]
+    monkeypatch.setenv("TVFEM_NEWTON_AHEAD", "1")
+    dev, _ = _pair(axes, preconditioner="gmg")
+    monkeypatch.setenv("TVFEM_NEWTON_AHEAD", "0")
+    base, _ = _pair(axes, preconditioner="gmg")
+    for p in (dev, base):
+        p.setup()
+    counts = []
+    for step, rtol in enumerate((1e-12, 1e-6, 1e-12, 1e-12)):
+        for p in (dev, base):
+            p.solver.rtol = rtol
+            p.solve_timestep()
+        counts.append((dev.last_newton_iterations, base.last_newton_iterations))
+        assert counts[-1][0] == counts[-1][1], (step, counts)
+        assert dev.last_krylov_iterations == base.last_krylov_iterations, step
+        for f in ("T", "T_prev", "phi", "Tf", "xi", "sigma"):
+            assert np.array_equal(dev.get_field(f), base.get_field(f), equal_nan=True), (step, f)
+    assert counts[1][0] < counts[0][0] and counts[2][0] > counts[1][0], counts  # both mispredictions happened
+    print(f"[gmg] Newton counts with the solve queued ahead: {counts}")
+    for p in (dev, base):
+        p.close()
+
+
 DG = {"element": "DG", "degree": 1}
 
 
