@@ -653,7 +653,6 @@ void tv_default_options(tv_options* o) {
   o->ksp_dtol = 1e5;
   o->ksp_max_it = 10000;
   o->materialize = 1;
-  o->use_graphs = 0;
   o->pcg_batch = 8;
   o->pcg_variant = TV_PCG_AUTO;
   o->model_mode = TV_MODEL_REFERENCE;

@@ -19,7 +19,7 @@ TV_MODEL_REFERENCE, TV_MODEL_PAPER = 0, 1
 TV_PC_JACOBI, TV_PC_GMG, TV_PC_AMG = 0, 1, 2
 TV_DG_KERNEL_AUTO, TV_DG_KERNEL_TILE, TV_DG_KERNEL_CELLS = 0, 1, 2
 TV_MG_COUPLING_AUTO, TV_MG_COUPLING_GLOBAL, TV_MG_COUPLING_LOCAL = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # field ids (tvfem.h enum, same order)
 FIELDS = [
@@ -90,7 +90,7 @@ class Options(C.Structure):
     _fields_ = [("newton_rtol", C.c_double), ("newton_atol", C.c_double), ("newton_max_it", C.c_int),
                 ("error_on_nonconvergence", C.c_int), ("ksp_rtol", C.c_double), ("ksp_atol", C.c_double),
                 ("ksp_dtol", C.c_double), ("ksp_max_it", C.c_int), ("materialize", C.c_int),
-                ("use_graphs", C.c_int), ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
+                ("pcg_batch", C.c_int), ("pcg_variant", C.c_int),
                 ("model_mode", C.c_int), ("preconditioner", C.c_int), ("mg_levels", C.c_int),
                 ("dg_kernel", C.c_int), ("dg_tile_chunk", C.c_int), ("mg_replicate_nodes", C.c_int),
                 ("ksp_fixed_its", C.c_int), ("mg_coupling", C.c_int)]

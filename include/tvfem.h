@@ -51,13 +51,14 @@
 extern "C" {
 #endif
 
-#define TV_ABI_VERSION 7  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
+#define TV_ABI_VERSION 8  /* 2: tv_options gained pcg_variant, model_mode, preconditioner, mg_levels;
                             3: dg_kernel, dg_tile_chunk, mg_replicate_nodes, ksp_fixed_its;
                             4: tv_upart_desc / tv_create_unstructured_part;
                             5: tv_comm_init_loopback, tv_comm_check, tv_options.mg_coupling;
                             6: tv_comm_time;
                             7: tv_get_options, tv_set_newton_tolerances, tv_set_ksp_tolerances,
-                               tv_last_converged */
+                               tv_last_converged;
+                            8: tv_options lost the unused use_graphs field */
 
 /* status codes */
 #define TV_OK 0
@@ -164,7 +165,6 @@ typedef struct {
   double ksp_rtol, ksp_atol, ksp_dtol;
   int ksp_max_it;
   int materialize;        /* 0: state fields only, 1: every reference field  */
-  int use_graphs;         /* reserved (no effect)                            */
   int pcg_batch;          /* iterations launched between convergence polls  */
   int pcg_variant;        /* TV_PCG_AUTO / TV_PCG_KSPCG / TV_PCG_SINGLE_REDUCTION */
   int model_mode;         /* TV_MODEL_REFERENCE (default) / TV_MODEL_PAPER       */

@@ -46,7 +46,7 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version_and_defaults(lib):
     from tvfem import _native as N
-    assert lib.tv_abi_version() == 7
+    assert lib.tv_abi_version() == 8
     o = N.default_options()
     assert o.newton_rtol == 1e-12 and o.newton_atol == 1e-10 and o.newton_max_it == 50
     assert o.ksp_rtol == 1e-5 and o.ksp_max_it == 10000
