@@ -678,12 +678,15 @@ int xfer_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + kBlock - 1) /
 //        U = RrMr (p + da q) + da RrKr p,  V = RrMr p,  S = Rr s
 //      and accumulates b_c(Q) = sum over the window of Rq S - RqMq U - da RqKq V
 //      (two accumulators: an even plane 2k completes coarse k - 2, opens k).
-// The loads of plane P + 1 are in flight while plane P is reduced and folded.
+// The loads of planes P + 1 .. P + kRRPF are in flight while plane P is reduced
+// and folded (a ring of kRRPF + 1 register sets; one workgroup per CU, so the
+// ring's registers cost no occupancy).
 constexpr int kRRSeg = kWave - 2;
 constexpr int kRRWaves = 8;
 constexpr int kRRRows = 2 * kRRWaves + 3;          // fine rows per plane (coarsened row axis)
 constexpr int kRRPer = (kRRRows + kRRWaves - 1) / kRRWaves;  // rows loaded per wave
 constexpr int kRRQMax = 64;  // coarse march planes per chunk (LDS weight stage)
+constexpr int kRRPF = 1;     // fine planes of loads in flight ahead of the one reduced (2, 3: slower, profiles/r06_rrestrict_loads_ab.txt)
 
 // buffer resource of a level vector (32-bit byte offsets: a per-lane x offset in
 // a VGPR plus a wave-uniform row / plane offset in an SGPR)
@@ -700,14 +703,22 @@ __device__ __forceinline__ d2a8 rr_ld2(rr_buf r, uint32_t voff, uint32_t soff) {
   const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
   return __builtin_bit_cast(d2a8, v);
 }
+__device__ __forceinline__ double rr_ld1(rr_buf r, uint32_t voff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 0, 0));
+}
 
+// one fine plane's loads; every load is issued unconditionally (lanes / waves
+// without the data carry an out-of-range offset): a load under a branch made
+// the wave wait for all its loads there (vmcnt counts in order), i.e. for the
+// prefetch of the next planes too
 struct RRSet {
   d2a8 xv[kRRPer], bv[kRRPer];
   double fx[kRRPer];  // the x-face facet term of each row at this lane's node (x-face lanes only)
+  d2a8 fr;            // the row-axis face term of this wave's face row (waves holding one)
 };
 
 template <int RA>
-__global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, const PcgState* __restrict__ st,
+__global__ __launch_bounds__(kRRWaves * kWave) void k_mg_rrestrict(RRArgs a, const PcgState* __restrict__ st,
                                                                    const double* __restrict__ b,
                                                                    const double* __restrict__ x, FaceAdd fa,
                                                                    double* __restrict__ bc,
@@ -771,9 +782,13 @@ __global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, 
   // axis' first / last row and the march-axis faces on the first / last fine
   // plane (wave-uniform branches, rare)
   const bool xl0 = fa.ff[0] != nullptr && e0 == 0, xl1 = fa.ff[1] != nullptr && e0 == nf0 - 1;
-  const bool xwave = __ballot(xl0 || xl1) != 0;  // wave-uniform
-  const double* fxp = xl0 ? fa.ff[0] : (xl1 ? fa.ff[1] : b);
   const int n1 = a.fn[1];
+  // the two x-face arrays through one resource: they lie in one allocation
+  // (CgGrid::ffbuf), face 1 at a uniform element distance from face 0
+  const double* fxb = fa.ff[0] ? fa.ff[0] : fa.ff[1];
+  const int64_t dx1 = (fa.ff[0] && fa.ff[1]) ? (int64_t)(fa.ff[1] - fa.ff[0]) : 0;
+  const rr_buf rfx = rr_rsrc(fxb, fxb ? (uint32_t)((dx1 + (int64_t)n1 * a.fn[2]) * 8) : 0u);
+  const uint32_t fxo = xl1 ? (uint32_t)dx1 : 0u;
   const uint32_t nfa = nbytes / (uint32_t)nfr, nfb = nbytes / (uint32_t)nfq;  // face array bytes
   const rr_buf frl = rr_rsrc(fa.ff[2 * ra], fa.ff[2 * ra] ? nfa : 0u);
   const rr_buf frh = rr_rsrc(fa.ff[2 * ra + 1], fa.ff[2 * ra + 1] ? nfa : 0u);
@@ -781,6 +796,19 @@ __global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, 
   const rr_buf fqh = rr_rsrc(fa.ff[2 * qa + 1], fa.ff[2 * qa + 1] ? nfb : 0u);
   const bool hrl = fa.ff[2 * ra] != nullptr, hrh = fa.ff[2 * ra + 1] != nullptr;
   const bool hql = fa.ff[2 * qa] != nullptr, hqh = fa.ff[2 * qa + 1] != nullptr;
+  // this wave's face row among its loaded rows (wave-uniform; at most one: the
+  // face rows are the first and the last of the axis)
+  int uf = -1;
+  bool uf_lo = false;
+#pragma unroll
+  for (int u = 0; u < kRRPer; ++u) {
+    const int fr = fr_first + wave + u * kRRWaves;
+    if (rload[u] && ((hrl && fr == 0) || (hrh && fr == nfr - 1))) {
+      uf = u;
+      uf_lo = hrl && fr == 0;
+    }
+  }
+  const rr_buf frs = uf_lo ? frl : frh;
   const int f0q = kld(a.ax[qa].f0, Q0);
   const int np = 2 * (Q1 - Q0) + 3;  // fine planes f0q .. f0q + np - 1
   auto fetch = [&](int P, RRSet& S) {
@@ -795,12 +823,10 @@ __global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, 
     for (int u = 0; u < kRRPer; ++u) {
       // storage (j, k) of (row frow[u], plane fq): the x-face index j + n1 k
       const int j = (ra == 1) ? frow[u] : fq, k = (ra == 1) ? fq : frow[u];
-      S.fx[u] = 0.0;
-      if (xwave) {
-        const double v = fxp[(xl0 || xl1) ? j + n1 * k : 0];
-        S.fx[u] = (xl0 || xl1) ? v : 0.0;
-      }
+      S.fx[u] = rr_ld1(rfx, ((xl0 || xl1) && rload[u]) ? (fxo + (uint32_t)(j + n1 * k)) * 8u : 0x40000000u);
     }
+    // the face row's pairs (face index i + n0 * plane)
+    S.fr = rr_ld2(frs, uf >= 0 ? voff : 0x40000000u, (uint32_t)(nf0 * fq) * 8u);
   };
   // the lane's x weights in registers (read for every loaded row)
   double wx[15];
@@ -809,19 +835,15 @@ __global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, 
   // the loaded rows of plane P: facet terms, x-reduction into slab buffer P & 1
   auto reduce = [&](int P, const RRSet& S) {
     const int fqr = f0q + P;
-    const int fqc = min(max(fqr, 0), nfq - 1);
     const bool qlo = hql && fqr == 0, qhi = hqh && fqr == nfq - 1;  // wave-uniform
     d2a8 sv[kRRPer];
 #pragma unroll
     for (int u = 0; u < kRRPer; ++u) {
       sv[u] = S.bv[u];
       sv[u].x -= S.fx[u];
-      const int fr = fr_first + wave + u * kRRWaves;
-      const bool rlo = hrl && fr == 0, rhi = hrh && fr == nfr - 1;  // wave-uniform
-      if (rlo || rhi) {  // a row-axis face row (face index i + n0 * plane)
-        const d2a8 f = rr_ld2(rlo ? frl : frh, voff, (uint32_t)(nf0 * fqc) * 8u);
-        sv[u].x -= f.x;
-        sv[u].y -= f.y;
+      if (u == uf) {  // a row-axis face row (wave-uniform)
+        sv[u].x -= S.fr.x;
+        sv[u].y -= S.fr.y;
       }
       if (qlo || qhi) {  // a march-axis face plane (face index i + n0 * row)
         const d2a8 f = rr_ld2(qlo ? fql : fqh, voff, (uint32_t)(nf0 * frow[u]) * 8u);
@@ -875,35 +897,54 @@ __global__ __launch_bounds__(kRRWaves * kWave, 4) void k_mg_rrestrict(RRArgs a, 
   // older, Y = the newer live coarse plane; an even plane 2k completes coarse
   // k - 2 (written out) and opens coarse k.
   double X = 0.0, Y = 0.0;
-  RRSet A, B;
-  fetch(0, A);
+  // D^-1 of the coarse node an even plane completes, loaded at the start of
+  // that plane's step (ahead of its prefetch, so waiting for it does not wait
+  // for the prefetch: a load at the store made every even plane wait for all)
+  const uint32_t ncb = (uint32_t)ncx * (uint32_t)a.cn[1] * (uint32_t)a.cn[2] * 8u;
+  const rr_buf rdc = rr_rsrc(dinv_c, xc != nullptr ? ncb : 0u);
+  auto coarse_off = [&](int Q) -> uint32_t {
+    const int J1 = (ra == 1) ? Jc : Q, K2 = (ra == 1) ? Q : Jc;
+    return ((uint32_t)I + (uint32_t)ncx * ((uint32_t)J1 + (uint32_t)a.cn[1] * (uint32_t)K2)) * 8u;
+  };
+  RRSet S[kRRPF + 1];
+#pragma unroll
+  for (int s = 0; s < kRRPF; ++s) fetch(min(s, np - 1), S[s]);
   __syncthreads();  // the weight stages
+  // slot s of the ring holds plane P0 + s when step s of the unrolled group
+  // starts; it fetches plane P0 + s + kRRPF into the slot consumed one step ago
+  // (planes past the chunk are clamped reloads, never reduced)
 #pragma unroll 1
-  for (int P = 0; P < np; ++P) {
-    fetch(min(P + 1, np - 1), B);  // in flight during this plane
-    reduce(P, A);
-    __syncthreads();
-    double U, V, Sv;
-    fold(P, U, V, Sv);
-    const int k = P >> 1;
-    if ((P & 1) == 0) {
-      if (k - 2 >= 0 && k - 2 < nQ) X += contrib(Q0 + k - 2, 4, U, V, Sv);
-      if (k - 1 >= 0 && k - 1 < nQ) Y += contrib(Q0 + k - 1, 2, U, V, Sv);
-      const double Z = (k < nQ) ? contrib(Q0 + k, 0, U, V, Sv) : 0.0;
-      if (k - 2 >= 0 && out_lane) {  // coarse Q0 + k - 2 complete
-        const int Q = Q0 + k - 2;
-        const int J1 = (ra == 1) ? Jc : Q, K2 = (ra == 1) ? Q : Jc;
-        const int64_t o = (int64_t)I + (int64_t)ncx * (J1 + (int64_t)a.cn[1] * K2);
-        bc[o] = X;
-        if (xc != nullptr) xc[o] = omega_c * dinv_c[o] * X;  // the coarse pre-smoothing step from 0
+  for (int P0 = 0; P0 < np; P0 += kRRPF + 1) {
+#pragma unroll
+    for (int s = 0; s <= kRRPF; ++s) {
+      const int P = P0 + s;
+      const bool completes = P < np && (P & 1) == 0 && (P >> 1) - 2 >= 0 && out_lane;
+      const double dcv = rr_ld1(rdc, completes ? coarse_off(Q0 + (P >> 1) - 2) : 0x40000000u);
+      __builtin_amdgcn_sched_barrier(0);  // issued ahead of the prefetch (vmcnt counts in order)
+      fetch(min(P + kRRPF, np - 1), S[(s + kRRPF) % (kRRPF + 1)]);
+      if (P < np) {  // workgroup-uniform
+        reduce(P, S[s]);
+        __syncthreads();
+        double U, V, Sv;
+        fold(P, U, V, Sv);
+        const int k = P >> 1;
+        if ((P & 1) == 0) {
+          if (k - 2 >= 0 && k - 2 < nQ) X += contrib(Q0 + k - 2, 4, U, V, Sv);
+          if (k - 1 >= 0 && k - 1 < nQ) Y += contrib(Q0 + k - 1, 2, U, V, Sv);
+          const double Z = (k < nQ) ? contrib(Q0 + k, 0, U, V, Sv) : 0.0;
+          if (completes) {  // coarse Q0 + k - 2 complete
+            const int64_t o = coarse_off(Q0 + k - 2) / 8u;
+            bc[o] = X;
+            if (xc != nullptr) xc[o] = omega_c * dcv * X;  // the coarse pre-smoothing step from 0
+          }
+          X = Y;
+          Y = Z;
+        } else {
+          if (k - 1 >= 0 && k - 1 < nQ) X += contrib(Q0 + k - 1, 3, U, V, Sv);
+          if (k < nQ) Y += contrib(Q0 + k, 1, U, V, Sv);
+        }
       }
-      X = Y;
-      Y = Z;
-    } else {
-      if (k - 1 >= 0 && k - 1 < nQ) X += contrib(Q0 + k - 1, 3, U, V, Sv);
-      if (k < nQ) Y += contrib(Q0 + k, 1, U, V, Sv);
     }
-    A = B;
   }
 }
 
