@@ -331,6 +331,62 @@ __device__ __forceinline__ double face_terms(const FaceAdd& fa, int64_t t) {
   return add;
 }
 
+// face_terms with every load issued unconditionally (for the latency-bound
+// coarse-level kernels: a load under the node's face test made the wave wait
+// for it at once, after everything in flight).  One buffer resource over the
+// level's face buffer (one allocation, the faces in order, CgGrid::ffbuf), an
+// out-of-range offset where the node is on neither face of a pair; the sum in
+// face_terms' order.
+struct FaceRsrc {
+  __amdgpu_buffer_rsrc_t r;
+  int64_t d[6];  // element offset of face g from the buffer's base
+};
+__device__ __forceinline__ FaceRsrc face_rsrc(const FaceAdd& fa) {
+  FaceRsrc fr{};
+  const double* fb = nullptr;
+  int64_t fend = 0;
+#pragma unroll
+  for (int g = 0; g < 6; ++g)
+    if (fa.ff[g] != nullptr) {
+      if (fb == nullptr) fb = fa.ff[g];
+      const int64_t sz = (g >> 1) == 0 ? (int64_t)fa.n1 * fa.n2
+                                        : ((g >> 1) == 1 ? (int64_t)fa.n0 * fa.n2 : (int64_t)fa.n0 * fa.n1);
+      fend = (int64_t)(fa.ff[g] - fb) + sz;
+    }
+#pragma unroll
+  for (int g = 0; g < 6; ++g) fr.d[g] = fa.ff[g] ? (int64_t)(fa.ff[g] - fb) : 0;
+  const uint64_t a = (uint64_t)fb;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | lo);
+  fr.r = __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane((uint32_t)(fb ? fend * 8 : 0)),
+                                           0x00020000);
+  return fr;
+}
+__device__ __forceinline__ double face_terms_nb(const FaceAdd& fa, const FaceRsrc& fr, int64_t t) {
+  const int nd = (int)(t + fa.t_off);
+  const int plane = fa.n0 * fa.n1;
+  int k = (int)((double)nd * fa.inv_plane);
+  k -= (k * plane > nd) ? 1 : 0;
+  k += ((k + 1) * plane <= nd) ? 1 : 0;
+  const int rem = nd - k * plane;
+  int j = (int)((double)rem * fa.inv_n0);
+  j -= (j * fa.n0 > rem) ? 1 : 0;
+  j += ((j + 1) * fa.n0 <= rem) ? 1 : 0;
+  const int i = rem - j * fa.n0;
+  const bool x0 = i == 0 && fa.ff[0], x1 = i == fa.n0 - 1 && fa.ff[1];
+  const bool y0 = j == 0 && fa.ff[2], y1 = j == fa.n1 - 1 && fa.ff[3];
+  const bool z0 = k == 0 && fa.ff[4], z1 = k == fa.n2 - 1 && fa.ff[5];
+  constexpr uint32_t kOut = 0x40000000u;
+  const uint32_t ox = (x0 || x1) ? (uint32_t)((x0 ? fr.d[0] : fr.d[1]) + j + (int64_t)fa.n1 * k) * 8u : kOut;
+  const uint32_t oy = (y0 || y1) ? (uint32_t)((y0 ? fr.d[2] : fr.d[3]) + i + (int64_t)fa.n0 * k) * 8u : kOut;
+  const uint32_t oz = (z0 || z1) ? (uint32_t)((z0 ? fr.d[4] : fr.d[5]) + i + (int64_t)fa.n0 * j) * 8u : kOut;
+  const double fx = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(fr.r, (int)ox, 0, 0));
+  const double fy = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(fr.r, (int)oy, 0, 0));
+  const double fz = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(fr.r, (int)oz, 0, 0));
+  return (fx + fy) + fz;
+}
+
 // the same at local node (i, j, k) (coordinates known)
 __device__ __forceinline__ double face_at(const FaceAdd& fa, int i, int j, int k) {
   double add = 0.0;

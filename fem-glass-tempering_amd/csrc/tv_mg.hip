@@ -177,6 +177,26 @@ __device__ __forceinline__ d2a8 ld_pair(const double* p) { return *reinterpret_c
 // a pair not read again: non-temporal (leaves the caches to the vectors that are)
 __device__ __forceinline__ d2a8 ld_pair_nt(const double* p) { return __builtin_nontemporal_load(reinterpret_cast<const d2a8*>(p)); }
 
+// the row-axis / plane-axis face terms of face_at (faces 2 .. 5), added to
+// `add` in face_at's order
+__device__ __forceinline__ double face_rows_add(const FaceAdd& fa, double add, int i, int j, int k) {
+  if (j == 0 && fa.ff[2]) add += fa.ff[2][i + fa.n0 * k];
+  if (j == fa.n1 - 1 && fa.ff[3]) add += fa.ff[3][i + fa.n0 * k];
+  if (k == 0 && fa.ff[4]) add += fa.ff[4][i + fa.n0 * j];
+  if (k == fa.n2 - 1 && fa.ff[5]) add += fa.ff[5][i + fa.n0 * j];
+  return add;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t xf_rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* q = (void*)(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ double xf_ld1(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 0, 0));
+}
+
 // Restriction, one wave per (coarse row, 63-node x segment); lane l is coarse
 // node I = 63 seg - 1 + l (lane 0 = the halo lane whose right fine node is
 // lane 1's left neighbour).  A lane whose fine centre is the row's last node
@@ -184,7 +204,10 @@ __device__ __forceinline__ d2a8 ld_pair_nt(const double* p) { return __builtin_n
 // FACES: wf is a partial J x (k_cg_march without k_cg_addfaces); the facet
 // terms of the face-workgroup faces (fa) are added here, on the boundary rows
 // (wave-uniform test) and the two x-boundary lanes only -- one launch fewer per
-// coarse level (bitwise the same r - (w + faces) as with k_cg_addfaces)
+// coarse level (bitwise the same r - (w + faces) as with k_cg_addfaces).  The
+// x-face terms are loaded with the rows, unconditionally (an out-of-range
+// offset off the x-boundary lanes): loaded under the lane test (face_at) they
+// made every segment-0 / last-segment wave wait for all its loads nine times
 template <bool MASK, bool FACES = false>
 __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const PcgState* __restrict__ st,
                                                              const double* __restrict__ bf,
@@ -229,6 +252,19 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
   d2a8 rv[9], wv[9], mv[9];
   int fjq[9], fkq[9];
   double dc[9], dr[9], wq[9];
+  // FACES: this lane's x-face node -- the pair's .x at fine x 0 (face 0), its
+  // .y at nf - 1 (face 1) or the odd tail lane's node nf - 1 (face 1); the two
+  // x-face arrays through one resource (one allocation, CgGrid::ffbuf)
+  const bool xlo = FACES && fa.ff[0] != nullptr && f1 == 0;
+  const bool xhi = FACES && fa.ff[1] != nullptr && (pair ? f1 + 1 == nf - 1 : f1 == nf - 1);
+  const double* fxb = fa.ff[0] ? fa.ff[0] : fa.ff[1];
+  const int64_t dx1 = (fa.ff[0] && fa.ff[1]) ? (int64_t)(fa.ff[1] - fa.ff[0]) : 0;
+  const __amdgpu_buffer_rsrc_t rfx =
+      xf_rsrc(fxb, (FACES && fxb) ? (uint32_t)((dx1 + (int64_t)fa.n1 * fa.n2) * 8) : 0u);
+  const uint32_t fxo = xhi ? (uint32_t)dx1 : 0u;
+  // only the waves holding an x-face lane issue them (segment 0 and the last)
+  const bool xwave = FACES && __ballot(xlo || xhi) != 0;  // wave-uniform
+  double xfv[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const int c = q / 3, b = q % 3;
@@ -240,18 +276,29 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
     rv[q] = ld_pair(bf + fp);
     wv[q] = (wf != nullptr) ? ld_pair_nt(wf + fp) : d2a8{0.0, 0.0};  // wf null: bf is the residual itself
     if (MASK) mv[q] = ld_pair(mask + fp);
+    xfv[q] = 0.0;
+  }
+  if (xwave) {  // all nine issued back to back, no wait between them
+#pragma unroll
+    for (int q = 0; q < 9; ++q)
+      xfv[q] = xf_ld1(rfx, (xlo || xhi) ? (fxo + (uint32_t)(fjr[q % 3] + fa.n1 * fkr[q / 3])) * 8u : 0x40000000u);
   }
 #pragma unroll
   for (int q = 0; q < 9; ++q) {
     const int fj = fjq[q], fk = fkq[q];
+    const bool rowface = FACES && ((fa.ff[2] && fj == 0) || (fa.ff[3] && fj == fa.n1 - 1) || (fa.ff[4] && fk == 0) ||
+                                   (fa.ff[5] && fk == fa.n2 - 1));  // wave-uniform
     if (pair) {
       const d2a8 r = rv[q];
       d2a8 w = wv[q];
-      if (FACES) {
-        const bool rowface = (fa.ff[2] && fj == 0) || (fa.ff[3] && fj == fa.n1 - 1) || (fa.ff[4] && fk == 0) ||
-                             (fa.ff[5] && fk == fa.n2 - 1);  // wave-uniform
-        if (rowface || f1 == 0) w.x += face_at(fa, f1, fj, fk);
-        if (rowface || f1 + 1 == nf - 1) w.y += face_at(fa, f1 + 1, fj, fk);
+      if (FACES) {  // face_at's sums: the x face first, then faces 2 .. 5 (rare rows: loads under the branch)
+        double ax = xlo ? xfv[q] : 0.0, ay = xhi ? xfv[q] : 0.0;
+        if (rowface) {
+          ax = face_rows_add(fa, ax, f1, fj, fk);
+          ay = face_rows_add(fa, ay, f1 + 1, fj, fk);
+        }
+        if (rowface || f1 == 0) w.x += ax;
+        if (rowface || f1 + 1 == nf - 1) w.y += ay;
       }
       dc[q] = r.x - w.x;
       dr[q] = r.y - w.y;
@@ -262,7 +309,11 @@ __global__ __launch_bounds__(kWave) void k_mg_restrict_pairs(MgXfer x, const Pcg
       }
     } else {
       double wt = wv[q].y;
-      if (FACES) wt += face_at(fa, f1, fj, fk);  // the row's last node: an x-face node
+      if (FACES) {  // the row's last node: an x-face node
+        double add = xhi ? xfv[q] : 0.0;
+        if (rowface) add = face_rows_add(fa, add, f1, fj, fk);
+        wt += add;
+      }
       double d = rv[q].y - wt;
       if (MASK && mv[q].y == 0.0) d = 0.0;
       dc[q] = dr[q] = d;
@@ -371,6 +422,29 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgSta
   // loads the pair ending at its node, rows past the grid a clamped row (not
   // stored); the fine-row weights are wave-uniform scalar loads
   double v[4], cw[4], cd[4], cb[4];
+  // SMOOTH: the coarse facet terms (face_at) with the operands -- one resource
+  // over the coarse level's face buffer (one allocation, faces in order), an
+  // out-of-range offset where a node is on no face of the pair; loaded under the
+  // face tests they cost the waves that hold face nodes another round trip each
+  const FaceAdd& fa = cp.fa;
+  const double* fb = nullptr;
+  int64_t fend = 0;
+  if (SMOOTH) {
+#pragma unroll
+    for (int g = 0; g < 6; ++g)
+      if (fa.ff[g] != nullptr) {
+        if (fb == nullptr) fb = fa.ff[g];
+        const int64_t sz = (g >> 1) == 0 ? (int64_t)fa.n1 * fa.n2 : ((g >> 1) == 1 ? (int64_t)fa.n0 * fa.n2 : (int64_t)fa.n0 * fa.n1);
+        fend = (int64_t)(fa.ff[g] - fb) + sz;
+      }
+  }
+  const __amdgpu_buffer_rsrc_t rfa = xf_rsrc(fb, SMOOTH && fb ? (uint32_t)(fend * 8) : 0u);
+  // element offsets of the six faces (uniform; selected per lane below, never
+  // indexed by a lane value: that puts the argument struct in memory)
+  int64_t fd[6];
+#pragma unroll
+  for (int g = 0; g < 6; ++g) fd[g] = (SMOOTH && fa.ff[g]) ? (int64_t)(fa.ff[g] - fb) : 0;
+  double fv[4][3];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
@@ -380,6 +454,26 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgSta
       cw[q] = cp.w[o];
       cd[q] = cp.dinv[o];
       cb[q] = cp.b[o];
+    }
+    fv[q][0] = fv[q][1] = fv[q][2] = 0.0;
+  }
+  // only the waves holding a face node issue the face loads (all twelve back to
+  // back): an x-boundary lane, or a boundary coarse row / plane (wave-uniform)
+  const bool fwave = SMOOTH && (__ballot(cc == 0 || cc == cn - 1) != 0 || jb == 0 || jc1 == fa.n1 - 1 || kb == 0 ||
+                                kc1 == fa.n2 - 1);
+  if (fwave) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
+      const bool x0 = cc == 0 && fa.ff[0], x1 = cc == fa.n0 - 1 && fa.ff[1];
+      const bool y0 = jcq == 0 && fa.ff[2], y1 = jcq == fa.n1 - 1 && fa.ff[3];
+      const bool z0 = kcq == 0 && fa.ff[4], z1 = kcq == fa.n2 - 1 && fa.ff[5];
+      const int64_t ex = (x0 ? fd[0] : fd[1]) + jcq + (int64_t)fa.n1 * kcq;
+      const int64_t ey = (y0 ? fd[2] : fd[3]) + cc + (int64_t)fa.n0 * kcq;
+      const int64_t ez = (z0 ? fd[4] : fd[5]) + cc + (int64_t)fa.n0 * jcq;
+      fv[q][0] = xf_ld1(rfa, (x0 || x1) ? (uint32_t)ex * 8u : 0x40000000u);
+      fv[q][1] = xf_ld1(rfa, (y0 || y1) ? (uint32_t)ey * 8u : 0x40000000u);
+      fv[q][2] = xf_ld1(rfa, (z0 || z1) ? (uint32_t)ez * 8u : 0x40000000u);
     }
   }
   bool rj[2], rk[2];
@@ -398,7 +492,9 @@ __global__ __launch_bounds__(kWave) void k_mg_prolong_blk(MgXfer x, const PcgSta
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int jcq = (q & 1) ? jc1 : jb, kcq = (q >> 1) ? kc1 : kb;
-      const double wt = cw[q] + face_at(cp.fa, cc, jcq, kcq);
+      (void)jcq;
+      (void)kcq;
+      const double wt = cw[q] + ((fv[q][0] + fv[q][1]) + fv[q][2]);  // face_at's order (0 where no face)
       v[q] += cp.omega * cd[q] * (cb[q] - wt);
     }
   }
@@ -464,12 +560,13 @@ __global__ __launch_bounds__(kBlock) void k_mg_jacobi(int64_t n, const PcgState*
                                                       FaceAdd fa, const double* __restrict__ dinv, double omega,
                                                       double* __restrict__ x) {
   if (st != nullptr && st->done) return;
+  const FaceRsrc fr = FACES ? face_rsrc(fa) : FaceRsrc{};
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     if (MODE == 0) {
       x[t] = omega * dinv[t] * b[t];
     } else {
       double wt = w[t];
-      if (FACES) wt += face_terms(fa, t);
+      if (FACES) wt += face_terms_nb(fa, fr, t);
       x[t] += omega * dinv[t] * (b[t] - wt);
     }
   }
@@ -495,9 +592,10 @@ __global__ __launch_bounds__(kBlock) void k_mg_resid(int64_t n, const PcgState* 
                                                      const double* __restrict__ b, double* __restrict__ w, FaceAdd fa,
                                                      const double* __restrict__ mask) {
   if (st != nullptr && st->done) return;
+  const FaceRsrc fr = FACES ? face_rsrc(fa) : FaceRsrc{};
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
     double wt = w[t];
-    if (FACES) wt += face_terms(fa, t);
+    if (FACES) wt += face_terms_nb(fa, fr, t);
     const double d = b[t] - wt;
     w[t] = (mask != nullptr && mask[t] == 0.0) ? 0.0 : d;
   }
