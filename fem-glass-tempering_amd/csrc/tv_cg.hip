@@ -572,6 +572,17 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, double* __rest
   const int nin = n[0] - 2 > 0 ? n[0] - 2 : 0;
   const int nfree = (raxis == 1) ? nk : n[1];
   const int64_t nB = 2 * (int64_t)nin * nfree;
+  // the face terms and the node's output through buffer loads issued together
+  // (out-of-range offsets where a face does not apply): loaded under the face
+  // tests, each was waited for at once and the output load after them
+  const double* fb = nullptr;
+#pragma unroll
+  for (int f = 0; f < 6; ++f)
+    if (fb == nullptr && g.fface[f] != nullptr) fb = g.fface[f] - g.ffoff[f];
+  const buf_t rsF = mk_rsrc(fb, fb ? (uint32_t)(g.ffsize * 8) : 0u);
+  const uint32_t obytes = (uint32_t)n[0] * (uint32_t)n[1] * (uint32_t)n[2] * 8u;
+  const buf_t rsO = mk_rsrc(out, obytes);
+  const int fr_lo = (raxis == 1) ? 2 : 4;
   for (int64_t e = blockIdx.x * (int64_t)kBlock + threadIdx.x; e < nA + nB; e += (int64_t)gridDim.x * kBlock) {
     int c[3];
     if (e < nA) {
@@ -596,18 +607,19 @@ __global__ __launch_bounds__(kBlock) void k_cg_addfaces(CgGrid g, double* __rest
         if (c[2] < kb || c[2] >= g.w_end) continue;  // that plane is not in the write window
       }
     }
-    double add = 0.0;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      if (a != 0 && a != raxis) continue;  // faces along the march: integrated inside the marching tiles
-      const int t1 = (a == 0) ? 1 : 0, t2 = (a == 2) ? 1 : 2;
-#pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const double* F = g.fface[2 * a + side];
-        if (F && c[a] == (side ? n[a] - 1 : 0)) add += F[c[t1] + n[t1] * c[t2]];
-      }
-    }
-    if (add != 0.0) out[c[0] + (int64_t)n[0] * (c[1] + (int64_t)n[1] * c[2])] += add;
+    // x faces (index c1 + n1 c2), then the row-axis faces (index c0 + n0 c_t2):
+    // the order of the face loop this replaced, so the sums are bitwise the same
+    const bool x0 = g.fface[0] && c[0] == 0, x1 = g.fface[1] && c[0] == n[0] - 1;
+    const bool r0 = g.fface[fr_lo] && c[raxis] == 0, r1 = g.fface[fr_lo + 1] && c[raxis] == n[raxis] - 1;
+    const int rt2 = (raxis == 1) ? c[2] : c[1];
+    const int64_t ex = (x0 ? g.ffoff[0] : g.ffoff[1]) + c[1] + (int64_t)n[1] * c[2];
+    const int64_t er = (r0 ? g.ffoff[fr_lo] : g.ffoff[fr_lo + 1]) + c[0] + (int64_t)n[0] * rt2;
+    const uint32_t oq = (uint32_t)(c[0] + (int64_t)n[0] * (c[1] + (int64_t)n[1] * c[2])) * 8u;
+    const double fx = bload(rsF, (x0 || x1) ? (uint32_t)ex * 8u : kBadOff);
+    const double fr = bload(rsF, (r0 || r1) ? (uint32_t)er * 8u : kBadOff);
+    const double old = bload(rsO, oq);
+    const double add = fx + fr;
+    if (add != 0.0) bstore(rsO, oq, old + add);
   }
 }
 
@@ -1762,6 +1774,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
   const int nO = (raxis == 2) ? n1 : n2;  // the free axis of the row-axis faces besides x
   const int64_t nB = 2 * (int64_t)(n0 - 2) * nO;
   double a0 = 0.0, a1 = 0.0;
+  const FaceRsrc fr = face_rsrc(fa);  // the face terms with the node's loads (a load under each face test waited at once)
   for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < nA + nB; t += (int64_t)gridDim.x * kBlock) {
     int i, j, k;
     if (t < nA) {
@@ -1789,7 +1802,7 @@ __global__ __launch_bounds__(kBlock) void k_mg_post_faces(FaceAdd fa, int raxis,
     const int64_t q = i + (int64_t)n0 * (j + (int64_t)n1 * k);
     // the node's three loads first, independent of the face lookups (one round trip)
     const double zo = z[q], dq = dinv[q], rq = r[q];
-    const double add = face_at(fa, i, j, k);
+    const double add = face_at_nb(fa, fr, i, j, k);
     const double zn = zo - omega * dq * add;
     z[q] = zn;
     if (k < kb || k >= ke) continue;  // a ghost plane: rewritten, not counted

@@ -387,6 +387,21 @@ __device__ __forceinline__ double face_terms_nb(const FaceAdd& fa, const FaceRsr
   return (fx + fy) + fz;
 }
 
+// face_at with every load issued unconditionally (FaceRsrc, as face_terms_nb)
+__device__ __forceinline__ double face_at_nb(const FaceAdd& fa, const FaceRsrc& fr, int i, int j, int k) {
+  const bool x0 = i == 0 && fa.ff[0], x1 = i == fa.n0 - 1 && fa.ff[1];
+  const bool y0 = j == 0 && fa.ff[2], y1 = j == fa.n1 - 1 && fa.ff[3];
+  const bool z0 = k == 0 && fa.ff[4], z1 = k == fa.n2 - 1 && fa.ff[5];
+  constexpr uint32_t kOut = 0x40000000u;
+  const uint32_t ox = (x0 || x1) ? (uint32_t)((x0 ? fr.d[0] : fr.d[1]) + j + (int64_t)fa.n1 * k) * 8u : kOut;
+  const uint32_t oy = (y0 || y1) ? (uint32_t)((y0 ? fr.d[2] : fr.d[3]) + i + (int64_t)fa.n0 * k) * 8u : kOut;
+  const uint32_t oz = (z0 || z1) ? (uint32_t)((z0 ? fr.d[4] : fr.d[5]) + i + (int64_t)fa.n0 * j) * 8u : kOut;
+  const double fx = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(fr.r, (int)ox, 0, 0));
+  const double fy = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(fr.r, (int)oy, 0, 0));
+  const double fz = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(fr.r, (int)oz, 0, 0));
+  return (fx + fy) + fz;
+}
+
 // the same at local node (i, j, k) (coordinates known)
 __device__ __forceinline__ double face_at(const FaceAdd& fa, int i, int j, int k) {
   double add = 0.0;
