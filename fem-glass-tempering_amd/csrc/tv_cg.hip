@@ -501,13 +501,22 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
     c[a] = side ? n[a] - 1 : 0;
     return c[0] + sst[1] * c[1] + sst[2] * c[2];
   };
-  auto stage = [&](int row, int cc2) {
+  // staging in two halves: every row's loads first (wave R - 1 stages two
+  // rows), then the LDS stores -- storing the first row before loading the
+  // second made that wave, and through the barrier the workgroup, wait for two
+  // memory round trips
+  struct Stg {
+    double tt, zz, oo;
+    bool ok;
+  };
+  auto stage_ld = [&](int cc2) -> Stg {
     const bool ok = ok1 && cc2 >= 0 && cc2 < n2;
     const int o = ok ? node_of(c1, cc2) : 0;
-    const double tt = T[o], zz = in0[o];
-    const double oo = FUSEP ? pold[o] : 0.0;
-    sT[row][lane] = ok ? tt : 0.0;
-    sP[row][lane] = ok ? ((FUSEP && !first) ? zz + bcoef * oo : zz) : 0.0;
+    return Stg{T[o], in0[o], FUSEP ? pold[o] : 0.0, ok};
+  };
+  auto stage_st = [&](int row, const Stg& v) {
+    sT[row][lane] = v.ok ? v.tt : 0.0;
+    sP[row][lane] = v.ok ? ((FUSEP && !first) ? v.zz + bcoef * v.oo : v.zz) : 0.0;
   };
   // facet (c1, c1 + 1) x (fr, fr + 1), corners a = (c1, fr), b = (c1+1, fr),
   // c = (c1, fr+1), d = (c1+1, fr+1); its cell lengths load with the staging
@@ -515,8 +524,11 @@ __device__ void face_block(const CgGrid& g, const double* __restrict__ T, const 
   const bool facet_ok = c1 >= 0 && c1 < n1 - 1 && fr >= 0 && fr < n2 - 1;
   const double h1 = g.coef[t1][(int64_t)(facet_ok ? c1 : 0) * C_NCOEF + C_HHI];
   const double h2 = g.coef[t2][(int64_t)(facet_ok ? fr : 0) * C_NCOEF + C_HHI];
-  stage(wave, r0 - 1 + wave);
-  if (wave == R - 1) stage(R, r0 + R - 1);
+  const Stg sa = stage_ld(r0 - 1 + wave);
+  Stg sb{0.0, 0.0, 0.0, false};
+  if (wave == R - 1) sb = stage_ld(r0 + R - 1);  // wave-uniform
+  stage_st(wave, sa);
+  if (wave == R - 1) stage_st(R, sb);
   __syncthreads();
   const double Pa = sP[wave][lane];
   double ya, yb, yc, yd;
@@ -1180,35 +1192,48 @@ __device__ void face_block_cgs(const CgGrid& g, const CgsBuffers& v, const CgsSc
   const bool ok1 = c1 >= 0 && c1 < n1;
   // T and z_i of one staged node; z_i from the previous iteration's r, s,
   // w + facet terms (x face, then row face: the order of the march's loads)
-  auto stage = [&](int row, int cc2) {
-    const bool ok = ok1 && cc2 >= 0 && cc2 < n2;
+  // staging in two halves: the loads of every staged row first (wave R - 1
+  // stages two; the facet terms by buffer loads with out-of-range offsets, not
+  // loads under the face tests), then the arithmetic and the LDS stores
+  const buf_t rsFin = mk_rsrc(v.fin, (uint32_t)(g.ffsize * 8));
+  struct Stg {
+    double tt, R_, D, S, W, fx, fr;
+    bool ok;
+  };
+  auto stage_ld = [&](int cc2) -> Stg {
+    Stg q{};
+    q.ok = ok1 && cc2 >= 0 && cc2 < n2;
     int c[3];
-    c[t1] = ok ? c1 : 0;
-    c[t2] = ok ? cc2 : 0;
+    c[t1] = q.ok ? c1 : 0;
+    c[t2] = q.ok ? cc2 : 0;
     c[a] = side ? n[a] - 1 : 0;
     const int64_t o = c[0] + (int64_t)g.n0 * c[1] + (int64_t)g.n0 * g.n1 * c[2];
-    const double tt = v.T[o], R_ = v.rin[o], D = v.dinv[o];
-    double S = 0.0, W = 0.0, ff = 0.0;
+    q.tt = v.T[o];
+    q.R_ = v.rin[o];
+    q.D = v.dinv[o];
     if (!INIT) {
-      S = ks.first ? 0.0 : v.sin[o];
-      W = v.win[o];
-      const uint32_t ox = ff_off_x(g, c[0], c[1], c[2]);
-      const uint32_t orr = ff_off_r(g, raxis, c[0], c[1], c[2]);
-      const double fx = (ox != kBadOff) ? v.fin[ox / 8u] : 0.0;
-      const double fr = (orr != kBadOff) ? v.fin[orr / 8u] : 0.0;
-      ff = fx + fr;
+      q.S = ks.first ? 0.0 : v.sin[o];
+      q.W = v.win[o];
+      q.fx = bload(rsFin, ff_off_x(g, c[0], c[1], c[2]));
+      q.fr = bload(rsFin, ff_off_r(g, raxis, c[0], c[1], c[2]));
     }
+    return q;
+  };
+  auto stage_st = [&](int row, const Stg& q) {
     double s, r, u;
-    cgs_node<INIT>(ks, R_, S, W, D, ff, s, r, u);
-    sT[row][lane] = ok ? tt : 0.0;
-    sP[row][lane] = ok ? u : 0.0;
+    cgs_node<INIT>(ks, q.R_, q.S, q.W, q.D, INIT ? 0.0 : q.fx + q.fr, s, r, u);
+    sT[row][lane] = q.ok ? q.tt : 0.0;
+    sP[row][lane] = q.ok ? u : 0.0;
   };
   const int fr = r0 - 1 + wave;
   const bool facet_ok = c1 >= 0 && c1 < n1 - 1 && fr >= 0 && fr < n2 - 1;
   const double h1 = g.coef[t1][(int64_t)(facet_ok ? c1 : 0) * C_NCOEF + C_HHI];
   const double h2 = g.coef[t2][(int64_t)(facet_ok ? fr : 0) * C_NCOEF + C_HHI];
-  stage(wave, r0 - 1 + wave);
-  if (wave == R - 1) stage(R, r0 + R - 1);
+  const Stg sa = stage_ld(r0 - 1 + wave);
+  Stg sb{};
+  if (wave == R - 1) sb = stage_ld(r0 + R - 1);  // wave-uniform
+  stage_st(wave, sa);
+  if (wave == R - 1) stage_st(R, sb);
   __syncthreads();
   const double Pa = sP[wave][lane];
   double ya, yb, yc, yd;
