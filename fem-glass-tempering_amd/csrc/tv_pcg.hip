@@ -334,27 +334,6 @@ __device__ __forceinline__ bool post_gate(const PcgState* st) {
   return st->done && !st->post && good;
 }
 
-// dx after the solve, from the device's iteration count (launch_mg_dx_finish);
-// pA == nullptr: the single-reduction form, whose updates keep dx complete --
-// only a solve that converged at its start (0 iterations) leaves dx to zero
-__global__ __launch_bounds__(kBlock) void k_dx_finish_gated(int64_t n, const PcgState* __restrict__ st,
-                                                            const double* __restrict__ pA,
-                                                            const double* __restrict__ pB, double* __restrict__ dx) {
-  if (!post_gate(st)) return;
-  const int its = st->it;
-  const double a = st->a;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  if (pA == nullptr) {
-    if (its == 0)
-      for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] = 0.0;
-  } else if (its <= 1) {
-    for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] = its == 0 ? 0.0 : a * pA[t];
-  } else if (its & 1) {
-    const double* __restrict__ p = ((its - 1) & 1) ? pB : pA;
-    for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += stride) dx[t] += a * p[t];
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __restrict__ T,
                                                           const double* __restrict__ dx,
                                                           double* __restrict__ partials, RedTail rt,
@@ -368,6 +347,44 @@ __global__ __launch_bounds__(kBlock) void k_newton_update(int64_t n, double* __r
   }
   block_partials<1>(acc, partials);
   fused_reduce_tail<1>(rt, gridDim.x);  // ||dx||^2 into rt.out (one partition: no separate reduce launch)
+}
+
+// the post-solve group in one pass: dx after the solve, from the device's
+// iteration count (pA == nullptr: the single-reduction form, whose updates keep
+// dx complete -- only a solve that converged at its start leaves dx to zero),
+// and k_newton_update's T <- T - dx with the ||dx||^2 records, the same values
+// and the same records (one launch and one dx read fewer per Newton iteration)
+__global__ __launch_bounds__(kBlock) void k_post_fused(int64_t n, const PcgState* __restrict__ st,
+                                                       const double* __restrict__ pA, const double* __restrict__ pB,
+                                                       double* __restrict__ dx, double* __restrict__ T,
+                                                       double* __restrict__ partials) {
+  if (!post_gate(st)) return;
+  const int its = st->it;
+  const double a = st->a;
+  // 0: dx as stored; 1: dx <- 0; 2: dx <- a pA; 3: dx <- dx + a p (the odd tail)
+  int mode = 0;
+  const double* __restrict__ p = pA;
+  if (pA == nullptr) {
+    if (its == 0) mode = 1;
+  } else if (its <= 1) {
+    mode = its == 0 ? 1 : 2;
+  } else if (its & 1) {
+    mode = 3;
+    p = ((its - 1) & 1) ? pB : pA;
+  }
+  double acc[1] = {0.0};
+  for (int64_t t = blockIdx.x * (int64_t)kBlock + threadIdx.x; t < n; t += (int64_t)gridDim.x * kBlock) {
+    double d;
+    if (mode == 0) {
+      d = dx[t];
+    } else {
+      d = mode == 1 ? 0.0 : (mode == 2 ? a * p[t] : dx[t] + a * p[t]);
+      dx[t] = d;
+    }
+    T[t] -= d;  // x <- x - relaxation * dx   (relaxation 1)
+    acc[0] += d * d;
+  }
+  block_partials<1>(acc, partials);
 }
 
 // One-block deterministic reduction of `n` partial records of width W, then
@@ -546,8 +563,7 @@ void launch_newton_update(int64_t n, double* T, const double* dx, double* partia
 
 void launch_post_group(int64_t n, const PcgState* st, const double* pA, const double* pB, double* dx, double* T,
                        double* partials, double* sums, hipStream_t s) {
-  hipLaunchKernelGGL(k_dx_finish_gated, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, dx);
-  hipLaunchKernelGGL(k_newton_update, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, T, dx, partials, RedTail{}, st);
+  hipLaunchKernelGGL(k_post_fused, dim3(vec_blocks(n)), dim3(kBlock), 0, s, n, st, pA, pB, dx, T, partials);
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, s, partials, vec_blocks(n), 1, sums, const_cast<PcgState*>(st), 0,
                      2);
 }

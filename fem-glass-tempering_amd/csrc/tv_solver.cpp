@@ -351,7 +351,7 @@ int dirichlet_pre(Ctx* c, const double* T) {
 // polls, ||dx||^2 and the Newton decision) written by a one-wave kernel with
 // system-scope stores straight into the pinned host slot, instead of a
 // hipMemcpyAsync: a copy in the stream left the GPU idle ~5 us each (C4 trace:
-// the gaps before k_dx_finish_gated and before every residual), a launch
+// the gaps before the post-solve group and before every residual), a launch
 // costs ~1.5 us (profiles/r06_launch_audit.json).  TVFEM_PUBLISH=0: the copies.
 __global__ void k_publish(const uint32_t* __restrict__ src, uint32_t* dst, int n) {
   const int t = threadIdx.x;
